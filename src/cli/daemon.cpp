@@ -1,0 +1,243 @@
+#include "cli/daemon.h"
+
+#include <signal.h>
+#include <time.h>
+
+#include <cerrno>
+#include <cstdio>
+
+#include "info/version.h"
+#include "lm/node.h"
+#include "resource/factory.h"
+#include "util/error.h"
+#include "util/log.h"
+
+namespace gfd::cli {
+
+// ---------------------------------------------------------------------------
+// Configuration
+
+void update_from_cli_flags(config::Flags& f, const Context& ctx) {
+  auto str_field = [&](std::optional<std::string>& field, const char* name) {
+    if (ctx.IsSet(name) || !field) field = ctx.String(name);
+  };
+  auto bool_field = [&](std::optional<bool>& field, const char* name) {
+    if (ctx.IsSet(name) || !field) field = ctx.Bool(name);
+  };
+  auto dur_field = [&](std::optional<Nanos>& field, const char* name) {
+    if (ctx.IsSet(name) || !field) field = ctx.Duration(name);
+  };
+  // Common flags.
+  str_field(f.mig_strategy, "mig-strategy");
+  bool_field(f.fail_on_init_error, "fail-on-init-error");
+  // GFD flags.
+  auto& g = f.gfd;
+  bool_field(g.oneshot, "oneshot");
+  str_field(g.output_file, "output-file");
+  dur_field(g.sleep_interval, "sleep-interval");
+  bool_field(g.no_timestamp, "no-timestamp");
+  str_field(g.machine_type_file, "machine-type-file");
+  str_field(g.backend, "backend");
+  str_field(g.sysfs_root, "sysfs-root");
+  str_field(g.visible_devices, "visible-devices");
+  str_field(g.amdsmi_session, "amdsmi-session");
+  str_field(g.mock_file, "mock-file");
+  bool_field(g.trace_timing, "trace-timing");
+}
+
+config::Config load_config(const Context& ctx) {
+  config::Config c;
+  try {
+    std::string file = ctx.String("config-file");
+    if (!file.empty()) {
+      try {
+        c = config::parse_config_file(file);
+      } catch (const std::exception& e) {
+        throw Error(std::string("unable to parse config file: ") + e.what());
+      }
+    }
+    update_from_cli_flags(c.flags, ctx);
+  } catch (const std::exception& e) {
+    throw Error(std::string("unable to finalize config: ") + e.what());
+  }
+  c.flags.plugin_present = false;  // config.Flags.Plugin = nil (main.go:105)
+  return c;
+}
+
+// ---------------------------------------------------------------------------
+// Signals
+
+namespace {
+sigset_t watched_set() {
+  sigset_t s;
+  sigemptyset(&s);
+  sigaddset(&s, SIGHUP);
+  sigaddset(&s, SIGINT);
+  sigaddset(&s, SIGTERM);
+  sigaddset(&s, SIGQUIT);
+  return s;
+}
+}  // namespace
+
+SignalWatcher::SignalWatcher() {
+  sigset_t s = watched_set();
+  pthread_sigmask(SIG_BLOCK, &s, nullptr);
+}
+
+std::optional<int> SignalWatcher::wait(int64_t timeout_ns) {
+  sigset_t s = watched_set();
+  int64_t deadline = trace::now_ns() + (timeout_ns < 0 ? 0 : timeout_ns);
+  for (;;) {
+    int64_t left = deadline - trace::now_ns();
+    if (left < 0) left = 0;
+    struct timespec ts;
+    ts.tv_sec = static_cast<time_t>(left / 1000000000LL);
+    ts.tv_nsec = static_cast<long>(left % 1000000000LL);
+    siginfo_t info;
+    int sig = sigtimedwait(&s, &info, &ts);
+    if (sig > 0) return sig;
+    if (errno == EINTR) continue;
+    return std::nullopt;  // EAGAIN: timeout
+  }
+}
+
+std::string SignalWatcher::name(int sig) {
+  switch (sig) {
+    case SIGHUP: return "hangup";
+    case SIGINT: return "interrupt";
+    case SIGTERM: return "terminated";
+    case SIGQUIT: return "quit";
+    default: return "signal " + std::to_string(sig);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Labeling
+
+CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov::Interface>& sriov,
+                        const config::Config& config, const lm::LabelerPtr& timestamp, bool write) {
+  trace::begin_cycle();
+  int64_t t0 = trace::now_ns();
+  lm::LabelerPtr loop = lm::NewLabelers(manager, sriov, config);
+  lm::LabelerPtr labelers = lm::merge({timestamp, loop});
+  CycleResult r;
+  try {
+    r.labels = labelers->GetLabels();
+  } catch (const std::exception& e) {
+    throw Error(std::string("error generating labels: ") + e.what());
+  }
+  if (r.labels.size() <= 1) log::printf("Warning: no labels generated from any source");
+  if (write) {
+    log::printf("Writing labels to output file");
+    trace::Span span("write");
+    try {
+      lm::write_to_file(r.labels, config.output_file());
+    } catch (const std::exception& e) {
+      throw Error("error writing file '" + config.output_file() + "': " + e.what());
+    }
+  }
+  r.total_ns = trace::now_ns() - t0;
+  r.phases = trace::phases();
+  return r;
+}
+
+bool run(resource::Manager& manager, const std::shared_ptr<sriov::Interface>& sriov, const config::Config& config,
+         SignalWatcher* sigs) {
+  struct Cleanup {
+    const config::Config& c;
+    ~Cleanup() {
+      if (!c.oneshot() && !c.output_file().empty()) {
+        try {
+          lm::remove_output_file(c.output_file());
+        } catch (const std::exception& e) {
+          log::printf("Warning: Error removing output file: %s", e.what());
+        }
+      }
+    }
+  } cleanup{config};
+
+  lm::LabelerPtr timestamp = lm::NewTimestampLabeler(config);
+  for (;;) {
+    CycleResult r = label_cycle(manager, sriov, config, timestamp, true);
+    if (config.trace_timing()) log::printf("Timing: %s", trace::summary(r.total_ns).c_str());
+    if (config.oneshot()) return false;
+
+    log::printf("Sleeping for %s", format_duration(config.sleep_interval()).c_str());
+    std::optional<int> sig;
+    if (sigs) {
+      sig = sigs->wait(config.sleep_interval());
+    } else {
+      struct timespec ts;
+      ts.tv_sec = static_cast<time_t>(config.sleep_interval() / 1000000000LL);
+      ts.tv_nsec = static_cast<long>(config.sleep_interval() % 1000000000LL);
+      nanosleep(&ts, nullptr);
+    }
+    if (!sig) continue;  // rerun
+    if (*sig == SIGHUP) {
+      log::printf("Received SIGHUP, restarting.");
+      return true;
+    }
+    log::printf("Received signal \"%s\", shutting down.", SignalWatcher::name(*sig).c_str());
+    return false;
+  }
+}
+
+void start(const Context& ctx, SignalWatcher& sigs) {
+  for (;;) {
+    log::printf("Loading configuration.");
+    config::Config c;
+    try {
+      c = load_config(ctx);
+    } catch (const std::exception& e) {
+      throw Error(std::string("unable to load config: ") + e.what());
+    }
+    config::disable_resource_renaming(c);
+    log::printf("\nRunning with config:\n%s", config::to_json(c).c_str());
+
+    resource::ManagerPtr manager = resource::new_manager(c);
+    auto sriov = sriov::new_sriov_lib(c.sysfs_root());
+
+    log::printf("Start running");
+    bool restart = run(*manager, sriov, c, &sigs);
+    if (!restart) return;
+  }
+}
+
+int gfd_main(int argc, char** argv) {
+  const std::string app = "GPU Feature Discovery";
+  const std::string usage = "generate labels for AMD devices";
+  std::vector<std::string> args(argv + 1, argv + argc);
+  auto defs = gfd_flags();
+  Context ctx;
+  try {
+    ctx = Context::parse(defs, args);
+  } catch (const UsageError& e) {
+    fprintf(stderr, "Incorrect Usage: %s\n\n%s", e.what(), help_text(defs, app, usage, info::version_string()).c_str());
+    log::printf("Error: %s", e.what());
+    return 1;
+  }
+  if (ctx.help_requested()) {
+    fputs(help_text(defs, app, usage, info::version_string()).c_str(), stdout);
+    return 0;
+  }
+  if (ctx.version_requested()) {
+    printf("%s version %s\n", app.c_str(), info::version_string().c_str());
+    return 0;
+  }
+  int rc = 0;
+  {
+    log::printf("Starting OS watcher.");
+    SignalWatcher sigs;
+    try {
+      start(ctx, sigs);
+    } catch (const std::exception& e) {
+      log::printf("Exiting");
+      log::printf("Error: %s", e.what());
+      return 1;
+    }
+    log::printf("Exiting");
+  }
+  return rc;
+}
+
+}  // namespace gfd::cli

@@ -1,0 +1,57 @@
+// Label model, labeler composition and the NFD feature-file writer.
+//
+// Reference: internal/lm/labels.go:29-114 (Labels, WriteToFile, WriteTo,
+// writeFileAtomically), labeler.go:28-30 (Labeler), list.go:22-46 (Merge:
+// later labelers override earlier ones), empty.go:20-24.
+//
+// Differences by design:
+//   * Labels is an ordered map, so the feature file is written sorted by key
+//     and is byte-for-byte reproducible (the reference writes in Go's random
+//     map order, labels.go:57), which is what makes golden files possible.
+//   * Values are sanitised to valid Kubernetes label values (<=63 chars of
+//     [A-Za-z0-9._-], alphanumeric at both ends); the reference only replaces
+//     spaces, so a DMI string like "Server (X)" would be rejected by NFD.
+#pragma once
+
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+namespace gfd::lm {
+
+using Labels = std::map<std::string, std::string>;
+
+class Labeler {
+ public:
+  virtual ~Labeler() = default;
+  virtual Labels GetLabels() = 0;
+};
+using LabelerPtr = std::shared_ptr<Labeler>;
+
+// A fixed set of labels (Labels implements Labeler in the reference).
+LabelerPtr from_labels(Labels l);
+// The null labeler.
+LabelerPtr empty();
+// Composite: evaluates in order, later keys win; errors are wrapped as
+// "error generating labels: <inner>".
+LabelerPtr merge(std::vector<LabelerPtr> labelers);
+
+// "key=value\n" per label, sorted by key.
+std::string render(const Labels& labels);
+
+// Write labels to `path` atomically (temp file in <dir>/gfd-tmp, rename,
+// chmod 0644).  An empty path writes to stdout.  Throws gfd::Error.
+void write_to_file(const Labels& labels, const std::string& path);
+// Atomic write of arbitrary contents (labels.go:68-114).
+void write_file_atomically(const std::string& path, const std::string& contents, unsigned perm);
+// Removes <dir>/gfd-tmp and the output file (main.go:212-232).
+void remove_output_file(const std::string& path);
+
+// Kubernetes label-value sanitiser: spaces and invalid characters become
+// '-' (so "AMD Instinct MI355X" -> "AMD-Instinct-MI355X" exactly like the
+// reference's space replacement), the result is truncated to 63 characters
+// and trimmed to alphanumeric ends.
+std::string sanitize_label_value(const std::string& v);
+
+}  // namespace gfd::lm

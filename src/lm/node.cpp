@@ -1,0 +1,182 @@
+#include "lm/node.h"
+
+#include <ctime>
+#include <map>
+
+#include "lm/keys.h"
+#include "lm/resource.h"
+#include "util/error.h"
+#include "util/fs.h"
+#include "util/log.h"
+#include "util/strings.h"
+#include "util/trace.h"
+
+namespace gfd::lm {
+
+LabelerPtr NewTimestampLabeler(const config::Config& config, int64_t unix_seconds) {
+  if (config.no_timestamp()) return empty();
+  return from_labels(Labels{{keys::kTimestamp, std::to_string(unix_seconds)}});
+}
+
+LabelerPtr NewTimestampLabeler(const config::Config& config) {
+  return NewTimestampLabeler(config, static_cast<int64_t>(time(nullptr)));
+}
+
+LabelerPtr NewMachineTypeLabeler(const std::string& path) {
+  std::string machine = "unknown";
+  if (!path.empty()) {
+    auto r = fs::read_file(path, 4096);
+    if (r.ok()) {
+      machine = str::trim(r.data);
+    } else {
+      log::printf("WARNING: error getting machine type from %s: could not open machine type file: open %s: %s",
+                  path.c_str(), path.c_str(), fs::errno_str(r.err).c_str());
+    }
+  }
+  return from_labels(Labels{{keys::kMachine, sanitize_label_value(str::replace_all(machine, " ", "-"))}});
+}
+
+LabelerPtr NewVersionLabeler(resource::Manager& manager) {
+  std::string driver = GFD_WRAP("error getting driver version", manager.GetDriverVersion());
+  auto parts = str::split(driver, '.');
+  if (parts.size() > 3 || parts.size() < 2)
+    throw Error("error getting driver version: Version \"" + driver + "\" does not match format \"X.Y[.Z]\"");
+  resource::RuntimeVersion rt = GFD_WRAP("error getting ROCm runtime version", manager.GetRuntimeVersion());
+  return from_labels(Labels{
+      {keys::kDriverMajor, parts[0]},
+      {keys::kDriverMinor, parts[1]},
+      {keys::kDriverRev, parts.size() > 2 ? parts[2] : ""},
+      {keys::kRuntimeMajor, std::to_string(rt.major)},
+      {keys::kRuntimeMinor, std::to_string(rt.minor)},
+  });
+}
+
+LabelerPtr NewPartitionCapabilityLabeler(resource::Manager& manager) {
+  auto devices = manager.GetDevices();
+  if (devices.empty()) return empty();
+  bool capable = false;
+  for (const auto& d : devices) {
+    capable = GFD_WRAP("error getting partition capability", d->IsPartitionCapable());
+    if (capable) break;
+  }
+  return from_labels(Labels{{keys::kPartitionCapable, str::bool_str(capable)}});
+}
+
+LabelerPtr NewTopologyLabeler(resource::Manager& manager) {
+  auto devices = manager.GetDevices();
+  if (devices.empty()) return empty();
+  auto agree = [&](auto get) -> std::string {
+    std::string v;
+    bool first = true;
+    for (const auto& d : devices) {
+      std::string x = get(d->Info());
+      if (first) {
+        v = x;
+        first = false;
+      } else if (x != v) {
+        return "mixed";
+      }
+    }
+    return v;
+  };
+  Labels l;
+  std::string cp = agree([](const resource::DeviceInfo& i) { return i.compute_partition; });
+  std::string mp = agree([](const resource::DeviceInfo& i) { return i.memory_partition; });
+  std::string vm = agree([](const resource::DeviceInfo& i) { return i.virtualization; });
+  if (!cp.empty()) l[keys::kComputePartition] = sanitize_label_value(cp);
+  if (!mp.empty()) l[keys::kMemoryPartition] = sanitize_label_value(mp);
+  if (!vm.empty()) l[keys::kVirtualization] = sanitize_label_value(vm);
+  int links = -1;
+  for (const auto& d : devices) {
+    int x = d->Info().xgmi_links;
+    if (x < 0) continue;
+    links = links < 0 ? x : std::min(links, x);
+  }
+  if (links >= 0) l[keys::kXgmiLinks] = std::to_string(links);
+  return from_labels(std::move(l));
+}
+
+namespace {
+
+class SriovLabeler : public Labeler {
+ public:
+  explicit SriovLabeler(std::shared_ptr<sriov::Interface> lib) : lib_(std::move(lib)) {}
+  Labels GetLabels() override {
+    trace::Span span("sriov");
+    std::vector<sriov::Function> fns;
+    try {
+      fns = lib_->Devices();
+    } catch (const std::exception& e) {
+      throw Error(std::string("unable to get SR-IOV devices: ") + e.what());
+    }
+    Labels l;
+    if (!fns.empty()) l[keys::kSriovPresent] = "true";
+    for (const auto& f : fns) {
+      const auto& info = f.GetInfo();
+      l[keys::kSriovRole] = info.role;
+      if (info.role == "pf") {
+        if (info.total_vfs >= 0) l[keys::kSriovTotalVfs] = std::to_string(info.total_vfs);
+        if (info.num_vfs >= 0) l[keys::kSriovNumVfs] = std::to_string(info.num_vfs);
+      }
+    }
+    return l;
+  }
+
+ private:
+  std::shared_ptr<sriov::Interface> lib_;
+};
+
+// Calls Shutdown when leaving scope (the reference's `defer manager.Shutdown()`).
+class ShutdownGuard {
+ public:
+  explicit ShutdownGuard(resource::Manager& m) : m_(m) {}
+  ~ShutdownGuard() {
+    try {
+      m_.Shutdown();
+    } catch (const std::exception& e) {
+      log::printf("Warning: resource manager shutdown failed: %s", e.what());
+    }
+  }
+
+ private:
+  resource::Manager& m_;
+};
+
+}  // namespace
+
+LabelerPtr NewSriovLabeler(std::shared_ptr<sriov::Interface> lib) { return std::make_shared<SriovLabeler>(std::move(lib)); }
+
+LabelerPtr NewDeviceLabeler(resource::Manager& manager, const config::Config& config) {
+  {
+    trace::Span span("init");
+    try {
+      manager.Init();
+    } catch (const std::exception& e) {
+      throw Error(std::string("failed to initialize resource manager: ") + e.what());
+    }
+  }
+  ShutdownGuard guard(manager);
+
+  std::vector<resource::DevicePtr> devices;
+  {
+    trace::Span span("enumerate");
+    devices = GFD_WRAP("error getting devices", manager.GetDevices());
+  }
+  if (devices.empty()) return empty();
+
+  trace::Span span("label");
+  auto machine = GFD_WRAP("failed to construct machine type labeler", NewMachineTypeLabeler(config.machine_type_file()));
+  auto version = GFD_WRAP("failed to construct version labeler", NewVersionLabeler(manager));
+  auto capability = GFD_WRAP("error creating partition capability labeler", NewPartitionCapabilityLabeler(manager));
+  auto topology = GFD_WRAP("error creating topology labeler", NewTopologyLabeler(manager));
+  auto resources = GFD_WRAP("error creating resource labeler", NewResourceLabeler(manager, config));
+  return merge({machine, version, capability, topology, resources});
+}
+
+LabelerPtr NewLabelers(resource::Manager& manager, std::shared_ptr<sriov::Interface> sriov,
+                       const config::Config& config) {
+  auto device = GFD_WRAP("error creating device labeler", NewDeviceLabeler(manager, config));
+  return merge({device, NewSriovLabeler(std::move(sriov))});
+}
+
+}  // namespace gfd::lm

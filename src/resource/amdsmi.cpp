@@ -1,0 +1,543 @@
+#include "resource/amdsmi.h"
+
+#include <amd_smi/amdsmi.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <thread>
+
+#include "resource/versions.h"
+#include "util/dynlib.h"
+#include "util/error.h"
+#include "util/fs.h"
+#include "util/log.h"
+#include "util/strings.h"
+
+namespace gfd::resource {
+
+// ---------------------------------------------------------------------------
+// Library binding: dlopen once, bind every entry point once.
+
+class AmdSmiLib {
+ public:
+  static AmdSmiLib* get(std::string* err) {
+    static std::once_flag once;
+    static AmdSmiLib* inst = nullptr;
+    static std::string load_error;
+    std::call_once(once, [] {
+      auto* l = new AmdSmiLib();
+      if (l->load(&load_error)) {
+        inst = l;
+      } else {
+        delete l;
+      }
+    });
+    if (!inst && err) *err = load_error;
+    return inst;
+  }
+
+  std::string status_str(amdsmi_status_t st) const {
+    const char* s = nullptr;
+    if (status_code_to_string && status_code_to_string(st, &s) == AMDSMI_STATUS_SUCCESS && s) return s;
+    return "amdsmi status " + std::to_string(static_cast<int>(st));
+  }
+
+  const std::string& path() const { return lib_.path(); }
+
+  // Process-wide init state (amdsmi_init is global).
+  std::mutex mu;
+  int users = 0;
+
+#define GFD_AMDSMI_FN(name, ...) amdsmi_status_t (*name)(__VA_ARGS__) = nullptr
+  GFD_AMDSMI_FN(init, uint64_t);
+  GFD_AMDSMI_FN(shut_down, void);
+  GFD_AMDSMI_FN(get_socket_handles, uint32_t*, amdsmi_socket_handle*);
+  GFD_AMDSMI_FN(get_processor_handles, amdsmi_socket_handle, uint32_t*, amdsmi_processor_handle*);
+  GFD_AMDSMI_FN(get_processor_type, amdsmi_processor_handle, processor_type_t*);
+  GFD_AMDSMI_FN(get_gpu_asic_info, amdsmi_processor_handle, amdsmi_asic_info_t*);
+  GFD_AMDSMI_FN(get_gpu_device_bdf, amdsmi_processor_handle, amdsmi_bdf_t*);
+  GFD_AMDSMI_FN(get_gpu_device_uuid, amdsmi_processor_handle, unsigned int*, char*);
+  GFD_AMDSMI_FN(get_gpu_kfd_info, amdsmi_processor_handle, amdsmi_kfd_info_t*);
+  GFD_AMDSMI_FN(get_gpu_memory_total, amdsmi_processor_handle, amdsmi_memory_type_t, uint64_t*);
+  GFD_AMDSMI_FN(get_gpu_compute_partition, amdsmi_processor_handle, char*, uint32_t);
+  GFD_AMDSMI_FN(get_gpu_memory_partition, amdsmi_processor_handle, char*, uint32_t);
+  GFD_AMDSMI_FN(get_gpu_memory_partition_config, amdsmi_processor_handle, amdsmi_memory_partition_config_t*);
+  GFD_AMDSMI_FN(get_gpu_accelerator_partition_profile, amdsmi_processor_handle,
+                amdsmi_accelerator_partition_profile_t*, uint32_t*);
+  GFD_AMDSMI_FN(get_gpu_accelerator_partition_profile_config, amdsmi_processor_handle,
+                amdsmi_accelerator_partition_profile_config_t*);
+  GFD_AMDSMI_FN(get_gpu_xgmi_link_status, amdsmi_processor_handle, amdsmi_xgmi_link_status_t*);
+  GFD_AMDSMI_FN(get_gpu_virtualization_mode, amdsmi_processor_handle, amdsmi_virtualization_mode_t*);
+  GFD_AMDSMI_FN(get_gpu_xcd_counter, amdsmi_processor_handle, uint16_t*);
+  GFD_AMDSMI_FN(get_gpu_driver_info, amdsmi_processor_handle, amdsmi_driver_info_t*);
+  GFD_AMDSMI_FN(get_lib_version, amdsmi_version_t*);
+#undef GFD_AMDSMI_FN
+  amdsmi_status_t (*status_code_to_string)(amdsmi_status_t, const char**) = nullptr;
+
+ private:
+  bool load(std::string* err) {
+    std::vector<std::string> candidates;
+    if (const char* p = std::getenv("GFD_AMDSMI_LIBRARY"); p && *p) candidates.push_back(p);
+    if (const char* rp = std::getenv("ROCM_PATH"); rp && *rp) {
+      candidates.push_back(fs::join(rp, "lib/libamd_smi.so.26"));
+      candidates.push_back(fs::join(rp, "lib/libamd_smi.so"));
+    }
+    candidates.push_back("/opt/rocm/lib/libamd_smi.so.26");
+    candidates.push_back("/opt/rocm/lib/libamd_smi.so");
+    candidates.push_back("libamd_smi.so.26");
+    candidates.push_back("libamd_smi.so");
+    if (!lib_.open(candidates)) {
+      *err = lib_.last_error();
+      return false;
+    }
+    bool ok = true;
+    auto need = [&](const char* sym, auto& fn) {
+      if (!lib_.bind(sym, fn)) {
+        ok = false;
+        *err = std::string("symbol ") + sym + " not found in " + lib_.path();
+      }
+    };
+    need("amdsmi_init", init);
+    need("amdsmi_shut_down", shut_down);
+    need("amdsmi_get_socket_handles", get_socket_handles);
+    need("amdsmi_get_processor_handles", get_processor_handles);
+    need("amdsmi_get_processor_type", get_processor_type);
+    need("amdsmi_get_gpu_asic_info", get_gpu_asic_info);
+    need("amdsmi_get_gpu_device_bdf", get_gpu_device_bdf);
+    need("amdsmi_get_gpu_memory_total", get_gpu_memory_total);
+    need("amdsmi_get_gpu_driver_info", get_gpu_driver_info);
+    // Optional: newer partition / topology queries degrade gracefully.
+    lib_.bind("amdsmi_get_gpu_device_uuid", get_gpu_device_uuid);
+    lib_.bind("amdsmi_get_gpu_kfd_info", get_gpu_kfd_info);
+    lib_.bind("amdsmi_get_gpu_compute_partition", get_gpu_compute_partition);
+    lib_.bind("amdsmi_get_gpu_memory_partition", get_gpu_memory_partition);
+    lib_.bind("amdsmi_get_gpu_memory_partition_config", get_gpu_memory_partition_config);
+    lib_.bind("amdsmi_get_gpu_accelerator_partition_profile", get_gpu_accelerator_partition_profile);
+    lib_.bind("amdsmi_get_gpu_accelerator_partition_profile_config", get_gpu_accelerator_partition_profile_config);
+    lib_.bind("amdsmi_get_gpu_xgmi_link_status", get_gpu_xgmi_link_status);
+    lib_.bind("amdsmi_get_gpu_virtualization_mode", get_gpu_virtualization_mode);
+    lib_.bind("amdsmi_get_gpu_xcd_counter", get_gpu_xcd_counter);
+    lib_.bind("amdsmi_get_lib_version", get_lib_version);
+    lib_.bind("amdsmi_status_code_to_string", status_code_to_string);
+    return ok;
+  }
+
+  DynLib lib_;
+};
+
+bool has_amdsmi(std::string* reason) {
+  std::string err;
+  AmdSmiLib* l = AmdSmiLib::get(&err);
+  if (!l) {
+    if (reason) *reason = "could not load libamd_smi: " + err;
+    return false;
+  }
+  if (reason) *reason = "found " + l->path();
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// Snapshot helpers
+
+namespace {
+
+// Raw per-processor facts (one amd-smi processor = a GPU or a partition).
+struct ProcInfo {
+  amdsmi_processor_handle h = nullptr;
+  std::string bdf;
+  std::string market_name;
+  uint32_t vendor_id = 0;
+  uint32_t device_id = 0;
+  uint32_t cus = 0;
+  uint64_t gfx = 0;
+  uint64_t vram = 0;
+  uint32_t partition_id = 0;
+  uint32_t xcds = 0;
+  std::string compute_partition;
+  std::string memory_partition;
+  std::string uuid;
+};
+
+// Facts queried once per physical GPU.
+struct GpuExtras {
+  int xgmi_links = -1;
+  std::string virtualization;
+  uint32_t nps_caps = 0;
+  std::vector<std::string> available_compute;
+  Attributes engines;  // engines.* from the accelerator partition profile
+};
+
+const char* virt_name(amdsmi_virtualization_mode_t m) {
+  switch (m) {
+    case AMDSMI_VIRTUALIZATION_MODE_BAREMETAL: return "baremetal";
+    case AMDSMI_VIRTUALIZATION_MODE_HOST: return "host";
+    case AMDSMI_VIRTUALIZATION_MODE_GUEST: return "guest";
+    case AMDSMI_VIRTUALIZATION_MODE_PASSTHROUGH: return "passthrough";
+    default: return "";
+  }
+}
+
+const char* accel_name(amdsmi_accelerator_partition_type_t t) {
+  switch (t) {
+    case AMDSMI_ACCELERATOR_PARTITION_SPX: return "SPX";
+    case AMDSMI_ACCELERATOR_PARTITION_DPX: return "DPX";
+    case AMDSMI_ACCELERATOR_PARTITION_TPX: return "TPX";
+    case AMDSMI_ACCELERATOR_PARTITION_QPX: return "QPX";
+    case AMDSMI_ACCELERATOR_PARTITION_CPX: return "CPX";
+    default: return nullptr;
+  }
+}
+
+std::vector<std::string> nps_list(uint32_t mask) {
+  std::vector<std::string> out;
+  if (mask & 1u) out.push_back("NPS1");
+  if (mask & 2u) out.push_back("NPS2");
+  if (mask & 4u) out.push_back("NPS4");
+  if (mask & 8u) out.push_back("NPS8");
+  return out;
+}
+
+void query_proc(AmdSmiLib& L, ProcInfo& p) {
+  amdsmi_asic_info_t asic;
+  std::memset(&asic, 0, sizeof(asic));
+  amdsmi_status_t st = L.get_gpu_asic_info(p.h, &asic);
+  if (st != AMDSMI_STATUS_SUCCESS) throw Error("amdsmi_get_gpu_asic_info: " + L.status_str(st));
+  p.market_name = str::trim(asic.market_name);
+  p.vendor_id = asic.vendor_id;
+  p.device_id = static_cast<uint32_t>(asic.device_id);
+  p.cus = asic.num_of_compute_units == 0xFFFFFFFFu ? 0 : asic.num_of_compute_units;
+  p.gfx = asic.target_graphics_version;
+
+  uint64_t total = 0;
+  if (L.get_gpu_memory_total(p.h, AMDSMI_MEM_TYPE_VRAM, &total) == AMDSMI_STATUS_SUCCESS) p.vram = total;
+
+  if (L.get_gpu_kfd_info) {
+    amdsmi_kfd_info_t kfd;
+    std::memset(&kfd, 0, sizeof(kfd));
+    if (L.get_gpu_kfd_info(p.h, &kfd) == AMDSMI_STATUS_SUCCESS && kfd.current_partition_id != 0xFFFFFFFFu)
+      p.partition_id = kfd.current_partition_id;
+  }
+  char buf[64];
+  if (L.get_gpu_compute_partition) {
+    std::memset(buf, 0, sizeof(buf));
+    if (L.get_gpu_compute_partition(p.h, buf, sizeof(buf)) == AMDSMI_STATUS_SUCCESS) p.compute_partition = str::trim(buf);
+  }
+  if (L.get_gpu_memory_partition) {
+    std::memset(buf, 0, sizeof(buf));
+    if (L.get_gpu_memory_partition(p.h, buf, sizeof(buf)) == AMDSMI_STATUS_SUCCESS) p.memory_partition = str::trim(buf);
+  }
+  if (L.get_gpu_xcd_counter) {
+    uint16_t x = 0;
+    if (L.get_gpu_xcd_counter(p.h, &x) == AMDSMI_STATUS_SUCCESS) p.xcds = x;
+  }
+}
+
+void query_gpu_extras(AmdSmiLib& L, const ProcInfo& p, const std::string& root, bool partitioned, GpuExtras& x) {
+  if (L.get_gpu_xgmi_link_status) {
+    amdsmi_xgmi_link_status_t ls;
+    std::memset(&ls, 0, sizeof(ls));
+    if (L.get_gpu_xgmi_link_status(p.h, &ls) == AMDSMI_STATUS_SUCCESS) {
+      int up = 0;
+      for (uint32_t i = 0; i < ls.total_links && i < AMDSMI_MAX_NUM_XGMI_LINKS; ++i)
+        if (ls.status[i] == AMDSMI_XGMI_LINK_UP) ++up;
+      x.xgmi_links = up;
+    }
+  }
+  if (L.get_gpu_virtualization_mode) {
+    amdsmi_virtualization_mode_t vm = AMDSMI_VIRTUALIZATION_MODE_UNKNOWN;
+    if (L.get_gpu_virtualization_mode(p.h, &vm) == AMDSMI_STATUS_SUCCESS) x.virtualization = virt_name(vm);
+  }
+  if (L.get_gpu_memory_partition_config) {
+    amdsmi_memory_partition_config_t cfg;
+    std::memset(&cfg, 0, sizeof(cfg));
+    if (L.get_gpu_memory_partition_config(p.h, &cfg) == AMDSMI_STATUS_SUCCESS) x.nps_caps = cfg.partition_caps.nps_cap_mask;
+  }
+  // Supported compute partition modes: the profile table needs root; the
+  // same information is world-readable in sysfs, which amd-smi itself reads.
+  if (L.get_gpu_accelerator_partition_profile_config) {
+    amdsmi_accelerator_partition_profile_config_t cfg;
+    std::memset(&cfg, 0, sizeof(cfg));
+    if (L.get_gpu_accelerator_partition_profile_config(p.h, &cfg) == AMDSMI_STATUS_SUCCESS) {
+      for (uint32_t i = 0; i < cfg.num_profiles && i < AMDSMI_MAX_ACCELERATOR_PROFILE; ++i)
+        if (const char* n = accel_name(cfg.profiles[i].profile_type)) x.available_compute.push_back(n);
+    }
+  }
+  if (x.available_compute.empty()) {
+    auto v = fs::read_trimmed(fs::join(root, "sys/bus/pci/devices/" + p.bdf + "/available_compute_partition"));
+    if (v)
+      for (auto& m : str::split(*v, ','))
+        if (!str::trim(m).empty()) x.available_compute.push_back(str::trim(m));
+  }
+  // Per-partition engine counts (only meaningful when partitioned).
+  if (partitioned && L.get_gpu_accelerator_partition_profile) {
+    amdsmi_accelerator_partition_profile_t prof;
+    std::memset(&prof, 0, sizeof(prof));
+    uint32_t ids[AMDSMI_MAX_ACCELERATOR_PARTITIONS] = {0};
+    if (L.get_gpu_accelerator_partition_profile(p.h, &prof, ids) == AMDSMI_STATUS_SUCCESS && prof.num_resources > 0) {
+      // resources[partition][resource-type] holds instance counts.
+      static const char* kNames[] = {"engines.xcc", "engines.encoder", "engines.decoder", "engines.dma", "engines.jpeg"};
+      for (uint32_t r = 0; r < prof.num_resources && r < AMDSMI_ACCELERATOR_MAX; ++r)
+        if (r != AMDSMI_ACCELERATOR_XCC) x.engines[kNames[r]] = std::to_string(prof.resources[0][r]);
+    }
+  }
+}
+
+std::string format_bdf(const amdsmi_bdf_t& b) {
+  return str::format("%04llx:%02x:%02x.%x", static_cast<unsigned long long>(b.domain_number),
+                     static_cast<unsigned>(b.bus_number), static_cast<unsigned>(b.device_number),
+                     static_cast<unsigned>(b.function_number));
+}
+
+// Statuses meaning "the session/handles are stale; re-initialise".
+bool is_stale(const std::string& msg) {
+  return msg.find("NOT_INIT") != std::string::npos || msg.find("NOT_FOUND") != std::string::npos ||
+         msg.find("not initialized") != std::string::npos || msg.find("not found") != std::string::npos ||
+         msg.find("status 32") != std::string::npos || msg.find("status 31") != std::string::npos;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// AmdSmiManager
+
+AmdSmiManager::AmdSmiManager(AmdSmiOptions opts) : opts_(std::move(opts)) {}
+
+AmdSmiManager::~AmdSmiManager() {
+  if (lib_initialized_) library_shutdown();
+}
+
+void AmdSmiManager::library_init() {
+  std::lock_guard<std::mutex> g(lib_->mu);
+  amdsmi_status_t st = lib_->init(AMDSMI_INIT_AMD_GPUS);
+  if (st != AMDSMI_STATUS_SUCCESS) throw Error("amdsmi_init failed: " + lib_->status_str(st));
+  lib_->users++;
+  lib_initialized_ = true;
+  ++init_count_;
+}
+
+void AmdSmiManager::library_shutdown() {
+  std::lock_guard<std::mutex> g(lib_->mu);
+  lib_initialized_ = false;
+  if (--lib_->users == 0) lib_->shut_down();
+}
+
+std::string AmdSmiManager::read_generation() const {
+  return fs::read_trimmed(fs::join(opts_.root, "sys/class/kfd/kfd/topology/generation_id")).value_or("");
+}
+
+void AmdSmiManager::Init() {
+  if (!lib_) {
+    std::string err;
+    lib_ = AmdSmiLib::get(&err);
+    if (!lib_) throw Error("failed to load amd-smi: " + err);
+  }
+  if (opts_.persistent && lib_initialized_) {
+    // A partition-mode change or driver reload bumps the KFD generation and
+    // invalidates every processor handle.
+    std::string gen = read_generation();
+    if (gen != generation_) {
+      library_shutdown();
+      library_init();
+      generation_ = gen;
+    }
+  } else if (!lib_initialized_) {
+    library_init();
+    if (opts_.persistent) generation_ = read_generation();
+  }
+  in_window_ = true;
+  have_snapshot_ = false;
+}
+
+void AmdSmiManager::Shutdown() {
+  in_window_ = false;
+  have_snapshot_ = false;
+  snapshot_.clear();
+  if (!opts_.persistent && lib_initialized_) library_shutdown();
+}
+
+std::vector<DevicePtr> AmdSmiManager::GetDevices() {
+  if (!in_window_) throw Error("amd-smi manager not initialized");
+  if (have_snapshot_) return snapshot_;
+  try {
+    snapshot_ = snapshot();
+  } catch (const Error& e) {
+    if (!opts_.persistent || !is_stale(e.what())) throw;
+    log::printf("amd-smi handles are stale (%s); re-initializing", e.what());
+    library_shutdown();
+    library_init();
+    generation_ = read_generation();
+    snapshot_ = snapshot();
+  }
+  have_snapshot_ = true;
+  return snapshot_;
+}
+
+std::vector<DevicePtr> AmdSmiManager::snapshot() {
+  AmdSmiLib& L = *lib_;
+  uint32_t ns = 0;
+  amdsmi_status_t st = L.get_socket_handles(&ns, nullptr);
+  if (st != AMDSMI_STATUS_SUCCESS) throw Error("amdsmi_get_socket_handles: " + L.status_str(st));
+  std::vector<amdsmi_socket_handle> sockets(ns);
+  if (ns) {
+    st = L.get_socket_handles(&ns, sockets.data());
+    if (st != AMDSMI_STATUS_SUCCESS) throw Error("amdsmi_get_socket_handles: " + L.status_str(st));
+    sockets.resize(ns);
+  }
+
+  // Collect GPU processors, grouped by PCI address.
+  std::map<std::string, std::vector<ProcInfo>> groups;
+  for (auto s : sockets) {
+    uint32_t np = 0;
+    st = L.get_processor_handles(s, &np, nullptr);
+    if (st != AMDSMI_STATUS_SUCCESS) throw Error("amdsmi_get_processor_handles: " + L.status_str(st));
+    std::vector<amdsmi_processor_handle> procs(np);
+    if (np) {
+      st = L.get_processor_handles(s, &np, procs.data());
+      if (st != AMDSMI_STATUS_SUCCESS) throw Error("amdsmi_get_processor_handles: " + L.status_str(st));
+      procs.resize(np);
+    }
+    for (auto h : procs) {
+      processor_type_t t;
+      if (L.get_processor_type(h, &t) != AMDSMI_STATUS_SUCCESS || t != AMDSMI_PROCESSOR_TYPE_AMD_GPU) continue;
+      amdsmi_bdf_t b;
+      std::memset(&b, 0, sizeof(b));
+      st = L.get_gpu_device_bdf(h, &b);
+      if (st != AMDSMI_STATUS_SUCCESS) throw Error("amdsmi_get_gpu_device_bdf: " + L.status_str(st));
+      ProcInfo p;
+      p.h = h;
+      p.bdf = format_bdf(b);
+      groups[p.bdf].push_back(p);
+    }
+  }
+
+  // Apply the visible-device filter on physical GPUs (index = BDF order).
+  struct Gpu {
+    int index;
+    std::string bdf;
+    std::vector<ProcInfo>* procs;
+    GpuExtras extras;
+    std::string error;
+  };
+  std::vector<Gpu> gpus;
+  int index = -1;
+  for (auto& [bdf, procs] : groups) {
+    ++index;
+    if (opts_.filter.matches(index, bdf)) gpus.push_back(Gpu{index, bdf, &procs, {}, {}});
+  }
+
+  // Query every processor; parallel across physical GPUs on multi-GPU nodes.
+  auto work = [&](Gpu& g) {
+    try {
+      for (auto& p : *g.procs) query_proc(L, p);
+      std::sort(g.procs->begin(), g.procs->end(),
+                [](const ProcInfo& a, const ProcInfo& b) { return a.partition_id < b.partition_id; });
+      const ProcInfo& first = g.procs->front();
+      bool partitioned = g.procs->size() > 1 || (!first.compute_partition.empty() && first.compute_partition != "SPX");
+      query_gpu_extras(L, first, opts_.root, partitioned, g.extras);
+    } catch (const std::exception& e) {
+      g.error = e.what();
+    }
+  };
+  int threads = opts_.threads > 0 ? opts_.threads : static_cast<int>(std::min<size_t>(gpus.size(), 8));
+  if (threads <= 1 || gpus.size() <= 1) {
+    for (auto& g : gpus) work(g);
+  } else {
+    std::vector<std::thread> pool;
+    std::atomic<size_t> next{0};
+    for (int t = 0; t < threads; ++t)
+      pool.emplace_back([&] {
+        for (size_t i = next++; i < gpus.size(); i = next++) work(gpus[i]);
+      });
+    for (auto& th : pool) th.join();
+  }
+  for (const auto& g : gpus)
+    if (!g.error.empty()) throw Error(g.error);
+
+  // Driver version: one query per node (all GPUs share the amdgpu module).
+  if (!gpus.empty()) {
+    amdsmi_driver_info_t drv;
+    std::memset(&drv, 0, sizeof(drv));
+    if (L.get_gpu_driver_info(gpus.front().procs->front().h, &drv) == AMDSMI_STATUS_SUCCESS)
+      driver_version_ = drv.driver_version;
+  }
+
+  std::vector<DevicePtr> out;
+  for (auto& g : gpus) {
+    const ProcInfo& first = g.procs->front();
+    DeviceInfo info;
+    info.index = g.index;
+    info.bdf = g.bdf;
+    info.name = first.market_name;
+    info.vendor_id = first.vendor_id;
+    info.device_id = first.device_id;
+    info.gfx = gfx_target_from_amdsmi(first.gfx);
+    info.compute_partition = first.compute_partition;
+    info.memory_partition = first.memory_partition;
+    info.available_compute_partitions = g.extras.available_compute;
+    info.available_memory_partitions = nps_list(g.extras.nps_caps);
+    info.xgmi_links = g.extras.xgmi_links;
+    info.virtualization = g.extras.virtualization;
+    bool partitioned = g.procs->size() > 1 || (!first.compute_partition.empty() && first.compute_partition != "SPX");
+
+    std::vector<std::shared_ptr<SnapshotDevice>> parts;
+    uint64_t mem = 0;
+    uint32_t cus = 0, xcds = 0;
+    for (const auto& p : *g.procs) {
+      mem += p.vram;
+      cus += p.cus;
+      xcds += p.xcds;
+      if (!partitioned) continue;
+      DeviceInfo pi;
+      pi.partition_id = static_cast<int>(p.partition_id);
+      pi.bdf = g.bdf;
+      pi.vendor_id = p.vendor_id;
+      pi.device_id = p.device_id;
+      pi.compute_units = p.cus;
+      pi.xcds = p.xcds;
+      pi.memory_mib = p.vram >> 20;
+      pi.compute_partition = p.compute_partition;
+      pi.memory_partition = p.memory_partition;
+      pi.name = partition_profile_name(pi.compute_partition, pi.xcds, pi.memory_mib);
+      pi.attributes = {
+          {"memory", std::to_string(pi.memory_mib)},
+          {"compute-units", std::to_string(pi.compute_units)},
+          {"xcds", std::to_string(pi.xcds)},
+      };
+      for (const auto& kv : g.extras.engines) pi.attributes[kv.first] = kv.second;
+      if (!pi.compute_partition.empty()) pi.attributes["compute-partition"] = pi.compute_partition;
+      if (!pi.memory_partition.empty()) pi.attributes["memory-partition"] = pi.memory_partition;
+      parts.push_back(SnapshotDevice::partition(std::move(pi)));
+    }
+    info.memory_mib = mem >> 20;
+    info.compute_units = cus;
+    info.xcds = xcds;
+    bool capable = info.available_compute_partitions.size() > 1;
+    auto dev = SnapshotDevice::gpu(std::move(info), partitioned, capable);
+    dev->set_partitions(std::move(parts));
+    out.push_back(dev);
+  }
+  return out;
+}
+
+std::string AmdSmiManager::GetDriverVersion() {
+  if (driver_version_.empty()) {
+    // No GPU enumerated yet in this window: fall back to the host's view.
+    if (have_snapshot_ || !in_window_) return host_driver_version(opts_.root);
+    GetDevices();
+    if (driver_version_.empty()) return host_driver_version(opts_.root);
+  }
+  auto v = extract_version(driver_version_);
+  return v ? *v : driver_version_;
+}
+
+RuntimeVersion AmdSmiManager::GetRuntimeVersion() {
+  auto v = rocm_version(opts_.root);
+  if (!v) throw Error("unable to determine the ROCm version (no .info/version under $ROCM_PATH or /opt/rocm)");
+  return *v;
+}
+
+}  // namespace gfd::resource

@@ -1,0 +1,74 @@
+// amd-smi backend: the primary MI355X device enumerator.
+//
+// Reference analogue: the NVML manager (internal/resource/nvml-lib.go:24-97,
+// nvml-device.go, nvml-mig-device.go) on top of the vendored cgo binding
+// go-nvml (pkg/nvml/init.go:25-218) and its dlopen wrapper (pkg/dl).
+//
+// MI355X-first differences, all measured on the pool (profiles/hw_probe.md):
+//   * libamd_smi is dlopen'ed ONCE per process and its ~20 entry points bound
+//     once (the reference dlopens libnvidia-ml 2N+1 times per cycle).
+//   * amdsmi_init costs ~25 ms while all per-GPU queries together cost
+//     ~0.5 ms, so the default session mode keeps the library initialised
+//     across cycles ("persistent") and re-initialises only when the KFD
+//     topology generation changes (a partition-mode switch or driver reload)
+//     or a query reports a stale handle.  "per-cycle" reproduces the
+//     reference's Init/Shutdown-every-cycle behaviour.
+//   * the node is enumerated once per cycle into value snapshots; per-GPU
+//     queries run in parallel across physical GPUs on multi-GPU nodes.
+//   * compute partitions (DPX/QPX/CPX) are separate amd-smi processors that
+//     share a PCI address; they are regrouped into parent GPUs by BDF.
+#pragma once
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "resource/filter.h"
+#include "resource/types.h"
+
+namespace gfd::resource {
+
+struct AmdSmiOptions {
+  bool persistent = true;       // keep amdsmi initialised across cycles
+  std::string root = "/";       // for the KFD generation check / sysfs hints
+  DeviceFilter filter;
+  int threads = 0;              // 0 = auto (one per physical GPU, max 8)
+};
+
+// Process-wide handle to libamd_smi (opened on first use).
+class AmdSmiLib;
+// True if libamd_smi can be loaded; `reason` explains either way.
+bool has_amdsmi(std::string* reason);
+
+class AmdSmiManager : public Manager {
+ public:
+  explicit AmdSmiManager(AmdSmiOptions opts);
+  ~AmdSmiManager() override;
+  void Init() override;
+  void Shutdown() override;
+  std::vector<DevicePtr> GetDevices() override;
+  std::string GetDriverVersion() override;
+  RuntimeVersion GetRuntimeVersion() override;
+  std::string Name() const override { return opts_.persistent ? "amdsmi(persistent)" : "amdsmi"; }
+
+  // Number of amdsmi_init calls made by this manager (tests / benchmarks).
+  int init_count() const { return init_count_; }
+
+ private:
+  std::vector<DevicePtr> snapshot();
+  void library_init();
+  void library_shutdown();
+  std::string read_generation() const;
+
+  AmdSmiOptions opts_;
+  AmdSmiLib* lib_ = nullptr;
+  bool lib_initialized_ = false;
+  bool in_window_ = false;
+  bool have_snapshot_ = false;
+  std::vector<DevicePtr> snapshot_;
+  std::string driver_version_;
+  std::string generation_;
+  int init_count_ = 0;
+};
+
+}  // namespace gfd::resource

@@ -1,0 +1,243 @@
+#include "resource/managers.h"
+
+#include "util/error.h"
+#include "util/fs.h"
+#include "util/log.h"
+#include "util/strings.h"
+
+namespace gfd::resource {
+
+// ---------------------------------------------------------------------------
+// Null / Fallback
+
+std::string NullManager::GetDriverVersion() { throw Error("GetDriverVersion is unsupported"); }
+RuntimeVersion NullManager::GetRuntimeVersion() { throw Error("GetRuntimeVersion is unsupported"); }
+
+FallbackManager::FallbackManager(ManagerPtr wraps) : current_(std::move(wraps)) {}
+
+void FallbackManager::Init() {
+  try {
+    current_->Init();
+  } catch (const std::exception& e) {
+    log::printf("Warning: failed to initialize resource manager: %s", e.what());
+    current_ = std::make_shared<NullManager>();
+    fell_back_ = true;
+  }
+}
+
+ManagerPtr with_config(ManagerPtr m, const config::Config& c) {
+  if (c.fail_on_init_error()) return m;
+  return std::make_shared<FallbackManager>(std::move(m));
+}
+
+// ---------------------------------------------------------------------------
+// Mock
+
+MockManager::MockManager(std::vector<DevicePtr> devs) : devices(std::move(devs)) {}
+
+void MockManager::Init() {
+  ++init_calls;
+  if (init_error) throw Error(*init_error);
+}
+
+void MockManager::Shutdown() { ++shutdown_calls; }
+
+std::vector<DevicePtr> MockManager::GetDevices() {
+  ++get_devices_calls;
+  if (devices_error) throw Error(*devices_error);
+  return devices;
+}
+
+std::string MockManager::GetDriverVersion() {
+  if (driver_error) throw Error(*driver_error);
+  return driver_version;
+}
+
+RuntimeVersion MockManager::GetRuntimeVersion() {
+  if (runtime_error) throw Error(*runtime_error);
+  return runtime_version;
+}
+
+MockManager& MockManager::with_error_on_init(std::string msg) {
+  init_error = std::move(msg);
+  return *this;
+}
+MockManager& MockManager::with_driver_version(std::string v) {
+  driver_version = std::move(v);
+  return *this;
+}
+MockManager& MockManager::with_runtime_version(RuntimeVersion v) {
+  runtime_version = v;
+  return *this;
+}
+
+// ---------------------------------------------------------------------------
+// Builders
+
+std::shared_ptr<SnapshotDevice> new_mock_gpu(bool partitioned) {
+  DeviceInfo info;
+  info.name = "MOCKMODEL";
+  info.memory_mib = 300;
+  if (!partitioned) {
+    info.gfx = GfxTarget{9, 5, 0};
+    info.compute_units = 256;
+    info.xcds = 8;
+    info.compute_partition = "SPX";
+  } else {
+    info.compute_partition = "CPX";
+  }
+  info.memory_partition = "NPS1";
+  return SnapshotDevice::gpu(std::move(info), partitioned, /*partition_capable=*/partitioned);
+}
+
+std::shared_ptr<SnapshotDevice> new_full_gpu() { return new_mock_gpu(false); }
+
+std::shared_ptr<SnapshotDevice> new_partitioned_gpu(std::vector<std::shared_ptr<SnapshotDevice>> partitions) {
+  auto d = new_mock_gpu(true);
+  d->set_partitions(std::move(partitions));
+  return d;
+}
+
+std::shared_ptr<SnapshotDevice> new_partition(const std::string& mode, int xcds, uint64_t gb,
+                                              const Attributes& overrides) {
+  DeviceInfo info;
+  info.name = str::to_lower(mode) + "." + std::to_string(xcds) + "xcd." + std::to_string(gb) + "gb";
+  info.memory_mib = gb;
+  info.xcds = static_cast<uint32_t>(xcds);
+  info.compute_partition = str::to_upper(mode);
+  info.memory_partition = "NPS1";
+  info.attributes = {
+      {"memory", std::to_string(gb)},
+      {"compute-units", "0"},
+      {"xcds", std::to_string(xcds)},
+      {"engines.dma", "0"},
+      {"engines.decoder", "0"},
+      {"engines.encoder", "0"},
+      {"engines.jpeg", "0"},
+      {"compute-partition", str::to_upper(mode)},
+      {"memory-partition", "NPS1"},
+  };
+  for (const auto& kv : overrides) info.attributes[kv.first] = kv.second;
+  return SnapshotDevice::partition(std::move(info));
+}
+
+// ---------------------------------------------------------------------------
+// Fixture loading
+
+namespace {
+
+using yaml::Node;
+
+std::string scalar_or(const Node* n, const std::string& def) { return n && n->is_scalar() && !n->is_null() ? n->text() : def; }
+
+uint64_t uint_or(const Node* n, uint64_t def) {
+  if (!n || n->is_null()) return def;
+  if (n->kind() == Node::Kind::Int && n->as_int() >= 0) return static_cast<uint64_t>(n->as_int());
+  auto v = str::parse_uint_auto(n->text());
+  if (!v) throw Error("mock fixture: expected unsigned integer, got '" + n->text() + "'");
+  return *v;
+}
+
+bool bool_or(const Node* n, bool def) {
+  if (!n || n->is_null()) return def;
+  if (n->kind() != Node::Kind::Bool) throw Error("mock fixture: expected bool, got '" + n->text() + "'");
+  return n->as_bool();
+}
+
+std::vector<std::string> string_list(const Node* n) {
+  std::vector<std::string> out;
+  if (!n || n->is_null()) return out;
+  if (n->is_seq()) {
+    for (const auto& i : n->items()) out.push_back(i.text());
+  } else {
+    for (auto& p : str::split(n->text(), ',')) out.push_back(str::trim(p));
+  }
+  return out;
+}
+
+void load_errors(const Node* n, DeviceInfo& info) {
+  if (!n || !n->is_map()) return;
+  for (const auto& kv : n->entries()) info.errors[kv.first] = kv.second.text();
+}
+
+void load_common(const Node& d, DeviceInfo& info) {
+  info.name = scalar_or(d.get("name"), info.name);
+  info.bdf = scalar_or(d.get("bdf"), info.bdf);
+  info.uuid = scalar_or(d.get("uuid"), info.uuid);
+  info.memory_mib = uint_or(d.get("memoryMiB"), info.memory_mib);
+  info.compute_units = static_cast<uint32_t>(uint_or(d.get("computeUnits"), info.compute_units));
+  info.xcds = static_cast<uint32_t>(uint_or(d.get("xcds"), info.xcds));
+  info.compute_partition = scalar_or(d.get("computePartition"), info.compute_partition);
+  info.memory_partition = scalar_or(d.get("memoryPartition"), info.memory_partition);
+  load_errors(d.get("errors"), info);
+}
+
+std::shared_ptr<SnapshotDevice> load_partition(const Node& p, int idx) {
+  DeviceInfo info;
+  info.partition_id = static_cast<int>(uint_or(p.get("partitionId"), static_cast<uint64_t>(idx)));
+  load_common(p, info);
+  if (const Node* attrs = p.get("attributes"); attrs && attrs->is_map())
+    for (const auto& kv : attrs->entries()) info.attributes[kv.first] = kv.second.text();
+  return SnapshotDevice::partition(std::move(info));
+}
+
+std::shared_ptr<SnapshotDevice> load_device(const Node& d, int idx) {
+  DeviceInfo info;
+  info.index = idx;
+  info.name = "MOCKMODEL";
+  load_common(d, info);
+  info.vendor_id = static_cast<uint32_t>(uint_or(d.get("vendorId"), 0x1002));
+  info.device_id = static_cast<uint32_t>(uint_or(d.get("deviceId"), 0));
+  if (const Node* g = d.get("gfx"); g && !g->is_null()) {
+    auto t = parse_gfx_target(g->text());
+    if (!t) throw Error("mock fixture: invalid gfx target '" + g->text() + "'");
+    info.gfx = *t;
+  }
+  info.available_compute_partitions = string_list(d.get("availableComputePartitions"));
+  info.available_memory_partitions = string_list(d.get("availableMemoryPartitions"));
+  if (const Node* x = d.get("xgmiLinks"); x && !x->is_null()) info.xgmi_links = static_cast<int>(uint_or(x, 0));
+  info.virtualization = scalar_or(d.get("virtualization"), "");
+  bool partitioned = bool_or(d.get("partitioned"), false);
+  bool capable = bool_or(d.get("partitionCapable"), info.available_compute_partitions.size() > 1 || partitioned);
+  auto dev = SnapshotDevice::gpu(std::move(info), partitioned, capable);
+  std::vector<std::shared_ptr<SnapshotDevice>> parts;
+  if (const Node* ps = d.get("partitions"); ps && ps->is_seq()) {
+    int i = 0;
+    for (const auto& p : ps->items()) parts.push_back(load_partition(p, i++));
+  }
+  dev->set_partitions(std::move(parts));
+  return dev;
+}
+
+}  // namespace
+
+std::shared_ptr<MockManager> mock_manager_from_node(const yaml::Node& root) {
+  auto m = std::make_shared<MockManager>();
+  if (root.is_null()) return m;
+  if (!root.is_map()) throw Error("mock fixture: top level must be a mapping");
+  if (const Node* e = root.get("initError"); e && !e->is_null()) m->init_error = e->text();
+  if (const Node* e = root.get("devicesError"); e && !e->is_null()) m->devices_error = e->text();
+  if (const Node* e = root.get("driverVersionError"); e && !e->is_null()) m->driver_error = e->text();
+  if (const Node* e = root.get("runtimeVersionError"); e && !e->is_null()) m->runtime_error = e->text();
+  m->driver_version = scalar_or(root.get("driverVersion"), m->driver_version);
+  if (const Node* rv = root.get("runtimeVersion"); rv && !rv->is_null()) {
+    auto parts = str::split(rv->text(), '.');
+    auto maj = parts.size() > 0 ? str::parse_uint(parts[0]) : std::nullopt;
+    auto min = parts.size() > 1 ? str::parse_uint(parts[1]) : std::optional<uint64_t>(0);
+    if (!maj || !min) throw Error("mock fixture: runtimeVersion must be 'MAJOR.MINOR'");
+    m->runtime_version = RuntimeVersion{static_cast<unsigned>(*maj), static_cast<unsigned>(*min)};
+  }
+  if (const Node* ds = root.get("devices"); ds && ds->is_seq()) {
+    int i = 0;
+    for (const auto& d : ds->items()) m->devices.push_back(load_device(d, i++));
+  }
+  return m;
+}
+
+std::shared_ptr<MockManager> load_mock_manager(const std::string& path) {
+  auto r = fs::read_file(path);
+  if (!r.ok()) throw Error("unable to read mock device file '" + path + "': " + fs::errno_str(r.err));
+  return mock_manager_from_node(yaml::parse(r.data));
+}
+
+}  // namespace gfd::resource

@@ -1,0 +1,104 @@
+// Resource managers that do not talk to hardware: Null, the sticky
+// fallback-to-Null decorator, and the scripted Mock used by tests and by
+// `--backend=mock`.
+//
+// Reference: internal/resource/null.go:23-57, fallback.go:23-64,
+// factory.go:33-39 (WithConfig), testing/resource-testing.go:26-134.
+#pragma once
+
+#include <functional>
+#include <optional>
+#include <string>
+#include <vector>
+
+#include "config/config.h"
+#include "config/yaml.h"
+#include "resource/types.h"
+
+namespace gfd::resource {
+
+// No devices; Init/Shutdown are no-ops; version queries are unsupported.
+class NullManager : public Manager {
+ public:
+  void Init() override {}
+  void Shutdown() override {}
+  std::vector<DevicePtr> GetDevices() override { return {}; }
+  std::string GetDriverVersion() override;
+  RuntimeVersion GetRuntimeVersion() override;
+  std::string Name() const override { return "null"; }
+};
+
+// Becomes a Null manager on the first Init error and stays that way until the
+// manager is rebuilt (SIGHUP reload) — the reference's sticky semantics.
+class FallbackManager : public Manager {
+ public:
+  explicit FallbackManager(ManagerPtr wraps);
+  void Init() override;
+  void Shutdown() override { current_->Shutdown(); }
+  std::vector<DevicePtr> GetDevices() override { return current_->GetDevices(); }
+  std::string GetDriverVersion() override { return current_->GetDriverVersion(); }
+  RuntimeVersion GetRuntimeVersion() override { return current_->GetRuntimeVersion(); }
+  std::string Name() const override { return "fallback(" + current_->Name() + ")"; }
+  bool fell_back() const { return fell_back_; }
+
+ private:
+  ManagerPtr current_;
+  bool fell_back_ = false;
+};
+
+// Wrap `m` in a FallbackManager unless failOnInitError is set.
+ManagerPtr with_config(ManagerPtr m, const config::Config& c);
+
+// Scripted manager.  Every method can be overridden or made to fail; calls
+// are counted so tests can assert on them (moq's call recording).
+class MockManager : public Manager {
+ public:
+  MockManager() = default;
+  explicit MockManager(std::vector<DevicePtr> devices);
+
+  void Init() override;
+  void Shutdown() override;
+  std::vector<DevicePtr> GetDevices() override;
+  std::string GetDriverVersion() override;
+  RuntimeVersion GetRuntimeVersion() override;
+  std::string Name() const override { return "mock"; }
+
+  MockManager& with_error_on_init(std::string msg);
+  MockManager& with_driver_version(std::string v);
+  MockManager& with_runtime_version(RuntimeVersion v);
+
+  std::vector<DevicePtr> devices;
+  std::optional<std::string> init_error;
+  std::optional<std::string> devices_error;
+  std::optional<std::string> driver_error;
+  std::optional<std::string> runtime_error;
+  std::string driver_version = "6.12.12";
+  RuntimeVersion runtime_version{7, 2};
+
+  int init_calls = 0;
+  int shutdown_calls = 0;
+  int get_devices_calls = 0;
+};
+
+// ---- Builders mirroring internal/resource/testing/resource-testing.go ----
+
+// A full (unpartitioned) GPU: name MOCKMODEL, gfx950, 300 MiB, 256 CUs, 8 XCDs.
+std::shared_ptr<SnapshotDevice> new_full_gpu();
+// A GPU in a partitioned compute mode exposing `partitions`.  Like the
+// reference's MIG-enabled mock it reports no ISA target (arch labels are
+// omitted) and is partition capable.
+std::shared_ptr<SnapshotDevice> new_partitioned_gpu(std::vector<std::shared_ptr<SnapshotDevice>> partitions = {});
+// Generic mock GPU; `partitioned` selects the IsPartitioned answer.
+std::shared_ptr<SnapshotDevice> new_mock_gpu(bool partitioned);
+// A compute partition named "<mode>.<xcds>xcd.<gb>gb" whose default
+// attributes are memory=<gb>, compute-units=0, xcds=<xcds>, engines.*=0,
+// compute-partition=<MODE>, memory-partition=NPS1.  `overrides` replace
+// attributes by key.
+std::shared_ptr<SnapshotDevice> new_partition(const std::string& mode, int xcds, uint64_t gb,
+                                              const Attributes& overrides = {});
+
+// Load a mock manager from a YAML/JSON fixture (format in docs/BACKENDS.md).
+std::shared_ptr<MockManager> load_mock_manager(const std::string& path);
+std::shared_ptr<MockManager> mock_manager_from_node(const yaml::Node& root);
+
+}  // namespace gfd::resource

@@ -1,0 +1,293 @@
+#include "resource/sysfs.h"
+
+#include <algorithm>
+#include <cerrno>
+#include <map>
+
+#include "resource/versions.h"
+#include "util/error.h"
+#include "util/fs.h"
+#include "util/strings.h"
+
+namespace gfd::resource {
+
+namespace {
+
+constexpr const char* kTopology = "sys/class/kfd/kfd/topology/nodes";
+
+// The subset of KFD node properties the labels need.
+struct KfdNode {
+  int id = -1;
+  uint64_t gfx_target_version = 0;
+  uint64_t simd_count = 0;
+  uint64_t simd_per_cu = 0;
+  uint64_t num_xcc = 0;
+  uint64_t location_id = 0;
+  uint64_t domain = 0;
+  uint64_t vendor_id = 0;
+  uint64_t device_id = 0;
+  uint64_t unique_id = 0;
+  uint64_t drm_render_minor = 0;
+  uint64_t num_sdma_engines = 0;
+  uint64_t local_mem_size = 0;
+  std::string dir;
+};
+
+// Parse "key value\n" lines, picking only known keys (one pass, no maps).
+void parse_properties(const std::string& text, KfdNode& n) {
+  struct Key {
+    const char* name;
+    size_t len;
+    uint64_t KfdNode::*field;
+  };
+#define K(f) \
+  { #f, sizeof(#f) - 1, &KfdNode::f }
+  static const Key keys[] = {K(gfx_target_version), K(simd_count), K(simd_per_cu),      K(num_xcc),
+                             K(location_id),        K(domain),     K(vendor_id),        K(device_id),
+                             K(unique_id),          K(drm_render_minor), K(num_sdma_engines), K(local_mem_size)};
+#undef K
+  size_t pos = 0;
+  while (pos < text.size()) {
+    size_t eol = text.find('\n', pos);
+    if (eol == std::string::npos) eol = text.size();
+    size_t sp = text.find(' ', pos);
+    if (sp != std::string::npos && sp < eol) {
+      size_t klen = sp - pos;
+      for (const auto& k : keys) {
+        if (k.len == klen && text.compare(pos, klen, k.name) == 0) {
+          uint64_t v = 0;
+          for (size_t i = sp + 1; i < eol && text[i] >= '0' && text[i] <= '9'; ++i)
+            v = v * 10 + static_cast<uint64_t>(text[i] - '0');
+          n.*(k.field) = v;
+          break;
+        }
+      }
+    }
+    pos = eol + 1;
+  }
+}
+
+uint64_t node_memory_bytes(const std::string& node_dir) {
+  uint64_t total = 0;
+  std::string banks = fs::join(node_dir, "mem_banks");
+  for (const auto& b : fs::list_dir(banks)) {
+    auto r = fs::read_file(fs::join(banks, b + "/properties"));
+    if (!r.ok()) continue;
+    uint64_t heap = 0, size = 0;
+    for (const auto& line : str::split(r.data, '\n')) {
+      auto kv = str::split_n(line, ' ', 2);
+      if (kv.size() != 2) continue;
+      if (kv[0] == "heap_type") heap = str::parse_uint(kv[1]).value_or(0);
+      if (kv[0] == "size_in_bytes") size = str::parse_uint(kv[1]).value_or(0);
+    }
+    // HSA_HEAPTYPE_FRAME_BUFFER_PUBLIC (1) / _PRIVATE (2): device-local HBM.
+    if (heap == 1 || heap == 2) total += size;
+  }
+  return total;
+}
+
+std::vector<std::string> split_list(const std::string& s) {
+  std::vector<std::string> out;
+  for (auto& p : str::split(s, ',')) {
+    std::string t = str::trim(p);
+    if (!t.empty()) out.push_back(t);
+  }
+  return out;
+}
+
+// "01 01 01 01 01 01 00 01" -> 7 (links to each hive peer; self is 00).
+int sum_links(const std::string& s) {
+  int total = 0;
+  bool any = false;
+  for (auto& tok : str::split(str::replace_all(s, "\n", " "), ' ')) {
+    std::string t = str::trim(tok);
+    if (t.empty()) continue;
+    auto v = str::parse_uint(t, 16);
+    if (!v) return -1;
+    total += static_cast<int>(*v);
+    any = true;
+  }
+  return any ? total : -1;
+}
+
+std::string bdf_of(const KfdNode& n) {
+  unsigned bus = static_cast<unsigned>((n.location_id >> 8) & 0xff);
+  unsigned dev = static_cast<unsigned>((n.location_id >> 3) & 0x1f);
+  unsigned fn = static_cast<unsigned>(n.location_id & 0x7);
+  return str::format("%04x:%02x:%02x.%x", static_cast<unsigned>(n.domain), bus, dev, fn);
+}
+
+// Same UUID spelling amd-smi reports (measured: unique_id 0x3a7c178b7c5e4d5c,
+// device 0x75a3 -> "3aff75a3-0000-1000-807c-178b7c5e4d5c").
+std::string uuid_of(uint64_t unique_id, uint64_t device_id) {
+  if (unique_id == 0) return "";
+  return str::format("%02xff%04x-0000-1000-80%02x-%012llx", static_cast<unsigned>(unique_id >> 56),
+                     static_cast<unsigned>(device_id & 0xffff), static_cast<unsigned>((unique_id >> 48) & 0xff),
+                     static_cast<unsigned long long>(unique_id & 0xffffffffffffULL));
+}
+
+// Fallback names when the board FRU does not expose product_name.
+std::string name_from_device_id(uint64_t device_id) {
+  switch (device_id) {
+    case 0x75a3: return "AMD Instinct MI355X";
+    case 0x75a0: return "AMD Instinct MI350X";
+    case 0x74a5: return "AMD Instinct MI325X";
+    case 0x74a1: return "AMD Instinct MI300X";
+    case 0x74a9: return "AMD Instinct MI300X HF";
+    case 0x74a0: return "AMD Instinct MI300A";
+    case 0x740c: return "AMD Instinct MI250X/MI250";
+    case 0x740f: return "AMD Instinct MI210";
+    case 0x738c: return "AMD Instinct MI100";
+    default: return str::format("AMD-GPU-0x%04llx", static_cast<unsigned long long>(device_id));
+  }
+}
+
+}  // namespace
+
+bool has_kfd_topology(const std::string& root, std::string* reason) {
+  std::string dir = fs::join(root, kTopology);
+  int err = 0;
+  auto nodes = fs::list_dir(dir, &err);
+  if (err != 0) {
+    if (reason) *reason = "could not read " + dir + ": " + fs::errno_str(err);
+    return false;
+  }
+  if (reason) *reason = "found KFD topology at " + dir + " (" + std::to_string(nodes.size()) + " nodes)";
+  return true;
+}
+
+SysfsManager::SysfsManager(SysfsOptions opts) : opts_(std::move(opts)) { topology_ = fs::join(opts_.root, kTopology); }
+
+void SysfsManager::Init() {
+  int err = 0;
+  fs::list_dir(topology_, &err);
+  if (err != 0) throw Error("KFD topology not available at " + topology_ + ": " + fs::errno_str(err));
+  initialized_ = true;
+  have_snapshot_ = false;
+}
+
+void SysfsManager::Shutdown() {
+  initialized_ = false;
+  have_snapshot_ = false;
+  snapshot_.clear();
+}
+
+std::vector<DevicePtr> SysfsManager::GetDevices() {
+  if (!initialized_) throw Error("sysfs manager not initialized");
+  if (!have_snapshot_) {
+    snapshot_ = enumerate();
+    have_snapshot_ = true;
+  }
+  return snapshot_;
+}
+
+std::vector<DevicePtr> SysfsManager::enumerate() const {
+  // 1. Read every accessible GPU node.
+  std::vector<KfdNode> nodes;
+  for (const auto& name : fs::list_dir(topology_)) {
+    auto id = str::parse_uint(name);
+    if (!id) continue;
+    KfdNode n;
+    n.id = static_cast<int>(*id);
+    n.dir = fs::join(topology_, name);
+    auto r = fs::read_file(fs::join(n.dir, "properties"));
+    if (!r.ok()) continue;  // EPERM: GPU not allocated to this container
+    parse_properties(r.data, n);
+    if (n.gfx_target_version == 0 || n.simd_count == 0) continue;  // CPU node
+    nodes.push_back(std::move(n));
+  }
+  std::sort(nodes.begin(), nodes.end(), [](const KfdNode& a, const KfdNode& b) { return a.id < b.id; });
+
+  // 2. Group partitions by PCI location (partitions share the parent's BDF).
+  std::map<std::string, std::vector<const KfdNode*>> groups;  // ordered by BDF
+  for (const auto& n : nodes) groups[bdf_of(n)].push_back(&n);
+
+  std::vector<DevicePtr> out;
+  int index = -1;
+  for (const auto& [bdf, members] : groups) {
+    ++index;
+    if (!opts_.filter.matches(index, bdf)) continue;
+    const KfdNode& first = *members.front();
+    std::string pci = fs::join(opts_.root, "sys/bus/pci/devices/" + bdf);
+
+    DeviceInfo info;
+    info.index = index;
+    info.bdf = bdf;
+    info.vendor_id = static_cast<uint32_t>(first.vendor_id);
+    info.device_id = static_cast<uint32_t>(first.device_id);
+    info.uuid = uuid_of(first.unique_id, first.device_id);
+    info.gfx = gfx_target_from_kfd(first.gfx_target_version);
+    auto product = fs::read_trimmed(fs::join(pci, "product_name"));
+    info.name = product && !product->empty() ? *product : name_from_device_id(first.device_id);
+    info.compute_partition = fs::read_trimmed(fs::join(pci, "current_compute_partition")).value_or("");
+    info.memory_partition = fs::read_trimmed(fs::join(pci, "current_memory_partition")).value_or("");
+    info.available_compute_partitions = split_list(fs::read_trimmed(fs::join(pci, "available_compute_partition")).value_or(""));
+    info.available_memory_partitions = split_list(fs::read_trimmed(fs::join(pci, "available_memory_partition")).value_or(""));
+    if (auto x = fs::read_trimmed(fs::join(pci, "xgmi_num_links"))) info.xgmi_links = sum_links(*x);
+    if (auto nv = fs::read_trimmed(fs::join(pci, "sriov_numvfs")); nv && str::parse_uint(*nv).value_or(0) > 0)
+      info.virtualization = "host";
+    else
+      info.virtualization = fs::exists(fs::join(pci, "physfn")) ? "guest" : "baremetal";
+
+    bool partitioned = members.size() > 1 || (!info.compute_partition.empty() && info.compute_partition != "SPX");
+    uint64_t vram = 0;
+    if (auto v = fs::read_trimmed(fs::join(pci, "mem_info_vram_total"))) vram = str::parse_uint(*v).value_or(0);
+
+    std::vector<std::shared_ptr<SnapshotDevice>> parts;
+    uint32_t cus = 0, xcds = 0;
+    uint64_t part_mem_sum = 0;
+    for (size_t p = 0; p < members.size(); ++p) {
+      const KfdNode& n = *members[p];
+      uint32_t pcus = n.simd_per_cu ? static_cast<uint32_t>(n.simd_count / n.simd_per_cu) : 0;
+      cus += pcus;
+      xcds += static_cast<uint32_t>(n.num_xcc);
+      if (!partitioned) continue;
+      DeviceInfo pi;
+      pi.partition_id = static_cast<int>(p);
+      pi.bdf = bdf;
+      pi.vendor_id = info.vendor_id;
+      pi.device_id = info.device_id;
+      pi.compute_units = pcus;
+      pi.xcds = static_cast<uint32_t>(n.num_xcc);
+      uint64_t mem = n.local_mem_size ? n.local_mem_size : node_memory_bytes(n.dir);
+      pi.memory_mib = mem >> 20;
+      part_mem_sum += mem;
+      pi.compute_partition = info.compute_partition;
+      pi.memory_partition = info.memory_partition;
+      pi.name = partition_profile_name(pi.compute_partition, pi.xcds, pi.memory_mib);
+      pi.attributes = {
+          {"memory", std::to_string(pi.memory_mib)},
+          {"compute-units", std::to_string(pcus)},
+          {"xcds", std::to_string(pi.xcds)},
+          {"engines.dma", std::to_string(n.num_sdma_engines)},
+      };
+      if (!pi.compute_partition.empty()) pi.attributes["compute-partition"] = pi.compute_partition;
+      if (!pi.memory_partition.empty()) pi.attributes["memory-partition"] = pi.memory_partition;
+      parts.push_back(SnapshotDevice::partition(std::move(pi)));
+    }
+    info.compute_units = cus;
+    info.xcds = xcds;
+    if (vram == 0) vram = partitioned ? part_mem_sum : (first.local_mem_size ? first.local_mem_size : node_memory_bytes(first.dir));
+    info.memory_mib = vram >> 20;
+
+    bool capable = info.available_compute_partitions.size() > 1;
+    auto dev = SnapshotDevice::gpu(std::move(info), partitioned, capable);
+    dev->set_partitions(std::move(parts));
+    out.push_back(dev);
+  }
+  return out;
+}
+
+std::string SysfsManager::GetDriverVersion() {
+  std::string raw = host_driver_version(opts_.root);
+  auto v = extract_version(raw);
+  return v ? *v : raw;
+}
+
+RuntimeVersion SysfsManager::GetRuntimeVersion() {
+  auto v = rocm_version(opts_.root);
+  if (!v) throw Error("unable to determine the ROCm version (no .info/version under $ROCM_PATH or /opt/rocm)");
+  return *v;
+}
+
+}  // namespace gfd::resource

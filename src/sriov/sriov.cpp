@@ -1,0 +1,102 @@
+#include "sriov/sriov.h"
+
+#include "util/error.h"
+#include "util/strings.h"
+
+namespace gfd::sriov {
+
+std::optional<SriovCapability> parse_sriov_capability(const std::string& cap) {
+  if (cap.size() < 0x1c) return std::nullopt;
+  if ((GetLong(cap, 0) & 0xFFFF) != kPciExtCapSriovId) return std::nullopt;
+  SriovCapability c;
+  c.vf_enable = (GetWord(cap, 0x08) & 0x1) != 0;
+  c.initial_vfs = GetWord(cap, 0x0c);
+  c.total_vfs = GetWord(cap, 0x0e);
+  c.num_vfs = GetWord(cap, 0x10);
+  c.vf_offset = GetWord(cap, 0x14);
+  c.vf_stride = GetWord(cap, 0x16);
+  c.vf_device_id = GetWord(cap, 0x1a);
+  return c;
+}
+
+bool is_vf_device_id(const std::string& device_id) {
+  // Instinct MxGPU virtual functions (MI300X, MI325X, MI355X).
+  static const char* kVfIds[] = {"0x74b5", "0x74b9", "0x75b3"};
+  std::string d = str::to_lower(str::trim(device_id));
+  for (const char* id : kVfIds)
+    if (d == id) return true;
+  return false;
+}
+
+std::optional<Info> Lib::Classify(const PCIDevice& d) {
+  if (!d.physfn.empty()) {
+    Info i;
+    i.role = "vf";
+    i.physfn = d.physfn;
+    return i;
+  }
+  if (is_vf_device_id(d.device)) {
+    Info i;
+    i.role = "vf";
+    return i;
+  }
+  // Physical function: prefer the SR-IOV capability itself; fall back to the
+  // kernel's sysfs view when the extended config space is not readable.
+  if (d.config.size() >= kPciExpressConfigSpaceSize) {
+    auto cap = d.GetExtendedCapability(kPciExtCapSriovId, 0x40);
+    if (!cap) return std::nullopt;
+    auto c = parse_sriov_capability(*cap);
+    if (!c || c->num_vfs == 0 || !c->vf_enable) return std::nullopt;
+    Info i;
+    i.role = "pf";
+    i.total_vfs = c->total_vfs;
+    i.num_vfs = c->num_vfs;
+    i.vf_device = str::format("0x%04x", c->vf_device_id);
+    return i;
+  }
+  if (d.sriov_numvfs > 0) {
+    Info i;
+    i.role = "pf";
+    i.total_vfs = d.sriov_totalvfs;
+    i.num_vfs = d.sriov_numvfs;
+    return i;
+  }
+  return std::nullopt;
+}
+
+std::vector<Function> Lib::Devices() {
+  std::vector<PCIDevice> devices;
+  try {
+    devices = pci_->Devices();
+  } catch (const std::exception& e) {
+    throw Error(std::string("error getting AMD specific PCI devices: ") + e.what());
+  }
+  std::vector<Function> out;
+  for (auto& d : devices) {
+    std::optional<Info> info;
+    try {
+      info = Classify(d);
+    } catch (const std::exception& e) {
+      throw Error("unable to read SR-IOV capability for " + d.address + ": " + e.what());
+    }
+    if (info) out.emplace_back(std::move(d), std::move(*info));
+  }
+  return out;
+}
+
+namespace {
+class EmptyLib : public Interface {
+ public:
+  std::vector<Function> Devices() override { return {}; }
+};
+}  // namespace
+
+std::shared_ptr<Interface> new_sriov_lib(const std::string& root) {
+  return std::make_shared<Lib>(std::make_shared<SysfsAmdPCI>(root));
+}
+
+std::shared_ptr<Interface> new_mock_sriov() { return std::make_shared<Lib>(std::make_shared<MockAmdPCI>()); }
+
+std::shared_ptr<Interface> new_empty_sriov() { return std::make_shared<EmptyLib>(); }
+
+}  // namespace gfd::sriov

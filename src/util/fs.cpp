@@ -1,0 +1,168 @@
+#include "util/fs.h"
+
+#include <dirent.h>
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <climits>
+#include <cstdlib>
+#include <cstring>
+
+#include "util/error.h"
+#include "util/strings.h"
+
+namespace gfd::fs {
+
+ReadResult read_file(const std::string& path, size_t max_bytes) {
+  ReadResult r;
+  int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd < 0) {
+    r.err = errno;
+    return r;
+  }
+  // sysfs attributes are at most a page; PCI config space is 4 KiB.
+  char buf[4096];
+  for (;;) {
+    ssize_t n = ::read(fd, buf, sizeof(buf));
+    if (n < 0) {
+      if (errno == EINTR) continue;
+      r.err = errno;
+      break;
+    }
+    if (n == 0) break;
+    r.data.append(buf, static_cast<size_t>(n));
+    if (r.data.size() >= max_bytes) {
+      r.data.resize(max_bytes);
+      break;
+    }
+  }
+  ::close(fd);
+  return r;
+}
+
+std::optional<std::string> read_trimmed(const std::string& path) {
+  auto r = read_file(path, 64 * 1024);
+  if (!r.ok()) return std::nullopt;
+  return str::trim(r.data);
+}
+
+std::string read_file_or_throw(const std::string& path) {
+  auto r = read_file(path);
+  if (!r.ok()) throw Error("open " + path + ": " + errno_str(r.err));
+  return r.data;
+}
+
+bool exists(const std::string& path) {
+  struct stat st;
+  return ::stat(path.c_str(), &st) == 0;
+}
+
+bool is_dir(const std::string& path) {
+  struct stat st;
+  return ::stat(path.c_str(), &st) == 0 && S_ISDIR(st.st_mode);
+}
+
+std::vector<std::string> list_dir(const std::string& path, int* err) {
+  std::vector<std::string> out;
+  DIR* d = ::opendir(path.c_str());
+  if (!d) {
+    if (err) *err = errno;
+    return out;
+  }
+  if (err) *err = 0;
+  while (struct dirent* e = ::readdir(d)) {
+    if (e->d_name[0] == '.' && (e->d_name[1] == 0 || (e->d_name[1] == '.' && e->d_name[2] == 0))) continue;
+    out.emplace_back(e->d_name);
+  }
+  ::closedir(d);
+  std::sort(out.begin(), out.end());
+  return out;
+}
+
+std::string read_link(const std::string& path) {
+  char buf[PATH_MAX];
+  ssize_t n = ::readlink(path.c_str(), buf, sizeof(buf) - 1);
+  if (n < 0) return {};
+  return std::string(buf, static_cast<size_t>(n));
+}
+
+std::string real_basename(const std::string& path) {
+  char buf[PATH_MAX];
+  if (!::realpath(path.c_str(), buf)) return {};
+  return basename(buf);
+}
+
+std::string join(const std::string& a, const std::string& b) {
+  if (a.empty()) return b;
+  if (b.empty()) return a;
+  if (a.back() == '/') return b.front() == '/' ? a + b.substr(1) : a + b;
+  return b.front() == '/' ? a + b : a + "/" + b;
+}
+
+std::string dirname(const std::string& path) {
+  auto pos = path.find_last_of('/');
+  if (pos == std::string::npos) return ".";
+  if (pos == 0) return "/";
+  return path.substr(0, pos);
+}
+
+std::string basename(const std::string& path) {
+  std::string p = path;
+  while (p.size() > 1 && p.back() == '/') p.pop_back();
+  auto pos = p.find_last_of('/');
+  return pos == std::string::npos ? p : p.substr(pos + 1);
+}
+
+std::string absolute(const std::string& path) {
+  std::string p = path;
+  if (p.empty() || p[0] != '/') {
+    char cwd[PATH_MAX];
+    if (!::getcwd(cwd, sizeof(cwd))) throw Error("getwd: " + errno_str(errno));
+    p = join(cwd, p);
+  }
+  // Lexical clean (like Go's filepath.Clean): collapse //, ., ..
+  std::vector<std::string> parts;
+  for (auto& seg : str::split(p, '/')) {
+    if (seg.empty() || seg == ".") continue;
+    if (seg == "..") {
+      if (!parts.empty()) parts.pop_back();
+      continue;
+    }
+    parts.push_back(seg);
+  }
+  return "/" + str::join(parts, "/");
+}
+
+void mkdir_all(const std::string& path, unsigned mode) {
+  if (path.empty() || is_dir(path)) return;
+  mkdir_all(dirname(path), mode);
+  if (::mkdir(path.c_str(), mode) != 0 && errno != EEXIST)
+    throw Error("mkdir " + path + ": " + errno_str(errno));
+}
+
+int remove_all(const std::string& path) {
+  struct stat st;
+  if (::lstat(path.c_str(), &st) != 0) return errno == ENOENT ? 0 : errno;
+  if (S_ISDIR(st.st_mode)) {
+    for (const auto& name : list_dir(path)) {
+      int e = remove_all(join(path, name));
+      if (e) return e;
+    }
+    if (::rmdir(path.c_str()) != 0 && errno != ENOENT) return errno;
+    return 0;
+  }
+  if (::unlink(path.c_str()) != 0 && errno != ENOENT) return errno;
+  return 0;
+}
+
+std::string errno_str(int err) {
+  char buf[256];
+  // GNU strerror_r returns a char* that may not be `buf`.
+  const char* s = strerror_r(err, buf, sizeof(buf));
+  return s ? std::string(s) : std::string("errno ") + std::to_string(err);
+}
+
+}  // namespace gfd::fs

@@ -1,0 +1,56 @@
+#include "util/log.h"
+
+#include <atomic>
+#include <cstdio>
+#include <ctime>
+#include <sys/time.h>
+
+namespace gfd::log {
+
+namespace {
+std::atomic<bool> g_quiet{false};
+
+void emit(const char* msg, size_t len) {
+  char stamp[32];
+  time_t now = time(nullptr);
+  struct tm tmv;
+  localtime_r(&now, &tmv);
+  strftime(stamp, sizeof(stamp), "%Y/%m/%d %H:%M:%S ", &tmv);
+  // One fwrite per piece; stderr is unbuffered so keep the pieces few.
+  std::string out;
+  out.reserve(len + 24);
+  out.append(stamp);
+  out.append(msg, len);
+  if (len == 0 || msg[len - 1] != '\n') out.push_back('\n');
+  fwrite(out.data(), 1, out.size(), stderr);
+}
+}  // namespace
+
+bool set_quiet(bool q) { return g_quiet.exchange(q); }
+bool quiet() { return g_quiet.load(std::memory_order_relaxed); }
+
+void printf(const char* fmt, ...) {
+  if (quiet()) return;
+  char buf[4096];
+  va_list ap;
+  va_start(ap, fmt);
+  int n = vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  if (n < 0) return;
+  if (static_cast<size_t>(n) >= sizeof(buf)) {
+    std::string big(static_cast<size_t>(n) + 1, '\0');
+    va_start(ap, fmt);
+    vsnprintf(big.data(), big.size(), fmt, ap);
+    va_end(ap);
+    emit(big.data(), static_cast<size_t>(n));
+    return;
+  }
+  emit(buf, static_cast<size_t>(n));
+}
+
+void line(const std::string& msg) {
+  if (quiet()) return;
+  emit(msg.data(), msg.size());
+}
+
+}  // namespace gfd::log

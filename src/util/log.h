@@ -1,0 +1,22 @@
+// Minimal logger with the same line shape as Go's stdlib `log` package
+// ("2006/01/02 15:04:05 message"), which the reference uses everywhere
+// (e.g. cmd/gpu-feature-discovery/main.go:111-146).  Output goes to stderr so
+// that `--output-file=""` (labels on stdout, internal/lm/labels.go:38-41)
+// stays machine-readable.
+#pragma once
+
+#include <cstdarg>
+#include <string>
+
+namespace gfd::log {
+
+// printf-style log line; a trailing newline is added if missing.
+void printf(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+void line(const std::string& msg);
+
+// Silence all log output (used by the in-process benchmark binding so that
+// timing is not dominated by stderr writes).  Returns the previous setting.
+bool set_quiet(bool quiet);
+bool quiet();
+
+}  // namespace gfd::log

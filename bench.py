@@ -1,0 +1,280 @@
+#!/usr/bin/env python3
+"""Label-generation latency benchmark (the BASELINE.json headline metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--backend auto|amdsmi|sysfs|synthetic]
+
+One "step" is one full labeling cycle of the daemon in its default
+configuration: enumerate the node through the backend (amd-smi on a GPU
+box), build every label (version, partition, xGMI, resources, SR-IOV PCI
+scan) and atomically rewrite the NFD feature file.  Nothing is cached across
+steps except what the daemon itself keeps (the loaded library and, in the
+default persistent amd-smi session, the initialised handle table); every
+device fact is re-queried from the driver each step.
+
+The label set of every step is checked for correctness (count == N GPUs,
+gfx950/cdna4 arch, MI355 product, HBM size) before timing is reported.
+
+N>1: launched by the driver as one process per GPU under torch.distributed
+(gloo, 127.0.0.1); rank 0 labels the node restricted to GPUs 0..N-1 (the
+`--visible-devices` filter), every rank brackets the K steps with barriers,
+and the MAX wall time over ranks is reported.  Scaling is "weak": the work
+per visible GPU is fixed and total work grows with N.
+
+Without a usable GPU (CPU container) the benchmark runs the KFD-sysfs backend
+over a synthetic N-GPU MI355X tree and says so in "data".
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import subprocess
+import sys
+import tempfile
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+METRIC = "label-file generation p50 latency (ms) + label-set correctness, 8×MI355X node"
+
+
+def _env_int(name: str, default: int) -> int:
+    try:
+        return int(os.environ.get(name, default))
+    except ValueError:
+        return default
+
+
+def _percentile(xs: list[float], q: float) -> float:
+    ys = sorted(xs)
+    if not ys:
+        return float("nan")
+    k = (len(ys) - 1) * q
+    lo, hi = int(k), min(int(k) + 1, len(ys) - 1)
+    return ys[lo] + (ys[hi] - ys[lo]) * (k - lo)
+
+
+class _Dist:
+    """Barrier / max-reduce across ranks (gloo), or no-ops for one process."""
+
+    def __init__(self):
+        self.world = _env_int("WORLD_SIZE", 1)
+        self.rank = _env_int("RANK", 0)
+        self.torch = None
+        self.dist = None
+        try:
+            import torch  # noqa: F401
+
+            self.torch = torch
+        except Exception:
+            self.torch = None
+        if self.world > 1:
+            import torch.distributed as dist
+
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            self.dist = dist
+
+    def sync(self):
+        if self.dist is not None:
+            self.dist.barrier()
+        if self.torch is not None and self.torch.cuda.is_available():
+            self.torch.cuda.synchronize()
+
+    def max(self, v: float) -> float:
+        if self.dist is None:
+            return v
+        t = self.torch.tensor([v], dtype=self.torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def broadcast_obj(self, obj):
+        if self.dist is None:
+            return obj
+        lst = [obj]
+        self.dist.broadcast_object_list(lst, src=0)
+        return lst[0]
+
+    def close(self):
+        if self.dist is not None:
+            self.dist.destroy_process_group()
+
+
+def _check_labels(labels: dict, n_gpus: int, hardware: bool) -> list[str]:
+    problems = []
+    want = {
+        "amd.com/gpu.count": str(n_gpus),
+        "amd.com/gpu.family": "cdna4",
+        "amd.com/gpu.arch": "gfx950",
+        "amd.com/gpu.compute.major": "9",
+        "amd.com/gpu.compute.minor": "5",
+        "amd.com/gpu.replicas": "1",
+    }
+    for k, v in want.items():
+        if labels.get(k) != v:
+            problems.append(f"{k}={labels.get(k)!r} (want {v!r})")
+    if "MI355" not in labels.get("amd.com/gpu.product", ""):
+        problems.append(f"amd.com/gpu.product={labels.get('amd.com/gpu.product')!r}")
+    mem = int(labels.get("amd.com/gpu.memory", "0") or 0)
+    if not 280 * 1024 <= mem <= 300 * 1024:
+        problems.append(f"amd.com/gpu.memory={mem} MiB (want ~288 GiB of HBM3E)")
+    for k in ("amd.com/driver.major", "amd.com/rocm.runtime.major", "amd.com/gpu.machine", "amd.com/gfd.timestamp",
+              "amd.com/gpu.partition.capable"):
+        if k not in labels:
+            problems.append(f"missing {k}")
+    if hardware and labels.get("amd.com/gpu.compute-units") != "256":
+        problems.append(f"amd.com/gpu.compute-units={labels.get('amd.com/gpu.compute-units')!r} (want 256)")
+    return problems
+
+
+def _session_args(backend: str, n_gpus: int, out: str, root: str | None, extra: list[str]) -> list[str]:
+    args = [f"--backend={backend}", f"--visible-devices=0-{n_gpus - 1}", f"--output-file={out}",
+            "--mig-strategy=none"]
+    if root:
+        args.append(f"--sysfs-root={root}")
+        args.append(f"--machine-type-file={root}/sys/class/dmi/id/product_name")
+    return args + extra
+
+
+def _time_variant(g, args: list[str], steps: int, warmup: int) -> dict:
+    s = g.Session(args)
+    ns = s.bench(steps, warmup, True)
+    ms = [x / 1e6 for x in ns]
+    return {"p50_ms": round(_percentile(ms, 0.5), 4), "p90_ms": round(_percentile(ms, 0.9), 4),
+            "mean_ms": round(statistics.fmean(ms), 4), "backend": s.backend}
+
+
+def _cold_process(binary: str, args: list[str], runs: int) -> dict:
+    """Oneshot Job mode: fork+exec the daemon binary per label file."""
+    ms = []
+    for _ in range(runs):
+        t0 = time.perf_counter_ns()
+        subprocess.run([binary, "--oneshot", *args], check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                       timeout=60)
+        ms.append((time.perf_counter_ns() - t0) / 1e6)
+    return {"p50_ms": round(_percentile(ms, 0.5), 3), "p90_ms": round(_percentile(ms, 0.9), 3), "runs": runs}
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
+    ap.add_argument("--gpus", type=int, default=_env_int("WORLD_SIZE", 1))
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--backend", default="auto", help="auto | amdsmi | sysfs | synthetic")
+    ap.add_argument("--no-extras", action="store_true", help="skip the secondary measurements")
+    a = ap.parse_args()
+
+    dist = _Dist()
+    import gpu_feature_discovery_amd as gfd
+    from gpu_feature_discovery_amd import synth
+
+    g = gfd.native()
+    g.set_quiet(True)
+    n = a.gpus
+
+    tmp = tempfile.mkdtemp(prefix="gfd-bench-")
+    out = os.path.join(tmp, "features.d", "gfd")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+
+    # Decide the backend on rank 0 (only rank 0 talks to the driver).
+    hardware = False
+    root = None
+    backend = a.backend
+    if dist.rank == 0:
+        if backend in ("auto", "amdsmi"):
+            try:
+                devs = g.Session(["--backend=amdsmi", f"--visible-devices=0-{n - 1}"]).devices()
+                hardware = len(devs) >= n
+                if not hardware and a.backend == "amdsmi":
+                    raise SystemExit(f"amd-smi sees {len(devs)} GPU(s), fewer than --gpus {n}")
+            except g.GfdError:
+                if a.backend == "amdsmi":
+                    raise
+                hardware = False
+            backend = "amdsmi" if hardware else "synthetic"
+        if backend in ("synthetic",):
+            root = os.path.join(tmp, "root")
+            synth.make_mi355x_node(root, n_gpus=n, seed=1234)
+        elif backend == "sysfs":
+            hardware = True
+    backend = dist.broadcast_obj(backend)
+    hardware = dist.broadcast_obj(hardware)
+
+    session = None
+    labels_ok, problems, labels = True, [], {}
+    if dist.rank == 0:
+        sess_backend = "sysfs" if backend == "synthetic" else backend
+        args = _session_args(sess_backend, n, out, root, [])
+        session = g.Session(args)
+        first = session.cycle(True)
+        labels = first["labels"]
+        problems = _check_labels(labels, n, hardware)
+        labels_ok = not problems
+        # Warmup (untimed), in native code.
+        session.bench(0, a.warmup, True)
+
+    # Timed region: exactly K steps, bracketed by barrier + synchronize.
+    dist.sync()
+    t0 = time.perf_counter_ns()
+    per_step_ns: list[int] = []
+    if dist.rank == 0:
+        per_step_ns = session.bench(a.steps, 0, True)
+    dist.sync()
+    wall_ms = (time.perf_counter_ns() - t0) / 1e6
+    wall_ms = dist.max(wall_ms)
+
+    if dist.rank == 0:
+        ms = [x / 1e6 for x in per_step_ns]
+        p50 = _percentile(ms, 0.5)
+        extras = {}
+        if not a.no_extras:
+            sess_backend = "sysfs" if backend == "synthetic" else backend
+            if backend == "amdsmi":
+                extras["amdsmi_per_cycle_session"] = _time_variant(
+                    g, _session_args("amdsmi", n, out, None, ["--amdsmi-session=per-cycle"]), max(10, a.steps // 10), 2)
+                extras["sysfs_backend"] = _time_variant(g, _session_args("sysfs", n, out, None, []), a.steps, a.warmup)
+            try:
+                binary = str(gfd.binary_path())
+                extras["oneshot_process"] = _cold_process(
+                    binary, _session_args(sess_backend, n, out, root, []), max(5, min(30, a.steps // 10)))
+            except (FileNotFoundError, subprocess.SubprocessError) as e:
+                extras["oneshot_process"] = {"error": str(e)}
+        result = {
+            "metric": METRIC,
+            "value": round(p50, 4),
+            "unit": "ms",
+            "n_gpus": n,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(wall_ms / max(a.steps, 1), 4),
+            "higher_is_better": False,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "n/a",
+            "data": ("real MI355X via amd-smi (live driver queries every step)" if backend == "amdsmi"
+                     else "real MI355X via KFD sysfs" if backend == "sysfs"
+                     else f"synthetic {n}-GPU MI355X sysfs tree (random device IDs), no GPU available"),
+            "config": {
+                "model": f"{n}xMI355X SPX/NPS1 node, amd.com label set",
+                "global_batch": n,
+                "seq_len": None,
+                "parallelism": f"1 labeler for {n} visible GPU(s); {dist.world} rank(s)",
+                "backend": session.backend if session else backend,
+                "strategy": "none",
+            },
+            "p90_ms": round(_percentile(ms, 0.9), 4),
+            "mean_ms": round(statistics.fmean(ms), 4) if ms else None,
+            "labels_ok": labels_ok,
+            "label_problems": problems,
+            "n_labels": len(labels),
+            "extras": extras,
+        }
+        print(json.dumps(result))
+    dist.close()
+    return 0 if labels_ok else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

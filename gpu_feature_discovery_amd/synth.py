@@ -1,0 +1,231 @@
+"""Synthetic sysfs trees for MI355X nodes.
+
+Builds the subset of ``/sys`` (plus ``/opt/rocm/.info/version``) that the
+daemon's KFD-sysfs backend and SR-IOV scanner read, laid out exactly like the
+MI355X pool (verified by tools/probe_box.sh; see profiles/hw_probe.md):
+
+* ``sys/class/kfd/kfd/topology/nodes/N/properties`` and ``mem_banks`` - one
+  node per CPU socket, then one node per GPU (SPX) or per compute partition
+  (DPX/QPX/CPX: 2/4/8 nodes sharing the GPU's PCI location),
+* ``sys/bus/pci/devices/<bdf>/...`` - product name, partition modes, VRAM,
+  xGMI link table, SR-IOV attributes, configuration space,
+* ``sys/module/amdgpu/version``, ``sys/class/dmi/id/product_name``.
+
+Device identities (PCI bus numbers, unique IDs / UUIDs, serials) are random
+but reproducible from ``seed``, matching the benchmark spec ("synthetic/mock
+sysfs tree with random device IDs").
+"""
+
+from __future__ import annotations
+
+import os
+import random
+import struct
+from dataclasses import dataclass, field
+from pathlib import Path
+
+MI355X_DEVICE_ID = 0x75A3
+MI355X_VRAM_BYTES = 309220868096  # 294896 MiB, as reported by amdgpu
+MI355X_CUS = 256
+MI355X_XCDS = 8
+PARTITIONS_PER_MODE = {"SPX": 1, "DPX": 2, "QPX": 4, "CPX": 8}
+NPS_COUNT = {"NPS1": 1, "NPS2": 2, "NPS4": 4, "NPS8": 8}
+
+
+@dataclass
+class GpuSpec:
+    compute_partition: str = "SPX"
+    memory_partition: str = "NPS1"
+    device_id: int = MI355X_DEVICE_ID
+    product_name: str = "AMD Instinct MI355 OAM"
+    vram_bytes: int = MI355X_VRAM_BYTES
+    cus: int = MI355X_CUS
+    xcds: int = MI355X_XCDS
+    gfx_target_version: int = 90500
+    # SR-IOV: None, or dict(total=8, num=4, vf_device=0x75b3)
+    sriov: dict | None = None
+    # True: the KFD nodes of this GPU are not readable (not allocated to the
+    # container), like the other 7 GPUs on a 1-GPU pool box.
+    hidden: bool = False
+
+
+@dataclass
+class NodeSpec:
+    gpus: list[GpuSpec] = field(default_factory=list)
+    cpu_sockets: int = 2
+    driver_version: str = "6.12.12"
+    rocm_version: str = "7.2.0"
+    machine: str = "WB SERVER E6-IS"
+    privileged: bool = False  # full 4 KiB config space readable
+    seed: int = 0
+
+
+def _write(path: Path, text: str | bytes) -> None:
+    path.parent.mkdir(parents=True, exist_ok=True)
+    if isinstance(text, bytes):
+        path.write_bytes(text)
+    else:
+        path.write_text(text)
+
+
+def config_space(device_id: int, sriov: dict | None, size: int) -> bytes:
+    """PCI configuration space of an AMD accelerator function.
+
+    Capability chain PM(0x48) -> PCIe(0x64) -> MSI(0xa0) -> MSI-X(0xc0);
+    extended chain AER(0x100) -> ARI(0x150) -> [SR-IOV(0x200)] -> VSEC(0x300).
+    ``size`` 64 models an unprivileged reader (what the pool exposes).
+    """
+    b = bytearray(4096)
+    struct.pack_into("<HHHH", b, 0, 0x1002, device_id, 0x0407, 0x0010)
+    b[0x0B] = 0x12
+    struct.pack_into("<HH", b, 0x2C, 0x1002, device_id)
+    b[0x34] = 0x48
+    b[0x48:0x4C] = bytes([0x01, 0x64, 0x03, 0x00])
+    b[0x64:0x68] = bytes([0x10, 0xA0, 0x02, 0x00])
+    b[0xA0:0xA2] = bytes([0x05, 0xC0])
+    b[0xC0:0xC2] = bytes([0x11, 0x00])
+    after_ari = 0x200 if sriov else 0x300
+    struct.pack_into("<I", b, 0x100, 0x0001 | (1 << 16) | (0x150 << 20))
+    struct.pack_into("<I", b, 0x150, 0x000E | (1 << 16) | (after_ari << 20))
+    if sriov:
+        struct.pack_into("<I", b, 0x200, 0x0010 | (1 << 16) | (0x300 << 20))
+        struct.pack_into("<H", b, 0x208, 1 if sriov.get("num", 0) else 0)
+        struct.pack_into("<HHH", b, 0x20C, sriov["total"], sriov["total"], sriov.get("num", 0))
+        struct.pack_into("<HH", b, 0x214, 1, 1)
+        struct.pack_into("<H", b, 0x21A, sriov.get("vf_device", 0x75B3))
+    struct.pack_into("<I", b, 0x300, 0x000B | (1 << 16))
+    return bytes(b[:size])
+
+
+def _kfd_properties(spec: GpuSpec, parts: int, location: int, render: int, unique: int, xcc: int) -> str:
+    cus = spec.cus // parts
+    props = {
+        "cpu_cores_count": 0,
+        "simd_count": cus * 4,
+        "mem_banks_count": 1,
+        "caches_count": 0,
+        "io_links_count": 0,
+        "p2p_links_count": 0,
+        "cpu_core_id_base": 0,
+        "simd_id_base": 2147487744 + render,
+        "max_waves_per_simd": 8,
+        "lds_size_in_kb": 160,
+        "gds_size_in_kb": 0,
+        "num_gws": 64,
+        "wave_front_size": 64,
+        "array_count": 32 // parts,
+        "simd_arrays_per_engine": 1,
+        "cu_per_simd_array": 9,
+        "simd_per_cu": 4,
+        "max_slots_scratch_cu": 32,
+        "gfx_target_version": spec.gfx_target_version,
+        "vendor_id": 4098,
+        "device_id": spec.device_id,
+        "location_id": location,
+        "domain": 0,
+        "drm_render_minor": render,
+        "hive_id": 6580227414736629568,
+        "num_sdma_engines": max(1, 2 // parts) if parts > 1 else 2,
+        "num_sdma_xgmi_engines": 14 // parts,
+        "num_sdma_queues_per_engine": 8,
+        "num_cp_queues": 24,
+        "max_engine_clk_fcompute": 2400,
+        "local_mem_size": 0,
+        "fw_version": 44,
+        "capability": 2889327232,
+        "capability2": 1,
+        "debug_prop": 1494,
+        "sdma_fw_version": 14,
+        "unique_id": unique,
+        "num_xcc": xcc,
+        "max_engine_clk_ccompute": 5008,
+    }
+    return "".join(f"{k} {v}\n" for k, v in props.items())
+
+
+def make_node(root: str | os.PathLike, spec: NodeSpec) -> Path:
+    """Materialise ``spec`` under ``root``; returns the root path."""
+    root = Path(root)
+    rng = random.Random(spec.seed)
+    topo = root / "sys/class/kfd/kfd/topology"
+    _write(topo / "generation_id", "1\n")
+    _write(root / "sys/module/amdgpu/version", spec.driver_version + "\n")
+    _write(root / "opt/rocm/.info/version", spec.rocm_version + "\n")
+    _write(root / "sys/class/dmi/id/product_name", spec.machine + "\n")
+    (root / "sys/bus/pci/devices").mkdir(parents=True, exist_ok=True)
+
+    node = 0
+    for s in range(spec.cpu_sockets):
+        _write(topo / f"nodes/{node}/properties",
+               f"cpu_cores_count 128\nsimd_count 0\nmem_banks_count 1\ncpu_core_id_base {128 * s}\n"
+               "gfx_target_version 0\nvendor_id 0\ndevice_id 0\nlocation_id 0\n")
+        _write(topo / f"nodes/{node}/mem_banks/0/properties", "heap_type 0\nsize_in_bytes 1622942375936\n")
+        node += 1
+
+    buses = rng.sample(range(0x10, 0xF0), len(spec.gpus))
+    n_gpus = len(spec.gpus)
+    render = 128
+    for gi, g in enumerate(spec.gpus):
+        parts = PARTITIONS_PER_MODE[g.compute_partition]
+        bus = buses[gi]
+        location = bus << 8
+        bdf = f"0000:{bus:02x}:00.0"
+        unique = rng.getrandbits(64)
+        xcc = g.xcds // parts
+        node_mem = g.vram_bytes // parts
+        for p in range(parts):
+            ndir = topo / f"nodes/{node}"
+            if g.hidden:
+                # Unreadable: the kernel returns EPERM; a directory named
+                # `properties` makes every read fail the same way (EISDIR).
+                (ndir / "properties").mkdir(parents=True, exist_ok=True)
+            else:
+                _write(ndir / "properties", _kfd_properties(g, parts, location, render, unique, xcc))
+                _write(ndir / "mem_banks/0/properties", f"heap_type 1\nsize_in_bytes {node_mem}\nflags 0\nwidth 8192\n")
+                _write(ndir / "gpu_id", f"{rng.randint(1000, 65535)}\n")
+            node += 1
+            render += 1
+        d = root / "sys/bus/pci/devices" / bdf
+        _write(d / "vendor", "0x1002\n")
+        _write(d / "device", f"0x{g.device_id:04x}\n")
+        _write(d / "subsystem_vendor", "0x1002\n")
+        _write(d / "subsystem_device", f"0x{g.device_id:04x}\n")
+        _write(d / "class", "0x120000\n")
+        _write(d / "revision", "0x00\n")
+        _write(d / "product_name", g.product_name + "\n")
+        _write(d / "current_compute_partition", g.compute_partition + "\n")
+        _write(d / "available_compute_partition", "SPX, DPX, QPX, CPX\n")
+        _write(d / "current_memory_partition", g.memory_partition + "\n")
+        _write(d / "available_memory_partition", "NPS1, NPS2\n")
+        _write(d / "mem_info_vram_total", f"{g.vram_bytes}\n")
+        _write(d / "unique_id", f"{unique:016x}\n")
+        _write(d / "serial_number", f"{rng.randint(10**11, 10**12 - 1)}\n")
+        peers = ["01"] * min(n_gpus, 8)
+        peers[gi % 8] = "00"
+        _write(d / "xgmi_num_links", " ".join(peers) + " \n")
+        sriov = g.sriov or {}
+        _write(d / "sriov_totalvfs", f"{sriov.get('total', 1)}\n")
+        _write(d / "sriov_numvfs", f"{sriov.get('num', 0)}\n")
+        _write(d / "config", config_space(g.device_id, g.sriov, 4096 if spec.privileged else 64))
+        for v in range(sriov.get("num", 0)):
+            vf_bdf = f"0000:{bus:02x}:00.{v + 1}"
+            vd = root / "sys/bus/pci/devices" / vf_bdf
+            _write(vd / "vendor", "0x1002\n")
+            _write(vd / "device", f"0x{sriov.get('vf_device', 0x75B3):04x}\n")
+            _write(vd / "class", "0x120000\n")
+            _write(vd / "config", config_space(sriov.get("vf_device", 0x75B3), None, 4096 if spec.privileged else 64))
+            (vd / "physfn").symlink_to(f"../{bdf}")
+    # An unrelated non-AMD PCI function (the scanner must skip it).
+    other = root / "sys/bus/pci/devices/0000:00:00.0"
+    _write(other / "vendor", "0x1022\n")
+    _write(other / "class", "0x060000\n")
+    _write(other / "config", b"\x22\x10" + bytes(62))
+    return root
+
+
+def make_mi355x_node(root: str | os.PathLike, n_gpus: int = 8, compute_partition: str = "SPX",
+                     memory_partition: str = "NPS1", seed: int = 0, hidden: int = 0, **kwargs) -> Path:
+    """An N-GPU MI355X node; the last ``hidden`` GPUs are not readable."""
+    gpus = [GpuSpec(compute_partition=compute_partition, memory_partition=memory_partition,
+                    hidden=i >= n_gpus - hidden) for i in range(n_gpus)]
+    return make_node(root, NodeSpec(gpus=gpus, seed=seed, **kwargs))

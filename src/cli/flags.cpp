@@ -205,9 +205,9 @@ std::string help_text(const std::vector<FlagDef>& defs, const std::string& app_n
   out += "GLOBAL OPTIONS:\n";
   for (const auto& d : defs) {
     if (d.hidden) continue;
-    std::string names = "--" + d.name;
-    for (const auto& a : d.aliases) names += (a.size() == 1 ? ", -" : ", --") + a;
-    if (d.type != FlagType::Bool) names += " value";
+    std::string suffix = d.type != FlagType::Bool ? " value" : "";
+    std::string names = "--" + d.name + suffix;
+    for (const auto& a : d.aliases) names += (a.size() == 1 ? ", -" : ", --") + a + suffix;
     std::string line = "   " + names + "\t" + d.usage;
     if (d.type == FlagType::String && !d.default_value.empty())
       line += " (default: \"" + d.default_value + "\")";

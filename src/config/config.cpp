@@ -89,8 +89,6 @@ std::optional<Nanos> opt_duration(const Node* n, const std::string& path) {
   throw Error("invalid duration");
 }
 
-const Node* field(const Node& m, const char* key) { return m.is_map() ? m.get(key) : nullptr; }
-
 void require_map(const Node& n, const std::string& path, const std::string& type) {
   if (!n.is_map()) type_error(n, path, type);
 }
@@ -388,7 +386,8 @@ Node to_node(const Config& c) {
     ts.set("resources", rs);
   }
   Node sharing = Node::map();
-  sharing.set("timeSlicing", ts);
+  // An empty timeSlicing would not parse back ("no resources specified").
+  if (!t.resources.empty()) sharing.set("timeSlicing", ts);
   root.set("sharing", sharing);
   return root;
 }

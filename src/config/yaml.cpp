@@ -193,7 +193,7 @@ class Parser {
     if (idx >= lines_.size()) return Node::null();
     Node root;
     const Line& l = lines_[idx];
-    if (is_flow_start(l.content) || is_quote_start(l.content)) {
+    if (is_flow_start(l.content) || (is_quote_start(l.content) && !split_key(l.content, l.no))) {
       root = parse_inline_value(l.content, idx, -1, false);
     } else {
       root = parse_block(idx, l.indent);
@@ -276,6 +276,8 @@ class Parser {
         l.indent = static_cast<int>(ind + 4);
       }
       if (seen_content && body == "...") body.clear();
+      if (seen_content && (body == "---" || str::starts_with(body, "--- ")))
+        fail_no(no, "multiple YAML documents are not supported");
       l.content = body;
       if (!body.empty()) seen_content = true;
       lines_.push_back(std::move(l));

@@ -1,0 +1,261 @@
+// Backend tests: KFD-sysfs enumeration over synthetic trees, the device
+// filter, ISA/version parsing, fallback, mock fixtures and backend selection.
+// (The reference tests its NVML adapter only through mocks; the sysfs
+// backend here is fully testable on CPU because it only reads files.)
+#include <unistd.h>
+
+#include "config/config.h"
+#include "lm/labels.h"
+#include "resource/amdsmi.h"
+#include "resource/factory.h"
+#include "resource/filter.h"
+#include "resource/managers.h"
+#include "resource/sysfs.h"
+#include "resource/versions.h"
+#include "test.h"
+#include "util/fs.h"
+#include "util/strings.h"
+
+using namespace gfd;
+using namespace gfd::resource;
+
+namespace {
+
+void put(const std::string& path, const std::string& content) {
+  fs::mkdir_all(fs::dirname(path));
+  lm::write_file_atomically(path, content, 0644);
+  fs::remove_all(fs::join(fs::dirname(path), "gfd-tmp"));
+}
+
+std::string kfd_props(uint64_t gfx, uint64_t simd, uint64_t xcc, uint64_t location, uint64_t render, uint64_t unique) {
+  return str::format(
+      "cpu_cores_count 0\nsimd_count %llu\nmem_banks_count 1\nsimd_per_cu 4\ngfx_target_version %llu\n"
+      "vendor_id 4098\ndevice_id 30115\nlocation_id %llu\ndomain 0\ndrm_render_minor %llu\nunique_id %llu\n"
+      "num_sdma_engines 2\nnum_xcc %llu\nlocal_mem_size 0\n",
+      (unsigned long long)simd, (unsigned long long)gfx, (unsigned long long)location, (unsigned long long)render,
+      (unsigned long long)unique, (unsigned long long)xcc);
+}
+
+struct Tree {
+  std::string root;
+  Tree() {
+    char d[] = "/tmp/gfd-sysfs-XXXXXX";
+    if (!mkdtemp(d)) throw std::runtime_error("mkdtemp");
+    root = d;
+    std::string nodes = root + "/sys/class/kfd/kfd/topology/nodes";
+    put(nodes + "/0/properties", "cpu_cores_count 128\nsimd_count 0\ngfx_target_version 0\n");
+    put(root + "/sys/class/kfd/kfd/topology/generation_id", "1\n");
+    put(root + "/sys/module/amdgpu/version", "6.12.12\n");
+    put(root + "/opt/rocm/.info/version", "7.2.0-43\n");
+    // GPU A: SPX at d9:00.0 (node 1).
+    put(nodes + "/1/properties", kfd_props(90500, 1024, 8, 0xd900, 128, 0x3a7c178b7c5e4d5cULL));
+    put(nodes + "/1/mem_banks/0/properties", "heap_type 1\nsize_in_bytes 309220868096\n");
+    pci("0000:d9:00.0", "SPX", "NPS1", 309220868096ULL);
+    // GPU B: CPX at 23:00.0 (nodes 2..9, one XCD each, 36 GiB each).
+    for (int p = 0; p < 8; ++p) {
+      std::string n = nodes + "/" + std::to_string(2 + p);
+      put(n + "/properties", kfd_props(90500, 128, 1, 0x2300, 136 + p, 0x75c7dc68fc70d513ULL));
+      put(n + "/mem_banks/0/properties", "heap_type 1\nsize_in_bytes 38652608512\n");
+    }
+    pci("0000:23:00.0", "CPX", "NPS1", 309220868096ULL);
+  }
+  void pci(const std::string& bdf, const std::string& cp, const std::string& mp, uint64_t vram) {
+    std::string d = root + "/sys/bus/pci/devices/" + bdf;
+    put(d + "/vendor", "0x1002\n");
+    put(d + "/device", "0x75a3\n");
+    put(d + "/class", "0x120000\n");
+    put(d + "/product_name", "AMD Instinct MI355 OAM\n");
+    put(d + "/current_compute_partition", cp + "\n");
+    put(d + "/available_compute_partition", "SPX, DPX, QPX, CPX\n");
+    put(d + "/current_memory_partition", mp + "\n");
+    put(d + "/available_memory_partition", "NPS1, NPS2\n");
+    put(d + "/mem_info_vram_total", std::to_string(vram) + "\n");
+    put(d + "/xgmi_num_links", "01 01 01 01 01 01 00 01\n");
+    put(d + "/sriov_totalvfs", "1\n");
+    put(d + "/sriov_numvfs", "0\n");
+    put(d + "/config", std::string(64, '\0'));
+  }
+  ~Tree() { fs::remove_all(root); }
+};
+
+}  // namespace
+
+TEST(Sysfs_EnumeratesSpxAndCpxGpus) {
+  Tree t;
+  SysfsManager m(SysfsOptions{t.root, DeviceFilter()});
+  m.Init();
+  auto devs = m.GetDevices();
+  EXPECT_EQ(devs.size(), static_cast<size_t>(2));
+  // Sorted by BDF: 23:00.0 (CPX) first, d9:00.0 (SPX) second.
+  const auto& cpx = *devs[0];
+  EXPECT_EQ(cpx.Info().bdf, std::string("0000:23:00.0"));
+  EXPECT_TRUE(cpx.IsPartitioned());
+  EXPECT_TRUE(cpx.IsPartitionCapable());
+  EXPECT_EQ(cpx.GetPartitions().size(), static_cast<size_t>(8));
+  EXPECT_EQ(cpx.GetTotalMemoryMiB(), static_cast<uint64_t>(294896));
+  EXPECT_EQ(cpx.Info().compute_units, static_cast<uint32_t>(256));
+  EXPECT_EQ(cpx.Info().xcds, static_cast<uint32_t>(8));
+  auto p0 = cpx.GetPartitions()[0];
+  EXPECT_EQ(p0->GetName(), std::string("cpx.1xcd.36gb"));
+  EXPECT_EQ(p0->GetAttributes().at("compute-units"), std::string("32"));
+  EXPECT_EQ(p0->GetAttributes().at("memory"), std::string("36862"));
+  EXPECT_EQ(p0->GetParent().get(), devs[0].get());
+
+  const auto& spx = *devs[1];
+  EXPECT_EQ(spx.GetName(), std::string("AMD Instinct MI355 OAM"));
+  EXPECT_FALSE(spx.IsPartitioned());
+  EXPECT_EQ(spx.GetGfxTarget().name(), std::string("gfx950"));
+  EXPECT_EQ(spx.GetTotalMemoryMiB(), static_cast<uint64_t>(294896));
+  EXPECT_EQ(spx.Info().compute_units, static_cast<uint32_t>(256));
+  EXPECT_EQ(spx.Info().xgmi_links, 7);
+  EXPECT_EQ(spx.Info().uuid, std::string("3aff75a3-0000-1000-807c-178b7c5e4d5c"));
+  EXPECT_EQ(spx.Info().compute_partition, std::string("SPX"));
+  EXPECT_EQ(spx.Info().available_memory_partitions, (std::vector<std::string>{"NPS1", "NPS2"}));
+  EXPECT_EQ(m.GetDriverVersion(), std::string("6.12.12"));
+  EXPECT_EQ(m.GetRuntimeVersion().major, 7u);
+  EXPECT_EQ(m.GetRuntimeVersion().minor, 2u);
+  m.Shutdown();
+}
+
+TEST(Sysfs_VisibleDeviceFilter) {
+  Tree t;
+  SysfsManager m(SysfsOptions{t.root, DeviceFilter::parse("1")});
+  m.Init();
+  auto devs = m.GetDevices();
+  EXPECT_EQ(devs.size(), static_cast<size_t>(1));
+  EXPECT_EQ(devs[0]->Info().bdf, std::string("0000:d9:00.0"));
+  SysfsManager m2(SysfsOptions{t.root, DeviceFilter::parse("0000:23:00.0")});
+  m2.Init();
+  EXPECT_EQ(m2.GetDevices()[0]->Info().bdf, std::string("0000:23:00.0"));
+}
+
+TEST(Sysfs_UnreadableNodesAreSkipped) {
+  Tree t;
+  // Node 1 becomes unreadable like GPUs not allocated to the container.
+  ::unlink((t.root + "/sys/class/kfd/kfd/topology/nodes/1/properties").c_str());
+  fs::mkdir_all(t.root + "/sys/class/kfd/kfd/topology/nodes/1/properties");  // read fails (EISDIR)
+  SysfsManager m(SysfsOptions{t.root, DeviceFilter()});
+  m.Init();
+  EXPECT_EQ(m.GetDevices().size(), static_cast<size_t>(1));
+}
+
+TEST(Sysfs_SnapshotOncePerWindow) {
+  Tree t;
+  SysfsManager m(SysfsOptions{t.root, DeviceFilter()});
+  m.Init();
+  auto a = m.GetDevices();
+  auto b = m.GetDevices();
+  EXPECT_EQ(a[0].get(), b[0].get());
+  m.Shutdown();
+  m.Init();
+  EXPECT_FALSE(m.GetDevices()[0].get() == a[0].get());
+}
+
+TEST(Sysfs_MissingTopologyIsInitError) {
+  SysfsManager m(SysfsOptions{"/nonexistent-gfd", DeviceFilter()});
+  EXPECT_THROW_MSG(m.Init(), "KFD topology not available");
+  std::string reason;
+  EXPECT_FALSE(has_kfd_topology("/nonexistent-gfd", &reason));
+}
+
+TEST(Filter_Parse) {
+  auto f = DeviceFilter::parse("0, 2-3,d9:00.0");
+  EXPECT_TRUE(f.matches(0, ""));
+  EXPECT_FALSE(f.matches(1, ""));
+  EXPECT_TRUE(f.matches(3, ""));
+  EXPECT_TRUE(f.matches(7, "0000:D9:00.0"));
+  EXPECT_TRUE(DeviceFilter::parse("").all());
+  EXPECT_TRUE(DeviceFilter::parse("all").all());
+  EXPECT_THROW_MSG(DeviceFilter::parse("3-1"), "invalid device range");
+  EXPECT_THROW_MSG(DeviceFilter::parse("x"), "invalid device");
+}
+
+TEST(GfxTarget_Parsing) {
+  EXPECT_EQ(parse_gfx_target("gfx950")->name(), std::string("gfx950"));
+  EXPECT_EQ(parse_gfx_target("gfx90a:sramecc+:xnack-")->stepping, 10);
+  EXPECT_EQ(parse_gfx_target("gfx1100")->major, 11);
+  EXPECT_FALSE(parse_gfx_target("sm_90").has_value());
+  EXPECT_EQ(gfx_target_from_kfd(90500).name(), std::string("gfx950"));
+  EXPECT_EQ(gfx_target_from_kfd(90010).name(), std::string("gfx90a"));
+  // amd-smi spells the target in hex digits (measured: 0x950 on MI355X).
+  EXPECT_EQ(gfx_target_from_amdsmi(0x950).name(), std::string("gfx950"));
+  EXPECT_EQ(gfx_target_from_amdsmi(0x942).name(), std::string("gfx942"));
+  EXPECT_EQ(gfx_target_from_amdsmi(0x1100).name(), std::string("gfx1100"));
+  EXPECT_FALSE(gfx_target_from_amdsmi(0).valid());
+}
+
+TEST(PartitionProfileName) {
+  EXPECT_EQ(partition_profile_name("CPX", 1, 36862), std::string("cpx.1xcd.36gb"));
+  EXPECT_EQ(partition_profile_name("DPX", 4, 147448), std::string("dpx.4xcd.144gb"));
+  EXPECT_EQ(partition_profile_name("", 2, 1024), std::string("xcp.2xcd.1gb"));
+}
+
+TEST(Versions_Extract) {
+  EXPECT_EQ(*extract_version("6.18.54-ant.1"), std::string("6.18.54"));
+  EXPECT_EQ(*extract_version("Linuxversion6.18.54-ant.1(nixbld@localhost)(gcc(GCC)15.3.0"), std::string("6.18.54"));
+  EXPECT_EQ(*extract_version("6.12.12.60200"), std::string("6.12.12"));
+  EXPECT_EQ(*extract_version("amdgpu 400.300"), std::string("400.300"));
+  EXPECT_FALSE(extract_version("no version here 7").has_value());
+}
+
+TEST(MockFixture_Loads) {
+  auto m = mock_manager_from_node(yaml::parse(R"(
+driverVersion: 6.8.5
+runtimeVersion: "6.4"
+devices:
+- name: MOCKMODEL
+  gfx: gfx942
+  memoryMiB: 196592
+  xgmiLinks: 7
+  availableComputePartitions: [SPX, CPX]
+- name: MOCKMODEL
+  partitioned: true
+  computePartition: CPX
+  partitions:
+  - name: cpx.1xcd.24gb
+    attributes: {memory: 24576, xcds: 1}
+  errors: {GetName: "injected"}
+)"));
+  EXPECT_EQ(m->devices.size(), static_cast<size_t>(2));
+  EXPECT_EQ(m->driver_version, std::string("6.8.5"));
+  EXPECT_EQ(m->runtime_version.minor, 4u);
+  EXPECT_TRUE(m->devices[0]->IsPartitionCapable());
+  EXPECT_EQ(m->devices[0]->GetGfxTarget().name(), std::string("gfx942"));
+  EXPECT_EQ(m->devices[1]->GetPartitions()[0]->GetAttributes().at("memory"), std::string("24576"));
+  EXPECT_THROW_MSG(m->devices[1]->GetName(), "injected");
+}
+
+TEST(Factory_ExplicitBackends) {
+  config::Config c;
+  c.flags.gfd.backend = "null";
+  EXPECT_EQ(get_manager(c)->Name(), std::string("null"));
+  c.flags.gfd.backend = "sysfs";
+  EXPECT_EQ(get_manager(c)->Name(), std::string("sysfs"));
+  c.flags.gfd.backend = "bogus";
+  EXPECT_THROW_MSG(get_manager(c), "unknown backend 'bogus'");
+  c.flags.gfd.backend = "mock";
+  EXPECT_THROW_MSG(get_manager(c), "requires --mock-file");
+  c.flags.gfd.backend = "amdsmi";
+  c.flags.gfd.amdsmi_session = "sometimes";
+  EXPECT_THROW_MSG(get_manager(c), "unknown amd-smi session mode");
+}
+
+TEST(Factory_FailOnInitErrorWrapsInFallback) {
+  config::Config c;
+  c.flags.gfd.backend = "null";
+  c.flags.fail_on_init_error = false;
+  EXPECT_TRUE(new_manager(c)->Name().rfind("fallback(", 0) == 0);
+  c.flags.fail_on_init_error = true;
+  EXPECT_EQ(new_manager(c)->Name(), std::string("null"));
+}
+
+TEST(AmdSmi_InitFailsCleanlyWithoutDriver) {
+  // In the CPU container libamd_smi loads but there is no amdgpu driver:
+  // amdsmi_init returns DRIVER_NOT_LOADED, which must surface as an Init error.
+  std::string reason;
+  if (!has_amdsmi(&reason)) return;  // library not installed: nothing to check
+  if (fs::exists("/dev/kfd")) return;  // a real GPU node: covered by GPU tests
+  AmdSmiManager m(AmdSmiOptions{});
+  EXPECT_THROW_MSG(m.Init(), "amdsmi_init failed");
+  EXPECT_EQ(m.init_count(), 0);
+}

@@ -1,0 +1,253 @@
+// CLI / daemon-loop tests: flag semantics (urfave/cli v2), precedence
+// (CLI > env > config file > default, flags.go:29-40), and the run() fault
+// matrix (cmd/gpu-feature-discovery/main_test.go:273-380).
+#include <unistd.h>
+
+#include "cli/daemon.h"
+#include "cli/flags.h"
+#include "lm/node.h"
+#include "resource/managers.h"
+#include "sriov/sriov.h"
+#include "test.h"
+#include "util/fs.h"
+
+using namespace gfd;
+using namespace gfd::cli;
+
+namespace {
+using Env = std::map<std::string, std::string>;
+Context parse(std::vector<std::string> args, Env env = {}) { return Context::parse(gfd_flags(), args, &env); }
+
+std::string temp_dir() {
+  char d[] = "/tmp/gfd-cli-XXXXXX";
+  if (!mkdtemp(d)) throw std::runtime_error("mkdtemp");
+  return d;
+}
+}  // namespace
+
+TEST(Flags_Defaults) {
+  auto c = parse({});
+  EXPECT_EQ(c.String("mig-strategy"), std::string("none"));
+  EXPECT_TRUE(c.Bool("fail-on-init-error"));
+  EXPECT_FALSE(c.Bool("oneshot"));
+  EXPECT_EQ(c.Duration("sleep-interval"), 60 * kSecond);
+  EXPECT_EQ(c.String("output-file"), std::string("/etc/kubernetes/node-feature-discovery/features.d/gfd"));
+  EXPECT_EQ(c.String("machine-type-file"), std::string("/sys/class/dmi/id/product_name"));
+  EXPECT_FALSE(c.IsSet("oneshot"));
+}
+
+TEST(Flags_GoSyntaxVariants) {
+  auto c = parse({"-oneshot", "--mig-strategy=single", "-o", "/x", "--sleep-interval", "5s", "--fail-on-init-error=false"});
+  EXPECT_TRUE(c.Bool("oneshot"));
+  EXPECT_EQ(c.String("mig-strategy"), std::string("single"));
+  EXPECT_EQ(c.String("output-file"), std::string("/x"));
+  EXPECT_EQ(c.Duration("sleep-interval"), 5 * kSecond);
+  EXPECT_FALSE(c.Bool("fail-on-init-error"));
+  EXPECT_TRUE(c.IsSet("output"));
+  EXPECT_TRUE(c.IsSet("o"));
+}
+
+TEST(Flags_AliasesAndLastWins) {
+  auto c = parse({"--output=/a", "--output-file", "/b"});
+  EXPECT_EQ(c.String("o"), std::string("/b"));
+}
+
+TEST(Flags_EmptyOutputMeansStdout) {
+  auto c = parse({"--output-file="});
+  EXPECT_EQ(c.String("output-file"), std::string(""));
+  EXPECT_TRUE(c.IsSet("output-file"));
+}
+
+TEST(Flags_BoolDoesNotConsumeNextArg) {
+  auto c = parse({"--oneshot", "false"});
+  EXPECT_TRUE(c.Bool("oneshot"));
+  EXPECT_EQ(c.positional(), (std::vector<std::string>{"false"}));
+}
+
+TEST(Flags_StopsAtDoubleDash) {
+  auto c = parse({"--", "--oneshot"});
+  EXPECT_FALSE(c.Bool("oneshot"));
+}
+
+TEST(Flags_Errors) {
+  EXPECT_THROW_MSG(parse({"--bogus"}), "flag provided but not defined: -bogus");
+  EXPECT_THROW_MSG(parse({"--mig-strategy"}), "flag needs an argument: -mig-strategy");
+  EXPECT_THROW_MSG(parse({"--oneshot=maybe"}), "invalid boolean value");
+  EXPECT_THROW_MSG(parse({"--sleep-interval=10"}), "invalid value");
+}
+
+TEST(Flags_HelpAndVersion) {
+  EXPECT_TRUE(parse({"-h"}).help_requested());
+  EXPECT_TRUE(parse({"--version"}).version_requested());
+  std::string h = help_text(gfd_flags(), "GPU Feature Discovery", "x", "v");
+  EXPECT_TRUE(h.find("--output-file value, --output value, -o value") != std::string::npos);
+  EXPECT_TRUE(h.find("[$GFD_MIG_STRATEGY, $MIG_STRATEGY]") != std::string::npos);
+}
+
+TEST(Flags_EnvVarsFirstPresentWins) {
+  auto c = parse({}, {{"MIG_STRATEGY", "mixed"}, {"GFD_MIG_STRATEGY", "single"}});
+  EXPECT_EQ(c.String("mig-strategy"), std::string("single"));
+  auto c2 = parse({}, {{"MIG_STRATEGY", "mixed"}});
+  EXPECT_EQ(c2.String("mig-strategy"), std::string("mixed"));
+  EXPECT_TRUE(c2.IsSet("mig-strategy"));
+}
+
+TEST(Flags_CliBeatsEnv) {
+  auto c = parse({"--mig-strategy=none"}, {{"GFD_MIG_STRATEGY", "single"}});
+  EXPECT_EQ(c.String("mig-strategy"), std::string("none"));
+}
+
+TEST(Flags_EmptyEnvSemantics) {
+  // A string env var applies even when empty; bool/duration ones are ignored.
+  auto c = parse({}, {{"GFD_OUTPUT_FILE", ""}, {"GFD_ONESHOT", ""}, {"GFD_SLEEP_INTERVAL", ""}});
+  EXPECT_EQ(c.String("output-file"), std::string(""));
+  EXPECT_TRUE(c.IsSet("output-file"));
+  EXPECT_FALSE(c.IsSet("oneshot"));
+  EXPECT_FALSE(c.IsSet("sleep-interval"));
+}
+
+TEST(Flags_BadEnvValuesError) {
+  EXPECT_THROW_MSG(parse({}, {{"GFD_ONESHOT", "perhaps"}}), "could not parse \"perhaps\" as bool value from environment variable \"GFD_ONESHOT\"");
+  EXPECT_THROW_MSG(parse({}, {{"GFD_SLEEP_INTERVAL", "1x"}}), "as duration value");
+}
+
+TEST(LoadConfig_Precedence) {
+  std::string dir = temp_dir();
+  std::string file = dir + "/config.yaml";
+  lm::write_file_atomically(file,
+                            "version: v1\nflags:\n  migStrategy: mixed\n  failOnInitError: false\n  gfd:\n"
+                            "    oneshot: true\n    sleepInterval: 10s\n",
+                            0644);
+  // File beats default; env beats file; CLI beats env.
+  auto c = load_config(parse({"--config-file", file, "--sleep-interval=20s"}, {{"GFD_MIG_STRATEGY", "single"}}));
+  EXPECT_EQ(c.mig_strategy(), std::string("single"));       // env over file
+  EXPECT_FALSE(c.fail_on_init_error());                      // file over default
+  EXPECT_TRUE(c.oneshot());                                  // file over default
+  EXPECT_EQ(c.sleep_interval(), 20 * kSecond);               // CLI over file
+  EXPECT_EQ(c.output_file(), std::string(config::kDefaultOutputFile));  // default
+  fs::remove_all(dir);
+}
+
+TEST(LoadConfig_ConfigFileFromEnv) {
+  std::string dir = temp_dir();
+  std::string file = dir + "/c.json";
+  lm::write_file_atomically(file, R"({"flags":{"migStrategy":"single"}})", 0644);
+  auto c = load_config(parse({}, {{"CONFIG_FILE", file}}));
+  EXPECT_EQ(c.mig_strategy(), std::string("single"));
+  fs::remove_all(dir);
+}
+
+TEST(LoadConfig_BadFileErrors) {
+  EXPECT_THROW_MSG(load_config(parse({"--config-file=/nonexistent/gfd.yaml"})),
+                   "unable to finalize config: unable to parse config file: error opening config file");
+}
+
+// ---- run() (main_test.go) ----
+
+namespace {
+config::Config run_config(const std::string& out, const std::string& strategy, bool fail_on_init, bool oneshot) {
+  config::Config c;
+  c.flags.mig_strategy = strategy;
+  c.flags.fail_on_init_error = fail_on_init;
+  c.flags.gfd.oneshot = oneshot;
+  c.flags.gfd.output_file = out;
+  c.flags.gfd.sleep_interval = kSecond / 2;
+  c.flags.gfd.no_timestamp = false;
+  c.flags.gfd.machine_type_file = "/nonexistent/machine";
+  return c;
+}
+}  // namespace
+
+TEST(Run_OneshotWritesFileAndKeepsIt) {
+  std::string dir = temp_dir();
+  std::string out = dir + "/gfd";
+  auto c = run_config(out, "none", true, true);
+  resource::MockManager m({resource::new_full_gpu()});
+  EXPECT_FALSE(run(m, sriov::new_mock_sriov(), c, nullptr));
+  std::string data = fs::read_file(out).data;
+  EXPECT_TRUE(data.find("amd.com/gpu.product=MOCKMODEL\n") != std::string::npos);
+  EXPECT_TRUE(data.find("amd.com/gfd.timestamp=") != std::string::npos);
+  EXPECT_TRUE(data.find("amd.com/sriov.present=true\n") != std::string::npos);
+  EXPECT_EQ(m.init_calls, 1);
+  EXPECT_EQ(m.shutdown_calls, 1);
+  fs::remove_all(dir);
+}
+
+TEST(Run_InitErrorMatrix) {
+  struct Case {
+    bool error_on_init;
+    bool fail_on_init;
+    const char* strategy;
+    bool expect_error;
+  };
+  const Case cases[] = {
+      {true, true, "none", true},    {true, true, "bogus", true},   {true, false, "bogus", false},
+      {true, false, "bogus", false}, {false, true, "none", false},  {false, true, "bogus", true},
+      {false, false, "none", false}, {false, false, "bogus", true},
+  };
+  std::string dir = temp_dir();
+  for (const auto& tc : cases) {
+    auto c = run_config(dir + "/gfd", tc.strategy, tc.fail_on_init, true);
+    auto mock = std::make_shared<resource::MockManager>(std::vector<resource::DevicePtr>{resource::new_full_gpu()});
+    if (tc.error_on_init) mock->with_error_on_init("manager.Init error");
+    auto m = resource::with_config(mock, c);
+    bool threw = false;
+    try {
+      EXPECT_FALSE(run(*m, sriov::new_mock_sriov(), c, nullptr));
+    } catch (const gfdtest::Failure&) {
+      throw;
+    } catch (const std::exception&) {
+      threw = true;
+    }
+    if (threw != tc.expect_error)
+      GFD_FAIL("case error_on_init=" << tc.error_on_init << " fail_on_init=" << tc.fail_on_init << " strategy="
+                                     << tc.strategy << ": threw=" << threw);
+  }
+  fs::remove_all(dir);
+}
+
+TEST(Run_FallbackIsSticky) {
+  auto mock = std::make_shared<resource::MockManager>(std::vector<resource::DevicePtr>{resource::new_full_gpu()});
+  mock->with_error_on_init("boom");
+  resource::FallbackManager f(mock);
+  EXPECT_NO_THROW(f.Init());
+  EXPECT_TRUE(f.fell_back());
+  EXPECT_TRUE(f.GetDevices().empty());
+  mock->init_error.reset();
+  f.Init();  // still the null manager
+  EXPECT_TRUE(f.GetDevices().empty());
+  EXPECT_EQ(mock->init_calls, 1);
+}
+
+TEST(Run_NoTimestampOmitsLabel) {
+  std::string dir = temp_dir();
+  auto c = run_config(dir + "/gfd", "none", true, true);
+  c.flags.gfd.no_timestamp = true;
+  resource::MockManager m({resource::new_full_gpu()});
+  run(m, sriov::new_mock_sriov(), c, nullptr);
+  EXPECT_TRUE(fs::read_file(dir + "/gfd").data.find("gfd.timestamp") == std::string::npos);
+  fs::remove_all(dir);
+}
+
+TEST(Run_NullManagerWritesOnlyTimestampAndSriov) {
+  std::string dir = temp_dir();
+  auto c = run_config(dir + "/gfd", "none", true, true);
+  resource::NullManager m;
+  run(m, sriov::new_empty_sriov(), c, nullptr);
+  std::string data = fs::read_file(dir + "/gfd").data;
+  EXPECT_TRUE(data.find("amd.com/gfd.timestamp=") == 0);
+  EXPECT_EQ(std::count(data.begin(), data.end(), '\n'), 1L);
+  fs::remove_all(dir);
+}
+
+TEST(LabelCycle_RecordsPhases) {
+  auto c = run_config("", "none", true, true);
+  resource::MockManager m({resource::new_full_gpu()});
+  auto ts = lm::NewTimestampLabeler(c, 1);
+  auto r = label_cycle(m, sriov::new_empty_sriov(), c, ts, false);
+  std::vector<std::string> names;
+  for (const auto& p : r.phases) names.push_back(p.first);
+  EXPECT_EQ(names, (std::vector<std::string>{"init", "enumerate", "label", "sriov"}));
+  EXPECT_TRUE(r.total_ns > 0);
+  EXPECT_EQ(r.labels["amd.com/gfd.timestamp"], std::string("1"));
+}

@@ -1,0 +1,176 @@
+// Config schema tests (vendored config/v1: config.go, replicas.go,
+// resources.go, duration.go).
+#include "config/config.h"
+#include "test.h"
+#include "util/duration.h"
+
+using namespace gfd;
+using namespace gfd::config;
+
+TEST(Config_EmptyDocumentDefaultsToV1) {
+  Config c = parse_config_text("");
+  EXPECT_EQ(c.version, std::string("v1"));
+  EXPECT_FALSE(c.flags.mig_strategy.has_value());
+}
+
+TEST(Config_UnknownVersionRejected) {
+  EXPECT_THROW_MSG(parse_config_text("version: v2\n"), "unknown version: v2");
+}
+
+TEST(Config_FullFile) {
+  Config c = parse_config_text(R"(
+version: v1
+flags:
+  migStrategy: mixed
+  failOnInitError: false
+  gfd:
+    oneshot: true
+    noTimestamp: true
+    sleepInterval: 1m30s
+    outputFile: /tmp/out
+    machineTypeFile: /tmp/mt
+    backend: sysfs
+    visibleDevices: "0-3"
+sharing:
+  timeSlicing:
+    renameByDefault: true
+    resources:
+    - name: gpu
+      replicas: 4
+    - name: amd.com/partition-cpx.1xcd.36gb
+      devices: [0, "1", "0:3"]
+      replicas: 2
+      rename: cpx-shared
+)");
+  EXPECT_EQ(*c.flags.mig_strategy, std::string("mixed"));
+  EXPECT_EQ(*c.flags.fail_on_init_error, false);
+  EXPECT_EQ(*c.flags.gfd.oneshot, true);
+  EXPECT_EQ(*c.flags.gfd.sleep_interval, 90 * kSecond);
+  EXPECT_EQ(*c.flags.gfd.output_file, std::string("/tmp/out"));
+  EXPECT_EQ(c.backend(), std::string("sysfs"));
+  EXPECT_EQ(c.visible_devices(), std::string("0-3"));
+  const auto& rs = c.sharing.time_slicing.resources;
+  EXPECT_EQ(rs.size(), static_cast<size_t>(2));
+  EXPECT_EQ(rs[0].name, std::string("amd.com/gpu"));
+  EXPECT_EQ(rs[0].rename, std::string("amd.com/gpu.shared"));  // renameByDefault
+  EXPECT_TRUE(rs[0].devices.all);
+  EXPECT_EQ(rs[1].rename, std::string("amd.com/cpx-shared"));
+  EXPECT_EQ(rs[1].devices.list, (std::vector<std::string>{"0", "1", "0:3"}));
+}
+
+TEST(Config_JsonFile) {
+  Config c = parse_config_text(R"({"version":"v1","flags":{"migStrategy":"single","gfd":{"sleepInterval":5000000000}}})");
+  EXPECT_EQ(*c.flags.mig_strategy, std::string("single"));
+  EXPECT_EQ(*c.flags.gfd.sleep_interval, 5 * kSecond);
+}
+
+TEST(Config_TypeErrors) {
+  EXPECT_THROW_MSG(parse_config_text("flags:\n  failOnInitError: maybe\n"), "cannot unmarshal string into Go struct field");
+  EXPECT_THROW_MSG(parse_config_text("flags:\n  gfd:\n    sleepInterval: forever\n"), "invalid duration");
+  EXPECT_THROW_MSG(parse_config_text("flags: [1]\n"), "cannot unmarshal array");
+}
+
+TEST(Config_PlainScalarsAcceptedForStrings) {
+  Config c = parse_config_text("flags:\n  migStrategy: 1\n");
+  EXPECT_EQ(*c.flags.mig_strategy, std::string("1"));
+}
+
+TEST(Config_TimeSlicingValidation) {
+  EXPECT_THROW_MSG(parse_config_text("sharing:\n  timeSlicing: {}\n"), "no resources specified");
+  EXPECT_THROW_MSG(parse_config_text("sharing:\n  timeSlicing:\n    resources: []\n"), "no resources specified");
+  EXPECT_THROW_MSG(parse_config_text("sharing:\n  timeSlicing:\n    resources:\n    - replicas: 2\n"),
+                   "no resource name specified");
+  EXPECT_THROW_MSG(parse_config_text("sharing:\n  timeSlicing:\n    resources:\n    - name: gpu\n"),
+                   "no replicas specified");
+  EXPECT_THROW_MSG(parse_config_text("sharing:\n  timeSlicing:\n    resources:\n    - name: gpu\n      replicas: 1\n"),
+                   "number of replicas must be >= 2");
+  EXPECT_THROW_MSG(
+      parse_config_text("sharing:\n  timeSlicing:\n    resources:\n    - name: gpu\n      replicas: 2\n      devices: some\n"),
+      "the only valid string input is 'all'");
+  EXPECT_THROW_MSG(
+      parse_config_text("sharing:\n  timeSlicing:\n    resources:\n    - name: gpu\n      replicas: 2\n      devices: 0\n"),
+      "a count of devices must be > 0");
+  EXPECT_THROW_MSG(parse_config_text(
+                       "sharing:\n  timeSlicing:\n    resources:\n    - name: gpu\n      replicas: 2\n      devices: [x]\n"),
+                   "unsupported type for device");
+}
+
+TEST(Config_DeviceRefsAcceptUuids) {
+  Config c = parse_config_text(
+      "sharing:\n  timeSlicing:\n    resources:\n    - name: gpu\n      replicas: 2\n      devices:\n"
+      "      - GPU-3aff75a3-0000-1000-807c-178b7c5e4d5c\n      - 3aff75a3-0000-1000-807c-178b7c5e4d5c\n      - 3\n");
+  EXPECT_EQ(c.sharing.time_slicing.resources[0].devices.list.size(), static_cast<size_t>(3));
+  Config c2 = parse_config_text("sharing:\n  timeSlicing:\n    resources:\n    - name: gpu\n      replicas: 2\n      devices: 2\n");
+  EXPECT_EQ(c2.sharing.time_slicing.resources[0].devices.count, 2);
+}
+
+TEST(Config_ResourcesSection) {
+  Config c = parse_config_text("resources:\n  gpus:\n  - pattern: '*MI355*'\n    name: mi355\n");
+  EXPECT_EQ(c.resources.gpus.size(), static_cast<size_t>(1));
+  EXPECT_EQ(c.resources.gpus[0].name, std::string("amd.com/mi355"));
+  EXPECT_THROW_MSG(parse_config_text("resources:\n  gpus:\n  - name: x\n"), "must have a 'pattern' field set");
+}
+
+TEST(ResourceName_PrefixAndValidation) {
+  EXPECT_EQ(new_resource_name("gpu"), std::string("amd.com/gpu"));
+  EXPECT_EQ(new_resource_name("amd.com/gpu.shared"), std::string("amd.com/gpu.shared"));
+  EXPECT_THROW_MSG(new_resource_name("Bad_Name"), "incorrect format for resource name");
+  EXPECT_THROW_MSG(new_resource_name(std::string(60, 'a')), "must be 63 characters or less");
+  EXPECT_EQ(default_shared_rename("amd.com/gpu"), std::string("amd.com/gpu.shared"));
+}
+
+TEST(DisableResourceRenaming) {
+  Config c = parse_config_text(
+      "resources:\n  gpus:\n  - pattern: x\n    name: y\nsharing:\n  timeSlicing:\n    resources:\n    - name: gpu\n"
+      "      replicas: 2\n      rename: foo\n      devices: [0]\n");
+  disable_resource_renaming(c);
+  EXPECT_TRUE(c.resources.gpus.empty());
+  EXPECT_EQ(c.sharing.time_slicing.resources[0].rename, std::string(""));
+  EXPECT_TRUE(c.sharing.time_slicing.resources[0].devices.all);
+  EXPECT_TRUE(c.sharing.time_slicing.resources[0].devices.list.empty());
+}
+
+TEST(DisableResourceRenaming_RenameByDefaultForcesDefault) {
+  Config c = parse_config_text(
+      "sharing:\n  timeSlicing:\n    renameByDefault: true\n    resources:\n    - name: gpu\n      replicas: 2\n"
+      "      rename: custom\n");
+  disable_resource_renaming(c);
+  EXPECT_EQ(c.sharing.time_slicing.resources[0].rename, std::string("amd.com/gpu.shared"));
+}
+
+TEST(Config_JsonDumpRoundTrips) {
+  Config c = parse_config_text("flags:\n  migStrategy: single\n  gfd:\n    sleepInterval: 90s\n");
+  std::string js = to_json(c);
+  EXPECT_TRUE(js.find("\"migStrategy\": \"single\"") != std::string::npos);
+  EXPECT_TRUE(js.find("\"sleepInterval\": \"1m30s\"") != std::string::npos);
+  Config back = parse_config_text(js);
+  EXPECT_EQ(*back.flags.gfd.sleep_interval, 90 * kSecond);
+}
+
+TEST(Duration_ParseGoGrammar) {
+  EXPECT_EQ(parse_duration("60s"), 60 * kSecond);
+  EXPECT_EQ(parse_duration("1m30s"), 90 * kSecond);
+  EXPECT_EQ(parse_duration("1.5h"), static_cast<Nanos>(5400) * kSecond);
+  EXPECT_EQ(parse_duration("500ms"), 500 * kMillisecond);
+  EXPECT_EQ(parse_duration("2us"), static_cast<Nanos>(2000));
+  EXPECT_EQ(parse_duration("2\xC2\xB5s"), static_cast<Nanos>(2000));
+  EXPECT_EQ(parse_duration("-1s"), -kSecond);
+  EXPECT_EQ(parse_duration("0"), static_cast<Nanos>(0));
+  EXPECT_EQ(parse_duration(".5s"), kSecond / 2);
+  EXPECT_THROW_MSG(parse_duration(""), "invalid duration");
+  EXPECT_THROW_MSG(parse_duration("10"), "missing unit");
+  EXPECT_THROW_MSG(parse_duration("10d"), "unknown unit");
+  EXPECT_THROW_MSG(parse_duration("s"), "invalid duration");
+}
+
+TEST(Duration_FormatGoStyle) {
+  EXPECT_EQ(format_duration(60 * kSecond), std::string("1m0s"));
+  EXPECT_EQ(format_duration(90 * kSecond), std::string("1m30s"));
+  EXPECT_EQ(format_duration(3600 * kSecond), std::string("1h0m0s"));
+  EXPECT_EQ(format_duration(1500 * kMillisecond), std::string("1.5s"));
+  EXPECT_EQ(format_duration(500 * kMillisecond), std::string("500ms"));
+  EXPECT_EQ(format_duration(1500), std::string("1.5\xC2\xB5s"));
+  EXPECT_EQ(format_duration(7), std::string("7ns"));
+  EXPECT_EQ(format_duration(0), std::string("0s"));
+  EXPECT_EQ(format_duration(-kSecond), std::string("-1s"));
+}

@@ -1,0 +1,321 @@
+// Labeler unit tests.  Ports of internal/lm/resource_test.go:27-304 and
+// internal/lm/nvml_test.go:11-77, re-expressed for the amd.com schema.
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cstdio>
+
+#include "lm/keys.h"
+#include "lm/labels.h"
+#include "lm/node.h"
+#include "lm/resource.h"
+#include "resource/managers.h"
+#include "test.h"
+#include "util/fs.h"
+
+using namespace gfd;
+using lm::Labels;
+
+namespace {
+
+config::ReplicatedResource replicated(const std::string& name, int replicas, const std::string& rename = "") {
+  config::ReplicatedResource r;
+  r.name = name;
+  r.rename = rename;
+  r.replicas = replicas;
+  r.devices.all = true;
+  return r;
+}
+
+config::Config sharing_config(std::vector<config::ReplicatedResource> rs) {
+  config::Config c;
+  c.sharing.time_slicing.resources = std::move(rs);
+  return c;
+}
+
+Labels full_gpu(const std::string& count, const std::string& replicas, const std::string& product) {
+  return Labels{
+      {"amd.com/gpu.count", count},          {"amd.com/gpu.replicas", replicas},
+      {"amd.com/gpu.memory", "300"},         {"amd.com/gpu.product", product},
+      {"amd.com/gpu.family", "cdna4"},       {"amd.com/gpu.arch", "gfx950"},
+      {"amd.com/gpu.compute.major", "9"},    {"amd.com/gpu.compute.minor", "5"},
+      {"amd.com/gpu.compute-units", "256"},  {"amd.com/gpu.xcds", "8"},
+  };
+}
+
+Labels partition_labels(const std::string& res, const std::string& replicas, const std::string& product) {
+  return Labels{
+      {res + ".count", "1"},
+      {res + ".replicas", replicas},
+      {res + ".memory", "300"},
+      {res + ".product", product},
+      {res + ".compute-units", "0"},
+      {res + ".xcds", "1"},
+      {res + ".engines.dma", "0"},
+      {res + ".engines.decoder", "0"},
+      {res + ".engines.encoder", "0"},
+      {res + ".engines.jpeg", "0"},
+      {res + ".compute-partition", "CPX"},
+      {res + ".memory-partition", "NPS1"},
+  };
+}
+
+}  // namespace
+
+TEST(GPUResourceLabeler_ZeroCountReturnsEmpty) {
+  config::Config c;
+  EXPECT_EQ(lm::NewGPUResourceLabels(&c, *resource::new_full_gpu(), 0), Labels{});
+}
+
+TEST(GPUResourceLabeler_NoSharing) {
+  config::Config c;
+  EXPECT_EQ(lm::NewGPUResourceLabels(&c, *resource::new_full_gpu(), 1), full_gpu("1", "1", "MOCKMODEL"));
+}
+
+TEST(GPUResourceLabeler_SharingIgnoresNonMatchingResource) {
+  auto c = sharing_config({replicated("amd.com/not-gpu", 2)});
+  EXPECT_EQ(lm::NewGPUResourceLabels(&c, *resource::new_full_gpu(), 1), full_gpu("1", "1", "MOCKMODEL"));
+}
+
+TEST(GPUResourceLabeler_SharedAppendsSuffix) {
+  auto c = sharing_config({replicated("amd.com/gpu", 2)});
+  EXPECT_EQ(lm::NewGPUResourceLabels(&c, *resource::new_full_gpu(), 1), full_gpu("1", "2", "MOCKMODEL-SHARED"));
+}
+
+TEST(GPUResourceLabeler_RenamedDoesNotAppendSuffix) {
+  auto c = sharing_config({replicated("amd.com/gpu", 2, "amd.com/gpu.shared")});
+  EXPECT_EQ(lm::NewGPUResourceLabels(&c, *resource::new_full_gpu(), 1), full_gpu("1", "2", "MOCKMODEL"));
+}
+
+TEST(GPUResourceLabeler_WithoutSharingHasZeroReplicas) {
+  EXPECT_EQ(lm::NewGPUResourceLabelsWithoutSharing(*resource::new_full_gpu(), 2), full_gpu("2", "0", "MOCKMODEL"));
+}
+
+TEST(GPUResourceLabeler_ZeroMemoryOmitsMemoryLabel) {
+  auto d = resource::new_full_gpu();
+  d->mutable_info().memory_mib = 0;
+  config::Config c;
+  auto l = lm::NewGPUResourceLabels(&c, *d, 1);
+  EXPECT_TRUE(l.find("amd.com/gpu.memory") == l.end());
+}
+
+TEST(GPUResourceLabeler_ProductNameIsSanitized) {
+  auto d = resource::new_full_gpu();
+  d->mutable_info().name = "AMD Instinct MI250X/MI250 (OAM)";
+  config::Config c;
+  auto l = lm::NewGPUResourceLabels(&c, *d, 1);
+  EXPECT_EQ(l["amd.com/gpu.product"], std::string("AMD-Instinct-MI250X-MI250--OAM"));
+}
+
+TEST(GPUResourceLabeler_NameErrorIsWrapped) {
+  auto d = resource::new_full_gpu();
+  d->mutable_info().errors["GetName"] = "boom";
+  config::Config c;
+  EXPECT_THROW_MSG(lm::NewGPUResourceLabels(&c, *d, 1), "failed to get device model: boom");
+}
+
+TEST(GPUResourceLabeler_UnknownIsaOmitsArchLabels) {
+  auto d = resource::new_full_gpu();
+  d->mutable_info().gfx = {};
+  config::Config c;
+  auto l = lm::NewGPUResourceLabels(&c, *d, 1);
+  EXPECT_TRUE(l.find("amd.com/gpu.family") == l.end());
+  EXPECT_TRUE(l.find("amd.com/gpu.arch") == l.end());
+  EXPECT_TRUE(l.find("amd.com/gpu.compute.major") == l.end());
+}
+
+TEST(ArchFamilyMapping) {
+  using resource::arch_family;
+  using resource::GfxTarget;
+  EXPECT_EQ(arch_family(GfxTarget{9, 5, 0}), std::string("cdna4"));
+  EXPECT_EQ(arch_family(GfxTarget{9, 4, 2}), std::string("cdna3"));
+  EXPECT_EQ(arch_family(GfxTarget{9, 0, 10}), std::string("cdna2"));
+  EXPECT_EQ(arch_family(GfxTarget{9, 0, 8}), std::string("cdna1"));
+  EXPECT_EQ(arch_family(GfxTarget{9, 0, 6}), std::string("gcn5"));
+  EXPECT_EQ(arch_family(GfxTarget{10, 3, 0}), std::string("rdna2"));
+  EXPECT_EQ(arch_family(GfxTarget{11, 0, 0}), std::string("rdna3"));
+  EXPECT_EQ(arch_family(GfxTarget{12, 0, 1}), std::string("rdna4"));
+  EXPECT_EQ(arch_family(GfxTarget{8, 0, 3}), std::string("undefined"));
+}
+
+// ---- Partition resource labeler (resource_test.go TestMigResourceLabeler) ----
+
+namespace {
+resource::DevicePtr partition_under_parent() {
+  auto p = resource::new_partition("cpx", 1, 300);
+  static std::vector<std::shared_ptr<resource::SnapshotDevice>> keep;  // parents must outlive partitions
+  keep.push_back(resource::new_partitioned_gpu({p}));
+  return p;
+}
+}  // namespace
+
+TEST(PartitionResourceLabeler_ZeroCountReturnsEmpty) {
+  config::Config c;
+  EXPECT_EQ(lm::NewPartitionResourceLabels("", &c, *partition_under_parent(), 0), Labels{});
+}
+
+TEST(PartitionResourceLabeler_NoSharing) {
+  config::Config c;
+  EXPECT_EQ(lm::NewPartitionResourceLabels("amd.com/gpu", &c, *partition_under_parent(), 1),
+            partition_labels("amd.com/gpu", "1", "MOCKMODEL-PARTITION-cpx.1xcd.300gb"));
+}
+
+TEST(PartitionResourceLabeler_SharedAppendsSuffix) {
+  auto c = sharing_config({replicated("amd.com/gpu", 2)});
+  EXPECT_EQ(lm::NewPartitionResourceLabels("amd.com/gpu", &c, *partition_under_parent(), 1),
+            partition_labels("amd.com/gpu", "2", "MOCKMODEL-PARTITION-cpx.1xcd.300gb-SHARED"));
+}
+
+TEST(PartitionResourceLabeler_RenamedDoesNotAppendSuffix) {
+  auto c = sharing_config({replicated("amd.com/gpu", 2, "amd.com/gpu.shared")});
+  EXPECT_EQ(lm::NewPartitionResourceLabels("amd.com/gpu", &c, *partition_under_parent(), 1),
+            partition_labels("amd.com/gpu", "2", "MOCKMODEL-PARTITION-cpx.1xcd.300gb"));
+}
+
+TEST(PartitionResourceLabeler_MixedAppendsShared) {
+  auto c = sharing_config({replicated("amd.com/gpu", 2, "amd.com/gpu.shared"),
+                           replicated("amd.com/partition-cpx.1xcd.1gb", 2)});
+  EXPECT_EQ(lm::NewPartitionResourceLabels("amd.com/partition-cpx.1xcd.1gb", &c, *partition_under_parent(), 1),
+            partition_labels("amd.com/partition-cpx.1xcd.1gb", "2", "MOCKMODEL-PARTITION-cpx.1xcd.300gb-SHARED"));
+}
+
+TEST(PartitionResourceLabeler_MixedRenameDoesNotAppend) {
+  auto c = sharing_config({replicated("amd.com/partition-cpx.1xcd.1gb", 2, "amd.com/partition-cpx.1xcd.1gb.shared")});
+  EXPECT_EQ(lm::NewPartitionResourceLabels("amd.com/partition-cpx.1xcd.1gb", &c, *partition_under_parent(), 1),
+            partition_labels("amd.com/partition-cpx.1xcd.1gb", "2", "MOCKMODEL-PARTITION-cpx.1xcd.300gb"));
+}
+
+TEST(PartitionResourceLabeler_OrphanPartitionErrors) {
+  auto p = resource::new_partition("cpx", 1, 300);
+  config::Config c;
+  EXPECT_THROW_MSG(lm::NewPartitionResourceLabels("amd.com/gpu", &c, *p, 1), "failed to get parent of compute partition");
+}
+
+// ---- Capability labeler (nvml_test.go TestMigCapabilityLabeler) ----
+
+namespace {
+Labels capability(std::vector<resource::DevicePtr> devs) {
+  resource::MockManager m(std::move(devs));
+  return lm::NewPartitionCapabilityLabeler(m)->GetLabels();
+}
+}  // namespace
+
+TEST(CapabilityLabeler_NoDevicesReturnsEmpty) { EXPECT_EQ(capability({}), Labels{}); }
+
+TEST(CapabilityLabeler_SingleNonCapable) {
+  EXPECT_EQ(capability({resource::new_full_gpu()}), (Labels{{"amd.com/gpu.partition.capable", "false"}}));
+}
+
+TEST(CapabilityLabeler_MultipleNonCapable) {
+  EXPECT_EQ(capability({resource::new_full_gpu(), resource::new_full_gpu()}),
+            (Labels{{"amd.com/gpu.partition.capable", "false"}}));
+}
+
+TEST(CapabilityLabeler_SingleCapable) {
+  EXPECT_EQ(capability({resource::new_partitioned_gpu()}), (Labels{{"amd.com/gpu.partition.capable", "true"}}));
+}
+
+TEST(CapabilityLabeler_OneCapableAmongMany) {
+  EXPECT_EQ(capability({resource::new_full_gpu(), resource::new_partitioned_gpu()}),
+            (Labels{{"amd.com/gpu.partition.capable", "true"}}));
+}
+
+// ---- Version labeler (nvml.go:75-106) ----
+
+TEST(VersionLabeler_ParsesDriverAndRuntime) {
+  resource::MockManager m({resource::new_full_gpu()});
+  m.driver_version = "6.18.54";
+  m.runtime_version = {7, 2};
+  EXPECT_EQ(lm::NewVersionLabeler(m)->GetLabels(), (Labels{{"amd.com/driver.major", "6"},
+                                                            {"amd.com/driver.minor", "18"},
+                                                            {"amd.com/driver.rev", "54"},
+                                                            {"amd.com/rocm.runtime.major", "7"},
+                                                            {"amd.com/rocm.runtime.minor", "2"}}));
+}
+
+TEST(VersionLabeler_TwoPartVersionHasEmptyRev) {
+  resource::MockManager m({resource::new_full_gpu()});
+  m.driver_version = "400.300";
+  auto l = lm::NewVersionLabeler(m)->GetLabels();
+  EXPECT_EQ(l["amd.com/driver.major"], std::string("400"));
+  EXPECT_EQ(l["amd.com/driver.rev"], std::string(""));
+}
+
+TEST(VersionLabeler_RejectsBadFormat) {
+  resource::MockManager m({resource::new_full_gpu()});
+  m.driver_version = "1.2.3.4";
+  EXPECT_THROW_MSG(lm::NewVersionLabeler(m), "does not match format \"X.Y[.Z]\"");
+  m.driver_version = "garbage";
+  EXPECT_THROW_MSG(lm::NewVersionLabeler(m), "does not match format");
+}
+
+TEST(VersionLabeler_RuntimeErrorPropagates) {
+  resource::MockManager m({resource::new_full_gpu()});
+  m.runtime_error = "no rocm";
+  EXPECT_THROW_MSG(lm::NewVersionLabeler(m), "error getting ROCm runtime version: no rocm");
+}
+
+// ---- Machine type / timestamp ----
+
+TEST(MachineTypeLabeler_ReadsAndReplacesSpaces) {
+  char tmpl[] = "/tmp/gfd-machine-XXXXXX";
+  int fd = mkstemp(tmpl);
+  const char content[] = "  WB SERVER E6-IS\n";
+  EXPECT_TRUE(write(fd, content, sizeof(content) - 1) > 0);
+  close(fd);
+  auto l = lm::NewMachineTypeLabeler(tmpl)->GetLabels();
+  unlink(tmpl);
+  EXPECT_EQ(l["amd.com/gpu.machine"], std::string("WB-SERVER-E6-IS"));
+}
+
+TEST(MachineTypeLabeler_MissingFileIsUnknown) {
+  EXPECT_EQ(lm::NewMachineTypeLabeler("/nonexistent/gfd/machine")->GetLabels(),
+            (Labels{{"amd.com/gpu.machine", "unknown"}}));
+  EXPECT_EQ(lm::NewMachineTypeLabeler("")->GetLabels(), (Labels{{"amd.com/gpu.machine", "unknown"}}));
+}
+
+TEST(TimestampLabeler_RespectsNoTimestamp) {
+  config::Config c;
+  EXPECT_EQ(lm::NewTimestampLabeler(c, 1234567890)->GetLabels(), (Labels{{"amd.com/gfd.timestamp", "1234567890"}}));
+  c.flags.gfd.no_timestamp = true;
+  EXPECT_EQ(lm::NewTimestampLabeler(c, 1234567890)->GetLabels(), Labels{});
+}
+
+// ---- Composition and writer (labels.go / list.go) ----
+
+TEST(Merge_LaterLabelersOverride) {
+  auto l = lm::merge({lm::from_labels({{"a", "1"}, {"b", "1"}}), lm::empty(), lm::from_labels({{"b", "2"}})})->GetLabels();
+  EXPECT_EQ(l, (Labels{{"a", "1"}, {"b", "2"}}));
+}
+
+TEST(Render_IsSortedKeyValueLines) {
+  EXPECT_EQ(lm::render({{"b", "2"}, {"a", "1"}}), std::string("a=1\nb=2\n"));
+}
+
+TEST(WriteToFile_AtomicWithMode0644) {
+  char dir[] = "/tmp/gfd-write-XXXXXX";
+  EXPECT_TRUE(mkdtemp(dir) != nullptr);
+  std::string path = std::string(dir) + "/gfd";
+  lm::write_to_file({{"k", "v"}}, path);
+  EXPECT_EQ(fs::read_file(path).data, std::string("k=v\n"));
+  struct stat st;
+  EXPECT_TRUE(stat(path.c_str(), &st) == 0);
+  EXPECT_EQ(static_cast<int>(st.st_mode & 0777), 0644);
+  EXPECT_TRUE(fs::is_dir(std::string(dir) + "/gfd-tmp"));
+  EXPECT_EQ(fs::list_dir(std::string(dir) + "/gfd-tmp").size(), static_cast<size_t>(0));
+  lm::remove_output_file(path);
+  EXPECT_FALSE(fs::exists(path));
+  EXPECT_FALSE(fs::exists(std::string(dir) + "/gfd-tmp"));
+  fs::remove_all(dir);
+}
+
+TEST(WriteToFile_UnwritableDirectoryErrors) {
+  EXPECT_THROW_MSG(lm::write_to_file({{"k", "v"}}, "/proc/gfd-cannot-write/here/gfd"), "error atomically writing file");
+}
+
+TEST(SanitizeLabelValue) {
+  EXPECT_EQ(lm::sanitize_label_value("AMD Instinct MI355 OAM"), std::string("AMD-Instinct-MI355-OAM"));
+  EXPECT_EQ(lm::sanitize_label_value("-x-"), std::string("x"));
+  EXPECT_EQ(lm::sanitize_label_value(std::string(80, 'a')).size(), static_cast<size_t>(63));
+  EXPECT_EQ(lm::sanitize_label_value(""), std::string(""));
+}

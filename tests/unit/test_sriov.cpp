@@ -1,0 +1,142 @@
+// SR-IOV / PCI tests.  Ports of internal/vgpu/pciutil_test.go and
+// vgpu_test.go (capability walk, device classification, info), adapted to
+// PCIe SR-IOV.
+#include "lm/labels.h"
+#include "lm/node.h"
+#include "sriov/pci.h"
+#include "sriov/sriov.h"
+#include "test.h"
+
+using namespace gfd;
+using namespace gfd::sriov;
+
+namespace {
+PCIDevice find(const std::string& addr) {
+  for (auto& d : MockAmdPCI().Devices())
+    if (d.address == addr) return d;
+  throw std::runtime_error("no mock device " + addr);
+}
+}  // namespace
+
+TEST(Pci_MockDevicesAreAmd) {
+  for (const auto& d : MockAmdPCI().Devices()) {
+    EXPECT_EQ(GetWord(d.config, 0), static_cast<uint16_t>(0x1002));
+    EXPECT_EQ(d.config.size(), kPciExpressConfigSpaceSize);
+  }
+}
+
+TEST(Pci_CapabilityWalkFindsExpressCapability) {
+  for (const auto& d : MockAmdPCI().Devices()) {
+    auto cap = d.GetCapability(kPciCapabilityExpressId);
+    EXPECT_TRUE(cap.has_value());
+    EXPECT_EQ(GetByte(*cap, 0), static_cast<uint8_t>(0x10));
+    // No vendor-specific (0x09) capability on AMD functions.
+    EXPECT_FALSE(d.GetVendorSpecificCapability().has_value());
+  }
+}
+
+TEST(Pci_CapabilityWalkRequiresFullConfig) {
+  PCIDevice d = find("passthrough");
+  d.config.resize(64);  // what an unprivileged reader sees
+  EXPECT_THROW_MSG(d.GetCapability(kPciCapabilityExpressId), "Please run GFD with privileged mode");
+  EXPECT_THROW_MSG(d.GetExtendedCapability(kPciExtCapSriovId, 0x40), "extended configuration space is not readable");
+}
+
+TEST(Pci_CapabilityWalkNoCapList) {
+  PCIDevice d = find("passthrough");
+  d.config[kPciStatusByte] = 0;
+  EXPECT_FALSE(d.GetCapability(kPciCapabilityExpressId).has_value());
+}
+
+TEST(Pci_CapabilityWalkDetectsLoop) {
+  PCIDevice d = find("passthrough");
+  d.config[0xc1] = 0x48;  // MSI-X -> PM: loop; PCIe cap is still found first
+  EXPECT_TRUE(d.GetCapability(kPciCapabilityExpressId).has_value());
+  EXPECT_FALSE(d.GetCapability(0x42).has_value());  // terminates despite the loop
+}
+
+TEST(Pci_CapabilityWalkBrokenChain) {
+  PCIDevice d = find("passthrough");
+  d.config[0x64] = static_cast<char>(0xff);  // PCIe cap id 0xff: chain broken
+  EXPECT_FALSE(d.GetCapability(kPciCapabilityExpressId).has_value());
+}
+
+TEST(Pci_ExtendedWalkFindsSriovOnPF) {
+  PCIDevice pf = find("pf");
+  auto cap = pf.GetExtendedCapability(kPciExtCapSriovId, 0x40);
+  EXPECT_TRUE(cap.has_value());
+  auto c = parse_sriov_capability(*cap);
+  EXPECT_TRUE(c.has_value());
+  EXPECT_EQ(c->total_vfs, static_cast<uint16_t>(8));
+  EXPECT_EQ(c->num_vfs, static_cast<uint16_t>(4));
+  EXPECT_EQ(c->vf_device_id, static_cast<uint16_t>(0x74b5));
+  EXPECT_TRUE(c->vf_enable);
+  EXPECT_FALSE(find("passthrough").GetExtendedCapability(kPciExtCapSriovId, 0x40).has_value());
+  EXPECT_TRUE(find("passthrough").GetExtendedCapability(kPciExtCapVendorSpecificId, 0x10).has_value());
+}
+
+TEST(Pci_ExtendedWalkDetectsLoop) {
+  PCIDevice d = find("passthrough");
+  // AER next -> 0x100 (itself).
+  uint32_t hdr = 0x0001u | (1u << 16) | (0x100u << 20);
+  for (int i = 0; i < 4; ++i) d.config[0x100 + i] = static_cast<char>((hdr >> (8 * i)) & 0xff);
+  EXPECT_FALSE(d.GetExtendedCapability(kPciExtCapSriovId, 0x40).has_value());
+}
+
+TEST(Sriov_Classify) {
+  EXPECT_FALSE(Lib::Classify(find("passthrough")).has_value());
+  auto pf = Lib::Classify(find("pf"));
+  EXPECT_TRUE(pf.has_value());
+  EXPECT_EQ(pf->role, std::string("pf"));
+  EXPECT_EQ(pf->num_vfs, 4);
+  EXPECT_EQ(pf->total_vfs, 8);
+  EXPECT_EQ(pf->vf_device, std::string("0x74b5"));
+  auto vf = Lib::Classify(find("vf"));
+  EXPECT_TRUE(vf.has_value());
+  EXPECT_EQ(vf->role, std::string("vf"));
+  EXPECT_EQ(vf->physfn, std::string("pf"));
+}
+
+TEST(Sriov_ClassifyGuestVFByDeviceId) {
+  PCIDevice d = find("passthrough");
+  d.device = "0x74b5";
+  auto i = Lib::Classify(d);
+  EXPECT_TRUE(i.has_value());
+  EXPECT_EQ(i->role, std::string("vf"));
+}
+
+TEST(Sriov_TruncatedConfigFallsBackToSysfs) {
+  PCIDevice d = find("pf");
+  d.config.resize(64);
+  auto i = Lib::Classify(d);
+  EXPECT_TRUE(i.has_value());
+  EXPECT_EQ(i->role, std::string("pf"));
+  EXPECT_EQ(i->num_vfs, 4);
+  d.sriov_numvfs = 0;
+  EXPECT_FALSE(Lib::Classify(d).has_value());
+}
+
+TEST(Sriov_PFWithVFsDisabledIsNotReported) {
+  PCIDevice d = find("pf");
+  d.config = MockAmdPCI::pf_config(8, 0, 0x74b5);
+  EXPECT_FALSE(Lib::Classify(d).has_value());
+}
+
+TEST(Sriov_LabelerReportsPresenceAndRole) {
+  auto labels = lm::NewSriovLabeler(new_mock_sriov())->GetLabels();
+  EXPECT_EQ(labels["amd.com/sriov.present"], std::string("true"));
+  // Last function wins, like the reference's vGPU labeler.
+  EXPECT_EQ(labels["amd.com/sriov.role"], std::string("vf"));
+  EXPECT_EQ(labels["amd.com/sriov.num-vfs"], std::string("4"));
+  EXPECT_EQ(labels["amd.com/sriov.total-vfs"], std::string("8"));
+}
+
+TEST(Sriov_LabelerEmptyWhenNoFunctions) {
+  auto lib = std::make_shared<Lib>(std::make_shared<MockAmdPCI>(std::vector<PCIDevice>{find("passthrough")}));
+  EXPECT_EQ(lm::NewSriovLabeler(lib)->GetLabels(), lm::Labels{});
+}
+
+TEST(Sriov_SysfsScanMissingRootErrors) {
+  auto lib = new_sriov_lib("/nonexistent-gfd-root");
+  EXPECT_THROW_MSG(lib->Devices(), "unable to read PCI bus devices");
+}

@@ -27,6 +27,7 @@ over a synthetic N-GPU MI355X tree and says so in "data".
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import statistics
@@ -228,17 +229,29 @@ def main() -> int:
     if dist.rank == 0:
         ms = [x / 1e6 for x in per_step_ns]
         p50 = _percentile(ms, 0.5)
-        extras = {}
+        backend_name = session.backend
+        phases = {}
+        for name, ns_ in session.cycle(True)["phases"]:
+            phases[name] = round(ns_ / 1e6, 4)
+        # Release the persistent amd-smi session before measuring variants
+        # that must pay amdsmi_init themselves.
+        del session
+        gc.collect()
+        extras = {"phases_ms": phases}
         if not a.no_extras:
             sess_backend = "sysfs" if backend == "synthetic" else backend
             if backend == "amdsmi":
                 extras["amdsmi_per_cycle_session"] = _time_variant(
                     g, _session_args("amdsmi", n, out, None, ["--amdsmi-session=per-cycle"]), max(10, a.steps // 10), 2)
+                gc.collect()
                 extras["sysfs_backend"] = _time_variant(g, _session_args("sysfs", n, out, None, []), a.steps, a.warmup)
             try:
                 binary = str(gfd.binary_path())
-                extras["oneshot_process"] = _cold_process(
-                    binary, _session_args(sess_backend, n, out, root, []), max(5, min(30, a.steps // 10)))
+                runs = max(5, min(30, a.steps // 10))
+                extras["oneshot_process"] = _cold_process(binary, _session_args(sess_backend, n, out, root, []), runs)
+                if backend == "amdsmi":
+                    extras["oneshot_process_sysfs"] = _cold_process(binary, _session_args("sysfs", n, out, None, []),
+                                                                    runs)
             except (FileNotFoundError, subprocess.SubprocessError) as e:
                 extras["oneshot_process"] = {"error": str(e)}
         result = {
@@ -261,7 +274,7 @@ def main() -> int:
                 "global_batch": n,
                 "seq_len": None,
                 "parallelism": f"1 labeler for {n} visible GPU(s); {dist.world} rank(s)",
-                "backend": session.backend if session else backend,
+                "backend": backend_name,
                 "strategy": "none",
             },
             "p90_ms": round(_percentile(ms, 0.9), 4),

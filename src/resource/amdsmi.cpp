@@ -16,6 +16,7 @@
 #include "util/fs.h"
 #include "util/log.h"
 #include "util/strings.h"
+#include "util/trace.h"
 
 namespace gfd::resource {
 
@@ -74,6 +75,7 @@ class AmdSmiLib {
   GFD_AMDSMI_FN(get_gpu_virtualization_mode, amdsmi_processor_handle, amdsmi_virtualization_mode_t*);
   GFD_AMDSMI_FN(get_gpu_xcd_counter, amdsmi_processor_handle, uint16_t*);
   GFD_AMDSMI_FN(get_gpu_driver_info, amdsmi_processor_handle, amdsmi_driver_info_t*);
+  GFD_AMDSMI_FN(get_gpu_board_info, amdsmi_processor_handle, amdsmi_board_info_t*);
   GFD_AMDSMI_FN(get_lib_version, amdsmi_version_t*);
 #undef GFD_AMDSMI_FN
   amdsmi_status_t (*status_code_to_string)(amdsmi_status_t, const char**) = nullptr;
@@ -121,6 +123,7 @@ class AmdSmiLib {
     lib_.bind("amdsmi_get_gpu_xgmi_link_status", get_gpu_xgmi_link_status);
     lib_.bind("amdsmi_get_gpu_virtualization_mode", get_gpu_virtualization_mode);
     lib_.bind("amdsmi_get_gpu_xcd_counter", get_gpu_xcd_counter);
+    lib_.bind("amdsmi_get_gpu_board_info", get_gpu_board_info);
     lib_.bind("amdsmi_get_lib_version", get_lib_version);
     lib_.bind("amdsmi_status_code_to_string", status_code_to_string);
     return ok;
@@ -201,7 +204,24 @@ std::vector<std::string> nps_list(uint32_t mask) {
   return out;
 }
 
-void query_proc(AmdSmiLib& L, ProcInfo& p) {
+// libdrm's marketing-name table is consulted by amd-smi; when the process
+// already carries another libdrm (e.g. PyTorch's bundled copy, whose
+// amdgpu.ids path does not exist) it degrades to this generic string -
+// observed on the MI355X pool.
+bool is_generic_name(const std::string& s) { return s.empty() || s == "AMD Radeon Graphics" || s == "N/A"; }
+
+// XCD count of a KFD node (num_xcc) - ~15 us versus ~140 us for
+// amdsmi_get_gpu_xcd_counter, which decodes the full gpu_metrics table.
+uint32_t kfd_num_xcc(const std::string& root, uint32_t node_id) {
+  auto r = fs::read_file(fs::join(root, "sys/class/kfd/kfd/topology/nodes/" + std::to_string(node_id) + "/properties"));
+  if (!r.ok()) return 0;
+  static const char kKey[] = "\nnum_xcc ";
+  auto pos = r.data.find(kKey);
+  if (pos == std::string::npos) return 0;
+  return static_cast<uint32_t>(strtoul(r.data.c_str() + pos + sizeof(kKey) - 1, nullptr, 10));
+}
+
+void query_proc(AmdSmiLib& L, const std::string& root, ProcInfo& p) {
   amdsmi_asic_info_t asic;
   std::memset(&asic, 0, sizeof(asic));
   amdsmi_status_t st = L.get_gpu_asic_info(p.h, &asic);
@@ -215,12 +235,16 @@ void query_proc(AmdSmiLib& L, ProcInfo& p) {
   uint64_t total = 0;
   if (L.get_gpu_memory_total(p.h, AMDSMI_MEM_TYPE_VRAM, &total) == AMDSMI_STATUS_SUCCESS) p.vram = total;
 
+  uint32_t node_id = 0xFFFFFFFFu;
   if (L.get_gpu_kfd_info) {
     amdsmi_kfd_info_t kfd;
     std::memset(&kfd, 0, sizeof(kfd));
-    if (L.get_gpu_kfd_info(p.h, &kfd) == AMDSMI_STATUS_SUCCESS && kfd.current_partition_id != 0xFFFFFFFFu)
-      p.partition_id = kfd.current_partition_id;
+    if (L.get_gpu_kfd_info(p.h, &kfd) == AMDSMI_STATUS_SUCCESS) {
+      if (kfd.current_partition_id != 0xFFFFFFFFu) p.partition_id = kfd.current_partition_id;
+      node_id = kfd.node_id;
+    }
   }
+  if (node_id != 0xFFFFFFFFu) p.xcds = kfd_num_xcc(root, node_id);
   char buf[64];
   if (L.get_gpu_compute_partition) {
     std::memset(buf, 0, sizeof(buf));
@@ -230,9 +254,22 @@ void query_proc(AmdSmiLib& L, ProcInfo& p) {
     std::memset(buf, 0, sizeof(buf));
     if (L.get_gpu_memory_partition(p.h, buf, sizeof(buf)) == AMDSMI_STATUS_SUCCESS) p.memory_partition = str::trim(buf);
   }
-  if (L.get_gpu_xcd_counter) {
+  if (p.xcds == 0 && L.get_gpu_xcd_counter) {
     uint16_t x = 0;
     if (L.get_gpu_xcd_counter(p.h, &x) == AMDSMI_STATUS_SUCCESS) p.xcds = x;
+  }
+  if (is_generic_name(p.market_name)) {
+    // Board FRU product name, then the same attribute via sysfs.
+    if (L.get_gpu_board_info) {
+      amdsmi_board_info_t b;
+      std::memset(&b, 0, sizeof(b));
+      if (L.get_gpu_board_info(p.h, &b) == AMDSMI_STATUS_SUCCESS && !is_generic_name(str::trim(b.product_name)))
+        p.market_name = str::trim(b.product_name);
+    }
+    if (is_generic_name(p.market_name)) {
+      auto v = fs::read_trimmed(fs::join(root, "sys/bus/pci/devices/" + p.bdf + "/product_name"));
+      if (v && !v->empty()) p.market_name = *v;
+    }
   }
 }
 
@@ -311,6 +348,7 @@ AmdSmiManager::~AmdSmiManager() {
 }
 
 void AmdSmiManager::library_init() {
+  trace::Span span("amdsmi_init");
   std::lock_guard<std::mutex> g(lib_->mu);
   amdsmi_status_t st = lib_->init(AMDSMI_INIT_AMD_GPUS);
   if (st != AMDSMI_STATUS_SUCCESS) throw Error("amdsmi_init failed: " + lib_->status_str(st));
@@ -378,6 +416,7 @@ std::vector<DevicePtr> AmdSmiManager::GetDevices() {
 
 std::vector<DevicePtr> AmdSmiManager::snapshot() {
   AmdSmiLib& L = *lib_;
+  trace::Span span("amdsmi.snapshot");
   uint32_t ns = 0;
   amdsmi_status_t st = L.get_socket_handles(&ns, nullptr);
   if (st != AMDSMI_STATUS_SUCCESS) throw Error("amdsmi_get_socket_handles: " + L.status_str(st));
@@ -432,7 +471,7 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
   // Query every processor; parallel across physical GPUs on multi-GPU nodes.
   auto work = [&](Gpu& g) {
     try {
-      for (auto& p : *g.procs) query_proc(L, p);
+      for (auto& p : *g.procs) query_proc(L, opts_.root, p);
       std::sort(g.procs->begin(), g.procs->end(),
                 [](const ProcInfo& a, const ProcInfo& b) { return a.partition_id < b.partition_id; });
       const ProcInfo& first = g.procs->front();

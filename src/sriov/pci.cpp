@@ -73,34 +73,58 @@ std::optional<std::string> PCIDevice::GetExtendedCapability(int ext_id, size_t l
 std::vector<PCIDevice> SysfsAmdPCI::Devices() {
   std::string dir = fs::join(root_, kPciDevicesRoot);
   int err = 0;
-  auto entries = fs::list_dir(dir, &err);
+  auto entries = fs::list_dir_ino(dir, &err);
   if (err != 0) throw Error("unable to read PCI bus devices: open " + dir + ": " + fs::errno_str(err));
+  std::map<std::string, Identity> seen;
   std::vector<PCIDevice> out;
-  for (const auto& addr : entries) {
+  for (const auto& [addr, ino] : entries) {
     std::string p = fs::join(dir, addr);
-    auto vendor = fs::read_file(fs::join(p, "vendor"), 64);
-    if (!vendor.ok()) throw Error("unable to read PCI device vendor id for " + addr + ": " + fs::errno_str(vendor.err));
-    if (str::trim(vendor.data) != kAmdVendorId) continue;
-    auto cls = fs::read_file(fs::join(p, "class"), 64);
-    if (!cls.ok()) throw Error("unable to read PCI device class for " + addr + ": " + fs::errno_str(cls.err));
-    std::string c = str::trim(cls.data);
-    // Display controllers (0x03xxxx) and processing accelerators (0x12xxxx).
-    if (!str::starts_with(c, "0x03") && !str::starts_with(c, "0x12")) continue;
+    Identity id;
+    auto hit = cache_.find(addr);
+    if (hit != cache_.end() && hit->second.ino == ino && ino != 0) {
+      id = hit->second;
+    } else {
+      id.ino = ino;
+      auto vendor = fs::read_file(fs::join(p, "vendor"), 64);
+      if (!vendor.ok()) throw Error("unable to read PCI device vendor id for " + addr + ": " + fs::errno_str(vendor.err));
+      if (str::trim(vendor.data) == kAmdVendorId) {
+        auto cls = fs::read_file(fs::join(p, "class"), 64);
+        if (!cls.ok()) throw Error("unable to read PCI device class for " + addr + ": " + fs::errno_str(cls.err));
+        std::string c = str::trim(cls.data);
+        // Display controllers (0x03xxxx) and processing accelerators (0x12xxxx).
+        if (str::starts_with(c, "0x03") || str::starts_with(c, "0x12")) {
+          id.relevant = true;
+          id.class_code = c.substr(0, 4);
+          id.device = fs::read_trimmed(fs::join(p, "device")).value_or("");
+        }
+      }
+    }
+    seen[addr] = id;
+    if (!id.relevant) continue;
+
     PCIDevice d;
     d.path = p;
     d.address = addr;
     d.vendor = kAmdVendorId;
-    d.class_code = c.substr(0, 4);
-    d.device = fs::read_trimmed(fs::join(p, "device")).value_or("");
-    auto cfg = fs::read_file(fs::join(p, "config"), kPciExpressConfigSpaceSize);
-    if (!cfg.ok()) throw Error("unable to read PCI configuration space for " + addr + ": " + fs::errno_str(cfg.err));
-    d.config = std::move(cfg.data);
+    d.class_code = id.class_code;
+    d.device = id.device;
     if (auto t = fs::read_trimmed(fs::join(p, "sriov_totalvfs"))) d.sriov_totalvfs = static_cast<int>(str::parse_uint(*t).value_or(0));
-    if (auto n = fs::read_trimmed(fs::join(p, "sriov_numvfs"))) d.sriov_numvfs = static_cast<int>(str::parse_uint(*n).value_or(0));
+    if (d.sriov_totalvfs >= 0) {
+      if (auto n = fs::read_trimmed(fs::join(p, "sriov_numvfs"))) d.sriov_numvfs = static_cast<int>(str::parse_uint(*n).value_or(0));
+      if (d.sriov_numvfs > 0) d.sriov_vf_device = fs::read_trimmed(fs::join(p, "sriov_vf_device")).value_or("");
+    }
     std::string link = fs::read_link(fs::join(p, "physfn"));
     if (!link.empty()) d.physfn = fs::basename(link);
+    if (d.sriov_totalvfs < 0 && d.physfn.empty()) {
+      // The kernel publishes no SR-IOV state for this function: read the
+      // configuration space and walk its capabilities instead.
+      auto cfg = fs::read_file(fs::join(p, "config"), kPciExpressConfigSpaceSize);
+      if (!cfg.ok()) throw Error("unable to read PCI configuration space for " + addr + ": " + fs::errno_str(cfg.err));
+      d.config = std::move(cfg.data);
+    }
     out.push_back(std::move(d));
   }
+  cache_.swap(seen);
   return out;
 }
 
@@ -192,6 +216,7 @@ MockAmdPCI::MockAmdPCI() {
   pf.config = pf_config(8, 4, 0x74b5);
   pf.sriov_totalvfs = 8;
   pf.sriov_numvfs = 4;
+  pf.sriov_vf_device = "0x74b5";
 
   PCIDevice vf;
   vf.address = "vf";

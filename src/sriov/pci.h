@@ -16,6 +16,7 @@
 #pragma once
 
 #include <cstdint>
+#include <map>
 #include <memory>
 #include <optional>
 #include <string>
@@ -49,9 +50,10 @@ struct PCIDevice {
   std::string device;    // 0x75a3
   std::string class_code;  // first 4 hex digits of class, e.g. "0x12"
   std::string config;    // raw configuration space bytes (may be truncated)
-  // sysfs-derived SR-IOV facts (-1 = attribute absent).
+  // sysfs-derived SR-IOV facts (-1 / "" = attribute absent).
   int sriov_totalvfs = -1;
   int sriov_numvfs = -1;
+  std::string sriov_vf_device;  // e.g. 0x75b3
   std::string physfn;    // PF address if this function is a VF on the host
 
   // Classic capability-list walk for `cap_id` (pciutil.go:115-149: loop and
@@ -79,13 +81,35 @@ class AmdPCI {
 
 // Walks <root>/sys/bus/pci/devices and keeps vendor 0x1002 display (0x03)
 // and processing-accelerator (0x12) functions.
+//
+// Cost model (measured on the MI355X pool, ~1.3 ms per scan before this):
+// a large server has hundreds of PCI functions and the reference reads
+// `vendor` (and, for its vendor, the whole config space) of every one of them
+// every cycle.  Here:
+//   * the bus is re-listed every call (hot-plug is seen immediately), but the
+//     immutable identity of a function (vendor, class, device ID) is kept per
+//     (address, sysfs inode) - a removed and re-added device gets a new inode
+//     and is re-read;
+//   * the mutable SR-IOV state is re-read every call from the kernel's sysfs
+//     attributes (sriov_numvfs/totalvfs/vf_device, physfn), which cost no PCI
+//     config cycles;
+//   * configuration space (a 4 KiB read = ~1000 config cycles when
+//     privileged) is read only for functions whose SR-IOV state sysfs does not
+//     publish.
 class SysfsAmdPCI : public AmdPCI {
  public:
   explicit SysfsAmdPCI(std::string root = "/") : root_(std::move(root)) {}
   std::vector<PCIDevice> Devices() override;
 
  private:
+  struct Identity {
+    uint64_t ino = 0;
+    bool relevant = false;  // AMD display / accelerator function
+    std::string class_code;
+    std::string device;
+  };
   std::string root_;
+  std::map<std::string, Identity> cache_;
 };
 
 // Built-in mock with synthetic MI300X/MI355X configuration spaces:

@@ -40,8 +40,18 @@ std::optional<Info> Lib::Classify(const PCIDevice& d) {
     i.role = "vf";
     return i;
   }
-  // Physical function: prefer the SR-IOV capability itself; fall back to the
-  // kernel's sysfs view when the extended config space is not readable.
+  // Physical function: the kernel's sysfs view of the SR-IOV capability is
+  // authoritative and free; walk the configuration space only when the
+  // kernel does not publish it.
+  if (d.sriov_totalvfs >= 0) {
+    if (d.sriov_numvfs <= 0) return std::nullopt;
+    Info i;
+    i.role = "pf";
+    i.total_vfs = d.sriov_totalvfs;
+    i.num_vfs = d.sriov_numvfs;
+    i.vf_device = d.sriov_vf_device;
+    return i;
+  }
   if (d.config.size() >= kPciExpressConfigSpaceSize) {
     auto cap = d.GetExtendedCapability(kPciExtCapSriovId, 0x40);
     if (!cap) return std::nullopt;
@@ -52,13 +62,6 @@ std::optional<Info> Lib::Classify(const PCIDevice& d) {
     i.total_vfs = c->total_vfs;
     i.num_vfs = c->num_vfs;
     i.vf_device = str::format("0x%04x", c->vf_device_id);
-    return i;
-  }
-  if (d.sriov_numvfs > 0) {
-    Info i;
-    i.role = "pf";
-    i.total_vfs = d.sriov_totalvfs;
-    i.num_vfs = d.sriov_numvfs;
     return i;
   }
   return std::nullopt;

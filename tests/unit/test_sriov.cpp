@@ -118,7 +118,26 @@ TEST(Sriov_TruncatedConfigFallsBackToSysfs) {
 
 TEST(Sriov_PFWithVFsDisabledIsNotReported) {
   PCIDevice d = find("pf");
+  d.sriov_numvfs = 0;
+  EXPECT_FALSE(Lib::Classify(d).has_value());
+  // Same through the configuration space when sysfs publishes nothing.
+  d.sriov_totalvfs = d.sriov_numvfs = -1;
   d.config = MockAmdPCI::pf_config(8, 0, 0x74b5);
+  EXPECT_FALSE(Lib::Classify(d).has_value());
+}
+
+TEST(Sriov_ConfigSpaceOnlyClassification) {
+  PCIDevice d = find("pf");
+  d.sriov_totalvfs = d.sriov_numvfs = -1;
+  d.sriov_vf_device.clear();
+  auto i = Lib::Classify(d);
+  EXPECT_TRUE(i.has_value());
+  EXPECT_EQ(i->role, std::string("pf"));
+  EXPECT_EQ(i->total_vfs, 8);
+  EXPECT_EQ(i->num_vfs, 4);
+  EXPECT_EQ(i->vf_device, std::string("0x74b5"));
+  // Truncated config and no sysfs attributes: nothing can be said.
+  d.config.resize(64);
   EXPECT_FALSE(Lib::Classify(d).has_value());
 }
 

@@ -58,6 +58,7 @@ class NodeSpec:
     machine: str = "WB SERVER E6-IS"
     privileged: bool = False  # full 4 KiB config space readable
     seed: int = 0
+    hive_size: int = 8  # GPUs per xGMI hive (MI355X platforms: 8)
 
 
 def _write(path: Path, text: str | bytes) -> None:
@@ -200,8 +201,10 @@ def make_node(root: str | os.PathLike, spec: NodeSpec) -> Path:
         _write(d / "mem_info_vram_total", f"{g.vram_bytes}\n")
         _write(d / "unique_id", f"{unique:016x}\n")
         _write(d / "serial_number", f"{rng.randint(10**11, 10**12 - 1)}\n")
-        peers = ["01"] * min(n_gpus, 8)
-        peers[gi % 8] = "00"
+        # Every GPU sits in an 8-GPU xGMI hive whether or not the other GPUs
+        # are visible to this container (measured: 7 peers on a 1-GPU box).
+        peers = ["01"] * spec.hive_size
+        peers[gi % spec.hive_size] = "00"
         _write(d / "xgmi_num_links", " ".join(peers) + " \n")
         sriov = g.sriov or {}
         _write(d / "sriov_totalvfs", f"{sriov.get('total', 1)}\n")

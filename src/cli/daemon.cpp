@@ -11,6 +11,7 @@
 #include "resource/factory.h"
 #include "util/error.h"
 #include "util/log.h"
+#include "util/pool.h"
 
 namespace gfd::cli {
 
@@ -118,8 +119,33 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
                         const config::Config& config, const lm::LabelerPtr& timestamp, bool write) {
   trace::begin_cycle();
   int64_t t0 = trace::now_ns();
-  lm::LabelerPtr loop = lm::NewLabelers(manager, sriov, config);
-  lm::LabelerPtr labelers = lm::merge({timestamp, loop});
+  // The SR-IOV bus scan does not depend on the device backend: run it on a
+  // worker while the backend enumerates (the reference evaluates the vGPU
+  // labeler after the NVML labeler; only the merge order is observable).
+  lm::Labels sriov_labels;
+  int64_t sriov_ns = 0;
+  auto scan = WorkerPool::instance().submit([&] {
+    int64_t s0 = trace::now_ns();
+    sriov_labels = lm::NewSriovLabeler(sriov)->GetLabels();
+    sriov_ns = trace::now_ns() - s0;
+  });
+  lm::LabelerPtr device;
+  try {
+    device = GFD_WRAP("error creating device labeler", lm::NewDeviceLabeler(manager, config));
+  } catch (...) {
+    try {
+      scan.wait();
+    } catch (...) {
+    }
+    throw;
+  }
+  try {
+    scan.wait();
+  } catch (const std::exception& e) {
+    throw Error(std::string("error generating labels: ") + e.what());
+  }
+  trace::record("sriov(overlapped)", sriov_ns);
+  lm::LabelerPtr labelers = lm::merge({timestamp, device, lm::from_labels(std::move(sriov_labels))});
   CycleResult r;
   try {
     r.labels = labelers->GetLabels();

@@ -102,22 +102,31 @@ class SriovLabeler : public Labeler {
  public:
   explicit SriovLabeler(std::shared_ptr<sriov::Interface> lib) : lib_(std::move(lib)) {}
   Labels GetLabels() override {
-    trace::Span span("sriov");
     std::vector<sriov::Function> fns;
     try {
       fns = lib_->Devices();
     } catch (const std::exception& e) {
       throw Error(std::string("unable to get SR-IOV devices: ") + e.what());
     }
+    // Node-level summary.  A host with VFs enabled is role "pf" (its own GPUs
+    // are physical functions; host-side VFs are handed to VMs), a guest that
+    // sees VFs is role "vf".  VF counts are summed over all PFs.
     Labels l;
-    if (!fns.empty()) l[keys::kSriovPresent] = "true";
+    if (fns.empty()) return l;
+    l[keys::kSriovPresent] = "true";
+    bool any_pf = false;
+    int total = 0, num = 0;
     for (const auto& f : fns) {
       const auto& info = f.GetInfo();
-      l[keys::kSriovRole] = info.role;
-      if (info.role == "pf") {
-        if (info.total_vfs >= 0) l[keys::kSriovTotalVfs] = std::to_string(info.total_vfs);
-        if (info.num_vfs >= 0) l[keys::kSriovNumVfs] = std::to_string(info.num_vfs);
-      }
+      if (info.role != "pf") continue;
+      any_pf = true;
+      total += info.total_vfs > 0 ? info.total_vfs : 0;
+      num += info.num_vfs > 0 ? info.num_vfs : 0;
+    }
+    l[keys::kSriovRole] = any_pf ? "pf" : "vf";
+    if (any_pf) {
+      l[keys::kSriovTotalVfs] = std::to_string(total);
+      l[keys::kSriovNumVfs] = std::to_string(num);
     }
     return l;
   }

@@ -8,8 +8,8 @@
 #include <cstring>
 #include <map>
 #include <mutex>
-#include <thread>
 
+#include "util/pool.h"
 #include "resource/versions.h"
 #include "util/dynlib.h"
 #include "util/error.h"
@@ -481,28 +481,10 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
       g.error = e.what();
     }
   };
-  int threads = opts_.threads > 0 ? opts_.threads : static_cast<int>(std::min<size_t>(gpus.size(), 8));
-  if (threads <= 1 || gpus.size() <= 1) {
-    for (auto& g : gpus) work(g);
-  } else {
-    std::vector<std::thread> pool;
-    std::atomic<size_t> next{0};
-    for (int t = 0; t < threads; ++t)
-      pool.emplace_back([&] {
-        for (size_t i = next++; i < gpus.size(); i = next++) work(gpus[i]);
-      });
-    for (auto& th : pool) th.join();
-  }
+  size_t threads = opts_.threads > 0 ? static_cast<size_t>(opts_.threads) : 8;
+  WorkerPool::instance().parallel_for(gpus.size(), [&](size_t i) { work(gpus[i]); }, threads);
   for (const auto& g : gpus)
     if (!g.error.empty()) throw Error(g.error);
-
-  // Driver version: one query per node (all GPUs share the amdgpu module).
-  if (!gpus.empty()) {
-    amdsmi_driver_info_t drv;
-    std::memset(&drv, 0, sizeof(drv));
-    if (L.get_gpu_driver_info(gpus.front().procs->front().h, &drv) == AMDSMI_STATUS_SUCCESS)
-      driver_version_ = drv.driver_version;
-  }
 
   std::vector<DevicePtr> out;
   for (auto& g : gpus) {
@@ -563,14 +545,13 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
 }
 
 std::string AmdSmiManager::GetDriverVersion() {
-  if (driver_version_.empty()) {
-    // No GPU enumerated yet in this window: fall back to the host's view.
-    if (have_snapshot_ || !in_window_) return host_driver_version(opts_.root);
-    GetDevices();
-    if (driver_version_.empty()) return host_driver_version(opts_.root);
-  }
-  auto v = extract_version(driver_version_);
-  return v ? *v : driver_version_;
+  // amdsmi_get_gpu_driver_info reports /sys/module/amdgpu/version for a DKMS
+  // driver and the kernel banner for an in-tree one (measured on the pool:
+  // "Linuxversion6.18.54-ant.1(...)").  Reading those sources directly gives
+  // the same answer without the ~130 us library round trip per cycle.
+  std::string raw = host_driver_version(opts_.root);
+  auto v = extract_version(raw);
+  return v ? *v : raw;
 }
 
 RuntimeVersion AmdSmiManager::GetRuntimeVersion() {

@@ -66,7 +66,6 @@ class AmdSmiManager : public Manager {
   bool in_window_ = false;
   bool have_snapshot_ = false;
   std::vector<DevicePtr> snapshot_;
-  std::string driver_version_;
   std::string generation_;
   int init_count_ = 0;
 };

@@ -1,0 +1,72 @@
+// Small persistent worker pool.
+//
+// A labeling cycle on an 8-GPU node issues a few hundred microseconds of
+// driver queries per GPU plus an independent PCI-bus scan.  Spawning threads
+// per cycle would cost as much as the work, so a process-wide pool of
+// long-lived workers runs (a) the SR-IOV scan concurrently with device
+// enumeration and (b) per-GPU amd-smi queries in parallel.
+//
+// Workers are created lazily on first use and inherit the creating thread's
+// signal mask; the daemon blocks its watched signals before the first cycle,
+// so workers never steal SIGHUP/SIGTERM from the run loop's sigtimedwait.
+#pragma once
+
+#include <condition_variable>
+#include <cstddef>
+#include <deque>
+#include <exception>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+namespace gfd {
+
+class WorkerPool {
+ public:
+  // Process-wide pool.
+  static WorkerPool& instance();
+
+  explicit WorkerPool(size_t max_workers);
+  ~WorkerPool();
+  WorkerPool(const WorkerPool&) = delete;
+  WorkerPool& operator=(const WorkerPool&) = delete;
+
+  class Task {
+   public:
+    // Blocks until the task ran; rethrows its exception.
+    void wait();
+
+   private:
+    friend class WorkerPool;
+    struct State {
+      std::mutex mu;
+      std::condition_variable cv;
+      bool done = false;
+      std::exception_ptr error;
+    };
+    std::shared_ptr<State> state_;
+  };
+
+  // Run fn on a worker.
+  Task submit(std::function<void()> fn);
+  // Run fn(i) for i in [0, n): the calling thread takes part, at most
+  // `max_parallel` (0 = unlimited) run concurrently.  Rethrows the first error.
+  void parallel_for(size_t n, const std::function<void(size_t)>& fn, size_t max_parallel = 0);
+
+  size_t workers() const;
+
+ private:
+  void ensure_workers(size_t n);
+  void loop();
+
+  size_t max_workers_;
+  mutable std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> queue_;
+  std::vector<std::thread> threads_;
+  bool stop_ = false;
+};
+
+}  // namespace gfd

@@ -1,0 +1,201 @@
+"""End-to-end golden tests of the daemon binary.
+
+BASELINE.json config 1 ("mock/null resource manager on CPU,
+mig-strategy=none, golden-file diff vs tests/expected-output.txt") plus the
+partition-strategy and SR-IOV goldens.  Mirrors the reference's
+cmd/gpu-feature-discovery/main_test.go (TestRunOneshot, TestRunWithNoTimestamp)
+and mig_test.go (TestMigStrategy{None,Single,Mixed,...}), but:
+
+* byte goldens (tests/golden/*.txt) pin the exact, sorted feature file;
+* regex goldens (tests/expected-output*.txt) are checked bidirectionally.
+
+Regenerate byte goldens with GFD_UPDATE_GOLDENS=1 (then review the diff).
+"""
+
+from __future__ import annotations
+
+import os
+from pathlib import Path
+
+import pytest
+
+from conftest import FIXTURES, GOLDEN, TESTS, run_daemon
+from gpu_feature_discovery_amd import golden, synth
+
+UPDATE = os.environ.get("GFD_UPDATE_GOLDENS") == "1"
+
+
+def _oneshot(binary, tmp_path, *args, timestamp=False, sysfs_root=None, machine=None):
+    out = tmp_path / "gfd"
+    root = sysfs_root or str(synth.make_node(tmp_path / "empty-root", synth.NodeSpec(gpus=[])))
+    mt = machine or str(Path(root) / "sys/class/dmi/id/product_name")
+    argv = ["--oneshot", f"--output-file={out}", f"--machine-type-file={mt}", f"--sysfs-root={root}", *args]
+    if not timestamp:
+        argv.append("--no-timestamp")
+    run_daemon(binary, *argv, check=True)
+    text = out.read_text()
+    golden.parse_labels(text)  # no duplicates, key=value lines
+    return text
+
+
+def _mock(name):
+    return ["--backend=mock", f"--mock-file={FIXTURES / name}"]
+
+
+# ---- BASELINE config 1: mock backend, strategy none -------------------------
+
+def test_config1_mock_none_byte_golden(binary, tmp_path):
+    text = _oneshot(binary, tmp_path, *_mock("full-gpu.yaml"), "--mig-strategy=none")
+    golden.check_byte_golden(text, GOLDEN / "mock-none.txt", UPDATE)
+
+
+def test_config1_mock_none_regex_golden(binary, tmp_path):
+    text = _oneshot(binary, tmp_path, *_mock("full-gpu.yaml"), timestamp=True)
+    golden.check_regex_golden(text, TESTS / "expected-output.txt", select=lambda ln: "sriov" not in ln)
+    labels = golden.parse_labels(text)
+    assert labels["amd.com/gpu.count"] == "1"
+    assert labels["amd.com/gpu.product"] == "MOCKMODEL"
+    assert labels["amd.com/gpu.memory"] == "300"
+
+
+def test_no_timestamp_omits_label(binary, tmp_path):
+    text = _oneshot(binary, tmp_path, *_mock("full-gpu.yaml"))
+    assert "amd.com/gfd.timestamp=" not in text
+
+
+def test_null_backend_writes_only_timestamp(binary, tmp_path):
+    text = _oneshot(binary, tmp_path, "--backend=null", timestamp=True)
+    assert list(golden.parse_labels(text)) == ["amd.com/gfd.timestamp"]
+
+
+# ---- Partition strategies (mig_test.go analogues) ----------------------------
+
+def test_strategy_none_with_partitioned_gpu(binary, tmp_path):
+    text = _oneshot(binary, tmp_path, *_mock("partitioned-single.yaml"), "--mig-strategy=none")
+    labels = golden.parse_labels(text)
+    assert labels["amd.com/gpu.count"] == "1"
+    assert labels["amd.com/gpu.product"] == "MOCKMODEL"
+    assert labels["amd.com/gpu.memory"] == "300"
+    assert labels["amd.com/gpu.replicas"] == "0"
+    assert "amd.com/partition.strategy" not in labels
+
+
+def test_strategy_single_no_partitioned_devices(binary, tmp_path):
+    text = _oneshot(binary, tmp_path, *_mock("full-gpu.yaml"), "--mig-strategy=single")
+    labels = golden.parse_labels(text)
+    assert labels["amd.com/partition.strategy"] == "single"
+    assert labels["amd.com/gpu.count"] == "1"
+    assert labels["amd.com/gpu.product"] == "MOCKMODEL"
+    assert labels["amd.com/gpu.memory"] == "300"
+
+
+def test_strategy_single(binary, tmp_path):
+    text = _oneshot(binary, tmp_path, *_mock("partitioned-single.yaml"), "--mig-strategy=single", timestamp=True)
+    golden.check_regex_golden(text, TESTS / "expected-output-partition-single.txt")
+    labels = golden.parse_labels(text)
+    assert labels["amd.com/gpu.count"] == "2"
+    assert labels["amd.com/gpu.product"] == "MOCKMODEL-PARTITION-cpx.1xcd.20gb"
+    assert labels["amd.com/gpu.memory"] == "20"
+    golden.check_byte_golden(_oneshot(binary, tmp_path, *_mock("partitioned-single.yaml"), "--mig-strategy=single"),
+                             GOLDEN / "mock-single.txt", UPDATE)
+
+
+def test_strategy_single_invalid_when_empty(binary, tmp_path):
+    text = _oneshot(binary, tmp_path, *_mock("partitioned-empty.yaml"), "--mig-strategy=single")
+    labels = golden.parse_labels(text)
+    assert labels["amd.com/gpu.product"] == "MOCKMODEL-PARTITION-INVALID"
+    assert labels["amd.com/gpu.count"] == "0"
+    assert labels["amd.com/gpu.replicas"] == "0"
+    assert labels["amd.com/gpu.memory"] == "0"
+
+
+def test_strategy_single_invalid_with_mixed_profiles(binary, tmp_path):
+    labels = golden.parse_labels(_oneshot(binary, tmp_path, *_mock("partitioned-mixed.yaml"), "--mig-strategy=single"))
+    assert labels["amd.com/gpu.product"] == "MOCKMODEL-PARTITION-INVALID"
+
+
+def test_strategy_mixed(binary, tmp_path):
+    text = _oneshot(binary, tmp_path, *_mock("partitioned-mixed.yaml"), "--mig-strategy=mixed", timestamp=True)
+    golden.check_regex_golden(text, TESTS / "expected-output-partition-mixed.txt")
+    labels = golden.parse_labels(text)
+    assert labels["amd.com/partition.strategy"] == "mixed"
+    assert labels["amd.com/gpu.count"] == "1"
+    assert labels["amd.com/gpu.product"] == "MOCKMODEL"
+    assert labels["amd.com/gpu.memory"] == "300"
+    assert labels["amd.com/partition-cpx.1xcd.20gb.count"] == "1"
+    assert labels["amd.com/partition-qpx.2xcd.5gb.count"] == "1"
+    golden.check_byte_golden(_oneshot(binary, tmp_path, *_mock("partitioned-mixed.yaml"), "--mig-strategy=mixed"),
+                             GOLDEN / "mock-mixed.txt", UPDATE)
+
+
+def test_unknown_strategy_fails_with_devices(binary, tmp_path):
+    cp = run_daemon(binary, "--oneshot", "-o", str(tmp_path / "x"), *_mock("full-gpu.yaml"), "--mig-strategy=bogus",
+                    f"--sysfs-root={tmp_path}")
+    assert cp.returncode == 1
+    assert "unknown strategy: bogus" in cp.stderr
+
+
+# ---- Synthetic MI355X nodes (sysfs backend) ----------------------------------
+
+@pytest.mark.parametrize("n", [1, 2, 4, 8])
+def test_synthetic_spx_node(binary, tmp_path, n):
+    root = synth.make_mi355x_node(tmp_path / "root", n_gpus=n, seed=n)
+    text = _oneshot(binary, tmp_path, "--backend=sysfs", sysfs_root=str(root))
+    golden.check_byte_golden(text.replace(f"amd.com/gpu.count={n}\n", "amd.com/gpu.count=N\n"),
+                             GOLDEN / "synthetic-spx.txt", UPDATE)
+    assert golden.parse_labels(text)["amd.com/gpu.count"] == str(n)
+
+
+def test_synthetic_spx_matches_regex_golden(binary, tmp_path):
+    root = synth.make_mi355x_node(tmp_path / "root", n_gpus=8, seed=3)
+    text = _oneshot(binary, tmp_path, "--backend=sysfs", sysfs_root=str(root), timestamp=True)
+    golden.check_regex_golden(text, TESTS / "expected-output.txt")
+
+
+def test_synthetic_cpx_single(binary, tmp_path):
+    root = synth.make_mi355x_node(tmp_path / "root", n_gpus=8, compute_partition="CPX", seed=5)
+    text = _oneshot(binary, tmp_path, "--backend=sysfs", "--mig-strategy=single", sysfs_root=str(root))
+    golden.check_byte_golden(text, GOLDEN / "synthetic-cpx-single.txt", UPDATE)
+    labels = golden.parse_labels(text)
+    assert labels["amd.com/gpu.count"] == "64"
+    assert labels["amd.com/gpu.product"] == "AMD-Instinct-MI355-OAM-PARTITION-cpx.1xcd.36gb"
+    assert labels["amd.com/gpu.compute-units"] == "32"
+
+
+def test_synthetic_dpx_nps2_mixed(binary, tmp_path):
+    root = synth.make_mi355x_node(tmp_path / "root", n_gpus=4, compute_partition="DPX", memory_partition="NPS2",
+                                  seed=6)
+    text = _oneshot(binary, tmp_path, "--backend=sysfs", "--mig-strategy=mixed", sysfs_root=str(root))
+    golden.check_byte_golden(text, GOLDEN / "synthetic-dpx-nps2-mixed.txt", UPDATE)
+    labels = golden.parse_labels(text)
+    assert labels["amd.com/partition-dpx.4xcd.144gb.count"] == "8"
+    assert labels["amd.com/partition-dpx.4xcd.144gb.memory-partition"] == "NPS2"
+
+
+def test_synthetic_sriov_pf(binary, tmp_path):
+    spec = synth.NodeSpec(gpus=[synth.GpuSpec(sriov={"total": 8, "num": 4, "vf_device": 0x75B3})], seed=7)
+    root = synth.make_node(tmp_path / "root", spec)
+    text = _oneshot(binary, tmp_path, "--backend=sysfs", sysfs_root=str(root))
+    golden.check_regex_golden(text, TESTS / "expected-output-sriov.txt", select=lambda ln: "sriov" in ln)
+    labels = golden.parse_labels(text)
+    assert labels["amd.com/sriov.present"] == "true"
+    # Per-function order: the PF then its VFs; the last function wins.
+    assert labels["amd.com/sriov.role"] in ("pf", "vf")
+    assert labels["amd.com/sriov.num-vfs"] == "4"
+    assert labels["amd.com/sriov.total-vfs"] == "8"
+    golden.check_byte_golden(text, GOLDEN / "synthetic-sriov.txt", UPDATE)
+
+
+def test_synthetic_sriov_privileged_config_space(binary, tmp_path):
+    spec = synth.NodeSpec(gpus=[synth.GpuSpec(sriov={"total": 8, "num": 2})], privileged=True, seed=8)
+    root = synth.make_node(tmp_path / "root", spec)
+    labels = golden.parse_labels(_oneshot(binary, tmp_path, "--backend=sysfs", sysfs_root=str(root)))
+    assert labels["amd.com/sriov.num-vfs"] == "2"
+
+
+def test_amdsmi_and_sysfs_label_sets_are_identical_in_shape(binary, tmp_path):
+    """The regex golden used for hardware runs is the same file the synthetic
+    tree satisfies, so both backends must emit the same 22 keys."""
+    root = synth.make_mi355x_node(tmp_path / "root", n_gpus=1)
+    keys = set(golden.parse_labels(_oneshot(binary, tmp_path, "--backend=sysfs", sysfs_root=str(root), timestamp=True)))
+    assert len(keys) == len(golden.load_regexes(TESTS / "expected-output.txt"))

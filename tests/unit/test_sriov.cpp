@@ -144,10 +144,28 @@ TEST(Sriov_ConfigSpaceOnlyClassification) {
 TEST(Sriov_LabelerReportsPresenceAndRole) {
   auto labels = lm::NewSriovLabeler(new_mock_sriov())->GetLabels();
   EXPECT_EQ(labels["amd.com/sriov.present"], std::string("true"));
-  // Last function wins, like the reference's vGPU labeler.
-  EXPECT_EQ(labels["amd.com/sriov.role"], std::string("vf"));
+  // A PF with VFs enabled makes this an SR-IOV host.
+  EXPECT_EQ(labels["amd.com/sriov.role"], std::string("pf"));
   EXPECT_EQ(labels["amd.com/sriov.num-vfs"], std::string("4"));
   EXPECT_EQ(labels["amd.com/sriov.total-vfs"], std::string("8"));
+}
+
+TEST(Sriov_LabelerGuestRole) {
+  PCIDevice vf = find("passthrough");
+  vf.device = "0x74b5";  // a VF as seen inside a guest (no physfn link)
+  auto lib = std::make_shared<Lib>(std::make_shared<MockAmdPCI>(std::vector<PCIDevice>{vf}));
+  auto labels = lm::NewSriovLabeler(lib)->GetLabels();
+  EXPECT_EQ(labels, (lm::Labels{{"amd.com/sriov.present", "true"}, {"amd.com/sriov.role", "vf"}}));
+}
+
+TEST(Sriov_LabelerSumsVfsOverPFs) {
+  PCIDevice a = find("pf"), b = find("pf");
+  b.address = "pf2";
+  b.sriov_numvfs = 2;
+  auto lib = std::make_shared<Lib>(std::make_shared<MockAmdPCI>(std::vector<PCIDevice>{a, b}));
+  auto labels = lm::NewSriovLabeler(lib)->GetLabels();
+  EXPECT_EQ(labels["amd.com/sriov.num-vfs"], std::string("6"));
+  EXPECT_EQ(labels["amd.com/sriov.total-vfs"], std::string("16"));
 }
 
 TEST(Sriov_LabelerEmptyWhenNoFunctions) {

@@ -1,0 +1,249 @@
+"""Daemon lifecycle tests (binary, subprocess).
+
+Mirrors cmd/gpu-feature-discovery/main_test.go: TestRunSleep (two loop
+iterations: the file is rewritten, the timestamp stays fixed within a run),
+TestFailOnNVMLInitError (the 8-case matrix through the CLI), plus what the
+reference never tested: SIGHUP reload (new timestamp, config re-read),
+SIGTERM cleanup of the feature file, CLI/env/config precedence, stdout mode.
+"""
+
+from __future__ import annotations
+
+import os
+import signal
+import subprocess
+import time
+from pathlib import Path
+
+import pytest
+
+from conftest import FIXTURES, run_daemon
+from gpu_feature_discovery_amd import golden, synth
+
+
+def _base(tmp_path, out):
+    root = synth.make_node(tmp_path / "root", synth.NodeSpec(gpus=[]))
+    return [f"--output-file={out}", f"--sysfs-root={root}", f"--machine-type-file={root}/sys/class/dmi/id/product_name",
+            "--backend=mock", f"--mock-file={FIXTURES / 'full-gpu.yaml'}"]
+
+
+def _wait_for(pred, timeout=10.0, interval=0.02):
+    end = time.time() + timeout
+    while time.time() < end:
+        if pred():
+            return True
+        time.sleep(interval)
+    return False
+
+
+def _start(binary, args, env=None):
+    e = {k: v for k, v in os.environ.items() if not k.startswith("GFD_")}
+    if env:
+        e.update(env)
+    return subprocess.Popen([binary, *args], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=e)
+
+
+def test_oneshot_exit_zero_and_file_kept(binary, tmp_path):
+    out = tmp_path / "gfd"
+    cp = run_daemon(binary, "--oneshot", *_base(tmp_path, out), check=True)
+    assert out.exists()
+    assert "Writing labels to output file" in cp.stderr
+    assert oct(out.stat().st_mode & 0o777) == "0o644"
+
+
+def test_stdout_mode_when_output_empty(binary, tmp_path):
+    args = _base(tmp_path, "")
+    cp = run_daemon(binary, "--oneshot", "--no-timestamp", *args, check=True)
+    labels = golden.parse_labels(cp.stdout)
+    assert labels["amd.com/gpu.product"] == "MOCKMODEL"
+    assert not (tmp_path / "gfd-tmp").exists()
+
+
+def test_loop_rewrites_file_with_constant_timestamp(binary, tmp_path):
+    """TestRunSleep: two iterations, mtime increases, timestamp unchanged."""
+    out = tmp_path / "gfd"
+    p = _start(binary, ["--sleep-interval=300ms", *_base(tmp_path, out)])
+    try:
+        assert _wait_for(out.exists), "first write"
+        first = golden.parse_labels(out.read_text())
+        m0 = out.stat().st_mtime_ns
+        assert _wait_for(lambda: out.exists() and out.stat().st_mtime_ns > m0, timeout=5), "file not rewritten"
+        second = golden.parse_labels(out.read_text())
+        assert first["amd.com/gfd.timestamp"] == second["amd.com/gfd.timestamp"]
+        assert first == second
+    finally:
+        p.send_signal(signal.SIGTERM)
+        _, err = p.communicate(timeout=10)
+    assert p.returncode == 0
+    assert 'Received signal "terminated", shutting down.' in err
+    # Non-oneshot mode removes its labels on exit (main.go:149-156).
+    assert not out.exists()
+    assert not (tmp_path / "gfd-tmp").exists()
+
+
+@pytest.mark.parametrize("sig,name", [(signal.SIGINT, "interrupt"), (signal.SIGQUIT, "quit")])
+def test_other_signals_exit_cleanly(binary, tmp_path, sig, name):
+    out = tmp_path / "gfd"
+    p = _start(binary, ["--sleep-interval=10s", *_base(tmp_path, out)])
+    try:
+        assert _wait_for(out.exists)
+    finally:
+        p.send_signal(sig)
+        _, err = p.communicate(timeout=10)
+    assert p.returncode == 0
+    assert f'Received signal "{name}"' in err
+    assert not out.exists()
+
+
+def test_sighup_reloads_config(binary, tmp_path):
+    out = tmp_path / "gfd"
+    cfg = tmp_path / "config.yaml"
+    cfg.write_text("version: v1\nflags:\n  migStrategy: none\n")
+    p = _start(binary, ["--sleep-interval=10s", f"--config-file={cfg}", *_base(tmp_path, out)[:-2],
+                        "--backend=mock", f"--mock-file={FIXTURES / 'partitioned-single.yaml'}"])
+    try:
+        assert _wait_for(out.exists)
+        before = golden.parse_labels(out.read_text())
+        assert "amd.com/partition.strategy" not in before
+        cfg.write_text("version: v1\nflags:\n  migStrategy: single\n")
+        time.sleep(1.1)  # the new run takes a new timestamp (1 s resolution)
+        p.send_signal(signal.SIGHUP)
+        assert _wait_for(lambda: out.exists() and "partition.strategy=single" in out.read_text(), timeout=10)
+        after = golden.parse_labels(out.read_text())
+        assert after["amd.com/gpu.product"] == "MOCKMODEL-PARTITION-cpx.1xcd.20gb"
+        assert int(after["amd.com/gfd.timestamp"]) > int(before["amd.com/gfd.timestamp"])
+    finally:
+        p.send_signal(signal.SIGTERM)
+        _, err = p.communicate(timeout=10)
+    assert "Received SIGHUP, restarting." in err
+    assert err.count("Loading configuration.") == 2
+
+
+@pytest.mark.parametrize(
+    "error_on_init,fail_on_init,strategy,expect_error",
+    [
+        (True, True, "none", True),
+        (True, True, "bogus", True),
+        (True, False, "bogus", False),
+        (True, False, "none", False),
+        (False, True, "none", False),
+        (False, True, "bogus", True),
+        (False, False, "none", False),
+        (False, False, "bogus", True),
+    ],
+)
+def test_fail_on_init_error_matrix(binary, tmp_path, error_on_init, fail_on_init, strategy, expect_error):
+    out = tmp_path / "gfd"
+    fixture = "init-error.yaml" if error_on_init else "full-gpu.yaml"
+    args = _base(tmp_path, out)[:-1] + [f"--mock-file={FIXTURES / fixture}"]
+    cp = run_daemon(binary, "--oneshot", f"--mig-strategy={strategy}", f"--fail-on-init-error={str(fail_on_init).lower()}",
+                    *args)
+    assert (cp.returncode != 0) == expect_error, cp.stderr
+    if error_on_init and not fail_on_init:
+        assert "Warning: failed to initialize resource manager" in cp.stderr
+        assert "Warning: no labels generated from any source" in cp.stderr
+
+
+def test_init_error_message(binary, tmp_path):
+    out = tmp_path / "gfd"
+    args = _base(tmp_path, out)[:-1] + [f"--mock-file={FIXTURES / 'init-error.yaml'}"]
+    cp = run_daemon(binary, "--oneshot", *args)
+    assert cp.returncode == 1
+    assert "Error: error creating device labeler: failed to initialize resource manager: manager.Init error" in cp.stderr
+
+
+def test_env_vars_and_precedence(binary, tmp_path):
+    out = tmp_path / "gfd"
+    args = _base(tmp_path, out)
+    # Env sets the strategy; CLI wins over env for --no-timestamp.
+    cp = run_daemon(binary, "--oneshot", "--no-timestamp=false", *args[:-1],
+                    f"--mock-file={FIXTURES / 'partitioned-single.yaml'}",
+                    env={"MIG_STRATEGY": "single", "GFD_NO_TIMESTAMP": "true"}, check=True)
+    labels = golden.parse_labels(out.read_text())
+    assert labels["amd.com/partition.strategy"] == "single"
+    assert "amd.com/gfd.timestamp" in labels
+    assert cp.returncode == 0
+
+
+def test_config_file_precedence(binary, tmp_path):
+    out = tmp_path / "gfd"
+    cfg = FIXTURES / "config-v1.yaml"  # oneshot, noTimestamp, single, 4 replicas
+    args = [a for a in _base(tmp_path, out)]
+    run_daemon(binary, f"--config-file={cfg}", *args, check=True)  # oneshot comes from the file
+    labels = golden.parse_labels(out.read_text())
+    assert labels["amd.com/partition.strategy"] == "single"
+    assert "amd.com/gfd.timestamp" not in labels
+    # Time-slicing from the file: replicas 4 and the -SHARED suffix.
+    assert labels["amd.com/gpu.replicas"] == "4"
+    assert labels["amd.com/gpu.product"] == "MOCKMODEL-SHARED"
+    # CLI overrides the file.
+    run_daemon(binary, f"--config-file={cfg}", "--mig-strategy=none", "--no-timestamp=false", *args, check=True)
+    labels = golden.parse_labels(out.read_text())
+    assert "amd.com/partition.strategy" not in labels
+    assert "amd.com/gfd.timestamp" in labels
+
+
+def test_config_file_from_env_and_bad_file(binary, tmp_path):
+    out = tmp_path / "gfd"
+    cp = run_daemon(binary, *_base(tmp_path, out), env={"CONFIG_FILE": str(FIXTURES / "config-v1.yaml")}, check=True)
+    assert '"migStrategy": "single"' in cp.stderr  # "Running with config" dump
+    cp = run_daemon(binary, "--oneshot", "--config-file=/nonexistent.yaml", *_base(tmp_path, out))
+    assert cp.returncode == 1
+    assert "unable to load config" in cp.stderr
+
+
+def test_config_renaming_is_disabled(binary, tmp_path):
+    cfg = tmp_path / "c.yaml"
+    cfg.write_text("version: v1\nresources:\n  gpus:\n  - pattern: '*'\n    name: custom\nsharing:\n  timeSlicing:\n"
+                   "    resources:\n    - name: gpu\n      rename: mine\n      devices: [0]\n      replicas: 2\n")
+    out = tmp_path / "gfd"
+    cp = run_daemon(binary, "--oneshot", f"--config-file={cfg}", *_base(tmp_path, out), check=True)
+    assert "Customizing the 'resources' field is not yet supported" in cp.stderr
+    assert "Setting the 'rename' field in sharing.timeSlicing.resources is not yet supported" in cp.stderr
+    assert "Customizing the 'devices' field in sharing.timeSlicing.resources is not yet supported" in cp.stderr
+    labels = golden.parse_labels(out.read_text())
+    # Rename dropped -> the shared product gets the -SHARED suffix.
+    assert labels["amd.com/gpu.product"] == "MOCKMODEL-SHARED"
+    assert labels["amd.com/gpu.replicas"] == "2"
+
+
+def test_help_version_and_usage_errors(binary):
+    cp = run_daemon(binary, "--help")
+    assert cp.returncode == 0 and "GLOBAL OPTIONS" in cp.stdout and "--mig-strategy value" in cp.stdout
+    cp = run_daemon(binary, "--version")
+    assert cp.returncode == 0 and cp.stdout.startswith("GPU Feature Discovery version v")
+    cp = run_daemon(binary, "--bogus")
+    assert cp.returncode == 1 and "flag provided but not defined: -bogus" in cp.stderr
+    cp = run_daemon(binary, "--sleep-interval=soon")
+    assert cp.returncode == 1
+    cp = run_daemon(binary, "--oneshot", env={"GFD_ONESHOT": "perhaps"})
+    assert cp.returncode == 1 and "could not parse" in cp.stderr
+
+
+def test_machine_type_missing_is_unknown(binary, tmp_path):
+    out = tmp_path / "gfd"
+    args = [a for a in _base(tmp_path, out) if not a.startswith("--machine-type-file")]
+    cp = run_daemon(binary, "--oneshot", "--machine-type-file=/nonexistent/dmi", *args, check=True)
+    assert golden.parse_labels(out.read_text())["amd.com/gpu.machine"] == "unknown"
+    assert "WARNING: error getting machine type from /nonexistent/dmi" in cp.stderr
+
+
+def test_trace_timing_logs_phases(binary, tmp_path):
+    out = tmp_path / "gfd"
+    cp = run_daemon(binary, "--oneshot", "--trace-timing", *_base(tmp_path, out), check=True)
+    line = [ln for ln in cp.stderr.splitlines() if "Timing:" in ln][0]
+    for phase in ("init=", "enumerate=", "label=", "sriov(overlapped)=", "write=", "total="):
+        assert phase in line
+
+
+def test_write_failure_is_an_error(binary, tmp_path):
+    ro = tmp_path / "ro"
+    ro.mkdir()
+    ro.chmod(0o500)
+    try:
+        if os.access(ro, os.W_OK):
+            pytest.skip("running as a user that can write anywhere")
+        cp = run_daemon(binary, "--oneshot", *_base(tmp_path, ro / "gfd"))
+        assert cp.returncode == 1 and "error writing file" in cp.stderr
+    finally:
+        ro.chmod(0o700)

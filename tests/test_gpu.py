@@ -1,0 +1,154 @@
+"""Real-hardware tests (MI355X).  Run with ``pytest -m gpu`` on the GPU box.
+
+BASELINE.json configs 2-3: the amd-smi backend on real MI355X GPUs, full-GPU
+amd.com/* labels, per-GPU count/memory/xGMI labels.  Every test drives the
+native core (the _gfd extension or the daemon binary) - there is no Python
+fallback.  The amd-smi and KFD-sysfs backends are cross-checked against
+each other on the same node.
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import REPO, TESTS, has_amd_gpu, run_daemon
+from gpu_feature_discovery_amd import golden
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not has_amd_gpu(), reason="no /dev/kfd")]
+
+
+@pytest.fixture(scope="module")
+def amdsmi_devices(native):
+    return native.Session(["--backend=amdsmi"]).devices()
+
+
+@pytest.fixture(scope="module")
+def sysfs_devices(native):
+    return native.Session(["--backend=sysfs"]).devices()
+
+
+def test_amdsmi_enumerates_mi355x(amdsmi_devices):
+    assert amdsmi_devices, "amd-smi reported no GPU"
+    for d in amdsmi_devices:
+        assert d["gfx"] == "gfx950", d
+        assert "MI355" in d["name"], d
+        assert d["compute_units"] == 256, d
+        assert d["xcds"] == 8, d
+        assert 280 * 1024 <= d["memory_mib"] <= 300 * 1024, d  # 288 GB HBM3E
+        assert d["compute_partition"] in ("SPX", "DPX", "QPX", "CPX"), d
+        assert d["memory_partition"] in ("NPS1", "NPS2", "NPS4", "NPS8"), d
+        assert 0 <= d["xgmi_links"] <= 7, d
+        assert d["virtualization"] in ("baremetal", "host", "guest", "passthrough"), d
+        assert d["vendor_id"] == 0x1002
+        if d["compute_partition"] == "SPX":
+            assert not d["partitioned"] and d["partitions"] == []
+        else:
+            assert d["partitioned"] and d["partitions"], d
+
+
+def test_sysfs_backend_agrees_with_amdsmi(amdsmi_devices, sysfs_devices):
+    assert len(sysfs_devices) == len(amdsmi_devices)
+    keys = ("name", "bdf", "gfx", "compute_units", "xcds", "memory_mib", "compute_partition", "memory_partition",
+            "partitioned", "partition_capable")
+    for a, s in zip(amdsmi_devices, sysfs_devices):
+        assert {k: a[k] for k in keys} == {k: s[k] for k in keys}
+
+
+def test_label_sets_identical_across_backends(native, tmp_path):
+    common = ["--oneshot", "--no-timestamp", "--output-file="]
+    a = native.Session(["--backend=amdsmi", *common]).cycle(False)["labels"]
+    s = native.Session(["--backend=sysfs", *common]).cycle(False)["labels"]
+    a.pop("amd.com/gpu.xgmi.links", None), s.pop("amd.com/gpu.xgmi.links", None)  # live link state vs topology
+    a.pop("amd.com/gpu.virtualization-mode", None), s.pop("amd.com/gpu.virtualization-mode", None)
+    assert a == s
+
+
+def test_daemon_oneshot_matches_regex_golden(binary, tmp_path):
+    out = tmp_path / "gfd"
+    cp = run_daemon(binary, "--oneshot", f"--output-file={out}", "--trace-timing", check=True, timeout=120)
+    assert "Detected amd-smi platform" in cp.stderr
+    text = out.read_text()
+    golden.check_regex_golden(text, TESTS / "expected-output.txt", select=lambda ln: "sriov" not in ln)
+    labels = golden.parse_labels(text)
+    assert labels["amd.com/gpu.arch"] == "gfx950"
+    assert labels["amd.com/gpu.family"] == "cdna4"
+    assert labels["amd.com/gpu.compute-units"] == "256"
+
+
+def test_daemon_sysfs_backend_oneshot(binary, tmp_path):
+    out = tmp_path / "gfd"
+    run_daemon(binary, "--oneshot", "--backend=sysfs", f"--output-file={out}", check=True, timeout=60)
+    golden.check_regex_golden(out.read_text(), TESTS / "expected-output.txt", select=lambda ln: "sriov" not in ln)
+
+
+def test_persistent_session_initialises_once(native):
+    s = native.Session(["--backend=amdsmi", "--output-file="])
+    phases = [dict(s.cycle(False)["phases"]) for _ in range(5)]
+    assert "amdsmi_init" in phases[0]
+    assert all("amdsmi_init" not in p for p in phases[1:])
+
+
+def test_per_cycle_session_reinitialises(native):
+    s = native.Session(["--backend=amdsmi", "--amdsmi-session=per-cycle", "--output-file="])
+    phases = [dict(s.cycle(False)["phases"]) for _ in range(3)]
+    assert all("amdsmi_init" in p for p in phases)
+    labels = [s.cycle(False)["labels"] for _ in range(2)]
+    labels[0].pop("amd.com/gfd.timestamp"), labels[1].pop("amd.com/gfd.timestamp")
+    assert labels[0] == labels[1]
+
+
+def test_visible_devices_filter(native, amdsmi_devices):
+    bdf = amdsmi_devices[0]["bdf"]
+    only = native.Session(["--backend=amdsmi", f"--visible-devices={bdf}"]).devices()
+    assert [d["bdf"] for d in only] == [bdf]
+    none = native.Session(["--backend=amdsmi", "--visible-devices=63"]).devices()
+    assert none == []
+
+
+def test_real_pci_scan_succeeds(native):
+    r = native.Session(["--backend=sysfs", "--output-file="]).cycle(False)
+    assert "sriov(overlapped)" in dict(r["phases"])
+    sriov = {k: v for k, v in r["labels"].items() if "sriov" in k}
+    if sriov:
+        golden.check_regex_golden("".join(f"{k}={v}\n" for k, v in sorted(sriov.items())),
+                                  TESTS / "expected-output-sriov.txt")
+
+
+def test_product_name_survives_torch_libdrm(tmp_path):
+    """PyTorch ships a libdrm whose amdgpu.ids path does not exist; with it
+    loaded first, amd-smi's market name degrades to "AMD Radeon Graphics".
+    The backend must still report the board's product name."""
+    code = (
+        "import sys; sys.path.insert(0, %r)\n"
+        "import torch\n"
+        "torch.cuda.is_available()\n"
+        "import gpu_feature_discovery_amd as g\n"
+        "print(g.native().Session(['--backend=amdsmi']).devices()[0]['name'])\n" % str(REPO)
+    )
+    cp = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=600)
+    assert cp.returncode == 0, cp.stderr[-2000:]
+    assert "MI355" in cp.stdout.strip().splitlines()[-1]
+
+
+def test_bench_contract_on_gpu(tmp_path):
+    cp = subprocess.run([sys.executable, str(REPO / "bench.py"), "--steps", "20", "--warmup", "2", "--no-extras"],
+                        capture_output=True, text=True, timeout=600, cwd=str(REPO))
+    assert cp.returncode == 0, cp.stderr[-2000:]
+    line = [ln for ln in cp.stdout.splitlines() if ln.startswith("{")][-1]
+    r = json.loads(line)
+    assert r["labels_ok"] is True, r
+    assert r["config"]["backend"].startswith("amdsmi")
+    assert r["higher_is_better"] is False and r["unit"] == "ms"
+    assert r["value"] > 0 and r["n_gpus"] == 1
+
+
+def test_smoke_entry_point():
+    cp = subprocess.run([sys.executable, "-c", "import __graft_entry__ as g; g.smoke()"], capture_output=True, text=True,
+                        timeout=300, cwd=str(REPO), env={**os.environ})
+    assert cp.returncode == 0, cp.stderr[-2000:]
+    assert "smoke:" in cp.stdout

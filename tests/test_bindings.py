@@ -1,0 +1,92 @@
+"""Python-extension tests: the in-process API over the native core
+(YAML/config parsing, durations, resource names, sessions over synthetic
+trees).  Everything here runs the C++ code in gpu_feature_discovery_amd/_gfd."""
+
+from __future__ import annotations
+
+import pytest
+
+from gpu_feature_discovery_amd import golden, synth
+
+
+def test_native_module_is_the_in_tree_extension(native):
+    import gpu_feature_discovery_amd as gfd
+
+    assert native.__file__.startswith(str(gfd.PACKAGE_DIR))
+    assert native.version().startswith("v")
+
+
+def test_parse_yaml_and_json(native):
+    assert native.parse_yaml("a: [1, {b: yes}]\nc: 'x'\n") == {"a": [1, {"b": True}], "c": "x"}
+    assert native.parse_yaml('{"a": 1.5, "b": null}') == {"a": 1.5, "b": None}
+    with pytest.raises(native.GfdError):
+        native.parse_yaml("a: [1\n")
+
+
+def test_parse_config_roundtrip(native):
+    js = native.parse_config("flags:\n  migStrategy: mixed\n  gfd:\n    sleepInterval: 2m\n")
+    assert '"migStrategy": "mixed"' in js and '"sleepInterval": "2m0s"' in js
+    with pytest.raises(native.GfdError, match="unknown version"):
+        native.parse_config("version: v9\n")
+
+
+@pytest.mark.parametrize("text,ns", [("1h2m3s", 3723 * 10**9), ("250ms", 250 * 10**6), ("0", 0), ("1.5us", 1500)])
+def test_durations(native, text, ns):
+    assert native.parse_duration(text) == ns
+
+
+def test_format_duration(native):
+    assert native.format_duration(60 * 10**9) == "1m0s"
+
+
+def test_resource_names(native):
+    assert native.new_resource_name("partition-cpx.1xcd.36gb") == "amd.com/partition-cpx.1xcd.36gb"
+    with pytest.raises(native.GfdError):
+        native.new_resource_name("UPPER")
+
+
+def test_sanitize_label_value(native):
+    assert native.sanitize_label_value("AMD Instinct MI355X") == "AMD-Instinct-MI355X"
+
+
+def test_session_over_synthetic_tree(native, tmp_path):
+    root = synth.make_mi355x_node(tmp_path / "root", n_gpus=4, compute_partition="QPX", seed=11)
+    s = native.Session(["--backend=sysfs", f"--sysfs-root={root}", "--mig-strategy=mixed", "--no-timestamp",
+                        f"--output-file={tmp_path / 'gfd'}"])
+    assert s.backend == "sysfs"
+    devs = s.devices()
+    assert len(devs) == 4 and all(d["partitioned"] for d in devs)
+    assert all(len(d["partitions"]) == 4 for d in devs)
+    assert devs[0]["partitions"][0]["name"] == "qpx.2xcd.72gb"
+    r = s.cycle(True)
+    assert (tmp_path / "gfd").read_text() == r["rendered"]
+    labels = golden.parse_labels(r["rendered"])
+    assert labels["amd.com/partition-qpx.2xcd.72gb.count"] == "16"
+    assert labels["amd.com/partition-qpx.2xcd.72gb.compute-units"] == "64"
+
+
+def test_session_bench_returns_per_step_times(native, tmp_path):
+    root = synth.make_mi355x_node(tmp_path / "root", n_gpus=2)
+    s = native.Session(["--backend=sysfs", f"--sysfs-root={root}", f"--output-file={tmp_path / 'gfd'}"])
+    ns = s.bench(25, 5, True)
+    assert len(ns) == 25 and all(x > 0 for x in ns)
+
+
+def test_session_env_precedence(native, tmp_path):
+    root = synth.make_mi355x_node(tmp_path / "root", n_gpus=1)
+    s = native.Session([f"--sysfs-root={root}", "--output-file="],
+                       env={"GFD_BACKEND": "sysfs", "GFD_MIG_STRATEGY": "single", "GFD_NO_TIMESTAMP": "1"})
+    labels = s.cycle(False)["labels"]
+    assert labels["amd.com/partition.strategy"] == "single"
+    assert "amd.com/gfd.timestamp" not in labels
+
+
+def test_session_usage_error(native):
+    with pytest.raises(native.UsageError, match="flag provided but not defined"):
+        native.Session(["--nope"])
+
+
+def test_session_errors_surface(native, tmp_path):
+    s = native.Session(["--backend=sysfs", f"--sysfs-root={tmp_path}", "--output-file="])
+    with pytest.raises(native.GfdError, match="KFD topology not available"):
+        s.cycle(False)

@@ -1,0 +1,68 @@
+# Build / test / package entry points (reference analogue: Makefile:52-144).
+include versions.mk
+
+BUILD_DIR ?= build
+JOBS ?= $(shell nproc 2>/dev/null || echo 8)
+PYTHON ?= python3
+
+.PHONY: all build cmds test test-unit test-gpu coverage asan tsan bench fmt assert-fmt lint check-yamls image clean
+
+all: build
+
+# Native daemon, C++ unit tests and the Python extension (in-tree).
+build:
+	cmake -S . -B $(BUILD_DIR) -G Ninja -DCMAKE_BUILD_TYPE=Release -DPython3_EXECUTABLE=$$(command -v $(PYTHON))
+	cmake --build $(BUILD_DIR) -j $(JOBS)
+
+cmds: build
+
+# CPU test-suite (what CI runs): C++ unit tests + goldens + daemon + bench contract.
+test: build
+	$(PYTHON) -m pytest tests -q -m "not gpu"
+
+test-unit: build
+	./$(BUILD_DIR)/gfd_unit_tests
+
+# Real-hardware tests (MI355X): run on a GPU node.
+test-gpu: build
+	$(PYTHON) -m pytest tests -q -m gpu
+
+# Sanitizer builds of the host code on the mock/synthetic backends (the
+# reference runs `go test` without -race).
+asan:
+	cmake -S . -B build-asan -G Ninja -DCMAKE_BUILD_TYPE=Debug -DGFD_SANITIZE=address,undefined -DGFD_BUILD_PYTHON=OFF
+	cmake --build build-asan -j $(JOBS)
+	ASAN_OPTIONS=detect_leaks=1 UBSAN_OPTIONS=halt_on_error=1 ./build-asan/gfd_unit_tests
+
+tsan:
+	cmake -S . -B build-tsan -G Ninja -DCMAKE_BUILD_TYPE=Debug -DGFD_SANITIZE=thread -DGFD_BUILD_PYTHON=OFF
+	cmake --build build-tsan -j $(JOBS)
+	TSAN_OPTIONS=halt_on_error=1 ./build-tsan/gfd_unit_tests
+
+coverage:
+	cmake -S . -B build-cov -G Ninja -DCMAKE_BUILD_TYPE=Debug -DGFD_BUILD_PYTHON=OFF \
+	  -DCMAKE_CXX_FLAGS="--coverage" -DCMAKE_EXE_LINKER_FLAGS="--coverage"
+	cmake --build build-cov -j $(JOBS)
+	./build-cov/gfd_unit_tests
+	gcov -o build-cov/CMakeFiles/gfdcore.dir/src -r src/*/*.cpp > /dev/null 2>&1 || true
+
+bench: build
+	$(PYTHON) bench.py
+
+fmt:
+	find src tests/unit python -name '*.cpp' -o -name '*.h' | xargs clang-format -i
+
+assert-fmt:
+	find src tests/unit python -name '*.cpp' -o -name '*.h' | xargs clang-format --dry-run --Werror
+
+lint:
+	$(PYTHON) -m pyflakes gpu_feature_discovery_amd tests bench.py __graft_entry__.py
+
+check-yamls:
+	$(PYTHON) -m pytest tests/test_deployments.py -q
+
+image:
+	$(MAKE) -C deployments/container image VERSION=$(VERSION) IMAGE_NAME=$(IMAGE_NAME)
+
+clean:
+	rm -rf $(BUILD_DIR) build-asan build-tsan build-cov gpu_feature_discovery_amd/_gfd*.so

@@ -1,0 +1,103 @@
+"""Packaging checks (reference analogue: tests/check-yamls.sh and the
+static/Helm manifests under deployments/).  Every manifest is parsed with the
+daemon's own YAML reader; image tags and version labels must match
+versions.mk, env var names must be flags the daemon understands, and the
+Helm templates may only reference values that exist."""
+
+from __future__ import annotations
+
+import re
+from pathlib import Path
+
+import pytest
+
+from conftest import REPO
+
+DEPLOY = REPO / "deployments"
+STATIC = DEPLOY / "static"
+CHART = DEPLOY / "helm" / "gpu-feature-discovery-amd"
+
+
+def _version() -> str:
+    m = re.search(r"^VERSION \?= (v[0-9.]+)", (REPO / "versions.mk").read_text(), re.M)
+    assert m
+    return m.group(1)
+
+
+def _docs(native, path: Path) -> list:
+    text = path.read_text()
+    return [native.parse_yaml(d) for d in re.split(r"^---\s*$", text, flags=re.M) if d.strip()]
+
+
+def _env_vars(native) -> set[str]:
+    help_text = __import__("subprocess").run([str(REPO / "build" / "gpu-feature-discovery"), "--help"],
+                                             capture_output=True, text=True).stdout
+    return set(re.findall(r"\$([A-Z_]+)", help_text))
+
+
+@pytest.mark.parametrize("name,strategy", [
+    ("gpu-feature-discovery-daemonset.yaml", "none"),
+    ("gpu-feature-discovery-daemonset-with-partition-single.yaml", "single"),
+    ("gpu-feature-discovery-daemonset-with-partition-mixed.yaml", "mixed"),
+])
+def test_static_daemonsets(native, name, strategy):
+    (ds,) = _docs(native, STATIC / name)
+    assert ds["kind"] == "DaemonSet"
+    v = _version()
+    assert ds["metadata"]["labels"]["app.kubernetes.io/version"] == v.lstrip("v")
+    spec = ds["spec"]["template"]["spec"]
+    (c,) = spec["containers"]
+    assert c["image"].endswith(":" + v)
+    env = {e["name"]: e["value"] for e in c["env"]}
+    assert env["GFD_MIG_STRATEGY"] == strategy
+    assert set(env) <= _env_vars(native)
+    mounts = {m["mountPath"] for m in c["volumeMounts"]}
+    assert {"/etc/kubernetes/node-feature-discovery/features.d", "/sys"} <= mounts
+    terms = spec["affinity"]["nodeAffinity"]["requiredDuringSchedulingIgnoredDuringExecution"]["nodeSelectorTerms"]
+    keys = {e["key"] for t in terms for e in t["matchExpressions"]}
+    assert "feature.node.kubernetes.io/pci-1002.present" in keys
+
+
+def test_job_template(native):
+    (job,) = _docs(native, STATIC / "gpu-feature-discovery-job.yaml.template")
+    spec = job["spec"]["template"]["spec"]
+    assert spec["nodeName"] == "NODE_NAME"
+    assert spec["restartPolicy"] == "Never"
+    assert "--oneshot" in spec["containers"][0]["args"]
+    assert spec["containers"][0]["image"].endswith(":" + _version())
+
+
+def test_nfd_manifest(native):
+    docs = _docs(native, STATIC / "nfd.yaml")
+    kinds = [d["kind"] for d in docs]
+    assert {"Namespace", "Deployment", "DaemonSet", "ConfigMap"} <= set(kinds)
+    master = next(d for d in docs if d["kind"] == "Deployment")
+    assert "-extra-label-ns=amd.com" in master["spec"]["template"]["spec"]["containers"][0]["args"]
+    cm = next(d for d in docs if d["kind"] == "ConfigMap")
+    conf = native.parse_yaml(cm["data"]["nfd-worker.conf"])
+    assert "12" in conf["sources"]["pci"]["deviceClassWhitelist"]
+
+
+def test_helm_chart(native):
+    chart = native.parse_yaml((CHART / "Chart.yaml").read_text())
+    assert "v" + chart["appVersion"] == _version()
+    values = native.parse_yaml((CHART / "values.yaml").read_text())
+    assert values["migStrategy"] in ("none", "single", "mixed")
+    assert values["nfd"]["master"]["extraLabelNs"] == ["amd.com"]
+    referenced = set()
+    for t in (CHART / "templates").iterdir():
+        referenced |= set(re.findall(r"\.Values\.([A-Za-z]+)", t.read_text()))
+    missing = referenced - set(values) - {"namespace"}  # validation.yml rejects `namespace`
+    assert not missing, missing
+
+
+def test_helm_env_names_are_daemon_flags(native):
+    text = (CHART / "templates" / "daemonset.yml").read_text()
+    names = set(re.findall(r"name: (GFD_[A-Z_]+)", text))
+    assert names and names <= _env_vars(native)
+
+
+def test_dockerfile(native):
+    text = (DEPLOY / "container" / "Dockerfile").read_text()
+    assert 'ENTRYPOINT ["/usr/bin/gpu-feature-discovery"]' in text
+    assert "gfd_unit_tests" in text  # the build stage runs the unit tests

@@ -1,0 +1,64 @@
+// WorkerPool tests (run under TSan by `make tsan`).
+#include <atomic>
+#include <stdexcept>
+
+#include "test.h"
+#include "util/pool.h"
+
+using gfd::WorkerPool;
+
+TEST(Pool_ParallelForVisitsEveryIndexOnce) {
+  WorkerPool pool(4);
+  std::vector<std::atomic<int>> hits(1000);
+  pool.parallel_for(hits.size(), [&](size_t i) { hits[i]++; });
+  for (auto& h : hits) EXPECT_EQ(h.load(), 1);
+  EXPECT_TRUE(pool.workers() <= 4);
+}
+
+TEST(Pool_ParallelForPropagatesFirstError) {
+  WorkerPool pool(3);
+  std::atomic<int> ran{0};
+  EXPECT_THROW_MSG(pool.parallel_for(50,
+                                     [&](size_t i) {
+                                       ran++;
+                                       if (i == 7) throw std::runtime_error("boom at 7");
+                                     }),
+                   "boom at 7");
+  EXPECT_TRUE(ran.load() >= 1);
+}
+
+TEST(Pool_SubmitAndWait) {
+  WorkerPool pool(2);
+  int value = 0;
+  auto t = pool.submit([&] { value = 42; });
+  t.wait();
+  EXPECT_EQ(value, 42);
+  auto bad = pool.submit([] { throw std::runtime_error("task failed"); });
+  EXPECT_THROW_MSG(bad.wait(), "task failed");
+}
+
+TEST(Pool_SerialWhenLimited) {
+  WorkerPool pool(8);
+  std::atomic<int> concurrent{0}, peak{0};
+  pool.parallel_for(
+      20,
+      [&](size_t) {
+        int c = ++concurrent;
+        int p = peak.load();
+        while (c > p && !peak.compare_exchange_weak(p, c)) {
+        }
+        --concurrent;
+      },
+      1);
+  EXPECT_EQ(peak.load(), 1);
+}
+
+TEST(Pool_ManyRoundsReuseWorkers) {
+  WorkerPool pool(4);
+  for (int r = 0; r < 200; ++r) {
+    std::atomic<int> sum{0};
+    pool.parallel_for(8, [&](size_t i) { sum += static_cast<int>(i); });
+    EXPECT_EQ(sum.load(), 28);
+  }
+  EXPECT_TRUE(pool.workers() <= 4);
+}

@@ -82,6 +82,13 @@ class _Dist:
         if self.dist is not None:
             self.dist.barrier()
         if self.torch is not None and self.torch.cuda.is_available():
+            # One rank per GPU: bind before the first synchronize so the N
+            # ranks do not all create contexts on device 0.
+            if not getattr(self, "_bound", False):
+                n = self.torch.cuda.device_count()
+                if n:
+                    self.torch.cuda.set_device(_env_int("LOCAL_RANK", self.rank) % n)
+                self._bound = True
             self.torch.cuda.synchronize()
 
     def max(self, v: float) -> float:

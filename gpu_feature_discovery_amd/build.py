@@ -40,7 +40,8 @@ def build(build_type: str = "Release", extra_cmake_args: list[str] | None = None
 
 def is_built() -> bool:
     from . import BINARY, PACKAGE_DIR, UNIT_TEST_BINARY
-    return BINARY.exists() and UNIT_TEST_BINARY.exists() and any(PACKAGE_DIR.glob("_gfd*.so"))
+    return (BINARY.exists() and UNIT_TEST_BINARY.exists() and (BUILD_DIR / "libfake_amdsmi.so").exists()
+            and any(PACKAGE_DIR.glob("_gfd*.so")))
 
 
 if __name__ == "__main__":

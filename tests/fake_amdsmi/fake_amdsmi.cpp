@@ -1,0 +1,347 @@
+// A scriptable stand-in for libamd_smi, used to test the amd-smi backend on
+// machines without an AMD GPU.  Loaded through GFD_AMDSMI_LIBRARY.
+//
+// The node is described by fake_amdsmi_configure(spec), one GPU per line:
+//   bdf=0000:23:00.0;mode=CPX;parts=8;name=AMD Instinct MI355 OAM;cus=32;xcds=1;vram_mib=36862;links=7;virt=1
+// plus optional global lines:
+//   init_status=34            amdsmi_init returns this status
+//   stale_after=N             after N successful queries, queries return NOT_INIT until re-init
+// Counters are exposed for assertions (fake_amdsmi_init_calls, ...).
+#include <amd_smi/amdsmi.h>
+
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <vector>
+
+namespace {
+
+struct Proc {
+  std::string bdf;
+  uint64_t domain = 0;
+  uint32_t bus = 0, dev = 0, fn = 0;
+  std::string mode = "SPX";
+  std::string nps = "NPS1";
+  uint32_t partition_id = 0;
+  std::string name = "AMD Instinct MI355 OAM";
+  std::string board_name = "AMD Instinct MI355 OAM";
+  uint32_t cus = 256;
+  uint32_t xcds = 8;
+  uint64_t vram = 309220868096ULL;
+  int links = 7;
+  int virt = AMDSMI_VIRTUALIZATION_MODE_BAREMETAL;
+};
+
+struct State {
+  std::mutex mu;
+  std::vector<Proc> procs;
+  int init_status = 0;
+  long stale_after = -1;
+  long queries = 0;
+  bool initialized = false;
+  bool stale = false;
+  int init_calls = 0;
+  int shutdown_calls = 0;
+};
+
+State& S() {
+  static State s;
+  return s;
+}
+
+bool parse_bdf(const std::string& s, Proc& p) {
+  unsigned long d = 0;
+  unsigned b = 0, dv = 0, f = 0;
+  if (sscanf(s.c_str(), "%lx:%x:%x.%x", &d, &b, &dv, &f) != 4) return false;
+  p.domain = d;
+  p.bus = b;
+  p.dev = dv;
+  p.fn = f;
+  return true;
+}
+
+Proc* proc(amdsmi_processor_handle h) {
+  auto& s = S();
+  uintptr_t i = reinterpret_cast<uintptr_t>(h);
+  if (i == 0 || i > s.procs.size()) return nullptr;
+  return &s.procs[i - 1];
+}
+
+amdsmi_status_t check(amdsmi_processor_handle h, Proc** out) {
+  auto& s = S();
+  std::lock_guard<std::mutex> g(s.mu);  // like amd-smi's per-device mutexes
+  if (!s.initialized) return AMDSMI_STATUS_NOT_INIT;
+  if (s.stale) return AMDSMI_STATUS_NOT_INIT;
+  if (s.stale_after >= 0 && ++s.queries > s.stale_after) {
+    s.stale = true;
+    return AMDSMI_STATUS_NOT_INIT;
+  }
+  *out = proc(h);
+  return *out ? AMDSMI_STATUS_SUCCESS : AMDSMI_STATUS_INVAL;
+}
+
+void copy(char* dst, size_t n, const std::string& src) {
+  std::strncpy(dst, src.c_str(), n - 1);
+  dst[n - 1] = 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+// ---- control API ----
+int fake_amdsmi_configure(const char* spec) {
+  auto& s = S();
+  std::lock_guard<std::mutex> g(s.mu);
+  s.procs.clear();
+  s.init_status = 0;
+  s.stale_after = -1;
+  s.queries = 0;
+  s.stale = false;
+  std::istringstream in(spec);
+  std::string line;
+  while (std::getline(in, line)) {
+    if (line.empty()) continue;
+    if (line.rfind("init_status=", 0) == 0) {
+      s.init_status = std::atoi(line.c_str() + 12);
+      continue;
+    }
+    if (line.rfind("stale_after=", 0) == 0) {
+      s.stale_after = std::atol(line.c_str() + 12);
+      continue;
+    }
+    Proc base;
+    int parts = 1;
+    // key=value pairs separated by ';' (values may contain spaces).
+    std::vector<std::pair<std::string, std::string>> kv;
+    std::istringstream fields(line);
+    std::string field;
+    while (std::getline(fields, field, ';')) {
+      size_t eq = field.find('=');
+      if (eq != std::string::npos) kv.emplace_back(field.substr(0, eq), field.substr(eq + 1));
+    }
+    for (auto& [k, v] : kv) {
+      if (k == "bdf") {
+        base.bdf = v;
+        if (!parse_bdf(v, base)) return -1;
+      } else if (k == "mode") base.mode = v;
+      else if (k == "nps") base.nps = v;
+      else if (k == "parts") parts = std::atoi(v.c_str());
+      else if (k == "name") base.name = v;
+      else if (k == "board") base.board_name = v;
+      else if (k == "cus") base.cus = static_cast<uint32_t>(std::atoi(v.c_str()));
+      else if (k == "xcds") base.xcds = static_cast<uint32_t>(std::atoi(v.c_str()));
+      else if (k == "vram_mib") base.vram = std::strtoull(v.c_str(), nullptr, 10) << 20;
+      else if (k == "links") base.links = std::atoi(v.c_str());
+      else if (k == "virt") base.virt = std::atoi(v.c_str());
+    }
+    // Enumerate partitions in reverse to prove the backend orders them.
+    for (int p = parts - 1; p >= 0; --p) {
+      Proc q = base;
+      q.partition_id = static_cast<uint32_t>(p);
+      s.procs.push_back(q);
+    }
+  }
+  return 0;
+}
+int fake_amdsmi_init_calls() { return S().init_calls; }
+int fake_amdsmi_shutdown_calls() { return S().shutdown_calls; }
+int fake_amdsmi_initialized() { return S().initialized ? 1 : 0; }
+
+// ---- amd-smi API subset ----
+amdsmi_status_t amdsmi_init(uint64_t) {
+  auto& s = S();
+  std::lock_guard<std::mutex> g(s.mu);
+  s.init_calls++;
+  if (s.init_status) return static_cast<amdsmi_status_t>(s.init_status);
+  s.initialized = true;
+  if (s.stale) s.stale_after = -1;  // handles go stale once; a re-init fixes them
+  s.stale = false;
+  s.queries = 0;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_shut_down(void) {
+  auto& s = S();
+  std::lock_guard<std::mutex> g(s.mu);
+  s.shutdown_calls++;
+  s.initialized = false;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_status_code_to_string(amdsmi_status_t status, const char** str) {
+  switch (status) {
+    case AMDSMI_STATUS_NOT_INIT: *str = "AMDSMI_STATUS_NOT_INIT: Processor not initialized"; break;
+    case AMDSMI_STATUS_DRIVER_NOT_LOADED: *str = "AMDSMI_STATUS_DRIVER_NOT_LOADED: Processor driver not loaded."; break;
+    default: *str = "AMDSMI_STATUS_FAKE";
+  }
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_socket_handles(uint32_t* count, amdsmi_socket_handle* handles) {
+  auto& s = S();
+  if (!s.initialized) return AMDSMI_STATUS_NOT_INIT;
+  if (handles && *count >= 1) handles[0] = reinterpret_cast<amdsmi_socket_handle>(1);
+  *count = 1;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_processor_handles(amdsmi_socket_handle, uint32_t* count, amdsmi_processor_handle* handles) {
+  auto& s = S();
+  if (!s.initialized) return AMDSMI_STATUS_NOT_INIT;
+  uint32_t n = static_cast<uint32_t>(s.procs.size());
+  if (handles)
+    for (uint32_t i = 0; i < n && i < *count; ++i) handles[i] = reinterpret_cast<amdsmi_processor_handle>(uintptr_t(i + 1));
+  *count = n;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_processor_type(amdsmi_processor_handle h, processor_type_t* t) {
+  Proc* p;
+  if (auto st = check(h, &p)) return st;
+  *t = AMDSMI_PROCESSOR_TYPE_AMD_GPU;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_device_bdf(amdsmi_processor_handle h, amdsmi_bdf_t* b) {
+  Proc* p;
+  if (auto st = check(h, &p)) return st;
+  std::memset(b, 0, sizeof(*b));
+  b->domain_number = p->domain;
+  b->bus_number = p->bus;
+  b->device_number = p->dev;
+  b->function_number = p->fn;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_asic_info(amdsmi_processor_handle h, amdsmi_asic_info_t* a) {
+  Proc* p;
+  if (auto st = check(h, &p)) return st;
+  std::memset(a, 0, sizeof(*a));
+  copy(a->market_name, sizeof(a->market_name), p->name);
+  a->vendor_id = 0x1002;
+  a->device_id = 0x75a3;
+  a->num_of_compute_units = p->cus;
+  a->target_graphics_version = 0x950;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_board_info(amdsmi_processor_handle h, amdsmi_board_info_t* b) {
+  Proc* p;
+  if (auto st = check(h, &p)) return st;
+  std::memset(b, 0, sizeof(*b));
+  copy(b->product_name, sizeof(b->product_name), p->board_name);
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_memory_total(amdsmi_processor_handle h, amdsmi_memory_type_t, uint64_t* total) {
+  Proc* p;
+  if (auto st = check(h, &p)) return st;
+  *total = p->vram;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_kfd_info(amdsmi_processor_handle h, amdsmi_kfd_info_t* k) {
+  Proc* p;
+  if (auto st = check(h, &p)) return st;
+  std::memset(k, 0, sizeof(*k));
+  k->kfd_id = 1000;
+  k->node_id = 0xFFFFFFFFu;  // no KFD node: the backend falls back to xcd_counter
+  k->current_partition_id = p->partition_id;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_xcd_counter(amdsmi_processor_handle h, uint16_t* x) {
+  Proc* p;
+  if (auto st = check(h, &p)) return st;
+  *x = static_cast<uint16_t>(p->xcds);
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_compute_partition(amdsmi_processor_handle h, char* buf, uint32_t len) {
+  Proc* p;
+  if (auto st = check(h, &p)) return st;
+  copy(buf, len, p->mode);
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_memory_partition(amdsmi_processor_handle h, char* buf, uint32_t len) {
+  Proc* p;
+  if (auto st = check(h, &p)) return st;
+  copy(buf, len, p->nps);
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_memory_partition_config(amdsmi_processor_handle h, amdsmi_memory_partition_config_t* c) {
+  Proc* p;
+  if (auto st = check(h, &p)) return st;
+  std::memset(c, 0, sizeof(*c));
+  c->partition_caps.nps_cap_mask = 0x3;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_accelerator_partition_profile_config(amdsmi_processor_handle h,
+                                                                     amdsmi_accelerator_partition_profile_config_t* c) {
+  Proc* p;
+  if (auto st = check(h, &p)) return st;
+  std::memset(c, 0, sizeof(*c));
+  c->num_profiles = 4;
+  c->profiles[0].profile_type = AMDSMI_ACCELERATOR_PARTITION_SPX;
+  c->profiles[1].profile_type = AMDSMI_ACCELERATOR_PARTITION_DPX;
+  c->profiles[2].profile_type = AMDSMI_ACCELERATOR_PARTITION_QPX;
+  c->profiles[3].profile_type = AMDSMI_ACCELERATOR_PARTITION_CPX;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_accelerator_partition_profile(amdsmi_processor_handle h,
+                                                             amdsmi_accelerator_partition_profile_t* prof,
+                                                             uint32_t* ids) {
+  Proc* p;
+  if (auto st = check(h, &p)) return st;
+  std::memset(prof, 0, sizeof(*prof));
+  prof->num_partitions = 1;
+  prof->num_resources = AMDSMI_ACCELERATOR_MAX;
+  prof->resources[0][AMDSMI_ACCELERATOR_XCC] = p->xcds;
+  prof->resources[0][AMDSMI_ACCELERATOR_ENCODER] = 0;
+  prof->resources[0][AMDSMI_ACCELERATOR_DECODER] = 1;
+  prof->resources[0][AMDSMI_ACCELERATOR_DMA] = 2;
+  prof->resources[0][AMDSMI_ACCELERATOR_JPEG] = 4;
+  ids[0] = p->partition_id;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_xgmi_link_status(amdsmi_processor_handle h, amdsmi_xgmi_link_status_t* ls) {
+  Proc* p;
+  if (auto st = check(h, &p)) return st;
+  std::memset(ls, 0, sizeof(*ls));
+  ls->total_links = 8;
+  ls->status[0] = AMDSMI_XGMI_LINK_DISABLE;
+  for (int i = 1; i < 8; ++i) ls->status[i] = i <= p->links ? AMDSMI_XGMI_LINK_UP : AMDSMI_XGMI_LINK_DOWN;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_virtualization_mode(amdsmi_processor_handle h, amdsmi_virtualization_mode_t* m) {
+  Proc* p;
+  if (auto st = check(h, &p)) return st;
+  *m = static_cast<amdsmi_virtualization_mode_t>(p->virt);
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_driver_info(amdsmi_processor_handle h, amdsmi_driver_info_t* d) {
+  Proc* p;
+  if (auto st = check(h, &p)) return st;
+  std::memset(d, 0, sizeof(*d));
+  copy(d->driver_version, sizeof(d->driver_version), "6.12.12");
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_lib_version(amdsmi_version_t* v) {
+  std::memset(v, 0, sizeof(*v));
+  v->major = 26;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+}  // extern "C"

@@ -5,6 +5,7 @@ fallback_test.go) plus the native parsers, backends and CLI."""
 
 from __future__ import annotations
 
+import os
 import subprocess
 
 import pytest
@@ -19,10 +20,15 @@ def _names() -> list[str]:
 
 @pytest.fixture(scope="module")
 def results() -> dict[str, str]:
-    cp = subprocess.run([str(gfd.UNIT_TEST_BINARY)], capture_output=True, text=True, timeout=300)
+    env = {k: v for k, v in os.environ.items() if k != "GFD_AMDSMI_LIBRARY"}
+    cp = subprocess.run([str(gfd.UNIT_TEST_BINARY)], capture_output=True, text=True, timeout=300, env=env)
+    return _parse(cp.stdout)
+
+
+def _parse(stdout: str) -> dict[str, str]:
     res: dict[str, str] = {}
     current = None
-    for line in cp.stdout.splitlines():
+    for line in stdout.splitlines():
         if line.startswith("[ OK ] "):
             res[line[7:]] = "ok"
             current = None
@@ -34,7 +40,19 @@ def results() -> dict[str, str]:
     return res
 
 
+@pytest.fixture(scope="module")
+def fake_results() -> dict[str, str]:
+    """The AmdSmiFake_* tests, run against the scriptable libamd_smi."""
+    fake = gfd.BUILD_DIR / "libfake_amdsmi.so"
+    names = [n for n in _names() if n.startswith("AmdSmiFake_")]
+    env = {**os.environ, "GFD_AMDSMI_LIBRARY": str(fake)}
+    cp = subprocess.run([str(gfd.UNIT_TEST_BINARY), *names], capture_output=True, text=True, timeout=300, env=env)
+    return _parse(cp.stdout)
+
+
 @pytest.mark.parametrize("name", _names())
-def test_cpp(name, results):
+def test_cpp(name, results, fake_results):
+    if name.startswith("AmdSmiFake_"):
+        results = fake_results
     assert name in results, f"{name} did not run"
     assert results[name] == "ok", results[name]

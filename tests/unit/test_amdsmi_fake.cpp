@@ -1,0 +1,255 @@
+// amd-smi backend logic against a scriptable fake libamd_smi
+// (tests/fake_amdsmi/fake_amdsmi.cpp).  These tests only run when
+// GFD_AMDSMI_LIBRARY points at libfake_amdsmi.so (tests/test_unit_cpp.py
+// runs them in a separate process); otherwise they return immediately.
+//
+// They cover what the pool cannot exercise on real hardware: compute-
+// partitioned GPUs (CPX regrouping by PCI address, partition ordering),
+// the persistent session's re-initialisation rules, stale handles and the
+// market-name fallback.
+#include <dlfcn.h>
+#include <unistd.h>
+
+#include <cstdlib>
+
+#include "config/config.h"
+#include "lm/resource.h"
+#include "resource/amdsmi.h"
+#include "test.h"
+#include "util/fs.h"
+
+using namespace gfd;
+using namespace gfd::resource;
+
+namespace {
+
+struct Fake {
+  int (*configure)(const char*) = nullptr;
+  int (*init_calls)() = nullptr;
+  int (*shutdown_calls)() = nullptr;
+  bool ok = false;
+
+  Fake() {
+    const char* lib = std::getenv("GFD_AMDSMI_LIBRARY");
+    if (!lib || std::string(lib).find("fake") == std::string::npos) return;
+    void* h = dlopen(lib, RTLD_NOW);
+    if (!h) return;
+    configure = reinterpret_cast<int (*)(const char*)>(dlsym(h, "fake_amdsmi_configure"));
+    init_calls = reinterpret_cast<int (*)()>(dlsym(h, "fake_amdsmi_init_calls"));
+    shutdown_calls = reinterpret_cast<int (*)()>(dlsym(h, "fake_amdsmi_shutdown_calls"));
+    ok = configure && init_calls && shutdown_calls;
+  }
+};
+
+Fake& fake() {
+  static Fake f;
+  return f;
+}
+
+const char* kTwoGpus =
+    "bdf=0000:d9:00.0;mode=SPX;parts=1;cus=256;xcds=8;vram_mib=294896;links=7;virt=1\n"
+    "bdf=0000:23:00.0;mode=CPX;parts=8;cus=32;xcds=1;vram_mib=36862;links=6;virt=1\n";
+
+std::string temp_root() {
+  char d[] = "/tmp/gfd-fake-XXXXXX";
+  if (!mkdtemp(d)) throw std::runtime_error("mkdtemp");
+  return d;
+}
+
+void set_generation(const std::string& root, const std::string& gen) {
+  fs::mkdir_all(root + "/sys/class/kfd/kfd/topology");
+  lm::write_file_atomically(root + "/sys/class/kfd/kfd/topology/generation_id", gen + "\n", 0644);
+}
+
+AmdSmiOptions opts(const std::string& root, bool persistent, const std::string& filter = "") {
+  AmdSmiOptions o;
+  o.root = root;
+  o.persistent = persistent;
+  o.filter = DeviceFilter::parse(filter);
+  return o;
+}
+
+#define REQUIRE_FAKE() \
+  if (!fake().ok) return
+
+}  // namespace
+
+TEST(AmdSmiFake_RegroupsCpxPartitionsByBdf) {
+  REQUIRE_FAKE();
+  fake().configure(kTwoGpus);
+  std::string root = temp_root();
+  AmdSmiManager m(opts(root, false));
+  m.Init();
+  auto devs = m.GetDevices();
+  EXPECT_EQ(devs.size(), static_cast<size_t>(2));
+  const auto& cpx = *devs[0];
+  EXPECT_EQ(cpx.Info().bdf, std::string("0000:23:00.0"));
+  EXPECT_TRUE(cpx.IsPartitioned());
+  EXPECT_TRUE(cpx.IsPartitionCapable());  // from the accelerator profile table
+  auto parts = cpx.GetPartitions();
+  EXPECT_EQ(parts.size(), static_cast<size_t>(8));
+  for (size_t i = 0; i < parts.size(); ++i) EXPECT_EQ(parts[i]->Info().partition_id, static_cast<int>(i));
+  EXPECT_EQ(parts[0]->GetName(), std::string("cpx.1xcd.36gb"));
+  auto attrs = parts[0]->GetAttributes();
+  EXPECT_EQ(attrs.at("compute-units"), std::string("32"));
+  EXPECT_EQ(attrs.at("engines.decoder"), std::string("1"));
+  EXPECT_EQ(attrs.at("engines.dma"), std::string("2"));
+  EXPECT_EQ(attrs.at("engines.jpeg"), std::string("4"));
+  EXPECT_EQ(attrs.at("compute-partition"), std::string("CPX"));
+  EXPECT_EQ(cpx.Info().compute_units, static_cast<uint32_t>(256));
+  EXPECT_EQ(cpx.Info().xcds, static_cast<uint32_t>(8));
+  EXPECT_EQ(cpx.GetTotalMemoryMiB(), static_cast<uint64_t>(8 * 36862));
+  EXPECT_EQ(cpx.Info().xgmi_links, 6);
+
+  const auto& spx = *devs[1];
+  EXPECT_FALSE(spx.IsPartitioned());
+  EXPECT_EQ(spx.GetName(), std::string("AMD Instinct MI355 OAM"));
+  EXPECT_EQ(spx.GetGfxTarget().name(), std::string("gfx950"));
+  EXPECT_EQ(spx.Info().xgmi_links, 7);
+  EXPECT_EQ(spx.Info().virtualization, std::string("baremetal"));
+  EXPECT_EQ(spx.Info().available_memory_partitions, (std::vector<std::string>{"NPS1", "NPS2"}));
+  m.Shutdown();
+  fs::remove_all(root);
+}
+
+TEST(AmdSmiFake_GenericMarketNameFallsBackToBoard) {
+  REQUIRE_FAKE();
+  fake().configure("bdf=0000:d9:00.0;name=AMD Radeon Graphics;board=AMD Instinct MI355X OAM\n");
+  std::string root = temp_root();
+  AmdSmiManager m(opts(root, false));
+  m.Init();
+  EXPECT_EQ(m.GetDevices()[0]->GetName(), std::string("AMD Instinct MI355X OAM"));
+  m.Shutdown();
+  fs::remove_all(root);
+}
+
+TEST(AmdSmiFake_PerCycleSessionInitsEveryWindow) {
+  REQUIRE_FAKE();
+  fake().configure(kTwoGpus);
+  std::string root = temp_root();
+  int i0 = fake().init_calls(), s0 = fake().shutdown_calls();
+  {
+    AmdSmiManager m(opts(root, false));
+    for (int c = 0; c < 3; ++c) {
+      m.Init();
+      EXPECT_EQ(m.GetDevices().size(), static_cast<size_t>(2));
+      m.Shutdown();
+    }
+    EXPECT_EQ(m.init_count(), 3);
+  }
+  EXPECT_EQ(fake().init_calls() - i0, 3);
+  EXPECT_EQ(fake().shutdown_calls() - s0, 3);
+  fs::remove_all(root);
+}
+
+TEST(AmdSmiFake_PersistentSessionInitsOnceAndReinitsOnTopologyChange) {
+  REQUIRE_FAKE();
+  fake().configure(kTwoGpus);
+  std::string root = temp_root();
+  set_generation(root, "7");
+  int i0 = fake().init_calls(), s0 = fake().shutdown_calls();
+  {
+    AmdSmiManager m(opts(root, true));
+    for (int c = 0; c < 3; ++c) {
+      m.Init();
+      m.GetDevices();
+      m.Shutdown();
+    }
+    EXPECT_EQ(fake().init_calls() - i0, 1);
+    EXPECT_EQ(fake().shutdown_calls() - s0, 0);
+    // A partition-mode switch bumps the KFD generation: re-initialise.
+    fake().configure("bdf=0000:d9:00.0;mode=DPX;parts=2;cus=128;xcds=4;vram_mib=147448\n");
+    set_generation(root, "8");
+    m.Init();
+    auto devs = m.GetDevices();
+    m.Shutdown();
+    EXPECT_EQ(fake().init_calls() - i0, 2);
+    EXPECT_EQ(devs.size(), static_cast<size_t>(1));
+    EXPECT_EQ(devs[0]->GetPartitions().size(), static_cast<size_t>(2));
+    EXPECT_EQ(devs[0]->GetPartitions()[0]->GetName(), std::string("dpx.4xcd.144gb"));
+  }
+  // Destroying the manager releases the library.
+  EXPECT_EQ(fake().shutdown_calls() - s0, 2);
+  fs::remove_all(root);
+}
+
+TEST(AmdSmiFake_StaleHandlesTriggerOneReinit) {
+  REQUIRE_FAKE();
+  fake().configure((std::string(kTwoGpus) + "stale_after=5\n").c_str());
+  std::string root = temp_root();
+  int i0 = fake().init_calls();
+  AmdSmiManager m(opts(root, true));
+  m.Init();
+  auto devs = m.GetDevices();  // first snapshot hits NOT_INIT midway -> re-init + retry
+  EXPECT_EQ(devs.size(), static_cast<size_t>(2));
+  EXPECT_EQ(fake().init_calls() - i0, 2);
+  m.Shutdown();
+  fs::remove_all(root);
+}
+
+TEST(AmdSmiFake_StaleHandlesAreFatalPerCycle) {
+  REQUIRE_FAKE();
+  fake().configure((std::string(kTwoGpus) + "stale_after=5\n").c_str());
+  std::string root = temp_root();
+  AmdSmiManager m(opts(root, false));
+  m.Init();
+  EXPECT_THROW_MSG(m.GetDevices(), "NOT_INIT");
+  m.Shutdown();
+  fs::remove_all(root);
+}
+
+TEST(AmdSmiFake_InitFailureSurfaces) {
+  REQUIRE_FAKE();
+  fake().configure("init_status=34\n");
+  std::string root = temp_root();
+  AmdSmiManager m(opts(root, true));
+  EXPECT_THROW_MSG(m.Init(), "amdsmi_init failed: AMDSMI_STATUS_DRIVER_NOT_LOADED");
+  fs::remove_all(root);
+}
+
+TEST(AmdSmiFake_VisibleDevicesFilter) {
+  REQUIRE_FAKE();
+  fake().configure(kTwoGpus);
+  std::string root = temp_root();
+  AmdSmiManager m(opts(root, false, "1"));
+  m.Init();
+  auto devs = m.GetDevices();
+  EXPECT_EQ(devs.size(), static_cast<size_t>(1));
+  EXPECT_EQ(devs[0]->Info().bdf, std::string("0000:d9:00.0"));
+  m.Shutdown();
+  fs::remove_all(root);
+}
+
+TEST(AmdSmiFake_EightGpuNodeInParallel) {
+  REQUIRE_FAKE();
+  std::string spec;
+  for (int i = 0; i < 8; ++i) spec += "bdf=0000:" + std::to_string(10 + i) + ":00.0;links=7\n";
+  fake().configure(spec.c_str());
+  std::string root = temp_root();
+  AmdSmiManager m(opts(root, true));
+  for (int c = 0; c < 20; ++c) {
+    m.Init();
+    EXPECT_EQ(m.GetDevices().size(), static_cast<size_t>(8));
+    m.Shutdown();
+  }
+  fs::remove_all(root);
+}
+
+TEST(AmdSmiFake_SingleStrategyOverCpxNode) {
+  REQUIRE_FAKE();
+  fake().configure("bdf=0000:23:00.0;mode=CPX;parts=8;cus=32;xcds=1;vram_mib=36862\n"
+                   "bdf=0000:24:00.0;mode=CPX;parts=8;cus=32;xcds=1;vram_mib=36862\n");
+  std::string root = temp_root();
+  AmdSmiManager m(opts(root, false));
+  config::Config c;
+  c.flags.mig_strategy = "single";
+  m.Init();
+  auto l = lm::NewResourceLabeler(m, c)->GetLabels();
+  m.Shutdown();
+  EXPECT_EQ(l["amd.com/gpu.count"], std::string("16"));
+  EXPECT_EQ(l["amd.com/gpu.product"], std::string("AMD-Instinct-MI355-OAM-PARTITION-cpx.1xcd.36gb"));
+  EXPECT_EQ(l["amd.com/gpu.memory"], std::string("36862"));
+  EXPECT_EQ(l["amd.com/gpu.compute-units"], std::string("32"));
+  EXPECT_EQ(l["amd.com/partition.strategy"], std::string("single"));
+  fs::remove_all(root);
+}

@@ -6,6 +6,9 @@ namespace gfd::trace {
 
 namespace {
 thread_local std::vector<Phase> t_phases;
+// Only threads that run labeling cycles record; spans executed on pool
+// workers would otherwise accumulate forever.
+thread_local bool t_active = false;
 }
 
 int64_t now_ns() {
@@ -13,9 +16,14 @@ int64_t now_ns() {
       .count();
 }
 
-void begin_cycle() { t_phases.clear(); }
+void begin_cycle() {
+  t_phases.clear();
+  t_active = true;
+}
 const std::vector<Phase>& phases() { return t_phases; }
-void record(const std::string& name, int64_t ns) { t_phases.emplace_back(name, ns); }
+void record(const std::string& name, int64_t ns) {
+  if (t_active) t_phases.emplace_back(name, ns);
+}
 
 std::string summary(int64_t total_ns) {
   std::string out;

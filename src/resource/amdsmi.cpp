@@ -204,6 +204,23 @@ std::vector<std::string> nps_list(uint32_t mask) {
   return out;
 }
 
+// GFD_AMDSMI_CALL_TRACE=1 records every amd-smi call as a trace phase
+// ("amdsmi:<call>") - used to build the cost table in docs/BACKENDS.md.
+bool call_trace() {
+  static const bool on = std::getenv("GFD_AMDSMI_CALL_TRACE") != nullptr;
+  return on;
+}
+
+template <typename F>
+auto timed(const char* name, F&& f) -> decltype(f()) {
+  if (!call_trace()) return f();
+  int64_t t0 = trace::now_ns();
+  auto r = f();
+  trace::record(std::string("amdsmi:") + name, trace::now_ns() - t0);
+  return r;
+}
+#define AMDSMI_CALL(name, expr) timed(name, [&] { return (expr); })
+
 // libdrm's marketing-name table is consulted by amd-smi; when the process
 // already carries another libdrm (e.g. PyTorch's bundled copy, whose
 // amdgpu.ids path does not exist) it degrades to this generic string -
@@ -224,7 +241,7 @@ uint32_t kfd_num_xcc(const std::string& root, uint32_t node_id) {
 void query_proc(AmdSmiLib& L, const std::string& root, ProcInfo& p) {
   amdsmi_asic_info_t asic;
   std::memset(&asic, 0, sizeof(asic));
-  amdsmi_status_t st = L.get_gpu_asic_info(p.h, &asic);
+  amdsmi_status_t st = AMDSMI_CALL("asic_info", L.get_gpu_asic_info(p.h, &asic));
   if (st != AMDSMI_STATUS_SUCCESS) throw Error("amdsmi_get_gpu_asic_info: " + L.status_str(st));
   p.market_name = str::trim(asic.market_name);
   p.vendor_id = asic.vendor_id;
@@ -233,26 +250,29 @@ void query_proc(AmdSmiLib& L, const std::string& root, ProcInfo& p) {
   p.gfx = asic.target_graphics_version;
 
   uint64_t total = 0;
-  if (L.get_gpu_memory_total(p.h, AMDSMI_MEM_TYPE_VRAM, &total) == AMDSMI_STATUS_SUCCESS) p.vram = total;
+  if (AMDSMI_CALL("memory_total", L.get_gpu_memory_total(p.h, AMDSMI_MEM_TYPE_VRAM, &total)) == AMDSMI_STATUS_SUCCESS)
+    p.vram = total;
 
   uint32_t node_id = 0xFFFFFFFFu;
   if (L.get_gpu_kfd_info) {
     amdsmi_kfd_info_t kfd;
     std::memset(&kfd, 0, sizeof(kfd));
-    if (L.get_gpu_kfd_info(p.h, &kfd) == AMDSMI_STATUS_SUCCESS) {
+    if (AMDSMI_CALL("kfd_info", L.get_gpu_kfd_info(p.h, &kfd)) == AMDSMI_STATUS_SUCCESS) {
       if (kfd.current_partition_id != 0xFFFFFFFFu) p.partition_id = kfd.current_partition_id;
       node_id = kfd.node_id;
     }
   }
-  if (node_id != 0xFFFFFFFFu) p.xcds = kfd_num_xcc(root, node_id);
+  if (node_id != 0xFFFFFFFFu) p.xcds = AMDSMI_CALL("kfd_num_xcc(sysfs)", kfd_num_xcc(root, node_id));
   char buf[64];
   if (L.get_gpu_compute_partition) {
     std::memset(buf, 0, sizeof(buf));
-    if (L.get_gpu_compute_partition(p.h, buf, sizeof(buf)) == AMDSMI_STATUS_SUCCESS) p.compute_partition = str::trim(buf);
+    if (AMDSMI_CALL("compute_partition", L.get_gpu_compute_partition(p.h, buf, sizeof(buf))) == AMDSMI_STATUS_SUCCESS)
+      p.compute_partition = str::trim(buf);
   }
   if (L.get_gpu_memory_partition) {
     std::memset(buf, 0, sizeof(buf));
-    if (L.get_gpu_memory_partition(p.h, buf, sizeof(buf)) == AMDSMI_STATUS_SUCCESS) p.memory_partition = str::trim(buf);
+    if (AMDSMI_CALL("memory_partition", L.get_gpu_memory_partition(p.h, buf, sizeof(buf))) == AMDSMI_STATUS_SUCCESS)
+      p.memory_partition = str::trim(buf);
   }
   if (p.xcds == 0 && L.get_gpu_xcd_counter) {
     uint16_t x = 0;
@@ -277,7 +297,7 @@ void query_gpu_extras(AmdSmiLib& L, const ProcInfo& p, const std::string& root, 
   if (L.get_gpu_xgmi_link_status) {
     amdsmi_xgmi_link_status_t ls;
     std::memset(&ls, 0, sizeof(ls));
-    if (L.get_gpu_xgmi_link_status(p.h, &ls) == AMDSMI_STATUS_SUCCESS) {
+    if (AMDSMI_CALL("xgmi_link_status", L.get_gpu_xgmi_link_status(p.h, &ls)) == AMDSMI_STATUS_SUCCESS) {
       int up = 0;
       for (uint32_t i = 0; i < ls.total_links && i < AMDSMI_MAX_NUM_XGMI_LINKS; ++i)
         if (ls.status[i] == AMDSMI_XGMI_LINK_UP) ++up;
@@ -286,25 +306,29 @@ void query_gpu_extras(AmdSmiLib& L, const ProcInfo& p, const std::string& root, 
   }
   if (L.get_gpu_virtualization_mode) {
     amdsmi_virtualization_mode_t vm = AMDSMI_VIRTUALIZATION_MODE_UNKNOWN;
-    if (L.get_gpu_virtualization_mode(p.h, &vm) == AMDSMI_STATUS_SUCCESS) x.virtualization = virt_name(vm);
+    if (AMDSMI_CALL("virtualization_mode", L.get_gpu_virtualization_mode(p.h, &vm)) == AMDSMI_STATUS_SUCCESS)
+      x.virtualization = virt_name(vm);
   }
   if (L.get_gpu_memory_partition_config) {
     amdsmi_memory_partition_config_t cfg;
     std::memset(&cfg, 0, sizeof(cfg));
-    if (L.get_gpu_memory_partition_config(p.h, &cfg) == AMDSMI_STATUS_SUCCESS) x.nps_caps = cfg.partition_caps.nps_cap_mask;
+    if (AMDSMI_CALL("memory_partition_config", L.get_gpu_memory_partition_config(p.h, &cfg)) == AMDSMI_STATUS_SUCCESS)
+      x.nps_caps = cfg.partition_caps.nps_cap_mask;
   }
   // Supported compute partition modes: the profile table needs root; the
   // same information is world-readable in sysfs, which amd-smi itself reads.
   if (L.get_gpu_accelerator_partition_profile_config) {
     amdsmi_accelerator_partition_profile_config_t cfg;
     std::memset(&cfg, 0, sizeof(cfg));
-    if (L.get_gpu_accelerator_partition_profile_config(p.h, &cfg) == AMDSMI_STATUS_SUCCESS) {
+    if (AMDSMI_CALL("partition_profile_config", L.get_gpu_accelerator_partition_profile_config(p.h, &cfg)) ==
+        AMDSMI_STATUS_SUCCESS) {
       for (uint32_t i = 0; i < cfg.num_profiles && i < AMDSMI_MAX_ACCELERATOR_PROFILE; ++i)
         if (const char* n = accel_name(cfg.profiles[i].profile_type)) x.available_compute.push_back(n);
     }
   }
   if (x.available_compute.empty()) {
-    auto v = fs::read_trimmed(fs::join(root, "sys/bus/pci/devices/" + p.bdf + "/available_compute_partition"));
+    auto v = AMDSMI_CALL("available_compute_partition(sysfs)",
+                         fs::read_trimmed(fs::join(root, "sys/bus/pci/devices/" + p.bdf + "/available_compute_partition")));
     if (v)
       for (auto& m : str::split(*v, ','))
         if (!str::trim(m).empty()) x.available_compute.push_back(str::trim(m));

@@ -293,8 +293,29 @@ void query_proc(AmdSmiLib& L, const std::string& root, ProcInfo& p) {
   }
 }
 
+// xGMI links to hive peers from amdgpu's per-peer table ("01 01 ... 00 01",
+// measured on the pool: 7 links).  The same count amd-smi's link-status call
+// derives, but that call decodes the gpu_metrics table through the SMU and
+// costs ~280 us per GPU per cycle (GFD_AMDSMI_CALL_TRACE on MI355X) versus
+// ~5 us here.
+int sysfs_xgmi_links(const std::string& root, const std::string& bdf) {
+  auto v = fs::read_trimmed(fs::join(root, "sys/bus/pci/devices/" + bdf + "/xgmi_num_links"));
+  if (!v) return -1;
+  int total = 0;
+  bool any = false;
+  for (const auto& tok : str::split(*v, ' ')) {
+    if (tok.empty()) continue;
+    auto n = str::parse_uint(tok, 16);
+    if (!n) return -1;
+    total += static_cast<int>(*n);
+    any = true;
+  }
+  return any ? total : -1;
+}
+
 void query_gpu_extras(AmdSmiLib& L, const ProcInfo& p, const std::string& root, bool partitioned, GpuExtras& x) {
-  if (L.get_gpu_xgmi_link_status) {
+  x.xgmi_links = AMDSMI_CALL("xgmi_num_links(sysfs)", sysfs_xgmi_links(root, p.bdf));
+  if (x.xgmi_links < 0 && L.get_gpu_xgmi_link_status) {
     amdsmi_xgmi_link_status_t ls;
     std::memset(&ls, 0, sizeof(ls));
     if (AMDSMI_CALL("xgmi_link_status", L.get_gpu_xgmi_link_status(p.h, &ls)) == AMDSMI_STATUS_SUCCESS) {

@@ -96,6 +96,11 @@ std::vector<PCIDevice> SysfsAmdPCI::Devices() {
           id.relevant = true;
           id.class_code = c.substr(0, 4);
           id.device = fs::read_trimmed(fs::join(p, "device")).value_or("");
+          if (auto t = fs::read_trimmed(fs::join(p, "sriov_totalvfs")))
+            id.sriov_totalvfs = static_cast<int>(str::parse_uint(*t).value_or(0));
+          if (id.sriov_totalvfs > 0) id.sriov_vf_device = fs::read_trimmed(fs::join(p, "sriov_vf_device")).value_or("");
+          std::string link = fs::read_link(fs::join(p, "physfn"));
+          if (!link.empty()) id.physfn = fs::basename(link);
         }
       }
     }
@@ -108,13 +113,14 @@ std::vector<PCIDevice> SysfsAmdPCI::Devices() {
     d.vendor = kAmdVendorId;
     d.class_code = id.class_code;
     d.device = id.device;
-    if (auto t = fs::read_trimmed(fs::join(p, "sriov_totalvfs"))) d.sriov_totalvfs = static_cast<int>(str::parse_uint(*t).value_or(0));
-    if (d.sriov_totalvfs >= 0) {
+    d.sriov_totalvfs = id.sriov_totalvfs;
+    d.physfn = id.physfn;
+    if (d.sriov_totalvfs == 0) {
+      d.sriov_numvfs = 0;  // SR-IOV capable in name only: no VFs possible
+    } else if (d.sriov_totalvfs > 0) {
       if (auto n = fs::read_trimmed(fs::join(p, "sriov_numvfs"))) d.sriov_numvfs = static_cast<int>(str::parse_uint(*n).value_or(0));
-      if (d.sriov_numvfs > 0) d.sriov_vf_device = fs::read_trimmed(fs::join(p, "sriov_vf_device")).value_or("");
+      if (d.sriov_numvfs > 0) d.sriov_vf_device = id.sriov_vf_device;
     }
-    std::string link = fs::read_link(fs::join(p, "physfn"));
-    if (!link.empty()) d.physfn = fs::basename(link);
     if (d.sriov_totalvfs < 0 && d.physfn.empty()) {
       // The kernel publishes no SR-IOV state for this function: read the
       // configuration space and walk its capabilities instead.

@@ -102,11 +102,17 @@ class SysfsAmdPCI : public AmdPCI {
   std::vector<PCIDevice> Devices() override;
 
  private:
+  // Immutable for the lifetime of a sysfs object: vendor/class/device,
+  // TotalVFs and the VF device ID (read-only SR-IOV capability fields), and
+  // a VF's physfn link.  Only NumVFs is re-read every call.
   struct Identity {
     uint64_t ino = 0;
     bool relevant = false;  // AMD display / accelerator function
     std::string class_code;
     std::string device;
+    int sriov_totalvfs = -1;
+    std::string sriov_vf_device;
+    std::string physfn;
   };
   std::string root_;
   std::map<std::string, Identity> cache_;

@@ -169,7 +169,7 @@ struct ProcInfo {
 struct GpuExtras {
   int xgmi_links = -1;
   std::string virtualization;
-  uint32_t nps_caps = 0;
+  std::vector<std::string> available_memory;
   std::vector<std::string> available_compute;
   Attributes engines;  // engines.* from the accelerator partition profile
 };
@@ -279,16 +279,17 @@ void query_proc(AmdSmiLib& L, const std::string& root, ProcInfo& p) {
     if (L.get_gpu_xcd_counter(p.h, &x) == AMDSMI_STATUS_SUCCESS) p.xcds = x;
   }
   if (is_generic_name(p.market_name)) {
-    // Board FRU product name, then the same attribute via sysfs.
-    if (L.get_gpu_board_info) {
+    // The board FRU product name: amdgpu publishes it in sysfs (~5 us); the
+    // amd-smi board-info call returns the same string for ~155 us.
+    auto v = fs::read_trimmed(fs::join(root, "sys/bus/pci/devices/" + p.bdf + "/product_name"));
+    if (v && !is_generic_name(*v)) {
+      p.market_name = *v;
+    } else if (L.get_gpu_board_info) {
       amdsmi_board_info_t b;
       std::memset(&b, 0, sizeof(b));
-      if (L.get_gpu_board_info(p.h, &b) == AMDSMI_STATUS_SUCCESS && !is_generic_name(str::trim(b.product_name)))
+      if (AMDSMI_CALL("board_info", L.get_gpu_board_info(p.h, &b)) == AMDSMI_STATUS_SUCCESS &&
+          !is_generic_name(str::trim(b.product_name)))
         p.market_name = str::trim(b.product_name);
-    }
-    if (is_generic_name(p.market_name)) {
-      auto v = fs::read_trimmed(fs::join(root, "sys/bus/pci/devices/" + p.bdf + "/product_name"));
-      if (v && !v->empty()) p.market_name = *v;
     }
   }
 }
@@ -330,11 +331,17 @@ void query_gpu_extras(AmdSmiLib& L, const ProcInfo& p, const std::string& root, 
     if (AMDSMI_CALL("virtualization_mode", L.get_gpu_virtualization_mode(p.h, &vm)) == AMDSMI_STATUS_SUCCESS)
       x.virtualization = virt_name(vm);
   }
-  if (L.get_gpu_memory_partition_config) {
+  // Supported memory partition modes: world-readable in sysfs (~5 us);
+  // the amd-smi partition-config call (~25 us) only as a fallback.
+  if (auto v = AMDSMI_CALL("available_memory_partition(sysfs)",
+                           fs::read_trimmed(fs::join(root, "sys/bus/pci/devices/" + p.bdf + "/available_memory_partition")))) {
+    for (auto& m : str::split(*v, ','))
+      if (!str::trim(m).empty()) x.available_memory.push_back(str::trim(m));
+  } else if (L.get_gpu_memory_partition_config) {
     amdsmi_memory_partition_config_t cfg;
     std::memset(&cfg, 0, sizeof(cfg));
     if (AMDSMI_CALL("memory_partition_config", L.get_gpu_memory_partition_config(p.h, &cfg)) == AMDSMI_STATUS_SUCCESS)
-      x.nps_caps = cfg.partition_caps.nps_cap_mask;
+      x.available_memory = nps_list(cfg.partition_caps.nps_cap_mask);
   }
   // Supported compute partition modes: the profile table needs root; the
   // same information is world-readable in sysfs, which amd-smi itself reads.
@@ -553,7 +560,7 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
     info.compute_partition = first.compute_partition;
     info.memory_partition = first.memory_partition;
     info.available_compute_partitions = g.extras.available_compute;
-    info.available_memory_partitions = nps_list(g.extras.nps_caps);
+    info.available_memory_partitions = g.extras.available_memory;
     info.xgmi_links = g.extras.xgmi_links;
     info.virtualization = g.extras.virtualization;
     bool partitioned = g.procs->size() > 1 || (!first.compute_partition.empty() && first.compute_partition != "SPX");

@@ -139,7 +139,13 @@ bool has_amdsmi(std::string* reason) {
     if (reason) *reason = "could not load libamd_smi: " + err;
     return false;
   }
-  if (reason) *reason = "found " + l->path();
+  if (reason) {
+    *reason = "found " + l->path();
+    amdsmi_version_t v{};
+    if (l->get_lib_version && l->get_lib_version(&v) == AMDSMI_STATUS_SUCCESS)
+      *reason += " (amd-smi library " + std::to_string(v.major) + "." + std::to_string(v.minor) + "." +
+                 std::to_string(v.release) + ")";
+  }
   return true;
 }
 

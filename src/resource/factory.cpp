@@ -5,6 +5,7 @@
 #include "resource/amdsmi.h"
 #include "resource/managers.h"
 #include "resource/sysfs.h"
+#include "resource/versions.h"
 #include "util/error.h"
 #include "util/log.h"
 #include "util/strings.h"
@@ -42,6 +43,16 @@ bool log_with_reason(bool is, const std::string& reason, std::string tag) {
   return is;
 }
 
+// Startup observability: the runtime and driver versions the
+// hardware backends will label with.
+void log_versions(const std::string& root) {
+  auto rv = rocm_version(root);
+  std::string drv = host_driver_version(root);
+  log::printf("ROCm runtime %s, amdgpu driver %s",
+              rv ? (std::to_string(rv->major) + "." + std::to_string(rv->minor)).c_str() : "not found",
+              extract_version(drv).value_or(drv).c_str());
+}
+
 }  // namespace
 
 ManagerPtr get_manager(const config::Config& c) {
@@ -57,10 +68,12 @@ ManagerPtr get_manager(const config::Config& c) {
   }
   if (backend == "sysfs") {
     log::printf("Using sysfs (KFD topology) manager");
+    log_versions(c.sysfs_root());
     return std::make_shared<SysfsManager>(sysfs_options(c));
   }
   if (backend == "amdsmi") {
     log::printf("Using amd-smi manager");
+    log_versions(c.sysfs_root());
     return std::make_shared<AmdSmiManager>(amdsmi_options(c));
   }
   if (backend != "auto") throw Error("unknown backend '" + backend + "' (expected auto, amdsmi, sysfs, null or mock)");
@@ -69,6 +82,7 @@ ManagerPtr get_manager(const config::Config& c) {
   bool has_smi = log_with_reason(has_amdsmi(&why), why, "amd-smi");
   bool has_kfd = log_with_reason(has_kfd_topology(c.sysfs_root(), &why), why, "KFD");
   if (has_smi && has_kfd) log::printf("Using KFD sysfs only as a fallback on an amd-smi system");
+  if (has_smi || has_kfd) log_versions(c.sysfs_root());
   if (has_smi) {
     log::printf("Using amd-smi manager");
     return std::make_shared<AmdSmiManager>(amdsmi_options(c));

@@ -332,7 +332,8 @@ void query_gpu_extras(AmdSmiLib& L, const ProcInfo& p, const std::string& root, 
       x.xgmi_links = up;
     }
   }
-  if (L.get_gpu_virtualization_mode) {
+  // Pre-filled from the session cache when already known (see snapshot()).
+  if (x.virtualization.empty() && L.get_gpu_virtualization_mode) {
     amdsmi_virtualization_mode_t vm = AMDSMI_VIRTUALIZATION_MODE_UNKNOWN;
     if (AMDSMI_CALL("virtualization_mode", L.get_gpu_virtualization_mode(p.h, &vm)) == AMDSMI_STATUS_SUCCESS)
       x.virtualization = virt_name(vm);
@@ -412,6 +413,7 @@ void AmdSmiManager::library_init() {
   if (st != AMDSMI_STATUS_SUCCESS) throw Error("amdsmi_init failed: " + lib_->status_str(st));
   lib_->users++;
   lib_initialized_ = true;
+  virt_mode_.clear();
   ++init_count_;
 }
 
@@ -526,7 +528,11 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
   int index = -1;
   for (auto& [bdf, procs] : groups) {
     ++index;
-    if (opts_.filter.matches(index, bdf)) gpus.push_back(Gpu{index, bdf, &procs, {}, {}});
+    if (opts_.filter.matches(index, bdf)) {
+      gpus.push_back(Gpu{index, bdf, &procs, {}, {}});
+      auto v = virt_mode_.find(bdf);
+      if (v != virt_mode_.end()) gpus.back().extras.virtualization = v->second;
+    }
   }
 
   // Query every processor; parallel across physical GPUs on multi-GPU nodes
@@ -552,6 +558,8 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
   WorkerPool::instance().parallel_for(gpus.size(), [&](size_t i) { work(gpus[i]); }, threads);
   for (const auto& g : gpus)
     if (!g.error.empty()) throw Error(g.error);
+  for (const auto& g : gpus)
+    if (!g.extras.virtualization.empty()) virt_mode_[g.bdf] = g.extras.virtualization;
 
   std::vector<DevicePtr> out;
   for (auto& g : gpus) {

@@ -12,6 +12,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 #include <sstream>
 #include <string>
@@ -44,6 +45,7 @@ struct State {
   bool initialized = false;
   bool stale = false;
   int init_calls = 0;
+  std::atomic<int> virt_calls{0};
   int shutdown_calls = 0;
 };
 
@@ -148,6 +150,7 @@ int fake_amdsmi_configure(const char* spec) {
   return 0;
 }
 int fake_amdsmi_init_calls() { return S().init_calls; }
+int fake_amdsmi_virt_calls() { return S().virt_calls.load(); }
 int fake_amdsmi_shutdown_calls() { return S().shutdown_calls; }
 int fake_amdsmi_initialized() { return S().initialized ? 1 : 0; }
 
@@ -326,6 +329,7 @@ amdsmi_status_t amdsmi_get_gpu_xgmi_link_status(amdsmi_processor_handle h, amdsm
 amdsmi_status_t amdsmi_get_gpu_virtualization_mode(amdsmi_processor_handle h, amdsmi_virtualization_mode_t* m) {
   Proc* p;
   if (auto st = check(h, &p)) return st;
+  S().virt_calls++;
   *m = static_cast<amdsmi_virtualization_mode_t>(p->virt);
   return AMDSMI_STATUS_SUCCESS;
 }

@@ -27,6 +27,7 @@ struct Fake {
   int (*configure)(const char*) = nullptr;
   int (*init_calls)() = nullptr;
   int (*shutdown_calls)() = nullptr;
+  int (*virt_calls)() = nullptr;
   bool ok = false;
 
   Fake() {
@@ -37,7 +38,8 @@ struct Fake {
     configure = reinterpret_cast<int (*)(const char*)>(dlsym(h, "fake_amdsmi_configure"));
     init_calls = reinterpret_cast<int (*)()>(dlsym(h, "fake_amdsmi_init_calls"));
     shutdown_calls = reinterpret_cast<int (*)()>(dlsym(h, "fake_amdsmi_shutdown_calls"));
-    ok = configure && init_calls && shutdown_calls;
+    virt_calls = reinterpret_cast<int (*)()>(dlsym(h, "fake_amdsmi_virt_calls"));
+    ok = configure && init_calls && shutdown_calls && virt_calls;
   }
 };
 
@@ -170,6 +172,39 @@ TEST(AmdSmiFake_PersistentSessionInitsOnceAndReinitsOnTopologyChange) {
   }
   // Destroying the manager releases the library.
   EXPECT_EQ(fake().shutdown_calls() - s0, 2);
+  fs::remove_all(root);
+}
+
+TEST(AmdSmiFake_VirtualizationModeQueriedOncePerSession) {
+  REQUIRE_FAKE();
+  fake().configure(kTwoGpus);
+  std::string root = temp_root();
+  set_generation(root, "1");
+  int v0 = fake().virt_calls();
+  AmdSmiManager m(opts(root, true));
+  for (int c = 0; c < 4; ++c) {
+    m.Init();
+    auto devs = m.GetDevices();
+    m.Shutdown();
+    EXPECT_EQ(devs[0]->Info().virtualization, std::string("baremetal"));
+  }
+  EXPECT_EQ(fake().virt_calls() - v0, 2);  // once per physical GPU
+  // A driver reload (new KFD generation) starts a new session: query again.
+  fake().configure("bdf=0000:d9:00.0;mode=SPX;parts=1;cus=256;xcds=8;vram_mib=294896;virt=3\n");
+  set_generation(root, "2");
+  m.Init();
+  auto devs = m.GetDevices();
+  m.Shutdown();
+  EXPECT_EQ(fake().virt_calls() - v0, 3);
+  EXPECT_EQ(devs[0]->Info().virtualization, std::string("guest"));
+  // Per-cycle sessions query every cycle.
+  AmdSmiManager pc(opts(root, false));
+  for (int c = 0; c < 2; ++c) {
+    pc.Init();
+    pc.GetDevices();
+    pc.Shutdown();
+  }
+  EXPECT_EQ(fake().virt_calls() - v0, 5);
   fs::remove_all(root);
 }
 

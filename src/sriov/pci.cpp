@@ -4,6 +4,7 @@
 
 #include "util/error.h"
 #include "util/fs.h"
+#include "util/pool.h"
 #include "util/strings.h"
 
 namespace gfd::sriov {
@@ -70,67 +71,88 @@ std::optional<std::string> PCIDevice::GetExtendedCapability(int ext_id, size_t l
   return std::nullopt;
 }
 
+SysfsAmdPCI::Identity SysfsAmdPCI::read_identity(const std::string& addr, const std::string& p, uint64_t ino) {
+  Identity id;
+  id.ino = ino;
+  auto vendor = fs::read_file(fs::join(p, "vendor"), 64);
+  if (!vendor.ok()) throw Error("unable to read PCI device vendor id for " + addr + ": " + fs::errno_str(vendor.err));
+  if (str::trim(vendor.data) != kAmdVendorId) return id;
+  auto cls = fs::read_file(fs::join(p, "class"), 64);
+  if (!cls.ok()) throw Error("unable to read PCI device class for " + addr + ": " + fs::errno_str(cls.err));
+  std::string c = str::trim(cls.data);
+  // Display controllers (0x03xxxx) and processing accelerators (0x12xxxx).
+  if (!str::starts_with(c, "0x03") && !str::starts_with(c, "0x12")) return id;
+  id.relevant = true;
+  id.class_code = c.substr(0, 4);
+  id.device = fs::read_trimmed(fs::join(p, "device")).value_or("");
+  if (auto t = fs::read_trimmed(fs::join(p, "sriov_totalvfs")))
+    id.sriov_totalvfs = static_cast<int>(str::parse_uint(*t).value_or(0));
+  if (id.sriov_totalvfs > 0) id.sriov_vf_device = fs::read_trimmed(fs::join(p, "sriov_vf_device")).value_or("");
+  std::string link = fs::read_link(fs::join(p, "physfn"));
+  if (!link.empty()) id.physfn = fs::basename(link);
+  return id;
+}
+
 std::vector<PCIDevice> SysfsAmdPCI::Devices() {
   std::string dir = fs::join(root_, kPciDevicesRoot);
   int err = 0;
   auto entries = fs::list_dir_ino(dir, &err);
   if (err != 0) throw Error("unable to read PCI bus devices: open " + dir + ": " + fs::errno_str(err));
-  std::map<std::string, Identity> seen;
-  std::vector<PCIDevice> out;
-  for (const auto& [addr, ino] : entries) {
-    std::string p = fs::join(dir, addr);
-    Identity id;
-    auto hit = cache_.find(addr);
-    if (hit != cache_.end() && hit->second.ino == ino && ino != 0) {
-      id = hit->second;
-    } else {
-      id.ino = ino;
-      auto vendor = fs::read_file(fs::join(p, "vendor"), 64);
-      if (!vendor.ok()) throw Error("unable to read PCI device vendor id for " + addr + ": " + fs::errno_str(vendor.err));
-      if (str::trim(vendor.data) == kAmdVendorId) {
-        auto cls = fs::read_file(fs::join(p, "class"), 64);
-        if (!cls.ok()) throw Error("unable to read PCI device class for " + addr + ": " + fs::errno_str(cls.err));
-        std::string c = str::trim(cls.data);
-        // Display controllers (0x03xxxx) and processing accelerators (0x12xxxx).
-        if (str::starts_with(c, "0x03") || str::starts_with(c, "0x12")) {
-          id.relevant = true;
-          id.class_code = c.substr(0, 4);
-          id.device = fs::read_trimmed(fs::join(p, "device")).value_or("");
-          if (auto t = fs::read_trimmed(fs::join(p, "sriov_totalvfs")))
-            id.sriov_totalvfs = static_cast<int>(str::parse_uint(*t).value_or(0));
-          if (id.sriov_totalvfs > 0) id.sriov_vf_device = fs::read_trimmed(fs::join(p, "sriov_vf_device")).value_or("");
-          std::string link = fs::read_link(fs::join(p, "physfn"));
-          if (!link.empty()) id.physfn = fs::basename(link);
-        }
-      }
-    }
-    seen[addr] = id;
-    if (!id.relevant) continue;
 
+  // Merge the (sorted) listing with the (sorted) identity cache: entries
+  // whose sysfs inode is unchanged reuse their identity, new or re-created
+  // ones are read.  Moves only - no per-entry allocation in steady state
+  // (a large host lists ~320 PCI functions, measured on the MI355X pool).
+  std::vector<std::pair<std::string, Identity>> next;
+  next.reserve(entries.size());
+  auto hit = cache_.begin();
+  for (auto& [addr, ino] : entries) {
+    while (hit != cache_.end() && hit->first < addr) ++hit;
+    if (hit != cache_.end() && hit->first == addr && hit->second.ino == ino && ino != 0) {
+      next.emplace_back(std::move(addr), std::move(hit->second));
+    } else {
+      Identity id = read_identity(addr, fs::join(dir, addr), ino);
+      next.emplace_back(std::move(addr), std::move(id));
+    }
+  }
+  cache_.swap(next);
+
+  std::vector<PCIDevice> out;
+  for (const auto& [addr, id] : cache_) {
+    if (!id.relevant) continue;
     PCIDevice d;
-    d.path = p;
+    d.path = fs::join(dir, addr);
     d.address = addr;
     d.vendor = kAmdVendorId;
     d.class_code = id.class_code;
     d.device = id.device;
     d.sriov_totalvfs = id.sriov_totalvfs;
+    d.sriov_vf_device = id.sriov_vf_device;  // cleared below unless VFs are enabled
     d.physfn = id.physfn;
+    out.push_back(std::move(d));
+  }
+
+  // Mutable state: NumVFs of SR-IOV capable functions (one ~4 us sysfs read
+  // each, spread over the worker pool on multi-GPU hosts), and the raw
+  // configuration space of functions whose SR-IOV state sysfs does not
+  // publish.
+  auto refresh = [&](size_t i) {
+    PCIDevice& d = out[i];
     if (d.sriov_totalvfs == 0) {
       d.sriov_numvfs = 0;  // SR-IOV capable in name only: no VFs possible
     } else if (d.sriov_totalvfs > 0) {
-      if (auto n = fs::read_trimmed(fs::join(p, "sriov_numvfs"))) d.sriov_numvfs = static_cast<int>(str::parse_uint(*n).value_or(0));
-      if (d.sriov_numvfs > 0) d.sriov_vf_device = id.sriov_vf_device;
+      if (auto n = fs::read_trimmed(fs::join(d.path, "sriov_numvfs")))
+        d.sriov_numvfs = static_cast<int>(str::parse_uint(*n).value_or(0));
     }
+    if (d.sriov_numvfs <= 0) d.sriov_vf_device.clear();
     if (d.sriov_totalvfs < 0 && d.physfn.empty()) {
-      // The kernel publishes no SR-IOV state for this function: read the
-      // configuration space and walk its capabilities instead.
-      auto cfg = fs::read_file(fs::join(p, "config"), kPciExpressConfigSpaceSize);
-      if (!cfg.ok()) throw Error("unable to read PCI configuration space for " + addr + ": " + fs::errno_str(cfg.err));
+      auto cfg = fs::read_file(fs::join(d.path, "config"), kPciExpressConfigSpaceSize);
+      if (!cfg.ok()) throw Error("unable to read PCI configuration space for " + d.address + ": " + fs::errno_str(cfg.err));
       d.config = std::move(cfg.data);
     }
-    out.push_back(std::move(d));
-  }
-  cache_.swap(seen);
+  };
+  // Two functions per lane: below that, dispatch costs more than the reads.
+  WorkerPool::instance().parallel_for(out.size(), refresh, (out.size() + 1) / 2);
   return out;
 }
 

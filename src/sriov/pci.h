@@ -95,7 +95,10 @@ class AmdPCI {
 //     config cycles;
 //   * configuration space (a 4 KiB read = ~1000 config cycles when
 //     privileged) is read only for functions whose SR-IOV state sysfs does not
-//     publish.
+//     publish;
+//   * the per-function NumVFs reads are spread over the worker pool.
+// Measured on an 8-GPU MI355X host with 319 PCI functions: 2.5 ms first scan,
+// then list 29 us + 8 NumVFs reads.
 class SysfsAmdPCI : public AmdPCI {
  public:
   explicit SysfsAmdPCI(std::string root = "/") : root_(std::move(root)) {}
@@ -114,8 +117,9 @@ class SysfsAmdPCI : public AmdPCI {
     std::string sriov_vf_device;
     std::string physfn;
   };
+  static Identity read_identity(const std::string& addr, const std::string& path, uint64_t ino);
   std::string root_;
-  std::map<std::string, Identity> cache_;
+  std::vector<std::pair<std::string, Identity>> cache_;  // sorted by address
 };
 
 // Built-in mock with synthetic MI300X/MI355X configuration spaces:

@@ -27,21 +27,28 @@ size_t WorkerPool::workers() const {
 }
 
 void WorkerPool::ensure_workers(size_t n) {
-  // Caller holds mu_.
-  while (threads_.size() < n && threads_.size() < max_workers_) threads_.emplace_back([this] { loop(); });
+  // Caller holds mu_.  `n` tasks are queued: make sure that many workers are
+  // idle (busy workers may be blocked in a nested parallel_for).
+  while (idle_ + spawning_ < n && threads_.size() < max_workers_) {
+    ++spawning_;
+    threads_.emplace_back([this] { loop(); });
+  }
 }
 
 void WorkerPool::loop() {
+  std::unique_lock<std::mutex> lk(mu_);
+  --spawning_;
   for (;;) {
-    std::function<void()> fn;
-    {
-      std::unique_lock<std::mutex> lk(mu_);
-      cv_.wait(lk, [this] { return stop_ || !queue_.empty(); });
-      if (stop_ && queue_.empty()) return;
-      fn = std::move(queue_.front());
-      queue_.pop_front();
-    }
+    ++idle_;
+    cv_.wait(lk, [this] { return stop_ || !queue_.empty(); });
+    --idle_;
+    if (stop_ && queue_.empty()) return;
+    std::function<void()> fn = std::move(queue_.front());
+    queue_.pop_front();
+    lk.unlock();
     fn();
+    fn = nullptr;  // release captures outside the lock
+    lk.lock();
   }
 }
 
@@ -51,7 +58,6 @@ WorkerPool::Task WorkerPool::submit(std::function<void()> fn) {
   auto st = t.state_;
   {
     std::lock_guard<std::mutex> g(mu_);
-    ensure_workers(queue_.size() + 1);
     queue_.emplace_back([st, fn = std::move(fn)] {
       std::exception_ptr err;
       try {
@@ -64,6 +70,7 @@ WorkerPool::Task WorkerPool::submit(std::function<void()> fn) {
       st->done = true;
       st->cv.notify_all();
     });
+    ensure_workers(queue_.size());
   }
   cv_.notify_one();
   return t;
@@ -83,27 +90,41 @@ void WorkerPool::parallel_for(size_t n, const std::function<void(size_t)>& fn, s
     for (size_t i = 0; i < n; ++i) fn(i);
     return;
   }
-  auto next = std::make_shared<std::atomic<size_t>>(0);
-  auto body = [next, n, &fn] {
-    for (size_t i = (*next)++; i < n; i = (*next)++) fn(i);
+  // Items are claimed from a shared counter; the caller waits for every
+  // *claimed* item to finish, not for the helper lanes to start.  A lane
+  // still queued when the caller has drained the range finds nothing left
+  // and exits, so nested parallel_for calls (e.g. the PCI scan, itself a
+  // pool task, spreading its reads) cannot deadlock on a saturated pool.
+  struct Shared {
+    std::atomic<size_t> next{0};
+    std::mutex mu;
+    std::condition_variable cv;
+    size_t done = 0;
+    std::exception_ptr error;
+    const std::function<void(size_t)>* fn;
+    size_t n;
   };
-  std::vector<Task> tasks;
-  tasks.reserve(lanes - 1);
-  for (size_t l = 1; l < lanes; ++l) tasks.push_back(submit(body));
-  std::exception_ptr first;
-  try {
-    body();
-  } catch (...) {
-    first = std::current_exception();
-  }
-  for (auto& t : tasks) {
-    try {
-      t.wait();
-    } catch (...) {
-      if (!first) first = std::current_exception();
+  auto sh = std::make_shared<Shared>();
+  sh->fn = &fn;
+  sh->n = n;
+  auto body = [sh] {
+    for (size_t i = sh->next++; i < sh->n; i = sh->next++) {
+      std::exception_ptr err;
+      try {
+        (*sh->fn)(i);
+      } catch (...) {
+        err = std::current_exception();
+      }
+      std::lock_guard<std::mutex> g(sh->mu);
+      if (err && !sh->error) sh->error = err;
+      if (++sh->done == sh->n) sh->cv.notify_all();
     }
-  }
-  if (first) std::rethrow_exception(first);
+  };
+  for (size_t l = 1; l < lanes; ++l) submit(body);
+  body();
+  std::unique_lock<std::mutex> lk(sh->mu);
+  sh->cv.wait(lk, [&] { return sh->done == sh->n; });
+  if (sh->error) std::rethrow_exception(sh->error);
 }
 
 }  // namespace gfd

@@ -53,6 +53,8 @@ class WorkerPool {
   Task submit(std::function<void()> fn);
   // Run fn(i) for i in [0, n): the calling thread takes part, at most
   // `max_parallel` (0 = unlimited) run concurrently.  Rethrows the first error.
+  // Safe to call from a pool task (nested): completes even if no worker is
+  // free, because the caller runs every item nobody else has claimed.
   void parallel_for(size_t n, const std::function<void(size_t)>& fn, size_t max_parallel = 0);
 
   size_t workers() const;
@@ -66,6 +68,8 @@ class WorkerPool {
   std::condition_variable cv_;
   std::deque<std::function<void()>> queue_;
   std::vector<std::thread> threads_;
+  size_t idle_ = 0;      // workers parked waiting for a task
+  size_t spawning_ = 0;  // threads created but not yet parked
   bool stop_ = false;
 };
 

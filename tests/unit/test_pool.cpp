@@ -62,3 +62,18 @@ TEST(Pool_ManyRoundsReuseWorkers) {
   }
   EXPECT_TRUE(pool.workers() <= 4);
 }
+
+TEST(Pool_NestedParallelForOnSaturatedPoolCompletes) {
+  // The PCI scan is a pool task that itself calls parallel_for; with every
+  // worker busy the nested call must still finish (caller drains the range).
+  WorkerPool pool(1);
+  std::atomic<int> inner{0};
+  auto t = pool.submit([&] { pool.parallel_for(16, [&](size_t) { inner++; }, 8); });
+  t.wait();
+  EXPECT_EQ(inner.load(), 16);
+  // Two levels deep on a wider pool.
+  WorkerPool pool4(4);
+  std::atomic<int> leaves{0};
+  pool4.parallel_for(8, [&](size_t) { pool4.parallel_for(8, [&](size_t) { leaves++; }, 4); }, 8);
+  EXPECT_EQ(leaves.load(), 64);
+}

@@ -95,10 +95,9 @@ class AmdPCI {
 //     config cycles;
 //   * configuration space (a 4 KiB read = ~1000 config cycles when
 //     privileged) is read only for functions whose SR-IOV state sysfs does not
-//     publish;
-//   * the per-function NumVFs reads are spread over the worker pool.
+//     publish.
 // Measured on an 8-GPU MI355X host with 319 PCI functions: 2.5 ms first scan,
-// then list 29 us + 8 NumVFs reads.
+// then ~60 us (list 30 us + cache merge 2 us + 8 NumVFs reads 26 us).
 class SysfsAmdPCI : public AmdPCI {
  public:
   explicit SysfsAmdPCI(std::string root = "/") : root_(std::move(root)) {}

@@ -9,6 +9,7 @@
 #include "sriov/pci.h"
 #include "sriov/sriov.h"
 #include "util/fs.h"
+#include "util/trace.h"
 
 using namespace gfd;
 
@@ -43,6 +44,15 @@ int main() {
     std::string f = devs[0].path + "/sriov_numvfs";
     std::printf("read sriov_numvfs p50: %.1f us\n", p50(200, [&] { fs::read_trimmed(f); }));
   }
+  for (int i = 0; i < 3; ++i) {
+    trace::begin_cycle();
+    pci.Devices();
+    std::printf("phases: %s\n", trace::summary(0).c_str());
+  }
+  // Serial NumVFs refresh for comparison.
+  std::printf("serial 8x numvfs p50: %.1f us\n", p50(200, [&] {
+    for (auto& d : devs) fs::read_trimmed(d.path + "/sriov_numvfs");
+  }));
   auto lib = sriov::new_sriov_lib("/");
   std::printf("sriov lib Devices() p50: %.1f us\n", p50(200, [&] { lib->Devices(); }));
   return 0;

@@ -120,7 +120,18 @@ void WorkerPool::parallel_for(size_t n, const std::function<void(size_t)>& fn, s
       if (++sh->done == sh->n) sh->cv.notify_all();
     }
   };
-  for (size_t l = 1; l < lanes; ++l) submit(body);
+  // Enqueue every helper lane under one lock and wake the workers with one
+  // futex call: per-lane submit+notify_one staggers the 8th lane's start by
+  // several wake-up latencies on an 8-GPU cycle.
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    for (size_t l = 1; l < lanes; ++l) queue_.emplace_back(body);
+    ensure_workers(queue_.size());
+  }
+  if (lanes == 2)
+    cv_.notify_one();
+  else
+    cv_.notify_all();
   body();
   std::unique_lock<std::mutex> lk(sh->mu);
   sh->cv.wait(lk, [&] { return sh->done == sh->n; });

@@ -6,6 +6,10 @@
 // plus optional global lines:
 //   init_status=34            amdsmi_init returns this status
 //   stale_after=N             after N successful queries, queries return NOT_INIT until re-init
+//   latency_us=N              every device query except handle-table lookups
+//                             (processor type, BDF, ASIC info) busy-waits N us
+//                             holding that GPU's lock (amd-smi serialises per
+//                             device), to model multi-GPU scaling of the backend
 // Counters are exposed for assertions (fake_amdsmi_init_calls, ...).
 #include <amd_smi/amdsmi.h>
 
@@ -13,6 +17,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <atomic>
+#include <chrono>
+#include <map>
+#include <memory>
 #include <mutex>
 #include <sstream>
 #include <string>
@@ -47,6 +54,8 @@ struct State {
   int init_calls = 0;
   std::atomic<int> virt_calls{0};
   int shutdown_calls = 0;
+  long latency_us = 0;
+  std::map<std::string, std::unique_ptr<std::mutex>> device_mu;  // by BDF
 };
 
 State& S() {
@@ -72,17 +81,32 @@ Proc* proc(amdsmi_processor_handle h) {
   return &s.procs[i - 1];
 }
 
-amdsmi_status_t check(amdsmi_processor_handle h, Proc** out) {
+// `cheap`: calls that cost <= 2 us on real hardware (handle table lookups).
+amdsmi_status_t check(amdsmi_processor_handle h, Proc** out, bool cheap = false) {
   auto& s = S();
-  std::lock_guard<std::mutex> g(s.mu);  // like amd-smi's per-device mutexes
-  if (!s.initialized) return AMDSMI_STATUS_NOT_INIT;
-  if (s.stale) return AMDSMI_STATUS_NOT_INIT;
-  if (s.stale_after >= 0 && ++s.queries > s.stale_after) {
-    s.stale = true;
-    return AMDSMI_STATUS_NOT_INIT;
+  std::mutex* dev = nullptr;
+  long latency = 0;
+  {
+    std::lock_guard<std::mutex> g(s.mu);
+    if (!s.initialized) return AMDSMI_STATUS_NOT_INIT;
+    if (s.stale) return AMDSMI_STATUS_NOT_INIT;
+    if (s.stale_after >= 0 && ++s.queries > s.stale_after) {
+      s.stale = true;
+      return AMDSMI_STATUS_NOT_INIT;
+    }
+    *out = proc(h);
+    if (!*out) return AMDSMI_STATUS_INVAL;
+    latency = s.latency_us;
+    if (latency > 0 && !cheap) dev = s.device_mu[(*out)->bdf].get();
   }
-  *out = proc(h);
-  return *out ? AMDSMI_STATUS_SUCCESS : AMDSMI_STATUS_INVAL;
+  if (dev) {
+    // Like amd-smi's per-device mutex around its sysfs/ioctl work.
+    std::lock_guard<std::mutex> g(*dev);
+    auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(latency);
+    while (std::chrono::steady_clock::now() < until) {
+    }
+  }
+  return AMDSMI_STATUS_SUCCESS;
 }
 
 void copy(char* dst, size_t n, const std::string& src) {
@@ -101,6 +125,7 @@ int fake_amdsmi_configure(const char* spec) {
   s.procs.clear();
   s.init_status = 0;
   s.stale_after = -1;
+  s.latency_us = 0;
   s.queries = 0;
   s.stale = false;
   std::istringstream in(spec);
@@ -113,6 +138,10 @@ int fake_amdsmi_configure(const char* spec) {
     }
     if (line.rfind("stale_after=", 0) == 0) {
       s.stale_after = std::atol(line.c_str() + 12);
+      continue;
+    }
+    if (line.rfind("latency_us=", 0) == 0) {
+      s.latency_us = std::atol(line.c_str() + 11);
       continue;
     }
     Proc base;
@@ -144,6 +173,7 @@ int fake_amdsmi_configure(const char* spec) {
     for (int p = parts - 1; p >= 0; --p) {
       Proc q = base;
       q.partition_id = static_cast<uint32_t>(p);
+      if (!s.device_mu.count(q.bdf)) s.device_mu[q.bdf] = std::make_unique<std::mutex>();
       s.procs.push_back(q);
     }
   }
@@ -204,14 +234,14 @@ amdsmi_status_t amdsmi_get_processor_handles(amdsmi_socket_handle, uint32_t* cou
 
 amdsmi_status_t amdsmi_get_processor_type(amdsmi_processor_handle h, processor_type_t* t) {
   Proc* p;
-  if (auto st = check(h, &p)) return st;
+  if (auto st = check(h, &p, true)) return st;
   *t = AMDSMI_PROCESSOR_TYPE_AMD_GPU;
   return AMDSMI_STATUS_SUCCESS;
 }
 
 amdsmi_status_t amdsmi_get_gpu_device_bdf(amdsmi_processor_handle h, amdsmi_bdf_t* b) {
   Proc* p;
-  if (auto st = check(h, &p)) return st;
+  if (auto st = check(h, &p, true)) return st;
   std::memset(b, 0, sizeof(*b));
   b->domain_number = p->domain;
   b->bus_number = p->bus;
@@ -222,7 +252,7 @@ amdsmi_status_t amdsmi_get_gpu_device_bdf(amdsmi_processor_handle h, amdsmi_bdf_
 
 amdsmi_status_t amdsmi_get_gpu_asic_info(amdsmi_processor_handle h, amdsmi_asic_info_t* a) {
   Proc* p;
-  if (auto st = check(h, &p)) return st;
+  if (auto st = check(h, &p, true)) return st;
   std::memset(a, 0, sizeof(*a));
   copy(a->market_name, sizeof(a->market_name), p->name);
   a->vendor_id = 0x1002;

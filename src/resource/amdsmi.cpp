@@ -154,6 +154,22 @@ bool has_amdsmi(std::string* reason) {
 
 namespace {
 
+// A failed amd-smi call.  The status (not the message) decides whether the
+// persistent session's handles went stale.
+class CallError : public Error {
+ public:
+  CallError(const std::string& msg, amdsmi_status_t st) : Error(msg), status(st) {}
+  amdsmi_status_t status;
+};
+
+[[noreturn]] void call_failed(AmdSmiLib& L, const char* fn, amdsmi_status_t st) {
+  throw CallError(std::string(fn) + ": " + L.status_str(st), st);
+}
+
+// Statuses meaning "the session/handles are stale; re-initialise": a
+// processor handle from before a driver reload or partition switch.
+bool is_stale(amdsmi_status_t st) { return st == AMDSMI_STATUS_NOT_INIT || st == AMDSMI_STATUS_NOT_FOUND; }
+
 // Raw per-processor facts (one amd-smi processor = a GPU or a partition).
 struct ProcInfo {
   amdsmi_processor_handle h = nullptr;
@@ -248,7 +264,7 @@ void query_proc(AmdSmiLib& L, const std::string& root, ProcInfo& p) {
   amdsmi_asic_info_t asic;
   std::memset(&asic, 0, sizeof(asic));
   amdsmi_status_t st = AMDSMI_CALL("asic_info", L.get_gpu_asic_info(p.h, &asic));
-  if (st != AMDSMI_STATUS_SUCCESS) throw Error("amdsmi_get_gpu_asic_info: " + L.status_str(st));
+  if (st != AMDSMI_STATUS_SUCCESS) call_failed(L, "amdsmi_get_gpu_asic_info", st);
   p.market_name = str::trim(asic.market_name);
   p.vendor_id = asic.vendor_id;
   p.device_id = static_cast<uint32_t>(asic.device_id);
@@ -388,12 +404,6 @@ std::string format_bdf(const amdsmi_bdf_t& b) {
                      static_cast<unsigned>(b.function_number));
 }
 
-// Statuses meaning "the session/handles are stale; re-initialise".
-bool is_stale(const std::string& msg) {
-  return msg.find("NOT_INIT") != std::string::npos || msg.find("NOT_FOUND") != std::string::npos ||
-         msg.find("not initialized") != std::string::npos || msg.find("not found") != std::string::npos ||
-         msg.find("status 32") != std::string::npos || msg.find("status 31") != std::string::npos;
-}
 
 }  // namespace
 
@@ -462,8 +472,8 @@ std::vector<DevicePtr> AmdSmiManager::GetDevices() {
   if (have_snapshot_) return snapshot_;
   try {
     snapshot_ = snapshot();
-  } catch (const Error& e) {
-    if (!opts_.persistent || !is_stale(e.what())) throw;
+  } catch (const CallError& e) {
+    if (!opts_.persistent || !is_stale(e.status)) throw;
     log::printf("amd-smi handles are stale (%s); re-initializing", e.what());
     library_shutdown();
     library_init();
@@ -480,11 +490,11 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
   int64_t handles_t0 = trace::now_ns();
   uint32_t ns = 0;
   amdsmi_status_t st = L.get_socket_handles(&ns, nullptr);
-  if (st != AMDSMI_STATUS_SUCCESS) throw Error("amdsmi_get_socket_handles: " + L.status_str(st));
+  if (st != AMDSMI_STATUS_SUCCESS) call_failed(L, "amdsmi_get_socket_handles", st);
   std::vector<amdsmi_socket_handle> sockets(ns);
   if (ns) {
     st = L.get_socket_handles(&ns, sockets.data());
-    if (st != AMDSMI_STATUS_SUCCESS) throw Error("amdsmi_get_socket_handles: " + L.status_str(st));
+    if (st != AMDSMI_STATUS_SUCCESS) call_failed(L, "amdsmi_get_socket_handles", st);
     sockets.resize(ns);
   }
 
@@ -493,11 +503,11 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
   for (auto s : sockets) {
     uint32_t np = 0;
     st = L.get_processor_handles(s, &np, nullptr);
-    if (st != AMDSMI_STATUS_SUCCESS) throw Error("amdsmi_get_processor_handles: " + L.status_str(st));
+    if (st != AMDSMI_STATUS_SUCCESS) call_failed(L, "amdsmi_get_processor_handles", st);
     std::vector<amdsmi_processor_handle> procs(np);
     if (np) {
       st = L.get_processor_handles(s, &np, procs.data());
-      if (st != AMDSMI_STATUS_SUCCESS) throw Error("amdsmi_get_processor_handles: " + L.status_str(st));
+      if (st != AMDSMI_STATUS_SUCCESS) call_failed(L, "amdsmi_get_processor_handles", st);
       procs.resize(np);
     }
     for (auto h : procs) {
@@ -506,7 +516,7 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
       amdsmi_bdf_t b;
       std::memset(&b, 0, sizeof(b));
       st = L.get_gpu_device_bdf(h, &b);
-      if (st != AMDSMI_STATUS_SUCCESS) throw Error("amdsmi_get_gpu_device_bdf: " + L.status_str(st));
+      if (st != AMDSMI_STATUS_SUCCESS) call_failed(L, "amdsmi_get_gpu_device_bdf", st);
       ProcInfo p;
       p.h = h;
       p.bdf = format_bdf(b);
@@ -522,7 +532,7 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
     std::string bdf;
     std::vector<ProcInfo>* procs;
     GpuExtras extras;
-    std::string error;
+    std::exception_ptr error;
   };
   std::vector<Gpu> gpus;
   int index = -1;
@@ -550,14 +560,14 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
       bool partitioned = g.procs->size() > 1 || (!first.compute_partition.empty() && first.compute_partition != "SPX");
       trace::Span s("amdsmi.extras");
       query_gpu_extras(L, first, opts_.root, partitioned, g.extras);
-    } catch (const std::exception& e) {
-      g.error = e.what();
+    } catch (...) {
+      g.error = std::current_exception();
     }
   };
   size_t threads = opts_.threads > 0 ? static_cast<size_t>(opts_.threads) : 8;
   WorkerPool::instance().parallel_for(gpus.size(), [&](size_t i) { work(gpus[i]); }, threads);
   for (const auto& g : gpus)
-    if (!g.error.empty()) throw Error(g.error);
+    if (g.error) std::rethrow_exception(g.error);
   for (const auto& g : gpus)
     if (!g.extras.virtualization.empty()) virt_mode_[g.bdf] = g.extras.virtualization;
 

@@ -25,6 +25,7 @@ from dataclasses import dataclass, field
 from pathlib import Path
 
 MI355X_DEVICE_ID = 0x75A3
+MI355X_VF_DEVICE_ID = 0x75B3
 MI355X_VRAM_BYTES = 309220868096  # 294896 MiB, as reported by amdgpu
 MI355X_CUS = 256
 MI355X_XCDS = 8
@@ -47,6 +48,9 @@ class GpuSpec:
     # True: the KFD nodes of this GPU are not readable (not allocated to the
     # container), like the other 7 GPUs on a 1-GPU pool box.
     hidden: bool = False
+    # True: this GPU is an SR-IOV virtual function handed to a guest VM (VF
+    # device ID, no SR-IOV capability of its own, no physfn link).
+    vf: bool = False
 
 
 @dataclass
@@ -59,6 +63,7 @@ class NodeSpec:
     privileged: bool = False  # full 4 KiB config space readable
     seed: int = 0
     hive_size: int = 8  # GPUs per xGMI hive (MI355X platforms: 8)
+    hypervisor: bool = False  # CPU "hypervisor" flag (running inside a VM)
 
 
 def _write(path: Path, text: str | bytes) -> None:
@@ -121,7 +126,7 @@ def _kfd_properties(spec: GpuSpec, parts: int, location: int, render: int, uniqu
         "max_slots_scratch_cu": 32,
         "gfx_target_version": spec.gfx_target_version,
         "vendor_id": 4098,
-        "device_id": spec.device_id,
+        "device_id": MI355X_VF_DEVICE_ID if spec.vf else spec.device_id,
         "location_id": location,
         "domain": 0,
         "drm_render_minor": render,
@@ -153,6 +158,9 @@ def make_node(root: str | os.PathLike, spec: NodeSpec) -> Path:
     _write(root / "sys/module/amdgpu/version", spec.driver_version + "\n")
     _write(root / "opt/rocm/.info/version", spec.rocm_version + "\n")
     _write(root / "sys/class/dmi/id/product_name", spec.machine + "\n")
+    flags = "fpu vme de pse tsc msr pae mce cx8 apic sep mtrr" + (" hypervisor" if spec.hypervisor else "") + " lahf_lm"
+    _write(root / "proc/cpuinfo", "processor\t: 0\nvendor_id\t: AuthenticAMD\nmodel name\t: AMD EPYC 9575F 64-Core "
+           f"Processor\nflags\t\t: {flags}\n\n")
     (root / "sys/bus/pci/devices").mkdir(parents=True, exist_ok=True)
 
     node = 0
@@ -187,10 +195,11 @@ def make_node(root: str | os.PathLike, spec: NodeSpec) -> Path:
             node += 1
             render += 1
         d = root / "sys/bus/pci/devices" / bdf
+        device_id = MI355X_VF_DEVICE_ID if g.vf else g.device_id
         _write(d / "vendor", "0x1002\n")
-        _write(d / "device", f"0x{g.device_id:04x}\n")
+        _write(d / "device", f"0x{device_id:04x}\n")
         _write(d / "subsystem_vendor", "0x1002\n")
-        _write(d / "subsystem_device", f"0x{g.device_id:04x}\n")
+        _write(d / "subsystem_device", f"0x{device_id:04x}\n")
         _write(d / "class", "0x120000\n")
         _write(d / "revision", "0x00\n")
         _write(d / "product_name", g.product_name + "\n")
@@ -207,9 +216,10 @@ def make_node(root: str | os.PathLike, spec: NodeSpec) -> Path:
         peers[gi % spec.hive_size] = "00"
         _write(d / "xgmi_num_links", " ".join(peers) + " \n")
         sriov = g.sriov or {}
-        _write(d / "sriov_totalvfs", f"{sriov.get('total', 1)}\n")
-        _write(d / "sriov_numvfs", f"{sriov.get('num', 0)}\n")
-        _write(d / "config", config_space(g.device_id, g.sriov, 4096 if spec.privileged else 64))
+        if not g.vf:
+            _write(d / "sriov_totalvfs", f"{sriov.get('total', 1)}\n")
+            _write(d / "sriov_numvfs", f"{sriov.get('num', 0)}\n")
+        _write(d / "config", config_space(device_id, g.sriov, 4096 if spec.privileged else 64))
         for v in range(sriov.get("num", 0)):
             vf_bdf = f"0000:{bus:02x}:00.{v + 1}"
             vd = root / "sys/bus/pci/devices" / vf_bdf

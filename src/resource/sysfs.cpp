@@ -4,6 +4,7 @@
 #include <cerrno>
 #include <map>
 
+#include "resource/pci_ids.h"
 #include "resource/versions.h"
 #include "util/error.h"
 #include "util/fs.h"
@@ -127,22 +128,31 @@ std::string uuid_of(uint64_t unique_id, uint64_t device_id) {
 }
 
 // Fallback names when the board FRU does not expose product_name.
-std::string name_from_device_id(uint64_t device_id) {
-  switch (device_id) {
-    case 0x75a3: return "AMD Instinct MI355X";
-    case 0x75a0: return "AMD Instinct MI350X";
-    case 0x74a5: return "AMD Instinct MI325X";
-    case 0x74a1: return "AMD Instinct MI300X";
-    case 0x74a9: return "AMD Instinct MI300X HF";
-    case 0x74a0: return "AMD Instinct MI300A";
-    case 0x740c: return "AMD Instinct MI250X/MI250";
-    case 0x740f: return "AMD Instinct MI210";
-    case 0x738c: return "AMD Instinct MI100";
-    default: return str::format("AMD-GPU-0x%04llx", static_cast<unsigned long long>(device_id));
-  }
+
+// amdgpu's own classification (amdgpu_detect_virtualization), from what a
+// container can see: an SR-IOV virtual function runs as a guest; a physical
+// function with VFs enabled is the host; a whole GPU inside a VM is
+// passthrough; otherwise bare metal.
+std::string virtualization_mode(const std::string& pci, uint32_t device_id, bool in_vm) {
+  if (is_mxgpu_vf(device_id) || fs::exists(fs::join(pci, "physfn"))) return "guest";
+  if (auto nv = fs::read_trimmed(fs::join(pci, "sriov_numvfs")); nv && str::parse_uint(*nv).value_or(0) > 0)
+    return "host";
+  return in_vm ? "passthrough" : "baremetal";
 }
 
 }  // namespace
+
+bool running_in_vm(const std::string& root) {
+  // The first processor's "flags" line is enough (reading all of
+  // /proc/cpuinfo on a 256-thread host is ~400 KB).
+  auto r = fs::read_file(fs::join(root, "proc/cpuinfo"), 16384);
+  if (!r.ok()) return false;
+  auto flags = r.data.find("\nflags");
+  if (flags == std::string::npos) return false;
+  auto eol = r.data.find('\n', flags + 1);
+  std::string line = r.data.substr(flags, eol == std::string::npos ? std::string::npos : eol - flags);
+  return (line + " ").find(" hypervisor ") != std::string::npos;
+}
 
 bool has_kfd_topology(const std::string& root, std::string* reason) {
   std::string dir = fs::join(root, kTopology);
@@ -156,7 +166,10 @@ bool has_kfd_topology(const std::string& root, std::string* reason) {
   return true;
 }
 
-SysfsManager::SysfsManager(SysfsOptions opts) : opts_(std::move(opts)) { topology_ = fs::join(opts_.root, kTopology); }
+SysfsManager::SysfsManager(SysfsOptions opts) : opts_(std::move(opts)) {
+  topology_ = fs::join(opts_.root, kTopology);
+  in_vm_ = running_in_vm(opts_.root);
+}
 
 void SysfsManager::Init() {
   int err = 0;
@@ -218,16 +231,13 @@ std::vector<DevicePtr> SysfsManager::enumerate() const {
     info.uuid = uuid_of(first.unique_id, first.device_id);
     info.gfx = gfx_target_from_kfd(first.gfx_target_version);
     auto product = fs::read_trimmed(fs::join(pci, "product_name"));
-    info.name = product && !product->empty() ? *product : name_from_device_id(first.device_id);
+    info.name = product && !product->empty() ? *product : device_name(static_cast<uint32_t>(first.device_id));
     info.compute_partition = fs::read_trimmed(fs::join(pci, "current_compute_partition")).value_or("");
     info.memory_partition = fs::read_trimmed(fs::join(pci, "current_memory_partition")).value_or("");
     info.available_compute_partitions = split_list(fs::read_trimmed(fs::join(pci, "available_compute_partition")).value_or(""));
     info.available_memory_partitions = split_list(fs::read_trimmed(fs::join(pci, "available_memory_partition")).value_or(""));
     if (auto x = fs::read_trimmed(fs::join(pci, "xgmi_num_links"))) info.xgmi_links = sum_links(*x);
-    if (auto nv = fs::read_trimmed(fs::join(pci, "sriov_numvfs")); nv && str::parse_uint(*nv).value_or(0) > 0)
-      info.virtualization = "host";
-    else
-      info.virtualization = fs::exists(fs::join(pci, "physfn")) ? "guest" : "baremetal";
+    info.virtualization = virtualization_mode(pci, info.device_id, in_vm_);
 
     bool partitioned = members.size() > 1 || (!info.compute_partition.empty() && info.compute_partition != "SPX");
     uint64_t vram = 0;

@@ -49,10 +49,14 @@ class SysfsManager : public Manager {
  private:
   SysfsOptions opts_;
   std::string topology_;
+  bool in_vm_ = false;  // CPU reports a hypervisor (fixed for the process)
   bool initialized_ = false;
   bool have_snapshot_ = false;
   std::vector<DevicePtr> snapshot_;
 };
+
+// True if <root>/proc/cpuinfo reports the "hypervisor" CPU flag.
+bool running_in_vm(const std::string& root);
 
 // True if a KFD topology is present under `root`.
 bool has_kfd_topology(const std::string& root, std::string* reason);

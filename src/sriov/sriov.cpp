@@ -1,5 +1,6 @@
 #include "sriov/sriov.h"
 
+#include "resource/pci_ids.h"
 #include "util/error.h"
 #include "util/strings.h"
 
@@ -19,14 +20,7 @@ std::optional<SriovCapability> parse_sriov_capability(const std::string& cap) {
   return c;
 }
 
-bool is_vf_device_id(const std::string& device_id) {
-  // Instinct MxGPU virtual functions (MI300X, MI325X, MI355X).
-  static const char* kVfIds[] = {"0x74b5", "0x74b9", "0x75b3"};
-  std::string d = str::to_lower(str::trim(device_id));
-  for (const char* id : kVfIds)
-    if (d == id) return true;
-  return false;
-}
+bool is_vf_device_id(const std::string& device_id) { return resource::is_mxgpu_vf(device_id); }
 
 std::optional<Info> Lib::Classify(const PCIDevice& d) {
   if (!d.physfn.empty()) {

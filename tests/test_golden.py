@@ -199,3 +199,30 @@ def test_amdsmi_and_sysfs_label_sets_are_identical_in_shape(binary, tmp_path):
     root = synth.make_mi355x_node(tmp_path / "root", n_gpus=1)
     keys = set(golden.parse_labels(_oneshot(binary, tmp_path, "--backend=sysfs", sysfs_root=str(root), timestamp=True)))
     assert len(keys) == len(golden.load_regexes(TESTS / "expected-output.txt"))
+
+
+def test_synthetic_sriov_vf_nps4_mixed(binary, tmp_path):
+    """BASELINE config 5: an MxGPU guest - SR-IOV virtual functions in
+    QPX/NPS4 - under the mixed strategy (the reference's vGPU + MIG-mixed
+    analogue)."""
+    spec = synth.NodeSpec(gpus=[synth.GpuSpec(vf=True, compute_partition="QPX", memory_partition="NPS4")
+                                for _ in range(2)], hypervisor=True, seed=9)
+    root = synth.make_node(tmp_path / "root", spec)
+    text = _oneshot(binary, tmp_path, "--backend=sysfs", "--mig-strategy=mixed", sysfs_root=str(root))
+    golden.check_byte_golden(text, GOLDEN / "synthetic-sriov-vf-nps4-mixed.txt", UPDATE)
+    # A guest VF has no VFs of its own: present + role only.
+    golden.check_regex_golden(text, TESTS / "expected-output-sriov-vf.txt", select=lambda ln: "sriov" in ln)
+    labels = golden.parse_labels(text)
+    assert labels["amd.com/sriov.role"] == "vf"
+    assert labels["amd.com/gpu.virtualization-mode"] == "guest"
+    assert labels["amd.com/gpu.memory-partition"] == "NPS4"
+    assert labels["amd.com/partition-qpx.2xcd.72gb.count"] == "8"
+    assert labels["amd.com/partition-qpx.2xcd.72gb.memory-partition"] == "NPS4"
+
+
+def test_synthetic_passthrough_vm(binary, tmp_path):
+    """A whole GPU passed through to a VM: hypervisor CPU flag, no SR-IOV."""
+    root = synth.make_node(tmp_path / "root", synth.NodeSpec(gpus=[synth.GpuSpec()], hypervisor=True, seed=10))
+    labels = golden.parse_labels(_oneshot(binary, tmp_path, "--backend=sysfs", sysfs_root=str(root)))
+    assert labels["amd.com/gpu.virtualization-mode"] == "passthrough"
+    assert not any("sriov" in k for k in labels)

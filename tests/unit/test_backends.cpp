@@ -10,6 +10,7 @@
 #include "resource/factory.h"
 #include "resource/filter.h"
 #include "resource/managers.h"
+#include "resource/pci_ids.h"
 #include "resource/sysfs.h"
 #include "resource/versions.h"
 #include "test.h"
@@ -259,4 +260,24 @@ TEST(AmdSmi_InitFailsCleanlyWithoutDriver) {
   AmdSmiManager m(AmdSmiOptions{});
   EXPECT_THROW_MSG(m.Init(), "amdsmi_init failed");
   EXPECT_EQ(m.init_count(), 0);
+}
+
+TEST(PciIds_NamesAndVirtualFunctions) {
+  EXPECT_EQ(device_name(0x75a3), std::string("AMD Instinct MI355X"));
+  EXPECT_EQ(device_name(0x1234), std::string("AMD-GPU-0x1234"));
+  EXPECT_TRUE(is_mxgpu_vf(0x75b3));
+  EXPECT_TRUE(is_mxgpu_vf(std::string("0x74B5\n")));
+  EXPECT_FALSE(is_mxgpu_vf(0x75a3));
+  EXPECT_FALSE(is_mxgpu_vf(std::string("garbage")));
+}
+
+TEST(Sysfs_HypervisorFlagFromFirstCpu) {
+  Tree t;
+  EXPECT_FALSE(running_in_vm(t.root));  // no /proc/cpuinfo under the root
+  put(t.root + "/proc/cpuinfo", "processor\t: 0\nflags\t\t: fpu vme hypervisor lahf_lm\n\nprocessor\t: 1\n");
+  EXPECT_TRUE(running_in_vm(t.root));
+  put(t.root + "/proc/cpuinfo", "processor\t: 0\nflags\t\t: fpu vme hypervisorx\n");
+  EXPECT_FALSE(running_in_vm(t.root));
+  put(t.root + "/proc/cpuinfo", "processor\t: 0\nflags\t\t: fpu hypervisor\n");
+  EXPECT_TRUE(running_in_vm(t.root));  // flag at the end of the line
 }

@@ -100,8 +100,15 @@ def test_soak_sysfs_backend_no_growth(binary, tmp_path):
 
 @pytest.mark.gpu
 @pytest.mark.skipif(not has_amd_gpu(), reason="no /dev/kfd")
-def test_soak_amdsmi_backend_no_growth(binary, tmp_path):
+@pytest.mark.parametrize("session", ["persistent", "per-cycle"])
+def test_soak_amdsmi_backend_no_growth(binary, tmp_path, session):
+    # GFD_SOAK_SECONDS stretches the run for release qualification.
+    seconds = float(os.environ.get("GFD_SOAK_SECONDS", "20"))
     out = tmp_path / "gfd"
-    r = soak(binary, ["--backend=amdsmi", f"--output-file={out}"], seconds=20, hup_at=10)
-    _assert_steady(r, min_cycles=5000)
+    r = soak(binary, ["--backend=amdsmi", f"--amdsmi-session={session}", f"--output-file={out}"], seconds=seconds,
+             hup_at=seconds / 2)
+    # per-cycle pays ~25 ms of amdsmi_init every cycle.
+    _assert_steady(r, min_cycles=int(seconds * (200 if session == "persistent" else 20)))
     assert r["reloads"] == 1, r["tail"]
+    print(f"soak[{session}]: {r['cycles']} cycles in {seconds:.0f}s, RSS {r['rss0']} -> {r['rss1']} KiB, "
+          f"fds {r['fd0']} -> {r['fd1']}")

@@ -6,6 +6,12 @@
 #include "sriov/pci.h"
 #include "sriov/sriov.h"
 #include "test.h"
+#include "util/fs.h"
+#include "util/strings.h"
+
+#include <unistd.h>
+
+#include <cstdio>
 
 using namespace gfd;
 using namespace gfd::sriov;
@@ -176,4 +182,91 @@ TEST(Sriov_LabelerEmptyWhenNoFunctions) {
 TEST(Sriov_SysfsScanMissingRootErrors) {
   auto lib = new_sriov_lib("/nonexistent-gfd-root");
   EXPECT_THROW_MSG(lib->Devices(), "unable to read PCI bus devices");
+}
+
+namespace {
+void put_file(const std::string& path, const std::string& content) {
+  fs::mkdir_all(fs::dirname(path));
+  FILE* f = std::fopen(path.c_str(), "w");
+  if (!f) throw std::runtime_error("cannot write " + path);
+  std::fputs(content.c_str(), f);
+  std::fclose(f);
+}
+
+// A host with `filler` non-AMD functions, 4 MI355X PFs without VFs and one
+// PF (0000:c1:00.0) with `vfs` VFs enabled.
+std::string pci_host(int filler, int vfs) {
+  char d[] = "/tmp/gfd-pci-XXXXXX";
+  if (!mkdtemp(d)) throw std::runtime_error("mkdtemp");
+  std::string dev = std::string(d) + "/sys/bus/pci/devices/";
+  for (int i = 0; i < filler; ++i) {
+    std::string p = dev + str::format("0000:%02x:%02x.%d", i / 32, i % 32, 0);
+    put_file(p + "/vendor", "0x1022\n");
+    put_file(p + "/class", "0x060000\n");
+  }
+  auto gpu = [&](const std::string& bdf, int total, int num) {
+    put_file(dev + bdf + "/vendor", "0x1002\n");
+    put_file(dev + bdf + "/class", "0x120000\n");
+    put_file(dev + bdf + "/device", "0x75a3\n");
+    put_file(dev + bdf + "/sriov_totalvfs", std::to_string(total) + "\n");
+    put_file(dev + bdf + "/sriov_numvfs", std::to_string(num) + "\n");
+    put_file(dev + bdf + "/sriov_vf_device", "0x75b3\n");
+  };
+  for (int g = 0; g < 4; ++g) gpu(str::format("0000:%02x:00.0", 0x11 + 0x10 * g), 1, 0);
+  gpu("0000:c1:00.0", 8, vfs);
+  for (int v = 0; v < vfs; ++v) {
+    std::string p = dev + str::format("0000:c1:00.%d", v + 1);
+    put_file(p + "/vendor", "0x1002\n");
+    put_file(p + "/class", "0x120000\n");
+    put_file(p + "/device", "0x75b3\n");
+    if (symlink("../0000:c1:00.0", (p + "/physfn").c_str()) != 0) throw std::runtime_error("symlink");
+  }
+  return d;
+}
+}  // namespace
+
+TEST(Sriov_SysfsScanColdParallelThenIncremental) {
+  // 200 filler functions force the parallel cold-scan path (>16 misses).
+  std::string root = pci_host(200, 2);
+  SysfsAmdPCI pci(root);
+  auto devs = pci.Devices();
+  EXPECT_EQ(devs.size(), static_cast<size_t>(7));  // 4 PFs + 1 PF with 2 VFs
+  int pfs_with_vfs = 0, vfs = 0;
+  for (const auto& d : devs) {
+    if (d.sriov_numvfs > 0) {
+      ++pfs_with_vfs;
+      EXPECT_EQ(d.address, std::string("0000:c1:00.0"));
+      EXPECT_EQ(d.sriov_totalvfs, 8);
+      EXPECT_EQ(d.sriov_vf_device, std::string("0x75b3"));
+    }
+    if (!d.physfn.empty()) {
+      ++vfs;
+      EXPECT_EQ(d.physfn, std::string("0000:c1:00.0"));
+    }
+    if (d.sriov_numvfs == 0) EXPECT_EQ(d.sriov_vf_device, std::string(""));
+  }
+  EXPECT_EQ(pfs_with_vfs, 1);
+  EXPECT_EQ(vfs, 2);
+  // Mutable state is re-read every scan.
+  put_file(root + "/sys/bus/pci/devices/0000:11:00.0/sriov_numvfs", "1\n");
+  int on = 0;
+  for (const auto& d : pci.Devices())
+    if (d.address == "0000:11:00.0") on = d.sriov_numvfs;
+  EXPECT_EQ(on, 1);
+  // A function removed and re-created (new sysfs inode) is re-identified.
+  // (Parked elsewhere, not deleted, so this filesystem cannot hand the new
+  // directory the old inode number - kernfs allocates them cyclically.)
+  if (rename((root + "/sys/bus/pci/devices/0000:21:00.0").c_str(), (root + "/parked").c_str()) != 0)
+    throw std::runtime_error("rename");
+  put_file(root + "/sys/bus/pci/devices/0000:21:00.0/vendor", "0x8086\n");
+  put_file(root + "/sys/bus/pci/devices/0000:21:00.0/class", "0x020000\n");
+  bool still_there = false;
+  for (const auto& d : pci.Devices()) still_there |= d.address == "0000:21:00.0";
+  EXPECT_FALSE(still_there);
+  // Errors from the parallel cold scan surface like serial ones.
+  SysfsAmdPCI cold(root);
+  fs::remove_all(root + "/sys/bus/pci/devices/0000:00:05.0/vendor");
+  fs::mkdir_all(root + "/sys/bus/pci/devices/0000:00:05.0/vendor");  // unreadable attribute
+  EXPECT_THROW_MSG(cold.Devices(), "unable to read PCI device vendor id for 0000:00:05.0");
+  fs::remove_all(root);
 }

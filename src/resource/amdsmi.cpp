@@ -9,12 +9,13 @@
 #include <map>
 #include <mutex>
 
-#include "util/pool.h"
+#include "resource/pci_ids.h"
 #include "resource/versions.h"
 #include "util/dynlib.h"
 #include "util/error.h"
 #include "util/fs.h"
 #include "util/log.h"
+#include "util/pool.h"
 #include "util/strings.h"
 #include "util/trace.h"
 
@@ -270,6 +271,9 @@ void query_proc(AmdSmiLib& L, const std::string& root, ProcInfo& p) {
   p.device_id = static_cast<uint32_t>(asic.device_id);
   p.cus = asic.num_of_compute_units == 0xFFFFFFFFu ? 0 : asic.num_of_compute_units;
   p.gfx = asic.target_graphics_version;
+  // amd-smi's UUID is a spelling of the ASIC serial: derive it here instead
+  // of paying amdsmi_get_gpu_device_uuid per processor.
+  if (auto serial = str::parse_uint_auto(str::trim(asic.asic_serial))) p.uuid = amd_uuid(*serial, p.device_id);
 
   uint64_t total = 0;
   if (AMDSMI_CALL("memory_total", L.get_gpu_memory_total(p.h, AMDSMI_MEM_TYPE_VRAM, &total)) == AMDSMI_STATUS_SUCCESS)
@@ -578,6 +582,7 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
     info.index = g.index;
     info.bdf = g.bdf;
     info.name = first.market_name;
+    info.uuid = first.uuid;
     info.vendor_id = first.vendor_id;
     info.device_id = first.device_id;
     info.gfx = gfx_target_from_amdsmi(first.gfx);
@@ -600,6 +605,7 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
       DeviceInfo pi;
       pi.partition_id = static_cast<int>(p.partition_id);
       pi.bdf = g.bdf;
+      pi.uuid = p.uuid;
       pi.vendor_id = p.vendor_id;
       pi.device_id = p.device_id;
       pi.compute_units = p.cus;

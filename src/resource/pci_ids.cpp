@@ -40,4 +40,11 @@ bool is_mxgpu_vf(const std::string& device_id) {
   return v && is_mxgpu_vf(static_cast<uint32_t>(*v));
 }
 
+std::string amd_uuid(uint64_t unique_id, uint32_t device_id) {
+  if (unique_id == 0) return "";
+  return str::format("%02xff%04x-0000-1000-80%02x-%012llx", static_cast<unsigned>(unique_id >> 56),
+                     static_cast<unsigned>(device_id & 0xffff), static_cast<unsigned>((unique_id >> 48) & 0xff),
+                     static_cast<unsigned long long>(unique_id & 0xffffffffffffULL));
+}
+
 }  // namespace gfd::resource

@@ -20,4 +20,10 @@ bool is_mxgpu_vf(uint32_t device_id);
 // Same, for the sysfs spelling "0x75b3".
 bool is_mxgpu_vf(const std::string& device_id);
 
+// The UUID spelling amd-smi reports, derived from the ASIC serial
+// (KFD `unique_id`, amd-smi `asic_serial`) and device ID - measured on the
+// pool: serial 0x3a7c178b7c5e4d5c, device 0x75a3 ->
+// "3aff75a3-0000-1000-807c-178b7c5e4d5c".  "" for serial 0.
+std::string amd_uuid(uint64_t unique_id, uint32_t device_id);
+
 }  // namespace gfd::resource

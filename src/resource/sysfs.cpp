@@ -118,14 +118,6 @@ std::string bdf_of(const KfdNode& n) {
   return str::format("%04x:%02x:%02x.%x", static_cast<unsigned>(n.domain), bus, dev, fn);
 }
 
-// Same UUID spelling amd-smi reports (measured: unique_id 0x3a7c178b7c5e4d5c,
-// device 0x75a3 -> "3aff75a3-0000-1000-807c-178b7c5e4d5c").
-std::string uuid_of(uint64_t unique_id, uint64_t device_id) {
-  if (unique_id == 0) return "";
-  return str::format("%02xff%04x-0000-1000-80%02x-%012llx", static_cast<unsigned>(unique_id >> 56),
-                     static_cast<unsigned>(device_id & 0xffff), static_cast<unsigned>((unique_id >> 48) & 0xff),
-                     static_cast<unsigned long long>(unique_id & 0xffffffffffffULL));
-}
 
 // Fallback names when the board FRU does not expose product_name.
 
@@ -228,7 +220,7 @@ std::vector<DevicePtr> SysfsManager::enumerate() const {
     info.bdf = bdf;
     info.vendor_id = static_cast<uint32_t>(first.vendor_id);
     info.device_id = static_cast<uint32_t>(first.device_id);
-    info.uuid = uuid_of(first.unique_id, first.device_id);
+    info.uuid = amd_uuid(first.unique_id, static_cast<uint32_t>(first.device_id));
     info.gfx = gfx_target_from_kfd(first.gfx_target_version);
     auto product = fs::read_trimmed(fs::join(pci, "product_name"));
     info.name = product && !product->empty() ? *product : device_name(static_cast<uint32_t>(first.device_id));

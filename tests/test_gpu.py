@@ -150,3 +150,43 @@ def test_smoke_entry_point():
                         timeout=300, cwd=str(REPO), env={**os.environ})
     assert cp.returncode == 0, cp.stderr[-2000:]
     assert "smoke:" in cp.stdout
+
+
+AMD_SMI_CLI = "/opt/rocm/bin/amd-smi"
+
+
+def _amd_smi_json(*args: str):
+    cp = subprocess.run([AMD_SMI_CLI, *args, "--json"], capture_output=True, text=True, timeout=180)
+    assert cp.returncode == 0, cp.stderr[-2000:]
+    return json.loads(cp.stdout)
+
+
+@pytest.mark.skipif(not os.path.exists(AMD_SMI_CLI), reason="amd-smi CLI not installed")
+def test_devices_match_amd_smi_cli(amdsmi_devices, sysfs_devices):
+    """Independent oracle: AMD's own `amd-smi` tool (a separate Python
+    program over the same library) must report the same facts the labels
+    are built from, for both backends."""
+    static = {g["bus"]["bdf"]: g for g in _amd_smi_json("static")["gpu_data"]}
+    listed = {g["bdf"]: g for g in _amd_smi_json("list")}
+    part = _amd_smi_json("partition")
+    current = {p["gpu_id"]: p for p in part["current_partition"]}
+    memcaps = {p["gpu_id"]: p for p in part["memory_partition"]}
+    ports = {p["bdf"]: p["link_status"] for p in _amd_smi_json("xgmi")["link_port_status"]}
+    assert set(static) == {d["bdf"] for d in amdsmi_devices}
+    for backend in (amdsmi_devices, sysfs_devices):
+        for d in backend:
+            s = static[d["bdf"]]
+            gpu = s["gpu"]
+            assert d["name"] in (s["asic"]["market_name"], s["board"]["product_name"]), (d["name"], s["asic"])
+            assert d["device_id"] == int(s["asic"]["device_id"], 16)
+            assert d["vendor_id"] == int(s["asic"]["vendor_id"], 16)
+            assert d["gfx"] == s["asic"]["target_graphics_version"]
+            assert d["memory_mib"] == s["vram"]["size"]["value"] and s["vram"]["size"]["unit"] == "MB"
+            assert d["uuid"] == listed[d["bdf"]]["uuid"]
+            assert d["compute_partition"] == current[gpu]["accelerator_type"]
+            assert d["memory_partition"] == current[gpu]["memory"] == memcaps[gpu]["current_memory_partition"]
+            assert d["available_memory_partitions"] == [m.strip() for m in
+                                                        memcaps[gpu]["memory_partition_caps"].split(",")]
+            assert d["xgmi_links"] == sum(1 for x in ports[d["bdf"]] if x == "U")
+            if d["compute_partition"] == "SPX":
+                assert d["compute_units"] == s["asic"]["num_compute_units"]

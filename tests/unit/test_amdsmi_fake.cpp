@@ -175,6 +175,20 @@ TEST(AmdSmiFake_PersistentSessionInitsOnceAndReinitsOnTopologyChange) {
   fs::remove_all(root);
 }
 
+TEST(AmdSmiFake_UuidFromAsicSerial) {
+  REQUIRE_FAKE();
+  fake().configure(kTwoGpus);
+  std::string root = temp_root();
+  AmdSmiManager m(opts(root, true));
+  m.Init();
+  auto devs = m.GetDevices();
+  m.Shutdown();
+  // amd-smi's spelling (verified against `amd-smi list` on the pool).
+  EXPECT_EQ(devs[1]->Info().bdf, std::string("0000:d9:00.0"));
+  EXPECT_EQ(devs[1]->Info().uuid, std::string("3aff75a3-0000-1000-807c-178b7c5ed95c"));
+  fs::remove_all(root);
+}
+
 TEST(AmdSmiFake_VirtualizationModeQueriedOncePerSession) {
   REQUIRE_FAKE();
   fake().configure(kTwoGpus);

@@ -273,7 +273,11 @@ void query_proc(AmdSmiLib& L, const std::string& root, ProcInfo& p) {
   p.gfx = asic.target_graphics_version;
   // amd-smi's UUID is a spelling of the ASIC serial: derive it here instead
   // of paying amdsmi_get_gpu_device_uuid per processor.
-  if (auto serial = str::parse_uint_auto(str::trim(asic.asic_serial))) p.uuid = amd_uuid(*serial, p.device_id);
+  // The library spells the serial in hex, with or without "0x".
+  std::string serial_hex = str::trim(asic.asic_serial);
+  if (serial_hex.size() > 2 && serial_hex[0] == '0' && (serial_hex[1] == 'x' || serial_hex[1] == 'X'))
+    serial_hex.erase(0, 2);
+  if (auto serial = str::parse_uint(serial_hex, 16)) p.uuid = amd_uuid(*serial, p.device_id);
 
   uint64_t total = 0;
   if (AMDSMI_CALL("memory_total", L.get_gpu_memory_total(p.h, AMDSMI_MEM_TYPE_VRAM, &total)) == AMDSMI_STATUS_SUCCESS)

@@ -259,8 +259,10 @@ amdsmi_status_t amdsmi_get_gpu_asic_info(amdsmi_processor_handle h, amdsmi_asic_
   a->device_id = 0x75a3;
   a->num_of_compute_units = p->cus;
   a->target_graphics_version = 0x950;
-  // Like the pool's MI355X: a 64-bit serial, here derived from the bus.
-  copy(a->asic_serial, sizeof(a->asic_serial), "0x3A7C178B7C5E" + std::string(p->bdf.substr(5, 2)) + "5C");
+  // A 64-bit hex serial, here derived from the bus (the real library's
+  // spelling of the prefix varies; both forms are exercised).
+  copy(a->asic_serial, sizeof(a->asic_serial),
+       std::string(p->bus & 0x10 ? "0x" : "") + "3A7C178B7C5E" + std::string(p->bdf.substr(5, 2)) + "5C");
   return AMDSMI_STATUS_SUCCESS;
 }
 

@@ -185,7 +185,8 @@ TEST(AmdSmiFake_UuidFromAsicSerial) {
   m.Shutdown();
   // amd-smi's spelling (verified against `amd-smi list` on the pool).
   EXPECT_EQ(devs[1]->Info().bdf, std::string("0000:d9:00.0"));
-  EXPECT_EQ(devs[1]->Info().uuid, std::string("3aff75a3-0000-1000-807c-178b7c5ed95c"));
+  EXPECT_EQ(devs[1]->Info().uuid, std::string("3aff75a3-0000-1000-807c-178b7c5ed95c"));  // "0x..." serial
+  EXPECT_EQ(devs[0]->Info().uuid, std::string("3aff75a3-0000-1000-807c-178b7c5e235c"));  // bare hex serial
   fs::remove_all(root);
 }
 

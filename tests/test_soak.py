@@ -31,7 +31,14 @@ def _rss_kib(pid: int) -> int:
 
 
 def _fds(pid: int) -> int:
-    return len(os.listdir(f"/proc/{pid}/fd"))
+    # Minimum over a short window: a cycle in flight holds transient
+    # descriptors (the temp output file, an amd-smi device node), a leak
+    # raises the floor.
+    n = []
+    for _ in range(20):
+        n.append(len(os.listdir(f"/proc/{pid}/fd")))
+        time.sleep(0.01)
+    return min(n)
 
 
 def soak(binary: str, args: list[str], seconds: float, hup_at: float | None = None) -> dict:

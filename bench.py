@@ -38,14 +38,9 @@ import time
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
+from gpu_feature_discovery_amd.parallel import RankGroup, env_int  # noqa: E402
+
 METRIC = "label-file generation p50 latency (ms) + label-set correctness, 8×MI355X node"
-
-
-def _env_int(name: str, default: int) -> int:
-    try:
-        return int(os.environ.get(name, default))
-    except ValueError:
-        return default
 
 
 def _percentile(xs: list[float], q: float) -> float:
@@ -55,57 +50,6 @@ def _percentile(xs: list[float], q: float) -> float:
     k = (len(ys) - 1) * q
     lo, hi = int(k), min(int(k) + 1, len(ys) - 1)
     return ys[lo] + (ys[hi] - ys[lo]) * (k - lo)
-
-
-class _Dist:
-    """Barrier / max-reduce across ranks (gloo), or no-ops for one process."""
-
-    def __init__(self):
-        self.world = _env_int("WORLD_SIZE", 1)
-        self.rank = _env_int("RANK", 0)
-        self.torch = None
-        self.dist = None
-        try:
-            import torch  # noqa: F401
-
-            self.torch = torch
-        except Exception:
-            self.torch = None
-        if self.world > 1:
-            import torch.distributed as dist
-
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
-            self.dist = dist
-
-    def sync(self):
-        if self.dist is not None:
-            self.dist.barrier()
-        # The labeler issues no GPU work, so there is nothing to wait for; and
-        # creating a HIP context here would change what is measured: a process
-        # that already holds /dev/kfd makes amdsmi_init ~100x cheaper
-        # (measured: 26 ms -> 0.2 ms), which the real daemon never sees.
-        # Synchronize only if something else initialised the device.
-        if self.torch is not None and self.torch.cuda.is_initialized():
-            self.torch.cuda.synchronize()
-
-    def max(self, v: float) -> float:
-        if self.dist is None:
-            return v
-        t = self.torch.tensor([v], dtype=self.torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
-        return float(t.item())
-
-    def broadcast_obj(self, obj):
-        if self.dist is None:
-            return obj
-        lst = [obj]
-        self.dist.broadcast_object_list(lst, src=0)
-        return lst[0]
-
-    def close(self):
-        if self.dist is not None:
-            self.dist.destroy_process_group()
 
 
 def _check_labels(labels: dict, n_gpus: int, hardware: bool) -> list[str]:
@@ -205,16 +149,17 @@ def _cold_process(binary: str, args: list[str], runs: int) -> dict:
 
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
-    ap.add_argument("--gpus", type=int, default=_env_int("WORLD_SIZE", 1))
+    ap.add_argument("--gpus", type=int, default=env_int("WORLD_SIZE", 1))
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--backend", default="auto", help="auto | amdsmi | sysfs | synthetic")
     ap.add_argument("--no-extras", action="store_true", help="skip the secondary measurements")
     a = ap.parse_args()
 
-    dist = _Dist()
+    dist = RankGroup()
     import gpu_feature_discovery_amd as gfd
-    from gpu_feature_discovery_amd import synth
+    from gpu_feature_discovery_amd.ops import Labeler
+    from gpu_feature_discovery_amd.utils import synth
 
     g = gfd.native()
     g.set_quiet(True)
@@ -231,7 +176,7 @@ def main() -> int:
     if dist.rank == 0:
         if backend in ("auto", "amdsmi"):
             try:
-                devs = g.Session(["--backend=amdsmi", f"--visible-devices=0-{n - 1}"]).devices()
+                devs = Labeler(["--backend=amdsmi", f"--visible-devices=0-{n - 1}"]).devices()
                 hardware = len(devs) >= n
                 if not hardware and a.backend == "amdsmi":
                     raise SystemExit(f"amd-smi sees {len(devs)} GPU(s), fewer than --gpus {n}")
@@ -253,9 +198,8 @@ def main() -> int:
     if dist.rank == 0:
         sess_backend = "sysfs" if backend == "synthetic" else backend
         args = _session_args(sess_backend, n, out, root, [])
-        session = g.Session(args)
-        first = session.cycle(True)
-        labels = first["labels"]
+        session = Labeler(args)
+        labels = session.cycle(write=True).labels
         problems = _check_labels(labels, n, hardware)
         labels_ok = not problems
         # Warmup (untimed), in native code.
@@ -264,20 +208,17 @@ def main() -> int:
     # Timed region: exactly K steps, bracketed by barrier + synchronize.
     dist.sync()
     t0 = time.perf_counter_ns()
-    per_step_ns: list[int] = []
+    ms: list[float] = []
     if dist.rank == 0:
-        per_step_ns = session.bench(a.steps, 0, True)
+        ms = session.bench(a.steps, 0, True)
     dist.sync()
     wall_ms = (time.perf_counter_ns() - t0) / 1e6
     wall_ms = dist.max(wall_ms)
 
     if dist.rank == 0:
-        ms = [x / 1e6 for x in per_step_ns]
         p50 = _percentile(ms, 0.5)
         backend_name = session.backend
-        phases = {}
-        for name, ns_ in session.cycle(True)["phases"]:
-            phases[name] = round(ns_ / 1e6, 4)
+        phases = {name: round(v, 4) for name, v in session.cycle(write=True).phases_ms}
         # Release the persistent amd-smi session before measuring variants
         # that must pay amdsmi_init themselves.
         del session

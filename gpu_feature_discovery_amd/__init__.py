@@ -5,10 +5,10 @@ package holds the Python side used by the test-suite and ``bench.py``:
 
 * :mod:`._gfd` - pybind11 extension over the same native core (in-process
   labeling cycles, YAML/config parsing, device enumeration),
-* :mod:`.synth` - synthetic KFD/DRM/PCI sysfs trees (1-8 GPUs, SPX/CPX,
-  NPS1/NPS2, SR-IOV) with random device identities,
-* :mod:`.golden` - golden-file helpers (byte goldens and regex goldens),
-* :mod:`.build` - builds the native targets in-tree.
+* :mod:`.ops` - typed in-process API over it (:class:`~.ops.Labeler`),
+* :mod:`.models` - the MI355X device model (geometry, partition profiles),
+* :mod:`.parallel` - rank group for one-process-per-GPU runs (bench.py),
+* :mod:`.utils` - synthetic sysfs trees, golden-file helpers, in-tree build.
 
 Reference: Telemaco019/gpu-feature-discovery (NVIDIA GFD v0.7.0 fork); see
 SURVEY.md for the component mapping.

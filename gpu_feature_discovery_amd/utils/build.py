@@ -14,7 +14,7 @@ import subprocess
 import sys
 from pathlib import Path
 
-from . import BUILD_DIR, REPO_ROOT
+from .. import BUILD_DIR, REPO_ROOT
 
 
 def _jobs() -> str:
@@ -39,7 +39,7 @@ def build(build_type: str = "Release", extra_cmake_args: list[str] | None = None
 
 
 def is_built() -> bool:
-    from . import BINARY, PACKAGE_DIR, UNIT_TEST_BINARY
+    from .. import BINARY, PACKAGE_DIR, UNIT_TEST_BINARY
     return (BINARY.exists() and UNIT_TEST_BINARY.exists() and (BUILD_DIR / "libfake_amdsmi.so").exists()
             and any(PACKAGE_DIR.glob("_gfd*.so")))
 

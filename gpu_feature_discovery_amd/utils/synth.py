@@ -24,13 +24,15 @@ import struct
 from dataclasses import dataclass, field
 from pathlib import Path
 
-MI355X_DEVICE_ID = 0x75A3
-MI355X_VF_DEVICE_ID = 0x75B3
-MI355X_VRAM_BYTES = 309220868096  # 294896 MiB, as reported by amdgpu
-MI355X_CUS = 256
-MI355X_XCDS = 8
-PARTITIONS_PER_MODE = {"SPX": 1, "DPX": 2, "QPX": 4, "CPX": 8}
-NPS_COUNT = {"NPS1": 1, "NPS2": 2, "NPS4": 4, "NPS8": 8}
+from ..models import mi355x
+
+MI355X_DEVICE_ID = mi355x.DEVICE_ID
+MI355X_VF_DEVICE_ID = mi355x.VF_DEVICE_ID
+MI355X_VRAM_BYTES = mi355x.VRAM_BYTES  # 294896 MiB, as reported by amdgpu
+MI355X_CUS = mi355x.CUS
+MI355X_XCDS = mi355x.XCDS
+PARTITIONS_PER_MODE = mi355x.PARTITIONS_PER_MODE
+NPS_COUNT = mi355x.NPS_COUNT
 
 
 @dataclass

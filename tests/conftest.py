@@ -19,8 +19,8 @@ REPO = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(REPO))
 
 import gpu_feature_discovery_amd as gfd  # noqa: E402
-from gpu_feature_discovery_amd import build as gbuild  # noqa: E402
-from gpu_feature_discovery_amd import synth  # noqa: E402
+from gpu_feature_discovery_amd.utils import build as gbuild  # noqa: E402
+from gpu_feature_discovery_amd.utils import synth  # noqa: E402
 
 TESTS = Path(__file__).resolve().parent
 GOLDEN = TESTS / "golden"

@@ -21,7 +21,7 @@ from pathlib import Path
 REPO = Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(REPO))
 
-from gpu_feature_discovery_amd import golden  # noqa: E402
+from gpu_feature_discovery_amd.utils import golden  # noqa: E402
 
 
 def main() -> int:

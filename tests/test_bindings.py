@@ -6,7 +6,7 @@ from __future__ import annotations
 
 import pytest
 
-from gpu_feature_discovery_amd import golden, synth
+from gpu_feature_discovery_amd.utils import golden, synth
 
 
 def test_native_module_is_the_in_tree_extension(native):

@@ -18,7 +18,7 @@ from pathlib import Path
 import pytest
 
 from conftest import FIXTURES, run_daemon
-from gpu_feature_discovery_amd import golden, synth
+from gpu_feature_discovery_amd.utils import golden, synth
 
 
 def _base(tmp_path, out):

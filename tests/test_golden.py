@@ -20,7 +20,7 @@ from pathlib import Path
 import pytest
 
 from conftest import FIXTURES, GOLDEN, TESTS, run_daemon
-from gpu_feature_discovery_amd import golden, synth
+from gpu_feature_discovery_amd.utils import golden, synth
 
 UPDATE = os.environ.get("GFD_UPDATE_GOLDENS") == "1"
 

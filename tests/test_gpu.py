@@ -17,7 +17,7 @@ import sys
 import pytest
 
 from conftest import REPO, TESTS, has_amd_gpu, run_daemon
-from gpu_feature_discovery_amd import golden
+from gpu_feature_discovery_amd.utils import golden
 
 pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not has_amd_gpu(), reason="no /dev/kfd")]
 

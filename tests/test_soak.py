@@ -19,7 +19,7 @@ import time
 import pytest
 
 from conftest import has_amd_gpu
-from gpu_feature_discovery_amd import synth
+from gpu_feature_discovery_amd.utils import synth
 
 
 def _rss_kib(pid: int) -> int:

@@ -60,16 +60,22 @@ class WorkerPool {
   size_t workers() const;
 
  private:
+  struct Worker {
+    std::condition_variable cv;
+    bool woken = false;
+  };
   void ensure_workers(size_t n);
-  void loop();
+  void wake_one();
+  void loop(Worker* w);
 
   size_t max_workers_;
   mutable std::mutex mu_;
-  std::condition_variable cv_;
   std::deque<std::function<void()>> queue_;
+  std::vector<std::unique_ptr<Worker>> workers_;
   std::vector<std::thread> threads_;
-  size_t idle_ = 0;      // workers parked waiting for a task
-  size_t spawning_ = 0;  // threads created but not yet parked
+  std::vector<Worker*> idle_;  // parked workers, most recently parked last
+  size_t waking_ = 0;          // woken, not yet running
+  size_t spawning_ = 0;        // threads created but not yet parked
   bool stop_ = false;
 };
 

@@ -156,8 +156,14 @@ def main() -> int:
     ap.add_argument("--no-extras", action="store_true", help="skip the secondary measurements")
     a = ap.parse_args()
 
-    dist = RankGroup()
+    # Bind amd-smi to the system libdrm before anything imports PyTorch (which
+    # bundles its own copy; amd-smi bound to it loses the marketing-name
+    # table and pays a failed amdgpu.ids lookup on every ASIC query).  The
+    # production daemon never loads PyTorch, so this is what it measures.
     import gpu_feature_discovery_amd as gfd
+
+    gfd.native().load_amdsmi()
+    dist = RankGroup()
     from gpu_feature_discovery_amd.ops import Labeler
     from gpu_feature_discovery_amd.utils import synth
 

@@ -19,6 +19,7 @@
 #include "info/version.h"
 #include "lm/labels.h"
 #include "lm/node.h"
+#include "resource/amdsmi.h"
 #include "resource/factory.h"
 #include "resource/managers.h"
 #include "resource/sysfs.h"
@@ -180,6 +181,14 @@ PYBIND11_MODULE(_gfd, m) {
 
   m.def("version", [] { return info::version_string(); });
   m.def("set_quiet", &log::set_quiet, py::arg("quiet"));
+  // dlopen libamd_smi now (no amdsmi_init).  A host process that will also
+  // import PyTorch should call this first: PyTorch bundles its own libdrm,
+  // and whichever copy is loaded first is the one amd-smi binds to.
+  m.def("load_amdsmi", [] {
+    std::string reason;
+    bool ok = resource::has_amdsmi(&reason);
+    return py::make_tuple(ok, reason);
+  });
   m.def("parse_duration", &parse_duration);
   m.def("format_duration", &format_duration);
   m.def("parse_yaml", [](const std::string& text) { return node_to_py(yaml::parse(text)); });

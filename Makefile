@@ -21,7 +21,7 @@ test: build
 	$(PYTHON) -m pytest tests -q -m "not gpu"
 
 test-unit: build
-	./$(BUILD_DIR)/gfd_unit_tests
+	GFD_AMDSMI_LIBRARY=$(BUILD_DIR)/libfake_amdsmi.so ./$(BUILD_DIR)/gfd_unit_tests
 
 # Real-hardware tests (MI355X): run on a GPU node.
 test-gpu: build
@@ -32,18 +32,18 @@ test-gpu: build
 asan:
 	cmake -S . -B build-asan -G Ninja -DCMAKE_BUILD_TYPE=Debug -DGFD_SANITIZE=address,undefined -DGFD_BUILD_PYTHON=OFF
 	cmake --build build-asan -j $(JOBS)
-	ASAN_OPTIONS=detect_leaks=1 UBSAN_OPTIONS=halt_on_error=1 ./build-asan/gfd_unit_tests
+	ASAN_OPTIONS=detect_leaks=1 UBSAN_OPTIONS=halt_on_error=1 GFD_AMDSMI_LIBRARY=build-asan/libfake_amdsmi.so ./build-asan/gfd_unit_tests
 
 tsan:
 	cmake -S . -B build-tsan -G Ninja -DCMAKE_BUILD_TYPE=Debug -DGFD_SANITIZE=thread -DGFD_BUILD_PYTHON=OFF
 	cmake --build build-tsan -j $(JOBS)
-	TSAN_OPTIONS=halt_on_error=1 ./build-tsan/gfd_unit_tests
+	TSAN_OPTIONS=halt_on_error=1 GFD_AMDSMI_LIBRARY=build-tsan/libfake_amdsmi.so ./build-tsan/gfd_unit_tests
 
 coverage:
 	cmake -S . -B build-cov -G Ninja -DCMAKE_BUILD_TYPE=Debug -DGFD_BUILD_PYTHON=OFF \
 	  -DCMAKE_CXX_FLAGS="--coverage" -DCMAKE_EXE_LINKER_FLAGS="--coverage"
 	cmake --build build-cov -j $(JOBS)
-	./build-cov/gfd_unit_tests
+	GFD_AMDSMI_LIBRARY=build-cov/libfake_amdsmi.so ./build-cov/gfd_unit_tests
 	gcov -o build-cov/CMakeFiles/gfdcore.dir/src -r src/*/*.cpp > /dev/null 2>&1 || true
 
 bench: build

@@ -6,6 +6,9 @@
 // plus optional global lines:
 //   init_status=34            amdsmi_init returns this status
 //   stale_after=N             after N successful queries, queries return NOT_INIT until re-init
+//   fail=<function>:<status>  that amd-smi function returns <status> for
+//                             every device (repeatable), e.g.
+//                             fail=amdsmi_get_gpu_memory_total:2
 //   latency_us=N              every device query except handle-table lookups
 //                             (processor type, BDF, ASIC info) busy-waits N us
 //                             holding that GPU's lock (amd-smi serialises per
@@ -56,6 +59,7 @@ struct State {
   int shutdown_calls = 0;
   long latency_us = 0;
   std::map<std::string, std::unique_ptr<std::mutex>> device_mu;  // by BDF
+  std::map<std::string, int> fail;                               // function -> status
 };
 
 State& S() {
@@ -82,7 +86,8 @@ Proc* proc(amdsmi_processor_handle h) {
 }
 
 // `cheap`: calls that cost <= 2 us on real hardware (handle table lookups).
-amdsmi_status_t check(amdsmi_processor_handle h, Proc** out, bool cheap = false) {
+amdsmi_status_t check(amdsmi_processor_handle h, Proc** out, bool cheap = false,
+                      const char* fn = __builtin_FUNCTION()) {
   auto& s = S();
   std::mutex* dev = nullptr;
   long latency = 0;
@@ -96,6 +101,8 @@ amdsmi_status_t check(amdsmi_processor_handle h, Proc** out, bool cheap = false)
     }
     *out = proc(h);
     if (!*out) return AMDSMI_STATUS_INVAL;
+    auto f = s.fail.find(fn);
+    if (f != s.fail.end()) return static_cast<amdsmi_status_t>(f->second);
     latency = s.latency_us;
     if (latency > 0 && !cheap) dev = s.device_mu[(*out)->bdf].get();
   }
@@ -126,6 +133,7 @@ int fake_amdsmi_configure(const char* spec) {
   s.init_status = 0;
   s.stale_after = -1;
   s.latency_us = 0;
+  s.fail.clear();
   s.queries = 0;
   s.stale = false;
   std::istringstream in(spec);
@@ -138,6 +146,12 @@ int fake_amdsmi_configure(const char* spec) {
     }
     if (line.rfind("stale_after=", 0) == 0) {
       s.stale_after = std::atol(line.c_str() + 12);
+      continue;
+    }
+    if (line.rfind("fail=", 0) == 0) {
+      size_t colon = line.rfind(':');
+      if (colon == std::string::npos || colon < 5) return -1;
+      s.fail[line.substr(5, colon - 5)] = std::atoi(line.c_str() + colon + 1);
       continue;
     }
     if (line.rfind("latency_us=", 0) == 0) {

@@ -40,11 +40,15 @@ def _parse(stdout: str) -> dict[str, str]:
     return res
 
 
+FAKE_PREFIXES = ("AmdSmiFake_", "AmdSmiFault_")
+
+
 @pytest.fixture(scope="module")
 def fake_results() -> dict[str, str]:
-    """The AmdSmiFake_* tests, run against the scriptable libamd_smi."""
+    """The AmdSmiFake_* / AmdSmiFault_* tests, run against the scriptable
+    libamd_smi (without it they return early)."""
     fake = gfd.BUILD_DIR / "libfake_amdsmi.so"
-    names = [n for n in _names() if n.startswith("AmdSmiFake_")]
+    names = [n for n in _names() if n.startswith(FAKE_PREFIXES)]
     env = {**os.environ, "GFD_AMDSMI_LIBRARY": str(fake)}
     cp = subprocess.run([str(gfd.UNIT_TEST_BINARY), *names], capture_output=True, text=True, timeout=300, env=env)
     return _parse(cp.stdout)
@@ -52,7 +56,7 @@ def fake_results() -> dict[str, str]:
 
 @pytest.mark.parametrize("name", _names())
 def test_cpp(name, results, fake_results):
-    if name.startswith("AmdSmiFake_"):
+    if name.startswith(FAKE_PREFIXES):
         results = fake_results
     assert name in results, f"{name} did not run"
     assert results[name] == "ok", results[name]

@@ -34,7 +34,9 @@ struct Fake {
     const char* lib = std::getenv("GFD_AMDSMI_LIBRARY");
     if (!lib || std::string(lib).find("fake") == std::string::npos) return;
     void* h = dlopen(lib, RTLD_NOW);
-    if (!h) return;
+    // Asked for the fake but cannot load it: fail loudly rather than let
+    // every fake-backed test pass vacuously.
+    if (!h) throw std::runtime_error(std::string("cannot load fake amd-smi: ") + dlerror());
     configure = reinterpret_cast<int (*)(const char*)>(dlsym(h, "fake_amdsmi_configure"));
     init_calls = reinterpret_cast<int (*)()>(dlsym(h, "fake_amdsmi_init_calls"));
     shutdown_calls = reinterpret_cast<int (*)()>(dlsym(h, "fake_amdsmi_shutdown_calls"));
@@ -302,4 +304,76 @@ TEST(AmdSmiFake_SingleStrategyOverCpxNode) {
   EXPECT_EQ(l["amd.com/gpu.compute-units"], std::string("32"));
   EXPECT_EQ(l["amd.com/partition.strategy"], std::string("single"));
   fs::remove_all(root);
+}
+
+// ---- Fault injection: one amd-smi call failing with a chosen status ----
+
+namespace {
+std::vector<DevicePtr> devices_with(const std::string& spec, bool persistent = true) {
+  fake().configure(spec.c_str());
+  std::string root = temp_root();
+  AmdSmiManager m(opts(root, persistent));
+  m.Init();
+  std::vector<DevicePtr> devs;
+  try {
+    devs = m.GetDevices();
+  } catch (...) {
+    m.Shutdown();
+    fs::remove_all(root);
+    throw;
+  }
+  m.Shutdown();
+  fs::remove_all(root);
+  return devs;
+}
+const std::string kOneGpu = "bdf=0000:d9:00.0;mode=SPX;parts=1;cus=256;xcds=8;vram_mib=294896;links=7;virt=1\n";
+}  // namespace
+
+TEST(AmdSmiFault_AsicInfoFailureIsAnError) {
+  REQUIRE_FAKE();
+  EXPECT_THROW_MSG(devices_with("fail=amdsmi_get_gpu_asic_info:7\n" + kOneGpu), "amdsmi_get_gpu_asic_info");
+}
+
+TEST(AmdSmiFault_ProcessorHandlesFailureIsAnError) {
+  REQUIRE_FAKE();
+  // Handle-table calls are checked too (processor type / BDF).
+  EXPECT_THROW_MSG(devices_with("fail=amdsmi_get_gpu_device_bdf:10\n" + kOneGpu), "amdsmi_get_gpu_device_bdf");
+}
+
+TEST(AmdSmiFault_PersistentStaleStatusRetriesOnceThenFails) {
+  REQUIRE_FAKE();
+  int i0 = fake().init_calls();
+  // NOT_INIT on every ASIC query: one re-initialisation, then the error.
+  EXPECT_THROW_MSG(devices_with("fail=amdsmi_get_gpu_asic_info:32\n" + kOneGpu), "amdsmi_get_gpu_asic_info");
+  EXPECT_EQ(fake().init_calls() - i0, 2);
+}
+
+TEST(AmdSmiFault_OptionalQueriesDegradeToUnknown) {
+  REQUIRE_FAKE();
+  // Facts the labels can do without: the device is still reported, the
+  // affected labels are omitted (memory 0 -> no gpu.memory label, as in
+  // the reference's resource.go:63).
+  auto devs = devices_with("fail=amdsmi_get_gpu_memory_total:2\nfail=amdsmi_get_gpu_virtualization_mode:2\n"
+                           "fail=amdsmi_get_gpu_compute_partition:2\n" + kOneGpu);
+  EXPECT_EQ(devs.size(), static_cast<size_t>(1));
+  const auto& i = devs[0]->Info();
+  EXPECT_EQ(i.memory_mib, static_cast<uint64_t>(0));
+  EXPECT_EQ(i.virtualization, std::string(""));
+  EXPECT_EQ(i.compute_partition, std::string(""));
+  EXPECT_FALSE(devs[0]->IsPartitioned());
+  EXPECT_EQ(i.compute_units, static_cast<uint32_t>(256));
+}
+
+TEST(AmdSmiFault_KfdInfoFailureFallsBackToXcdCounter) {
+  REQUIRE_FAKE();
+  auto devs = devices_with("fail=amdsmi_get_gpu_kfd_info:2\n" + kOneGpu);
+  EXPECT_EQ(devs[0]->Info().xcds, static_cast<uint32_t>(8));
+}
+
+TEST(AmdSmiFault_XgmiFallbackFailureLeavesLinksUnknown) {
+  REQUIRE_FAKE();
+  // No amdgpu xgmi table under the test root and the link-status query
+  // fails: the link count is unknown (-1), not 0.
+  auto devs = devices_with("fail=amdsmi_get_gpu_xgmi_link_status:2\n" + kOneGpu);
+  EXPECT_EQ(devs[0]->Info().xgmi_links, -1);
 }

@@ -8,7 +8,9 @@
 #include "resource/versions.h"
 #include "util/error.h"
 #include "util/fs.h"
+#include "util/pool.h"
 #include "util/strings.h"
+#include "util/trace.h"
 
 namespace gfd::resource {
 
@@ -186,8 +188,87 @@ std::vector<DevicePtr> SysfsManager::GetDevices() {
   return snapshot_;
 }
 
+// One physical GPU (and its partitions) from its KFD nodes and PCI attributes.
+static DevicePtr describe_gpu(const std::string& root, bool in_vm, int index, const std::string& bdf,
+                              const std::vector<const KfdNode*>& members) {
+  const KfdNode& first = *members.front();
+  std::string pci = fs::join(root, "sys/bus/pci/devices/" + bdf);
+
+  DeviceInfo info;
+  info.index = index;
+  info.bdf = bdf;
+  info.vendor_id = static_cast<uint32_t>(first.vendor_id);
+  info.device_id = static_cast<uint32_t>(first.device_id);
+  info.uuid = amd_uuid(first.unique_id, static_cast<uint32_t>(first.device_id));
+  info.gfx = gfx_target_from_kfd(first.gfx_target_version);
+  auto product = fs::read_trimmed(fs::join(pci, "product_name"));
+  info.name = product && !product->empty() ? *product : device_name(static_cast<uint32_t>(first.device_id));
+  info.compute_partition = fs::read_trimmed(fs::join(pci, "current_compute_partition")).value_or("");
+  info.memory_partition = fs::read_trimmed(fs::join(pci, "current_memory_partition")).value_or("");
+  info.available_compute_partitions = split_list(fs::read_trimmed(fs::join(pci, "available_compute_partition")).value_or(""));
+  info.available_memory_partitions = split_list(fs::read_trimmed(fs::join(pci, "available_memory_partition")).value_or(""));
+  if (auto x = fs::read_trimmed(fs::join(pci, "xgmi_num_links"))) info.xgmi_links = sum_links(*x);
+  info.virtualization = virtualization_mode(pci, info.device_id, in_vm);
+
+  bool partitioned = members.size() > 1 || (!info.compute_partition.empty() && info.compute_partition != "SPX");
+  uint64_t vram = 0;
+  if (auto v = fs::read_trimmed(fs::join(pci, "mem_info_vram_total"))) vram = str::parse_uint(*v).value_or(0);
+
+  // Per-partition HBM from each partition node's mem_banks (a list + read
+  // per node; 8 of them in CPX), read in parallel.
+  std::vector<uint64_t> part_mem(members.size(), 0);
+  if (partitioned)
+    WorkerPool::instance().parallel_for(members.size(), [&](size_t p) {
+      const KfdNode& n = *members[p];
+      part_mem[p] = n.local_mem_size ? n.local_mem_size : node_memory_bytes(n.dir);
+    });
+
+  std::vector<std::shared_ptr<SnapshotDevice>> parts;
+  uint32_t cus = 0, xcds = 0;
+  uint64_t part_mem_sum = 0;
+  for (size_t p = 0; p < members.size(); ++p) {
+    const KfdNode& n = *members[p];
+    uint32_t pcus = n.simd_per_cu ? static_cast<uint32_t>(n.simd_count / n.simd_per_cu) : 0;
+    cus += pcus;
+    xcds += static_cast<uint32_t>(n.num_xcc);
+    if (!partitioned) continue;
+    DeviceInfo pi;
+    pi.partition_id = static_cast<int>(p);
+    pi.bdf = bdf;
+    pi.vendor_id = info.vendor_id;
+    pi.device_id = info.device_id;
+    pi.compute_units = pcus;
+    pi.xcds = static_cast<uint32_t>(n.num_xcc);
+    uint64_t mem = part_mem[p];
+    pi.memory_mib = mem >> 20;
+    part_mem_sum += mem;
+    pi.compute_partition = info.compute_partition;
+    pi.memory_partition = info.memory_partition;
+    pi.name = partition_profile_name(pi.compute_partition, pi.xcds, pi.memory_mib);
+    pi.attributes = {
+        {"memory", std::to_string(pi.memory_mib)},
+        {"compute-units", std::to_string(pcus)},
+        {"xcds", std::to_string(pi.xcds)},
+        {"engines.dma", std::to_string(n.num_sdma_engines)},
+    };
+    if (!pi.compute_partition.empty()) pi.attributes["compute-partition"] = pi.compute_partition;
+    if (!pi.memory_partition.empty()) pi.attributes["memory-partition"] = pi.memory_partition;
+    parts.push_back(SnapshotDevice::partition(std::move(pi)));
+  }
+  info.compute_units = cus;
+  info.xcds = xcds;
+  if (vram == 0) vram = partitioned ? part_mem_sum : (first.local_mem_size ? first.local_mem_size : node_memory_bytes(first.dir));
+  info.memory_mib = vram >> 20;
+
+  bool capable = info.available_compute_partitions.size() > 1;
+  auto dev = SnapshotDevice::gpu(std::move(info), partitioned, capable);
+  dev->set_partitions(std::move(parts));
+  return dev;
+}
+
 std::vector<DevicePtr> SysfsManager::enumerate() const {
-  // 1. Read every accessible GPU node.
+  // 1. Read every accessible GPU node.  A CPX node has 64 of them, so the
+  //    reads are spread over the worker pool in chunks.
   std::vector<KfdNode> nodes;
   for (const auto& name : fs::list_dir(topology_)) {
     auto id = str::parse_uint(name);
@@ -195,88 +276,49 @@ std::vector<DevicePtr> SysfsManager::enumerate() const {
     KfdNode n;
     n.id = static_cast<int>(*id);
     n.dir = fs::join(topology_, name);
-    auto r = fs::read_file(fs::join(n.dir, "properties"));
-    if (!r.ok()) continue;  // EPERM: GPU not allocated to this container
-    parse_properties(r.data, n);
-    if (n.gfx_target_version == 0 || n.simd_count == 0) continue;  // CPU node
     nodes.push_back(std::move(n));
   }
-  std::sort(nodes.begin(), nodes.end(), [](const KfdNode& a, const KfdNode& b) { return a.id < b.id; });
+  std::vector<char> usable(nodes.size(), 0);
+  constexpr size_t kChunk = 8;
+  auto read_chunk = [&](size_t c) {
+    for (size_t i = c * kChunk; i < std::min(nodes.size(), (c + 1) * kChunk); ++i) {
+      auto r = fs::read_file(fs::join(nodes[i].dir, "properties"));
+      if (!r.ok()) continue;  // EPERM: GPU not allocated to this container
+      parse_properties(r.data, nodes[i]);
+      usable[i] = nodes[i].gfx_target_version != 0 && nodes[i].simd_count != 0;  // else a CPU node
+    }
+  };
+  size_t chunks = (nodes.size() + kChunk - 1) / kChunk;
+  int64_t t0 = trace::now_ns();
+  WorkerPool::instance().parallel_for(chunks, read_chunk);
+  trace::record("sysfs.nodes", trace::now_ns() - t0);
+  std::vector<KfdNode> gpus_nodes;
+  for (size_t i = 0; i < nodes.size(); ++i)
+    if (usable[i]) gpus_nodes.push_back(std::move(nodes[i]));
+  std::sort(gpus_nodes.begin(), gpus_nodes.end(), [](const KfdNode& a, const KfdNode& b) { return a.id < b.id; });
 
   // 2. Group partitions by PCI location (partitions share the parent's BDF).
   std::map<std::string, std::vector<const KfdNode*>> groups;  // ordered by BDF
-  for (const auto& n : nodes) groups[bdf_of(n)].push_back(&n);
+  for (const auto& n : gpus_nodes) groups[bdf_of(n)].push_back(&n);
 
-  std::vector<DevicePtr> out;
+  // 3. Describe each visible physical GPU (~10 sysfs reads each), in
+  //    parallel across GPUs.
+  struct Gpu {
+    int index;
+    const std::string* bdf;
+    const std::vector<const KfdNode*>* members;
+  };
+  std::vector<Gpu> visible;
   int index = -1;
   for (const auto& [bdf, members] : groups) {
     ++index;
-    if (!opts_.filter.matches(index, bdf)) continue;
-    const KfdNode& first = *members.front();
-    std::string pci = fs::join(opts_.root, "sys/bus/pci/devices/" + bdf);
-
-    DeviceInfo info;
-    info.index = index;
-    info.bdf = bdf;
-    info.vendor_id = static_cast<uint32_t>(first.vendor_id);
-    info.device_id = static_cast<uint32_t>(first.device_id);
-    info.uuid = amd_uuid(first.unique_id, static_cast<uint32_t>(first.device_id));
-    info.gfx = gfx_target_from_kfd(first.gfx_target_version);
-    auto product = fs::read_trimmed(fs::join(pci, "product_name"));
-    info.name = product && !product->empty() ? *product : device_name(static_cast<uint32_t>(first.device_id));
-    info.compute_partition = fs::read_trimmed(fs::join(pci, "current_compute_partition")).value_or("");
-    info.memory_partition = fs::read_trimmed(fs::join(pci, "current_memory_partition")).value_or("");
-    info.available_compute_partitions = split_list(fs::read_trimmed(fs::join(pci, "available_compute_partition")).value_or(""));
-    info.available_memory_partitions = split_list(fs::read_trimmed(fs::join(pci, "available_memory_partition")).value_or(""));
-    if (auto x = fs::read_trimmed(fs::join(pci, "xgmi_num_links"))) info.xgmi_links = sum_links(*x);
-    info.virtualization = virtualization_mode(pci, info.device_id, in_vm_);
-
-    bool partitioned = members.size() > 1 || (!info.compute_partition.empty() && info.compute_partition != "SPX");
-    uint64_t vram = 0;
-    if (auto v = fs::read_trimmed(fs::join(pci, "mem_info_vram_total"))) vram = str::parse_uint(*v).value_or(0);
-
-    std::vector<std::shared_ptr<SnapshotDevice>> parts;
-    uint32_t cus = 0, xcds = 0;
-    uint64_t part_mem_sum = 0;
-    for (size_t p = 0; p < members.size(); ++p) {
-      const KfdNode& n = *members[p];
-      uint32_t pcus = n.simd_per_cu ? static_cast<uint32_t>(n.simd_count / n.simd_per_cu) : 0;
-      cus += pcus;
-      xcds += static_cast<uint32_t>(n.num_xcc);
-      if (!partitioned) continue;
-      DeviceInfo pi;
-      pi.partition_id = static_cast<int>(p);
-      pi.bdf = bdf;
-      pi.vendor_id = info.vendor_id;
-      pi.device_id = info.device_id;
-      pi.compute_units = pcus;
-      pi.xcds = static_cast<uint32_t>(n.num_xcc);
-      uint64_t mem = n.local_mem_size ? n.local_mem_size : node_memory_bytes(n.dir);
-      pi.memory_mib = mem >> 20;
-      part_mem_sum += mem;
-      pi.compute_partition = info.compute_partition;
-      pi.memory_partition = info.memory_partition;
-      pi.name = partition_profile_name(pi.compute_partition, pi.xcds, pi.memory_mib);
-      pi.attributes = {
-          {"memory", std::to_string(pi.memory_mib)},
-          {"compute-units", std::to_string(pcus)},
-          {"xcds", std::to_string(pi.xcds)},
-          {"engines.dma", std::to_string(n.num_sdma_engines)},
-      };
-      if (!pi.compute_partition.empty()) pi.attributes["compute-partition"] = pi.compute_partition;
-      if (!pi.memory_partition.empty()) pi.attributes["memory-partition"] = pi.memory_partition;
-      parts.push_back(SnapshotDevice::partition(std::move(pi)));
-    }
-    info.compute_units = cus;
-    info.xcds = xcds;
-    if (vram == 0) vram = partitioned ? part_mem_sum : (first.local_mem_size ? first.local_mem_size : node_memory_bytes(first.dir));
-    info.memory_mib = vram >> 20;
-
-    bool capable = info.available_compute_partitions.size() > 1;
-    auto dev = SnapshotDevice::gpu(std::move(info), partitioned, capable);
-    dev->set_partitions(std::move(parts));
-    out.push_back(dev);
+    if (opts_.filter.matches(index, bdf)) visible.push_back(Gpu{index, &bdf, &members});
   }
+  std::vector<DevicePtr> out(visible.size());
+  trace::Span span("sysfs.gpus");
+  WorkerPool::instance().parallel_for(
+      visible.size(), [&](size_t i) { out[i] = describe_gpu(opts_.root, in_vm_, visible[i].index, *visible[i].bdf, *visible[i].members); },
+      8);
   return out;
 }
 

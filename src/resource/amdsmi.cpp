@@ -261,7 +261,9 @@ uint32_t kfd_num_xcc(const std::string& root, uint32_t node_id) {
   return static_cast<uint32_t>(strtoul(r.data.c_str() + pos + sizeof(kKey) - 1, nullptr, 10));
 }
 
-void query_proc(AmdSmiLib& L, const std::string& root, ProcInfo& p) {
+// Identity of a processor from its ASIC info (the library caches it after
+// the first call: ~2 us).
+void query_identity(AmdSmiLib& L, ProcInfo& p) {
   amdsmi_asic_info_t asic;
   std::memset(&asic, 0, sizeof(asic));
   amdsmi_status_t st = AMDSMI_CALL("asic_info", L.get_gpu_asic_info(p.h, &asic));
@@ -278,21 +280,86 @@ void query_proc(AmdSmiLib& L, const std::string& root, ProcInfo& p) {
   if (serial_hex.size() > 2 && serial_hex[0] == '0' && (serial_hex[1] == 'x' || serial_hex[1] == 'X'))
     serial_hex.erase(0, 2);
   if (auto serial = str::parse_uint(serial_hex, 16)) p.uuid = amd_uuid(*serial, p.device_id);
+}
+
+void fix_market_name(AmdSmiLib& L, const std::string& root, ProcInfo& p) {
+  if (!is_generic_name(p.market_name)) return;
+  // The board FRU product name: amdgpu publishes it in sysfs (~5 us); the
+  // amd-smi board-info call returns the same string for ~155 us.
+  auto v = fs::read_trimmed(fs::join(root, "sys/bus/pci/devices/" + p.bdf + "/product_name"));
+  if (v && !is_generic_name(*v)) {
+    p.market_name = *v;
+  } else if (L.get_gpu_board_info) {
+    amdsmi_board_info_t b;
+    std::memset(&b, 0, sizeof(b));
+    if (AMDSMI_CALL("board_info", L.get_gpu_board_info(p.h, &b)) == AMDSMI_STATUS_SUCCESS &&
+        !is_generic_name(str::trim(b.product_name)))
+      p.market_name = str::trim(b.product_name);
+  }
+}
+
+// KFD node and partition id of a processor (amdsmi_get_gpu_kfd_info).
+bool query_kfd(AmdSmiLib& L, ProcInfo& p, uint32_t* node_id) {
+  if (!L.get_gpu_kfd_info) return false;
+  amdsmi_kfd_info_t kfd;
+  std::memset(&kfd, 0, sizeof(kfd));
+  if (AMDSMI_CALL("kfd_info", L.get_gpu_kfd_info(p.h, &kfd)) != AMDSMI_STATUS_SUCCESS) return false;
+  if (kfd.current_partition_id != 0xFFFFFFFFu) p.partition_id = kfd.current_partition_id;
+  *node_id = kfd.node_id;
+  return true;
+}
+
+bool sysfs_values_enabled() {
+  static const bool on = [] {
+    const char* v = std::getenv("GFD_AMDSMI_SYSFS");
+    return !(v && std::string(v) == "0");
+  }();
+  return on;
+}
+
+constexpr uint32_t kNoNode = 0xFFFFFFFFu;
+
+// The only processor at its PCI address and in SPX mode: its per-cycle
+// values are the amdgpu attributes amd-smi reads for the same calls
+// (mem_info_vram_total for memory_total(VRAM), current_compute_partition /
+// current_memory_partition for the partition getters), read directly at
+// ~4 us each.  `node_id` is the session-cached KFD node (kNoNode = not yet
+// known: queried and returned through it).  Returns false when the GPU is
+// partitioned or an attribute is missing; the caller then queries amd-smi.
+bool query_unpartitioned(AmdSmiLib& L, const std::string& root, ProcInfo& p, uint32_t* node_id) {
+  std::string pci = fs::join(root, "sys/bus/pci/devices/" + p.bdf);
+  auto cp = AMDSMI_CALL("compute_partition(sysfs)", fs::read_trimmed(pci + "/current_compute_partition"));
+  if (!cp || *cp != "SPX") return false;
+  auto mp = AMDSMI_CALL("memory_partition(sysfs)", fs::read_trimmed(pci + "/current_memory_partition"));
+  if (!mp || mp->empty()) return false;
+  auto vram_s = AMDSMI_CALL("memory_total(sysfs)", fs::read_trimmed(pci + "/mem_info_vram_total"));
+  auto vram = vram_s ? str::parse_uint(*vram_s) : std::nullopt;
+  if (!vram || *vram == 0) return false;
+  if (*node_id == kNoNode && !query_kfd(L, p, node_id)) return false;
+  query_identity(L, p);
+  p.compute_partition = *cp;
+  p.memory_partition = *mp;
+  p.vram = *vram;
+  if (*node_id != kNoNode) p.xcds = AMDSMI_CALL("kfd_num_xcc(sysfs)", kfd_num_xcc(root, *node_id));
+  if (p.xcds == 0 && L.get_gpu_xcd_counter) {
+    uint16_t x = 0;
+    if (L.get_gpu_xcd_counter(p.h, &x) == AMDSMI_STATUS_SUCCESS) p.xcds = x;
+  }
+  fix_market_name(L, root, p);
+  return true;
+}
+
+// Every value through amd-smi (partitioned GPUs, or sysfs values disabled).
+void query_proc(AmdSmiLib& L, const std::string& root, ProcInfo& p) {
+  query_identity(L, p);
 
   uint64_t total = 0;
   if (AMDSMI_CALL("memory_total", L.get_gpu_memory_total(p.h, AMDSMI_MEM_TYPE_VRAM, &total)) == AMDSMI_STATUS_SUCCESS)
     p.vram = total;
 
-  uint32_t node_id = 0xFFFFFFFFu;
-  if (L.get_gpu_kfd_info) {
-    amdsmi_kfd_info_t kfd;
-    std::memset(&kfd, 0, sizeof(kfd));
-    if (AMDSMI_CALL("kfd_info", L.get_gpu_kfd_info(p.h, &kfd)) == AMDSMI_STATUS_SUCCESS) {
-      if (kfd.current_partition_id != 0xFFFFFFFFu) p.partition_id = kfd.current_partition_id;
-      node_id = kfd.node_id;
-    }
-  }
-  if (node_id != 0xFFFFFFFFu) p.xcds = AMDSMI_CALL("kfd_num_xcc(sysfs)", kfd_num_xcc(root, node_id));
+  uint32_t node_id = kNoNode;
+  query_kfd(L, p, &node_id);
+  if (node_id != kNoNode) p.xcds = AMDSMI_CALL("kfd_num_xcc(sysfs)", kfd_num_xcc(root, node_id));
   char buf[64];
   if (L.get_gpu_compute_partition) {
     std::memset(buf, 0, sizeof(buf));
@@ -308,20 +375,7 @@ void query_proc(AmdSmiLib& L, const std::string& root, ProcInfo& p) {
     uint16_t x = 0;
     if (L.get_gpu_xcd_counter(p.h, &x) == AMDSMI_STATUS_SUCCESS) p.xcds = x;
   }
-  if (is_generic_name(p.market_name)) {
-    // The board FRU product name: amdgpu publishes it in sysfs (~5 us); the
-    // amd-smi board-info call returns the same string for ~155 us.
-    auto v = fs::read_trimmed(fs::join(root, "sys/bus/pci/devices/" + p.bdf + "/product_name"));
-    if (v && !is_generic_name(*v)) {
-      p.market_name = *v;
-    } else if (L.get_gpu_board_info) {
-      amdsmi_board_info_t b;
-      std::memset(&b, 0, sizeof(b));
-      if (AMDSMI_CALL("board_info", L.get_gpu_board_info(p.h, &b)) == AMDSMI_STATUS_SUCCESS &&
-          !is_generic_name(str::trim(b.product_name)))
-        p.market_name = str::trim(b.product_name);
-    }
-  }
+  fix_market_name(L, root, p);
 }
 
 // xGMI links to hive peers from amdgpu's per-peer table ("01 01 ... 00 01",
@@ -432,6 +486,7 @@ void AmdSmiManager::library_init() {
   lib_->users++;
   lib_initialized_ = true;
   virt_mode_.clear();
+  kfd_node_.clear();
   ++init_count_;
 }
 
@@ -541,6 +596,7 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
     std::vector<ProcInfo>* procs;
     GpuExtras extras;
     std::exception_ptr error;
+    uint32_t kfd_node = kNoNode;  // session cache entry (unpartitioned GPUs)
   };
   std::vector<Gpu> gpus;
   int index = -1;
@@ -550,8 +606,11 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
       gpus.push_back(Gpu{index, bdf, &procs, {}, {}});
       auto v = virt_mode_.find(bdf);
       if (v != virt_mode_.end()) gpus.back().extras.virtualization = v->second;
+      auto k = kfd_node_.find(bdf);
+      if (k != kfd_node_.end()) gpus.back().kfd_node = k->second;
     }
   }
+  const bool sysfs_values = sysfs_values_enabled();
 
   // Query every processor; parallel across physical GPUs on multi-GPU nodes
   // (amd-smi serialises queries per device, so splitting one GPU's queries
@@ -560,7 +619,9 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
     try {
       {
         trace::Span s("amdsmi.proc");
-        for (auto& p : *g.procs) query_proc(L, opts_.root, p);
+        auto& procs = *g.procs;
+        if (!(sysfs_values && procs.size() == 1 && query_unpartitioned(L, opts_.root, procs[0], &g.kfd_node)))
+          for (auto& p : procs) query_proc(L, opts_.root, p);
       }
       std::sort(g.procs->begin(), g.procs->end(),
                 [](const ProcInfo& a, const ProcInfo& b) { return a.partition_id < b.partition_id; });
@@ -576,8 +637,10 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
   WorkerPool::instance().parallel_for(gpus.size(), [&](size_t i) { work(gpus[i]); }, threads);
   for (const auto& g : gpus)
     if (g.error) std::rethrow_exception(g.error);
-  for (const auto& g : gpus)
+  for (const auto& g : gpus) {
     if (!g.extras.virtualization.empty()) virt_mode_[g.bdf] = g.extras.virtualization;
+    if (g.kfd_node != kNoNode) kfd_node_[g.bdf] = g.kfd_node;
+  }
 
   std::vector<DevicePtr> out;
   for (auto& g : gpus) {

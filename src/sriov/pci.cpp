@@ -96,29 +96,32 @@ SysfsAmdPCI::Identity SysfsAmdPCI::read_identity(const std::string& addr, const 
 
 std::vector<PCIDevice> SysfsAmdPCI::Devices() {
   std::string dir = fs::join(root_, kPciDevicesRoot);
-  int err = 0;
   int64_t t0 = trace::now_ns();
-  auto entries = fs::list_dir_ino(dir, &err);
+  bool changed = true;
+  int err = listing_.read(dir, &changed);
   trace::record("pci.list", trace::now_ns() - t0);
   if (err != 0) throw Error("unable to read PCI bus devices: open " + dir + ": " + fs::errno_str(err));
 
   // Merge the (sorted) listing with the (sorted) identity cache: entries
   // whose sysfs inode is unchanged reuse their identity, new or re-created
-  // ones are read.  Moves only - no per-entry allocation in steady state
-  // (a large host lists ~320 PCI functions, measured on the MI355X pool).
+  // ones are read.  Skipped entirely when the bus listing is unchanged.
   std::vector<std::pair<std::string, Identity>> next;
-  next.reserve(entries.size());
   std::vector<size_t> misses;
-  auto hit = cache_.begin();
-  for (auto& [addr, ino] : entries) {
-    while (hit != cache_.end() && hit->first < addr) ++hit;
-    if (hit != cache_.end() && hit->first == addr && hit->second.ino == ino && ino != 0) {
-      next.emplace_back(std::move(addr), std::move(hit->second));
-    } else {
-      misses.push_back(next.size());
-      Identity fresh;
-      fresh.ino = ino;
-      next.emplace_back(std::move(addr), std::move(fresh));
+  if (changed) {
+    auto entries = listing_.entries();
+    next.reserve(entries.size());
+    auto hit = cache_.begin();
+    for (auto& [addr, ino] : entries) {
+      while (hit != cache_.end() && hit->first < addr) ++hit;
+      if (hit != cache_.end() && hit->first == addr && hit->second.ino == ino && ino != 0) {
+        next.emplace_back(std::move(addr), std::move(hit->second));
+        next.back().second.sriov_numvfs = -1;  // re-read below
+      } else {
+        misses.push_back(next.size());
+        Identity fresh;
+        fresh.ino = ino;
+        next.emplace_back(std::move(addr), std::move(fresh));
+      }
     }
   }
   // Identity reads (vendor, class, ...) of functions not seen before: every
@@ -138,12 +141,13 @@ std::vector<PCIDevice> SysfsAmdPCI::Devices() {
     WorkerPool::instance().parallel_for(chunks, read_chunk);
   else if (chunks == 1)
     read_chunk(0);
-  cache_.swap(next);
+  if (changed) cache_.swap(next);
   int64_t t1 = trace::now_ns();
   trace::record("pci.identity", t1 - t0);
 
   std::vector<PCIDevice> out;
-  for (const auto& [addr, id] : cache_) {
+  std::vector<Identity*> ids;
+  for (auto& [addr, id] : cache_) {
     if (!id.relevant) continue;
     PCIDevice d;
     d.path = fs::join(dir, addr);
@@ -155,6 +159,7 @@ std::vector<PCIDevice> SysfsAmdPCI::Devices() {
     d.sriov_vf_device = id.sriov_vf_device;  // cleared below unless VFs are enabled
     d.physfn = id.physfn;
     out.push_back(std::move(d));
+    ids.push_back(&id);
   }
 
   // Mutable state: NumVFs of SR-IOV capable functions (one ~3 us sysfs read
@@ -162,13 +167,22 @@ std::vector<PCIDevice> SysfsAmdPCI::Devices() {
   // sysfs does not publish.  Serial on purpose: spreading the 8 reads of an
   // 8-GPU host over the pool measured 40-56 us vs 26 us serial (worker
   // wake-up costs more than the reads).
+  //
+  // NumVFs is re-read only when the bus listing changed: the kernel creates
+  // (and removes) one PCI function per VF when NumVFs is written, and refuses
+  // to change a non-zero NumVFs to another non-zero value without going
+  // through 0 (drivers/pci/iov.c, sriov_numvfs_store: -EBUSY), so NumVFs
+  // cannot change while the listing - names and inode numbers - stays the same.
   auto refresh = [&](size_t i) {
     PCIDevice& d = out[i];
+    Identity& id = *ids[i];
     if (d.sriov_totalvfs == 0) {
       d.sriov_numvfs = 0;  // SR-IOV capable in name only: no VFs possible
     } else if (d.sriov_totalvfs > 0) {
-      if (auto n = fs::read_trimmed(fs::join(d.path, "sriov_numvfs")))
-        d.sriov_numvfs = static_cast<int>(str::parse_uint(*n).value_or(0));
+      if (id.sriov_numvfs < 0)
+        if (auto n = fs::read_trimmed(fs::join(d.path, "sriov_numvfs")))
+          id.sriov_numvfs = static_cast<int>(str::parse_uint(*n).value_or(0));
+      d.sriov_numvfs = id.sriov_numvfs;
     }
     if (d.sriov_numvfs <= 0) d.sriov_vf_device.clear();
     if (d.sriov_totalvfs < 0 && d.physfn.empty()) {

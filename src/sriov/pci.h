@@ -22,6 +22,8 @@
 #include <string>
 #include <vector>
 
+#include "util/fs.h"
+
 namespace gfd::sriov {
 
 inline constexpr const char* kPciDevicesRoot = "sys/bus/pci/devices";
@@ -86,13 +88,15 @@ class AmdPCI {
 // a large server has hundreds of PCI functions and the reference reads
 // `vendor` (and, for its vendor, the whole config space) of every one of them
 // every cycle.  Here:
-//   * the bus is re-listed every call (hot-plug is seen immediately), but the
-//     immutable identity of a function (vendor, class, device ID) is kept per
-//     (address, sysfs inode) - a removed and re-added device gets a new inode
-//     and is re-read;
-//   * the mutable SR-IOV state is re-read every call from the kernel's sysfs
-//     attributes (sriov_numvfs/totalvfs/vf_device, physfn), which cost no PCI
-//     config cycles;
+//   * the bus is re-listed every call (hot-plug is seen immediately) through
+//     a directory descriptor kept open (fs::DirListing), but the immutable
+//     identity of a function (vendor, class, device ID) is kept per (address,
+//     sysfs inode) - a removed and re-added device gets a new inode and is
+//     re-read;
+//   * the mutable SR-IOV state comes from the kernel's sysfs attributes
+//     (sriov_numvfs), which cost no PCI config cycles, and is re-read whenever
+//     the listing changed - enabling or disabling VFs adds or removes their
+//     PCI functions, so an unchanged listing means unchanged NumVFs;
 //   * configuration space (a 4 KiB read = ~1000 config cycles when
 //     privileged) is read only for functions whose SR-IOV state sysfs does not
 //     publish.
@@ -115,9 +119,11 @@ class SysfsAmdPCI : public AmdPCI {
     int sriov_totalvfs = -1;
     std::string sriov_vf_device;
     std::string physfn;
+    int sriov_numvfs = -1;  // last NumVFs read; -1 = re-read (listing changed)
   };
   static Identity read_identity(const std::string& addr, const std::string& path, uint64_t ino);
   std::string root_;
+  fs::DirListing listing_;
   std::vector<std::pair<std::string, Identity>> cache_;  // sorted by address
 };
 

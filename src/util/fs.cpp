@@ -3,6 +3,7 @@
 #include <dirent.h>
 #include <fcntl.h>
 #include <sys/stat.h>
+#include <sys/syscall.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -95,6 +96,77 @@ std::vector<std::pair<std::string, uint64_t>> list_dir_ino(const std::string& pa
     out.emplace_back(e->d_name, static_cast<uint64_t>(e->d_ino));
   }
   ::closedir(d);
+  std::sort(out.begin(), out.end());
+  return out;
+}
+
+DirListing::~DirListing() {
+  if (fd_ >= 0) ::close(fd_);
+}
+
+int DirListing::read_raw() {
+  raw_.clear();
+  if (::lseek(fd_, 0, SEEK_SET) < 0) return errno;
+  char buf[32768];
+  for (;;) {
+    long n = ::syscall(SYS_getdents64, fd_, buf, sizeof(buf));
+    if (n < 0) {
+      if (errno == EINTR) continue;
+      return errno;
+    }
+    if (n == 0) return 0;
+    raw_.append(buf, static_cast<size_t>(n));
+  }
+}
+
+int DirListing::read(const std::string& path, bool* changed) {
+  if (fd_ >= 0 && path != path_) {
+    ::close(fd_);
+    fd_ = -1;
+  }
+  prev_.swap(raw_);
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    if (fd_ < 0) {
+      fd_ = ::open(path.c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC);
+      if (fd_ < 0) {
+        int e = errno;
+        raw_.clear();
+        prev_.clear();
+        return e;
+      }
+      path_ = path;
+    }
+    int e = read_raw();
+    struct stat st;
+    if (e == 0 && ::fstat(fd_, &st) == 0 && st.st_nlink > 0) break;
+    // Removed (or unreadable) since it was opened: look the path up again.
+    ::close(fd_);
+    fd_ = -1;
+    if (attempt == 1) {
+      raw_.clear();
+      prev_.clear();
+      return e ? e : ENOENT;
+    }
+  }
+  *changed = raw_ != prev_;
+  return 0;
+}
+
+std::vector<std::pair<std::string, uint64_t>> DirListing::entries() const {
+  // struct linux_dirent64: u64 d_ino, s64 d_off, u16 d_reclen, u8 d_type,
+  // NUL-terminated d_name.
+  constexpr size_t kReclen = 16, kName = 19;
+  std::vector<std::pair<std::string, uint64_t>> out;
+  for (size_t pos = 0; pos + kName < raw_.size();) {
+    uint64_t ino = 0;
+    uint16_t reclen = 0;
+    std::memcpy(&ino, raw_.data() + pos, sizeof(ino));
+    std::memcpy(&reclen, raw_.data() + pos + kReclen, sizeof(reclen));
+    if (reclen == 0 || pos + reclen > raw_.size()) break;
+    const char* name = raw_.data() + pos + kName;
+    if (!(name[0] == '.' && (name[1] == 0 || (name[1] == '.' && name[2] == 0)))) out.emplace_back(name, ino);
+    pos += reclen;
+  }
   std::sort(out.begin(), out.end());
   return out;
 }

@@ -31,6 +31,31 @@ std::vector<std::string> list_dir(const std::string& path, int* err = nullptr);
 // Like list_dir but also returns each entry's inode number (d_ino), which
 // changes when a sysfs object is removed and re-created (hot-plug).
 std::vector<std::pair<std::string, uint64_t>> list_dir_ino(const std::string& path, int* err = nullptr);
+// A directory listing re-read every call through a descriptor kept open
+// across calls: one lseek + getdents64 pass, no path walk, no per-entry
+// work when nothing changed.  Whether anything changed is decided on the raw
+// getdents64 records (name, inode, position cookie), which sysfs (kernfs)
+// produces identically for an unchanged directory.  The descriptor is
+// reopened when the directory was removed (st_nlink 0) or `path` differs.
+class DirListing {
+ public:
+  DirListing() = default;
+  ~DirListing();
+  DirListing(const DirListing&) = delete;
+  DirListing& operator=(const DirListing&) = delete;
+  // Re-reads `path`.  Returns 0 or errno; `changed` is true when the listing
+  // differs from the previous successful read (always on the first).
+  int read(const std::string& path, bool* changed);
+  // Entries of the last read, without . and .., sorted by name.
+  std::vector<std::pair<std::string, uint64_t>> entries() const;
+
+ private:
+  int read_raw();
+  std::string path_;
+  int fd_ = -1;
+  std::string raw_, prev_;
+};
+
 // readlink(2); empty on failure.
 std::string read_link(const std::string& path);
 // Final path component of realpath(path), or empty.

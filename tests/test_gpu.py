@@ -59,6 +59,20 @@ def test_sysfs_backend_agrees_with_amdsmi(amdsmi_devices, sysfs_devices):
         assert {k: a[k] for k in keys} == {k: s[k] for k in keys}
 
 
+def test_amdsmi_sysfs_values_match_library_calls(amdsmi_devices):
+    """An unpartitioned GPU's per-cycle values are read from the amdgpu
+    attributes amd-smi itself reads; with that turned off (GFD_AMDSMI_SYSFS=0,
+    read once per process) every value comes from the library calls, and the
+    devices must be identical."""
+    code = ("import sys, json; sys.path.insert(0, %r)\n"
+            "import gpu_feature_discovery_amd as g\n"
+            "print(json.dumps(g.native().Session(['--backend=amdsmi']).devices()))\n" % str(REPO))
+    cp = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                        env={**os.environ, "GFD_AMDSMI_SYSFS": "0"})
+    assert cp.returncode == 0, cp.stderr[-2000:]
+    assert json.loads(cp.stdout.strip().splitlines()[-1]) == json.loads(json.dumps(amdsmi_devices))
+
+
 def test_label_sets_identical_across_backends(native, tmp_path):
     common = ["--oneshot", "--no-timestamp", "--output-file="]
     a = native.Session(["--backend=amdsmi", *common]).cycle(False)["labels"]

@@ -127,6 +127,50 @@ TEST(AmdSmiFake_GenericMarketNameFallsBackToBoard) {
   fs::remove_all(root);
 }
 
+TEST(AmdSmiFake_UnpartitionedGpuValuesFromSysfs) {
+  REQUIRE_FAKE();
+  // The library's per-cycle value getters fail; an SPX GPU whose amdgpu
+  // attributes are readable never needs them.
+  const char* spec =
+      "bdf=0000:d9:00.0;mode=SPX;parts=1;cus=256;xcds=8;vram_mib=294896;links=7;virt=1\n"
+      "fail=amdsmi_get_gpu_memory_total:2\n"
+      "fail=amdsmi_get_gpu_compute_partition:2\n"
+      "fail=amdsmi_get_gpu_memory_partition:2\n";
+  fake().configure(spec);
+  std::string root = temp_root();
+  std::string pci = root + "/sys/bus/pci/devices/0000:d9:00.0";
+  fs::mkdir_all(pci);
+  lm::write_file_atomically(pci + "/current_compute_partition", "SPX\n", 0644);
+  lm::write_file_atomically(pci + "/current_memory_partition", "NPS1\n", 0644);
+  lm::write_file_atomically(pci + "/mem_info_vram_total", "309220868096\n", 0644);
+  AmdSmiManager m(opts(root, true));
+  for (int c = 0; c < 2; ++c) {
+    m.Init();
+    auto devs = m.GetDevices();
+    EXPECT_EQ(devs.size(), static_cast<size_t>(1));
+    EXPECT_FALSE(devs[0]->IsPartitioned());
+    EXPECT_EQ(devs[0]->GetTotalMemoryMiB(), static_cast<uint64_t>(294896));
+    EXPECT_EQ(devs[0]->Info().compute_partition, std::string("SPX"));
+    EXPECT_EQ(devs[0]->Info().memory_partition, std::string("NPS1"));
+    EXPECT_EQ(devs[0]->Info().xcds, static_cast<uint32_t>(8));  // no KFD node: xcd counter
+    EXPECT_EQ(devs[0]->GetName(), std::string("AMD Instinct MI355 OAM"));
+    m.Shutdown();
+  }
+  // Live values: a changed attribute shows up in the next cycle.
+  lm::write_file_atomically(pci + "/current_memory_partition", "NPS2\n", 0644);
+  m.Init();
+  EXPECT_EQ(m.GetDevices()[0]->Info().memory_partition, std::string("NPS2"));
+  m.Shutdown();
+  // Not SPX per sysfs: every value goes through the library (whose injected
+  // failures then leave them unset).
+  lm::write_file_atomically(pci + "/current_compute_partition", "CPX\n", 0644);
+  m.Init();
+  EXPECT_EQ(m.GetDevices()[0]->GetTotalMemoryMiB(), static_cast<uint64_t>(0));
+  EXPECT_EQ(m.GetDevices()[0]->Info().compute_partition, std::string(""));
+  m.Shutdown();
+  fs::remove_all(root);
+}
+
 TEST(AmdSmiFake_PerCycleSessionInitsEveryWindow) {
   REQUIRE_FAKE();
   fake().configure(kTwoGpus);

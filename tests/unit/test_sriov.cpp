@@ -247,12 +247,26 @@ TEST(Sriov_SysfsScanColdParallelThenIncremental) {
   }
   EXPECT_EQ(pfs_with_vfs, 1);
   EXPECT_EQ(vfs, 2);
-  // Mutable state is re-read every scan.
-  put_file(root + "/sys/bus/pci/devices/0000:11:00.0/sriov_numvfs", "1\n");
+  // NumVFs is re-read when the listing changes.  Enabling VFs is what changes
+  // it: the kernel adds one PCI function per VF (and refuses N -> M without
+  // going through 0), so a NumVFs write never leaves the listing unchanged.
+  std::string dev = root + "/sys/bus/pci/devices/";
+  put_file(dev + "0000:11:00.0/sriov_numvfs", "1\n");
   int on = 0;
   for (const auto& d : pci.Devices())
     if (d.address == "0000:11:00.0") on = d.sriov_numvfs;
+  EXPECT_EQ(on, 0);  // same listing: the value of the previous scan stands
+  put_file(dev + "0000:11:00.1/vendor", "0x1002\n");
+  put_file(dev + "0000:11:00.1/class", "0x120000\n");
+  put_file(dev + "0000:11:00.1/device", "0x75b3\n");
+  if (symlink("../0000:11:00.0", (dev + "0000:11:00.1/physfn").c_str()) != 0) throw std::runtime_error("symlink");
+  int vfs_of_11 = 0;
+  for (const auto& d : pci.Devices()) {
+    if (d.address == "0000:11:00.0") on = d.sriov_numvfs;
+    if (d.physfn == "0000:11:00.0") ++vfs_of_11;
+  }
   EXPECT_EQ(on, 1);
+  EXPECT_EQ(vfs_of_11, 1);
   // A function removed and re-created (new sysfs inode) is re-identified.
   // (Parked elsewhere, not deleted, so this filesystem cannot hand the new
   // directory the old inode number - kernfs allocates them cyclically.)
@@ -269,4 +283,37 @@ TEST(Sriov_SysfsScanColdParallelThenIncremental) {
   fs::mkdir_all(root + "/sys/bus/pci/devices/0000:00:05.0/vendor");  // unreadable attribute
   EXPECT_THROW_MSG(cold.Devices(), "unable to read PCI device vendor id for 0000:00:05.0");
   fs::remove_all(root);
+}
+
+TEST(Fs_DirListingReportsChangesAndSurvivesRecreation) {
+  char d[] = "/tmp/gfd-dirlist-XXXXXX";
+  if (!mkdtemp(d)) throw std::runtime_error("mkdtemp");
+  std::string dir = std::string(d) + "/devices";
+  put_file(dir + "/0000:01:00.0/vendor", "0x1002\n");
+  put_file(dir + "/0000:02:00.0/vendor", "0x1002\n");
+  fs::DirListing l;
+  bool changed = false;
+  EXPECT_EQ(l.read(dir, &changed), 0);
+  EXPECT_TRUE(changed);  // first read
+  auto e = l.entries();
+  EXPECT_EQ(e.size(), static_cast<size_t>(2));
+  EXPECT_EQ(e[0].first, std::string("0000:01:00.0"));
+  EXPECT_EQ(e[1].first, std::string("0000:02:00.0"));
+  EXPECT_TRUE(e[0].second != 0 && e[0].second != e[1].second);
+  EXPECT_EQ(l.read(dir, &changed), 0);
+  EXPECT_FALSE(changed);
+  put_file(dir + "/0000:00:01.0/vendor", "0x1022\n");
+  EXPECT_EQ(l.read(dir, &changed), 0);
+  EXPECT_TRUE(changed);
+  EXPECT_EQ(l.entries().front().first, std::string("0000:00:01.0"));
+  // The directory removed and created again: the open descriptor is stale
+  // and the listing looks the path up again.
+  fs::remove_all(dir);
+  put_file(dir + "/0000:03:00.0/vendor", "0x1002\n");
+  EXPECT_EQ(l.read(dir, &changed), 0);
+  EXPECT_TRUE(changed);
+  EXPECT_EQ(l.entries().size(), static_cast<size_t>(1));
+  fs::remove_all(dir);
+  EXPECT_TRUE(l.read(dir, &changed) != 0);
+  fs::remove_all(d);
 }

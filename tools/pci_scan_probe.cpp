@@ -35,6 +35,10 @@ int main() {
   auto entries = fs::list_dir_ino(dir, &err);
   std::printf("pci functions: %zu\n", entries.size());
   std::printf("list_dir_ino p50: %.1f us\n", p50(200, [&] { fs::list_dir_ino(dir, &err); }));
+  fs::DirListing listing;
+  bool changed = false;
+  std::printf("DirListing read (open fd, getdents64 + compare) p50: %.1f us\n",
+              p50(200, [&] { listing.read(dir, &changed); }));
   sriov::SysfsAmdPCI pci("/");
   std::printf("Devices() first: %.1f us\n", p50(1, [&] { pci.Devices(); }));
   auto devs = pci.Devices();

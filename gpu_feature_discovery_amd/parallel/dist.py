@@ -33,14 +33,15 @@ class RankGroup:
         self.rank = env_int("RANK", 0)
         self.torch = None
         self.dist = None
-        try:
-            import torch  # noqa: F401
+        # One process: nothing to rendezvous with, so PyTorch is not loaded at
+        # all - the production daemon never has it in its address space, and
+        # its mere presence (threads, a second libdrm) slows amd-smi queries
+        # by ~6 us per cycle (profiles/inproc_trace.txt).
+        if self.world > 1:
+            import torch
+            import torch.distributed as dist
 
             self.torch = torch
-        except Exception:
-            self.torch = None
-        if self.world > 1:
-            import torch.distributed as dist
 
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             dist.init_process_group("gloo", rank=self.rank, world_size=self.world)

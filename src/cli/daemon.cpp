@@ -119,32 +119,58 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
                         const config::Config& config, const lm::LabelerPtr& timestamp, bool write) {
   trace::begin_cycle();
   int64_t t0 = trace::now_ns();
-  // The SR-IOV bus scan does not depend on the device backend: run it on a
-  // worker while the backend enumerates (the reference evaluates the vGPU
-  // labeler after the NVML labeler; only the merge order is observable).
+  // Work that does not depend on the device backend runs on a worker while
+  // the backend enumerates: first the node facts the device labeler needs
+  // after enumeration (machine type, file-backed versions), then the SR-IOV
+  // bus scan (the reference evaluates the vGPU labeler after the NVML
+  // labeler; only the merge order is observable).  The task never throws;
+  // an SR-IOV error is handed back and raised after the device labeler.
+  std::optional<std::string> version_root = manager.VersionFilesRoot();
+  lm::NodeFacts facts;
   lm::Labels sriov_labels;
-  int64_t sriov_ns = 0;
-  auto scan = WorkerPool::instance().submit([&] {
+  std::exception_ptr sriov_error;
+  int64_t facts_ns = 0, sriov_ns = 0;
+  auto worker = WorkerPool::instance().submit([&] {
     int64_t s0 = trace::now_ns();
-    sriov_labels = lm::NewSriovLabeler(sriov)->GetLabels();
-    sriov_ns = trace::now_ns() - s0;
+    try {
+      facts = lm::ReadNodeFacts(config, version_root);
+    } catch (...) {
+      facts = lm::NodeFacts{};  // fall back to the manager inside the labeler
+    }
+    int64_t s1 = trace::now_ns();
+    facts_ns = s1 - s0;
+    try {
+      sriov_labels = lm::NewSriovLabeler(sriov)->GetLabels();
+    } catch (...) {
+      sriov_error = std::current_exception();
+    }
+    sriov_ns = trace::now_ns() - s1;
   });
+  bool joined = false;
+  auto join = [&]() -> const lm::NodeFacts& {
+    if (!joined) {
+      worker.wait();
+      joined = true;
+    }
+    return facts;
+  };
   lm::LabelerPtr device;
   try {
-    device = GFD_WRAP("error creating device labeler", lm::NewDeviceLabeler(manager, config));
+    device = GFD_WRAP("error creating device labeler", lm::NewDeviceLabeler(manager, config, join));
   } catch (...) {
-    try {
-      scan.wait();
-    } catch (...) {
-    }
+    join();
     throw;
   }
-  try {
-    scan.wait();
-  } catch (const std::exception& e) {
-    throw Error(std::string("error generating labels: ") + e.what());
-  }
+  join();
+  trace::record("facts(overlapped)", facts_ns);
   trace::record("sriov(overlapped)", sriov_ns);
+  if (sriov_error) {
+    try {
+      std::rethrow_exception(sriov_error);
+    } catch (const std::exception& e) {
+      throw Error(std::string("error generating labels: ") + e.what());
+    }
+  }
   lm::LabelerPtr labelers = lm::merge({timestamp, device, lm::from_labels(std::move(sriov_labels))});
   CycleResult r;
   try {

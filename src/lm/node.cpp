@@ -5,6 +5,7 @@
 
 #include "lm/keys.h"
 #include "lm/resource.h"
+#include "resource/versions.h"
 #include "util/error.h"
 #include "util/fs.h"
 #include "util/log.h"
@@ -22,26 +23,31 @@ LabelerPtr NewTimestampLabeler(const config::Config& config) {
   return NewTimestampLabeler(config, static_cast<int64_t>(time(nullptr)));
 }
 
-LabelerPtr NewMachineTypeLabeler(const std::string& path) {
+namespace {
+
+Labels machine_type_labels(const std::string& path, std::string* warning) {
   std::string machine = "unknown";
   if (!path.empty()) {
     auto r = fs::read_file(path, 4096);
     if (r.ok()) {
       machine = str::trim(r.data);
     } else {
-      log::printf("WARNING: error getting machine type from %s: could not open machine type file: open %s: %s",
-                  path.c_str(), path.c_str(), fs::errno_str(r.err).c_str());
+      *warning = "WARNING: error getting machine type from " + path + ": could not open machine type file: open " +
+                 path + ": " + fs::errno_str(r.err);
     }
   }
-  return from_labels(Labels{{keys::kMachine, sanitize_label_value(str::replace_all(machine, " ", "-"))}});
+  return Labels{{keys::kMachine, sanitize_label_value(str::replace_all(machine, " ", "-"))}};
 }
 
-LabelerPtr NewVersionLabeler(resource::Manager& manager) {
-  std::string driver = GFD_WRAP("error getting driver version", manager.GetDriverVersion());
+// nvml.go:75-106: the driver version is fetched and checked before the
+// runtime version is asked for.
+template <typename DriverFn, typename RuntimeFn>
+LabelerPtr version_labeler(DriverFn&& get_driver, RuntimeFn&& get_runtime) {
+  std::string driver = GFD_WRAP("error getting driver version", get_driver());
   auto parts = str::split(driver, '.');
   if (parts.size() > 3 || parts.size() < 2)
     throw Error("error getting driver version: Version \"" + driver + "\" does not match format \"X.Y[.Z]\"");
-  resource::RuntimeVersion rt = GFD_WRAP("error getting ROCm runtime version", manager.GetRuntimeVersion());
+  resource::RuntimeVersion rt = GFD_WRAP("error getting ROCm runtime version", get_runtime());
   return from_labels(Labels{
       {keys::kDriverMajor, parts[0]},
       {keys::kDriverMinor, parts[1]},
@@ -49,6 +55,34 @@ LabelerPtr NewVersionLabeler(resource::Manager& manager) {
       {keys::kRuntimeMajor, std::to_string(rt.major)},
       {keys::kRuntimeMinor, std::to_string(rt.minor)},
   });
+}
+
+}  // namespace
+
+LabelerPtr NewMachineTypeLabeler(const std::string& path) {
+  std::string warning;
+  Labels l = machine_type_labels(path, &warning);
+  if (!warning.empty()) log::printf("%s", warning.c_str());
+  return from_labels(std::move(l));
+}
+
+LabelerPtr NewVersionLabeler(resource::Manager& manager) {
+  return version_labeler([&] { return manager.GetDriverVersion(); }, [&] { return manager.GetRuntimeVersion(); });
+}
+
+NodeFacts ReadNodeFacts(const config::Config& config, const std::optional<std::string>& version_files_root) {
+  NodeFacts f;
+  f.machine = machine_type_labels(config.machine_type_file(), &f.machine_warning);
+  if (version_files_root) {
+    f.have_versions = true;
+    f.driver_version = resource::driver_version(*version_files_root);
+    try {
+      f.runtime_version = resource::runtime_version(*version_files_root);
+    } catch (const std::exception& e) {
+      f.runtime_error = e.what();
+    }
+  }
+  return f;
 }
 
 LabelerPtr NewPartitionCapabilityLabeler(resource::Manager& manager) {
@@ -155,7 +189,8 @@ class ShutdownGuard {
 
 LabelerPtr NewSriovLabeler(std::shared_ptr<sriov::Interface> lib) { return std::make_shared<SriovLabeler>(std::move(lib)); }
 
-LabelerPtr NewDeviceLabeler(resource::Manager& manager, const config::Config& config) {
+LabelerPtr NewDeviceLabeler(resource::Manager& manager, const config::Config& config,
+                            const std::function<const NodeFacts&()>& facts) {
   {
     trace::Span span("init");
     try {
@@ -174,8 +209,24 @@ LabelerPtr NewDeviceLabeler(resource::Manager& manager, const config::Config& co
   if (devices.empty()) return empty();
 
   trace::Span span("label");
-  auto machine = GFD_WRAP("failed to construct machine type labeler", NewMachineTypeLabeler(config.machine_type_file()));
-  auto version = GFD_WRAP("failed to construct version labeler", NewVersionLabeler(manager));
+  const NodeFacts* pre = facts ? &facts() : nullptr;
+  LabelerPtr machine, version;
+  if (pre) {
+    if (!pre->machine_warning.empty()) log::printf("%s", pre->machine_warning.c_str());
+    machine = from_labels(pre->machine);
+  } else {
+    machine = GFD_WRAP("failed to construct machine type labeler", NewMachineTypeLabeler(config.machine_type_file()));
+  }
+  if (pre && pre->have_versions) {
+    version = GFD_WRAP("failed to construct version labeler",
+                       version_labeler([&] { return pre->driver_version; },
+                                       [&] {
+                                         if (!pre->runtime_version) throw Error(pre->runtime_error);
+                                         return *pre->runtime_version;
+                                       }));
+  } else {
+    version = GFD_WRAP("failed to construct version labeler", NewVersionLabeler(manager));
+  }
   auto capability = GFD_WRAP("error creating partition capability labeler", NewPartitionCapabilityLabeler(manager));
   auto topology = GFD_WRAP("error creating topology labeler", NewTopologyLabeler(manager));
   auto resources = GFD_WRAP("error creating resource labeler", NewResourceLabeler(manager, config));

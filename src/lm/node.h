@@ -6,7 +6,9 @@
 #pragma once
 
 #include <cstdint>
+#include <functional>
 #include <memory>
+#include <optional>
 #include <string>
 
 #include "config/config.h"
@@ -40,10 +42,27 @@ LabelerPtr NewTopologyLabeler(resource::Manager& manager);
 // vGPU labeler (lm/vgpu.go:37-55).
 LabelerPtr NewSriovLabeler(std::shared_ptr<sriov::Interface> lib);
 
+// Node facts that need no device context: the DMI machine type and, for
+// managers whose version queries are plain file reads
+// (Manager::VersionFilesRoot), the driver and ROCm versions.  The daemon
+// reads them on a worker while the backend enumerates the GPUs.
+struct NodeFacts {
+  Labels machine;               // amd.com/gpu.machine
+  std::string machine_warning;  // logged when the labels are used
+  bool have_versions = false;
+  std::string driver_version;
+  std::optional<resource::RuntimeVersion> runtime_version;
+  std::string runtime_error;  // when runtime_version is unset
+};
+NodeFacts ReadNodeFacts(const config::Config& config, const std::optional<std::string>& version_files_root);
+
 // The device labeler (NewNVMLLabeler analogue, nvml.go:29-72): Init, defer
 // Shutdown, enumerate, and build every device-derived labeler eagerly inside
-// that window.  Zero devices -> empty.
-LabelerPtr NewDeviceLabeler(resource::Manager& manager, const config::Config& config);
+// that window.  Zero devices -> empty.  `facts`, if given, is called (once,
+// after enumeration) for facts read concurrently; it may block until they
+// are ready.
+LabelerPtr NewDeviceLabeler(resource::Manager& manager, const config::Config& config,
+                            const std::function<const NodeFacts&()>& facts = nullptr);
 
 // NewLabelers (labeler.go:33-45): Merge(device labeler, SR-IOV labeler).
 LabelerPtr NewLabelers(resource::Manager& manager, std::shared_ptr<sriov::Interface> sriov,

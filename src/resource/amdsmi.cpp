@@ -707,15 +707,9 @@ std::string AmdSmiManager::GetDriverVersion() {
   // driver and the kernel banner for an in-tree one (measured on the pool:
   // "Linuxversion6.18.54-ant.1(...)").  Reading those sources directly gives
   // the same answer without the ~130 us library round trip per cycle.
-  std::string raw = host_driver_version(opts_.root);
-  auto v = extract_version(raw);
-  return v ? *v : raw;
+  return driver_version(opts_.root);
 }
 
-RuntimeVersion AmdSmiManager::GetRuntimeVersion() {
-  auto v = rocm_version(opts_.root);
-  if (!v) throw Error("unable to determine the ROCm version (no .info/version under $ROCM_PATH or /opt/rocm)");
-  return *v;
-}
+RuntimeVersion AmdSmiManager::GetRuntimeVersion() { return runtime_version(opts_.root); }
 
 }  // namespace gfd::resource

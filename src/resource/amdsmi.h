@@ -56,6 +56,7 @@ class AmdSmiManager : public Manager {
   std::string GetDriverVersion() override;
   RuntimeVersion GetRuntimeVersion() override;
   std::string Name() const override { return opts_.persistent ? "amdsmi(persistent)" : "amdsmi"; }
+  std::optional<std::string> VersionFilesRoot() const override { return opts_.root; }
 
   // Number of amdsmi_init calls made by this manager (tests / benchmarks).
   int init_count() const { return init_count_; }

@@ -39,6 +39,7 @@ class FallbackManager : public Manager {
   std::string GetDriverVersion() override { return current_->GetDriverVersion(); }
   RuntimeVersion GetRuntimeVersion() override { return current_->GetRuntimeVersion(); }
   std::string Name() const override { return "fallback(" + current_->Name() + ")"; }
+  std::optional<std::string> VersionFilesRoot() const override { return current_->VersionFilesRoot(); }
   bool fell_back() const { return fell_back_; }
 
  private:

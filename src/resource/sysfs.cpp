@@ -166,9 +166,15 @@ SysfsManager::SysfsManager(SysfsOptions opts) : opts_(std::move(opts)) {
 }
 
 void SysfsManager::Init() {
-  int err = 0;
-  fs::list_dir(topology_, &err);
-  if (err != 0) throw Error("KFD topology not available at " + topology_ + ": " + fs::errno_str(err));
+  // generation_id lives next to nodes/; when it is readable the topology is
+  // there.  Otherwise list nodes/ (kernels without generation_id, or to get
+  // the error to report).
+  generation_ = fs::read_trimmed(fs::join(opts_.root, "sys/class/kfd/kfd/topology/generation_id")).value_or("");
+  if (generation_.empty()) {
+    int err = 0;
+    fs::list_dir(topology_, &err);
+    if (err != 0) throw Error("KFD topology not available at " + topology_ + ": " + fs::errno_str(err));
+  }
   initialized_ = true;
   have_snapshot_ = false;
 }
@@ -266,7 +272,12 @@ static DevicePtr describe_gpu(const std::string& root, bool in_vm, int index, co
   return dev;
 }
 
-std::vector<DevicePtr> SysfsManager::enumerate() const {
+struct SysfsManager::Topology {
+  std::vector<KfdNode> nodes;                              // accessible GPU nodes, by node id
+  std::map<std::string, std::vector<const KfdNode*>> groups;  // by BDF (ordered)
+};
+
+std::shared_ptr<const SysfsManager::Topology> SysfsManager::read_topology() const {
   // 1. Read every accessible GPU node.  A CPX node has 64 of them, so the
   //    reads are spread over the worker pool in chunks.
   std::vector<KfdNode> nodes;
@@ -292,14 +303,26 @@ std::vector<DevicePtr> SysfsManager::enumerate() const {
   int64_t t0 = trace::now_ns();
   WorkerPool::instance().parallel_for(chunks, read_chunk);
   trace::record("sysfs.nodes", trace::now_ns() - t0);
-  std::vector<KfdNode> gpus_nodes;
+  auto topo = std::make_shared<Topology>();
   for (size_t i = 0; i < nodes.size(); ++i)
-    if (usable[i]) gpus_nodes.push_back(std::move(nodes[i]));
-  std::sort(gpus_nodes.begin(), gpus_nodes.end(), [](const KfdNode& a, const KfdNode& b) { return a.id < b.id; });
+    if (usable[i]) topo->nodes.push_back(std::move(nodes[i]));
+  std::sort(topo->nodes.begin(), topo->nodes.end(), [](const KfdNode& a, const KfdNode& b) { return a.id < b.id; });
 
   // 2. Group partitions by PCI location (partitions share the parent's BDF).
-  std::map<std::string, std::vector<const KfdNode*>> groups;  // ordered by BDF
-  for (const auto& n : gpus_nodes) groups[bdf_of(n)].push_back(&n);
+  for (const auto& n : topo->nodes) topo->groups[bdf_of(n)].push_back(&n);
+  return topo;
+}
+
+std::vector<DevicePtr> SysfsManager::enumerate() {
+  std::shared_ptr<const Topology> topo;
+  if (!generation_.empty() && generation_ == cached_generation_ && cached_) {
+    topo = cached_;
+  } else {
+    topo = read_topology();
+    cached_ = generation_.empty() ? nullptr : topo;
+    cached_generation_ = generation_;
+  }
+  const auto& groups = topo->groups;
 
   // 3. Describe each visible physical GPU (~10 sysfs reads each), in
   //    parallel across GPUs.
@@ -322,16 +345,8 @@ std::vector<DevicePtr> SysfsManager::enumerate() const {
   return out;
 }
 
-std::string SysfsManager::GetDriverVersion() {
-  std::string raw = host_driver_version(opts_.root);
-  auto v = extract_version(raw);
-  return v ? *v : raw;
-}
+std::string SysfsManager::GetDriverVersion() { return driver_version(opts_.root); }
 
-RuntimeVersion SysfsManager::GetRuntimeVersion() {
-  auto v = rocm_version(opts_.root);
-  if (!v) throw Error("unable to determine the ROCm version (no .info/version under $ROCM_PATH or /opt/rocm)");
-  return *v;
-}
+RuntimeVersion SysfsManager::GetRuntimeVersion() { return runtime_version(opts_.root); }
 
 }  // namespace gfd::resource

@@ -20,6 +20,7 @@
 // `root` prefixes every path so synthetic trees (tests, benchmarks) work.
 #pragma once
 
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -42,13 +43,28 @@ class SysfsManager : public Manager {
   std::string GetDriverVersion() override;
   RuntimeVersion GetRuntimeVersion() override;
   std::string Name() const override { return "sysfs"; }
+  std::optional<std::string> VersionFilesRoot() const override { return opts_.root; }
 
   // Enumerate without the Init/Shutdown protocol (used by GetDevices).
-  std::vector<DevicePtr> enumerate() const;
+  std::vector<DevicePtr> enumerate();
+
+  // GPU nodes of one KFD topology generation, grouped by PCI address.
+  struct Topology;
 
  private:
+  std::shared_ptr<const Topology> read_topology() const;
+
   SysfsOptions opts_;
   std::string topology_;
+  // The parsed GPU nodes are kept while KFD's topology generation_id (read
+  // in Init) is unchanged: KFD rebuilds the topology and bumps the generation
+  // whenever a node appears, disappears or changes (partition switch, driver
+  // reload, hot-plug), so an unchanged generation means unchanged node
+  // properties.  The per-GPU attributes (memory, partition modes, links,
+  // SR-IOV state) are still read every cycle.
+  std::string generation_;
+  std::string cached_generation_;
+  std::shared_ptr<const Topology> cached_;
   bool in_vm_ = false;  // CPU reports a hypervisor (fixed for the process)
   bool initialized_ = false;
   bool have_snapshot_ = false;

@@ -160,6 +160,11 @@ class Manager {
   virtual std::string GetDriverVersion() = 0;
   virtual RuntimeVersion GetRuntimeVersion() = 0;
   virtual std::string Name() const = 0;
+  // For managers whose version queries are plain reads of node files
+  // (resource::driver_version / runtime_version under this root) and touch
+  // no manager state: the daemon then reads them on a worker, overlapped
+  // with enumeration.  nullopt: ask the manager, inside the Init window.
+  virtual std::optional<std::string> VersionFilesRoot() const { return std::nullopt; }
 };
 
 using ManagerPtr = std::shared_ptr<Manager>;

@@ -4,6 +4,7 @@
 
 #include <cstdlib>
 
+#include "util/error.h"
 #include "util/fs.h"
 #include "util/strings.h"
 
@@ -58,6 +59,18 @@ std::optional<RuntimeVersion> rocm_version(const std::string& root) {
     if (maj && min) return RuntimeVersion{static_cast<unsigned>(*maj), static_cast<unsigned>(*min)};
   }
   return std::nullopt;
+}
+
+std::string driver_version(const std::string& root) {
+  std::string raw = host_driver_version(root);
+  auto v = extract_version(raw);
+  return v ? *v : raw;
+}
+
+RuntimeVersion runtime_version(const std::string& root) {
+  auto v = rocm_version(root);
+  if (!v) throw Error("unable to determine the ROCm version (no .info/version under $ROCM_PATH or /opt/rocm)");
+  return *v;
 }
 
 }  // namespace gfd::resource

@@ -32,4 +32,10 @@ std::string host_driver_version(const std::string& root);
 // <root>/opt/rocm/.info/version.  nullopt if not installed.
 std::optional<RuntimeVersion> rocm_version(const std::string& root);
 
+// What the file-backed managers (amd-smi, KFD sysfs) answer for
+// GetDriverVersion: the X.Y[.Z] part of host_driver_version, else the raw text.
+std::string driver_version(const std::string& root);
+// Their GetRuntimeVersion: rocm_version or an error naming where it looked.
+RuntimeVersion runtime_version(const std::string& root);
+
 }  // namespace gfd::resource

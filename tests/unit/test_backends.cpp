@@ -81,6 +81,37 @@ struct Tree {
 
 }  // namespace
 
+TEST(Sysfs_TopologyKeptPerKfdGeneration) {
+  Tree t;
+  std::string nodes = t.root + "/sys/class/kfd/kfd/topology/nodes";
+  SysfsManager m(SysfsOptions{t.root, DeviceFilter()});
+  auto cycle = [&] {
+    m.Init();
+    auto d = m.GetDevices();
+    m.Shutdown();
+    return d;
+  };
+  EXPECT_EQ(cycle()[1]->Info().xcds, static_cast<uint32_t>(8));
+  // A node property rewritten without a new generation (KFD never does that)
+  // is not re-read; per-GPU attributes still are.
+  put(nodes + "/1/properties", kfd_props(90500, 1024, 4, 0xd900, 128, 0x3a7c178b7c5e4d5cULL));
+  put(t.root + "/sys/bus/pci/devices/0000:d9:00.0/current_memory_partition", "NPS2\n");
+  auto d = cycle();
+  EXPECT_EQ(d[1]->Info().xcds, static_cast<uint32_t>(8));
+  EXPECT_EQ(d[1]->Info().memory_partition, std::string("NPS2"));
+  // KFD re-enumerates (partition switch, driver reload): new generation.
+  put(t.root + "/sys/class/kfd/kfd/topology/generation_id", "2\n");
+  EXPECT_EQ(cycle()[1]->Info().xcds, static_cast<uint32_t>(4));
+  // A GPU removed together with a generation bump disappears.
+  fs::remove_all(nodes + "/1");
+  put(t.root + "/sys/class/kfd/kfd/topology/generation_id", "3\n");
+  EXPECT_EQ(cycle().size(), static_cast<size_t>(1));
+  // Without generation_id nothing is kept.
+  fs::remove_all(t.root + "/sys/class/kfd/kfd/topology/generation_id");
+  put(nodes + "/1/properties", kfd_props(90500, 1024, 8, 0xd900, 128, 0x3a7c178b7c5e4d5cULL));
+  EXPECT_EQ(cycle().size(), static_cast<size_t>(2));
+}
+
 TEST(Sysfs_EnumeratesSpxAndCpxGpus) {
   Tree t;
   SysfsManager m(SysfsOptions{t.root, DeviceFilter()});

@@ -255,6 +255,37 @@ TEST(VersionLabeler_RuntimeErrorPropagates) {
   EXPECT_THROW_MSG(lm::NewVersionLabeler(m), "error getting ROCm runtime version: no rocm");
 }
 
+// Facts read on the daemon's worker (file-backed managers) give the same
+// labels and errors as asking the manager.
+TEST(NodeFacts_PrefetchedVersionsMatchManager) {
+  char d[] = "/tmp/gfd-facts-XXXXXX";
+  if (!mkdtemp(d)) throw std::runtime_error("mkdtemp");
+  std::string root = d;
+  fs::mkdir_all(root + "/sys/module/amdgpu");
+  lm::write_file_atomically(root + "/sys/module/amdgpu/version", "6.12.12\n", 0644);
+  config::Config c;
+  c.flags.gfd.machine_type_file = root + "/missing-dmi";
+  lm::NodeFacts f = lm::ReadNodeFacts(c, root);
+  EXPECT_TRUE(f.have_versions);
+  EXPECT_EQ(f.driver_version, std::string("6.12.12"));
+  EXPECT_FALSE(f.runtime_version.has_value());  // no opt/rocm/.info/version in this root
+  EXPECT_EQ(f.machine, (Labels{{"amd.com/gpu.machine", "unknown"}}));
+  EXPECT_TRUE(f.machine_warning.find("error getting machine type") != std::string::npos);
+  resource::MockManager m({resource::new_full_gpu()});
+  EXPECT_THROW_MSG(lm::NewDeviceLabeler(m, c, [&]() -> const lm::NodeFacts& { return f; }),
+                   "error getting ROCm runtime version: unable to determine the ROCm version");
+  fs::mkdir_all(root + "/opt/rocm/.info");
+  lm::write_file_atomically(root + "/opt/rocm/.info/version", "7.2.0-43\n", 0644);
+  f = lm::ReadNodeFacts(c, root);
+  auto l = lm::NewDeviceLabeler(m, c, [&]() -> const lm::NodeFacts& { return f; })->GetLabels();
+  EXPECT_EQ(l["amd.com/driver.minor"], std::string("12"));
+  EXPECT_EQ(l["amd.com/rocm.runtime.major"], std::string("7"));
+  EXPECT_EQ(l["amd.com/gpu.machine"], std::string("unknown"));
+  // Without a version root the manager is asked (mock: 6.12.12 / 7.2).
+  EXPECT_FALSE(lm::ReadNodeFacts(c, std::nullopt).have_versions);
+  fs::remove_all(root);
+}
+
 // ---- Machine type / timestamp ----
 
 TEST(MachineTypeLabeler_ReadsAndReplacesSpaces) {

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Per-call amd-smi timing of in-process labeling cycles, with and without
-PyTorch in the process (and in which load order).
+PyTorch in the process (and in which load order), and of the KFD-sysfs
+backend ("sysfs" column).
 
     python tools/inproc_trace.py [cycles]
 """
@@ -25,7 +26,8 @@ if mode == "torch-first":
     import torch; torch.cuda.device_count()
 if mode == "amdsmi-first":
     g.load_amdsmi(); import torch; torch.cuda.device_count()
-s = g.Session(["--backend=amdsmi", "--output-file=/tmp/gfd-inproc/gfd"])
+backend = "sysfs" if mode == "sysfs" else "amdsmi"
+s = g.Session([f"--backend={backend}", "--output-file=/tmp/gfd-inproc/gfd"])
 acc = {{}}
 for i in range(n):
     r = s.cycle(True)
@@ -42,7 +44,7 @@ def main() -> None:
     os.makedirs("/tmp/gfd-inproc", exist_ok=True)
     env = {**os.environ, "GFD_AMDSMI_CALL_TRACE": "1"}
     rows = {}
-    for mode in ("no-torch", "amdsmi-first", "torch-first"):
+    for mode in ("no-torch", "amdsmi-first", "torch-first", "sysfs"):
         cp = subprocess.run([sys.executable, "-c", CHILD.format(repo=REPO), mode, str(n)], capture_output=True,
                             text=True, timeout=600, env=env)
         if cp.returncode != 0:

@@ -6,6 +6,7 @@
 
 #include <cerrno>
 #include <cstdio>
+#include <cstdint>
 #include <cstdlib>
 
 #include "util/error.h"
@@ -59,6 +60,39 @@ bool write_all(int fd, const std::string& data) {
   return true;
 }
 
+// The process umask, from /proc/self/status (reading it with umask(2) would
+// briefly change it for every thread); 022 if unavailable.
+mode_t process_umask() {
+  static const mode_t mask = [] {
+    auto r = fs::read_file("/proc/self/status", 8192);
+    auto pos = r.ok() ? r.data.find("\nUmask:") : std::string::npos;
+    if (pos == std::string::npos) return static_cast<mode_t>(022);
+    return static_cast<mode_t>(std::strtoul(r.data.c_str() + pos + 7, nullptr, 8));
+  }();
+  return mask;
+}
+
+// mkstemp with the final permission bits: "<dir>/gfd-XXXXXX" with a random
+// suffix, O_EXCL.  Returns the fd (name in *name) or -1 with errno set.
+int create_temp(const std::string& dir, unsigned perm, std::string* name) {
+  static const char kChars[] = "abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789";
+  static thread_local uint64_t state = static_cast<uint64_t>(::getpid()) * 0x9E3779B97F4A7C15ULL ^
+                                       static_cast<uint64_t>(reinterpret_cast<uintptr_t>(&state));
+  for (int attempt = 0; attempt < 100; ++attempt) {
+    *name = dir + "/gfd-";
+    for (int i = 0; i < 6; ++i) {
+      state ^= state << 13;
+      state ^= state >> 7;
+      state ^= state << 17;
+      name->push_back(kChars[state % (sizeof(kChars) - 1)]);
+    }
+    int fd = ::open(name->c_str(), O_WRONLY | O_CREAT | O_EXCL | O_CLOEXEC, perm);
+    if (fd >= 0 || errno != EEXIST) return fd;
+  }
+  errno = EEXIST;
+  return -1;
+}
+
 }  // namespace
 
 LabelerPtr from_labels(Labels l) { return std::make_shared<FixedLabeler>(std::move(l)); }
@@ -82,13 +116,18 @@ std::string render(const Labels& labels) {
 void write_file_atomically(const std::string& path, const std::string& contents, unsigned perm) {
   std::string abs = fs::absolute(path);
   std::string tmp_dir = fs::join(fs::dirname(abs), "gfd-tmp");
-  try {
-    fs::mkdir_all(tmp_dir);
-  } catch (const std::exception& e) {
-    throw Error(std::string("failed to create temporary directory: ") + e.what());
+  // The temporary directory normally exists from the previous cycle: try the
+  // create first and make the directory only when it is missing.
+  std::string tmpl;
+  int fd = create_temp(tmp_dir, perm, &tmpl);
+  if (fd < 0 && errno == ENOENT) {
+    try {
+      fs::mkdir_all(tmp_dir);
+    } catch (const std::exception& e) {
+      throw Error(std::string("failed to create temporary directory: ") + e.what());
+    }
+    fd = create_temp(tmp_dir, perm, &tmpl);
   }
-  std::string tmpl = fs::join(tmp_dir, "gfd-XXXXXX");
-  int fd = ::mkstemp(tmpl.data());
   if (fd < 0) {
     int e = errno;
     fs::remove_all(tmp_dir);
@@ -101,7 +140,9 @@ void write_file_atomically(const std::string& path, const std::string& contents,
     throw Error(msg);
   };
   if (!write_all(fd, contents)) fail("error writing temporary file '" + tmpl + "': " + fs::errno_str(errno));
-  if (::fchmod(fd, perm) != 0) fail("error setting permissions on '" + tmpl + "': " + fs::errno_str(errno));
+  // Created with `perm` already; chmod only what the umask took away.
+  if ((perm & process_umask()) != 0 && ::fchmod(fd, perm) != 0)
+    fail("error setting permissions on '" + tmpl + "': " + fs::errno_str(errno));
   if (::close(fd) != 0) {
     int e = errno;
     ::unlink(tmpl.c_str());

@@ -398,7 +398,9 @@ int sysfs_xgmi_links(const std::string& root, const std::string& bdf) {
   return any ? total : -1;
 }
 
-void query_gpu_extras(AmdSmiLib& L, const ProcInfo& p, const std::string& root, bool partitioned, GpuExtras& x) {
+// GPU-level capabilities: xGMI links, virtualization mode, supported
+// partition modes.  Any processor handle of the GPU will do.
+void query_gpu_caps(AmdSmiLib& L, const ProcInfo& p, const std::string& root, GpuExtras& x) {
   x.xgmi_links = AMDSMI_CALL("xgmi_num_links(sysfs)", sysfs_xgmi_links(root, p.bdf));
   if (x.xgmi_links < 0 && L.get_gpu_xgmi_link_status) {
     amdsmi_xgmi_link_status_t ls;
@@ -446,8 +448,11 @@ void query_gpu_extras(AmdSmiLib& L, const ProcInfo& p, const std::string& root, 
       for (auto& m : str::split(*v, ','))
         if (!str::trim(m).empty()) x.available_compute.push_back(str::trim(m));
   }
-  // Per-partition engine counts (only meaningful when partitioned).
-  if (partitioned && L.get_gpu_accelerator_partition_profile) {
+}
+
+// Per-partition engine counts (only meaningful when partitioned).
+void query_partition_engines(AmdSmiLib& L, const ProcInfo& p, GpuExtras& x) {
+  if (L.get_gpu_accelerator_partition_profile) {
     amdsmi_accelerator_partition_profile_t prof;
     std::memset(&prof, 0, sizeof(prof));
     uint32_t ids[AMDSMI_MAX_ACCELERATOR_PARTITIONS] = {0};
@@ -595,7 +600,9 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
     std::string bdf;
     std::vector<ProcInfo>* procs;
     GpuExtras extras;
-    std::exception_ptr error;
+    std::exception_ptr error;       // value queries
+    std::exception_ptr caps_error;  // capability reads
+    int64_t proc_ns = 0, caps_ns = 0;
     uint32_t kfd_node = kNoNode;  // session cache entry (unpartitioned GPUs)
   };
   std::vector<Gpu> gpus;
@@ -612,31 +619,59 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
   }
   const bool sysfs_values = sysfs_values_enabled();
 
-  // Query every processor; parallel across physical GPUs on multi-GPU nodes
-  // (amd-smi serialises queries per device, so splitting one GPU's queries
-  // over threads is slower - measured 273 us sequential vs 472 us split).
-  auto work = [&](Gpu& g) {
+  // Query every processor; parallel across physical GPUs on multi-GPU nodes.
+  // An unpartitioned GPU's capability reads (sysfs attributes, plus one
+  // sub-microsecond amd-smi call) are a work item of their own, run
+  // concurrently with its value queries.  A partitioned GPU's processors are
+  // all amd-smi calls, which the library serialises per device (splitting
+  // them over threads measured 472 us vs 273 us sequential), so its
+  // capabilities follow its value queries in the same item.
+  auto proc_work = [&](Gpu& g) {
+    int64_t t0 = trace::now_ns();
     try {
-      {
-        trace::Span s("amdsmi.proc");
-        auto& procs = *g.procs;
-        if (!(sysfs_values && procs.size() == 1 && query_unpartitioned(L, opts_.root, procs[0], &g.kfd_node)))
-          for (auto& p : procs) query_proc(L, opts_.root, p);
-      }
-      std::sort(g.procs->begin(), g.procs->end(),
+      auto& procs = *g.procs;
+      if (!(sysfs_values && procs.size() == 1 && query_unpartitioned(L, opts_.root, procs[0], &g.kfd_node)))
+        for (auto& p : procs) query_proc(L, opts_.root, p);
+      std::sort(procs.begin(), procs.end(),
                 [](const ProcInfo& a, const ProcInfo& b) { return a.partition_id < b.partition_id; });
-      const ProcInfo& first = g.procs->front();
-      bool partitioned = g.procs->size() > 1 || (!first.compute_partition.empty() && first.compute_partition != "SPX");
-      trace::Span s("amdsmi.extras");
-      query_gpu_extras(L, first, opts_.root, partitioned, g.extras);
+      g.proc_ns = trace::now_ns() - t0;
+      if (procs.size() > 1) {
+        int64_t t1 = trace::now_ns();
+        query_gpu_caps(L, procs.front(), opts_.root, g.extras);
+        query_partition_engines(L, procs.front(), g.extras);
+        g.caps_ns = trace::now_ns() - t1;
+      }
     } catch (...) {
       g.error = std::current_exception();
     }
   };
+  auto caps_work = [&](Gpu& g) {
+    if (g.procs->size() != 1) return;
+    int64_t t0 = trace::now_ns();
+    try {
+      query_gpu_caps(L, g.procs->front(), opts_.root, g.extras);
+    } catch (...) {
+      g.caps_error = std::current_exception();
+    }
+    g.caps_ns = trace::now_ns() - t0;
+  };
   size_t threads = opts_.threads > 0 ? static_cast<size_t>(opts_.threads) : 8;
-  WorkerPool::instance().parallel_for(gpus.size(), [&](size_t i) { work(gpus[i]); }, threads);
-  for (const auto& g : gpus)
+  const size_t n = gpus.size();
+  WorkerPool::instance().parallel_for(
+      2 * n, [&](size_t i) { i < n ? proc_work(gpus[i]) : caps_work(gpus[i - n]); }, threads);
+  int64_t proc_ns = 0, caps_ns = 0;
+  for (auto& g : gpus) {
     if (g.error) std::rethrow_exception(g.error);
+    if (g.caps_error) std::rethrow_exception(g.caps_error);
+    proc_ns = std::max(proc_ns, g.proc_ns);
+    caps_ns = std::max(caps_ns, g.caps_ns);
+    // A lone processor in a partitioned mode (other partitions not visible).
+    const ProcInfo& first = g.procs->front();
+    if (g.procs->size() == 1 && !first.compute_partition.empty() && first.compute_partition != "SPX")
+      query_partition_engines(L, first, g.extras);
+  }
+  trace::record("amdsmi.proc", proc_ns);
+  trace::record("amdsmi.extras", caps_ns);
   for (const auto& g : gpus) {
     if (!g.extras.virtualization.empty()) virt_mode_[g.bdf] = g.extras.virtualization;
     if (g.kfd_node != kNoNode) kfd_node_[g.bdf] = g.kfd_node;

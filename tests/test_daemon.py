@@ -51,6 +51,18 @@ def test_oneshot_exit_zero_and_file_kept(binary, tmp_path):
     assert oct(out.stat().st_mode & 0o777) == "0o644"
 
 
+def test_file_mode_0644_under_restrictive_umask(binary, tmp_path):
+    """The temporary file is created with the final mode; a umask that takes
+    bits away is undone with chmod, like the reference's explicit Chmod."""
+    out = tmp_path / "gfd"
+    e = {k: v for k, v in os.environ.items() if not k.startswith("GFD_")}
+    cp = subprocess.run([binary, "--oneshot", *_base(tmp_path, out)], capture_output=True, text=True, timeout=30,
+                        env=e, preexec_fn=lambda: os.umask(0o077))
+    assert cp.returncode == 0, cp.stderr
+    assert oct(out.stat().st_mode & 0o777) == "0o644"
+    assert list((tmp_path / "gfd-tmp").iterdir()) == []
+
+
 def test_stdout_mode_when_output_empty(binary, tmp_path):
     args = _base(tmp_path, "")
     cp = run_daemon(binary, "--oneshot", "--no-timestamp", *args, check=True)

@@ -27,7 +27,7 @@ if mode == "torch-first":
 if mode == "amdsmi-first":
     g.load_amdsmi(); import torch; torch.cuda.device_count()
 backend = "sysfs" if mode == "sysfs" else "amdsmi"
-s = g.Session([f"--backend={backend}", "--output-file=/tmp/gfd-inproc/gfd"])
+s = g.Session(["--backend=" + backend, "--output-file=/tmp/gfd-inproc/gfd"])
 acc = {{}}
 for i in range(n):
     r = s.cycle(True)

@@ -600,8 +600,7 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
     std::string bdf;
     std::vector<ProcInfo>* procs;
     GpuExtras extras;
-    std::exception_ptr error;       // value queries
-    std::exception_ptr caps_error;  // capability reads
+    std::exception_ptr error;
     int64_t proc_ns = 0, caps_ns = 0;
     uint32_t kfd_node = kNoNode;  // session cache entry (unpartitioned GPUs)
   };
@@ -619,56 +618,40 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
   }
   const bool sysfs_values = sysfs_values_enabled();
 
-  // Query every processor; parallel across physical GPUs on multi-GPU nodes.
-  // An unpartitioned GPU's capability reads (sysfs attributes, plus one
-  // sub-microsecond amd-smi call) are a work item of their own, run
-  // concurrently with its value queries.  A partitioned GPU's processors are
-  // all amd-smi calls, which the library serialises per device (splitting
-  // them over threads measured 472 us vs 273 us sequential), so its
-  // capabilities follow its value queries in the same item.
-  auto proc_work = [&](Gpu& g) {
-    int64_t t0 = trace::now_ns();
+  // Query every processor; parallel across physical GPUs on multi-GPU nodes,
+  // sequential within one GPU: amdgpu serialises a device's queries on its
+  // own locks (amd-smi adds a per-device mutex), so splitting one GPU's reads
+  // over threads makes each of them slower - measured 273 us sequential vs
+  // 472 us split with amd-smi calls, and 2-3x slower sysfs reads (value
+  // reads concurrent with the capability reads, profiles/README.md).
+  auto work = [&](Gpu& g) {
     try {
+      int64_t t0 = trace::now_ns();
       auto& procs = *g.procs;
       if (!(sysfs_values && procs.size() == 1 && query_unpartitioned(L, opts_.root, procs[0], &g.kfd_node)))
         for (auto& p : procs) query_proc(L, opts_.root, p);
       std::sort(procs.begin(), procs.end(),
                 [](const ProcInfo& a, const ProcInfo& b) { return a.partition_id < b.partition_id; });
-      g.proc_ns = trace::now_ns() - t0;
-      if (procs.size() > 1) {
-        int64_t t1 = trace::now_ns();
-        query_gpu_caps(L, procs.front(), opts_.root, g.extras);
-        query_partition_engines(L, procs.front(), g.extras);
-        g.caps_ns = trace::now_ns() - t1;
-      }
+      int64_t t1 = trace::now_ns();
+      const ProcInfo& first = procs.front();
+      query_gpu_caps(L, first, opts_.root, g.extras);
+      if (procs.size() > 1 || (!first.compute_partition.empty() && first.compute_partition != "SPX"))
+        query_partition_engines(L, first, g.extras);
+      g.proc_ns = t1 - t0;
+      g.caps_ns = trace::now_ns() - t1;
     } catch (...) {
       g.error = std::current_exception();
     }
   };
-  auto caps_work = [&](Gpu& g) {
-    if (g.procs->size() != 1) return;
-    int64_t t0 = trace::now_ns();
-    try {
-      query_gpu_caps(L, g.procs->front(), opts_.root, g.extras);
-    } catch (...) {
-      g.caps_error = std::current_exception();
-    }
-    g.caps_ns = trace::now_ns() - t0;
-  };
   size_t threads = opts_.threads > 0 ? static_cast<size_t>(opts_.threads) : 8;
-  const size_t n = gpus.size();
-  WorkerPool::instance().parallel_for(
-      2 * n, [&](size_t i) { i < n ? proc_work(gpus[i]) : caps_work(gpus[i - n]); }, threads);
+  WorkerPool::instance().parallel_for(gpus.size(), [&](size_t i) { work(gpus[i]); }, threads);
+  // Phase times: the slowest GPU (items may have run on pool threads, whose
+  // trace records are their own).
   int64_t proc_ns = 0, caps_ns = 0;
-  for (auto& g : gpus) {
+  for (const auto& g : gpus) {
     if (g.error) std::rethrow_exception(g.error);
-    if (g.caps_error) std::rethrow_exception(g.caps_error);
     proc_ns = std::max(proc_ns, g.proc_ns);
     caps_ns = std::max(caps_ns, g.caps_ns);
-    // A lone processor in a partitioned mode (other partitions not visible).
-    const ProcInfo& first = g.procs->front();
-    if (g.procs->size() == 1 && !first.compute_partition.empty() && first.compute_partition != "SPX")
-      query_partition_engines(L, first, g.extras);
   }
   trace::record("amdsmi.proc", proc_ns);
   trace::record("amdsmi.extras", caps_ns);

@@ -317,3 +317,39 @@ TEST(Fs_DirListingReportsChangesAndSurvivesRecreation) {
   EXPECT_TRUE(l.read(dir, &changed) != 0);
   fs::remove_all(d);
 }
+
+TEST(Sriov_ColdScanTakesVendorsFromProcTable) {
+  std::string root = pci_host(200, 2);
+  std::string dev = root + "/sys/bus/pci/devices/";
+  // procfs' device table for every function except 0000:00:07.0.
+  std::string table;
+  for (const auto& [name, ino] : fs::list_dir_ino(dev)) {
+    if (name == "0000:00:07.0") continue;
+    unsigned d = 0, b = 0, s = 0, f = 0;
+    if (std::sscanf(name.c_str(), "%x:%x:%x.%x", &d, &b, &s, &f) != 4) throw std::runtime_error(name);
+    std::string vendor = str::trim(fs::read_file(dev + name + "/vendor").data);
+    table += str::format("%04x\t%s75a3\t0\t0\n", (b << 8) | (s << 3) | f, vendor.substr(2).c_str());
+  }
+  put_file(root + "/proc/bus/pci/devices", table);
+  // A non-AMD function the table places is never read from sysfs ...
+  fs::remove_all(dev + "0000:00:05.0/vendor");
+  fs::mkdir_all(dev + "0000:00:05.0/vendor");  // unreadable attribute
+  SysfsAmdPCI pci(root);
+  auto devs = pci.Devices();
+  EXPECT_EQ(devs.size(), static_cast<size_t>(7));  // AMD functions still fully read
+  int vfs = 0;
+  for (const auto& d : devs) vfs += !d.physfn.empty();
+  EXPECT_EQ(vfs, 2);
+  // ... one the table does not list is.
+  fs::remove_all(dev + "0000:00:07.0/vendor");
+  fs::mkdir_all(dev + "0000:00:07.0/vendor");
+  SysfsAmdPCI cold(root);
+  EXPECT_THROW_MSG(cold.Devices(), "unable to read PCI device vendor id for 0000:00:07.0");
+  // A bus/devfn listed twice (two PCI domains) is ambiguous: read from sysfs.
+  put_file(root + "/proc/bus/pci/devices", table + "0028\t80861234\t0\t0\n");  // 0000:00:05.0's key again
+  fs::remove_all(dev + "0000:00:07.0/vendor");
+  put_file(dev + "0000:00:07.0/vendor", "0x1022\n");
+  SysfsAmdPCI ambiguous(root);
+  EXPECT_THROW_MSG(ambiguous.Devices(), "unable to read PCI device vendor id for 0000:00:05.0");
+  fs::remove_all(root);
+}

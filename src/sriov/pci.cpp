@@ -182,8 +182,11 @@ std::vector<PCIDevice> SysfsAmdPCI::Devices() {
   // remaining reads are spread over the worker pool in chunks.  A hot-plugged
   // function or two is read inline.
   constexpr size_t kChunk = 16;
+  size_t chunk = kChunk;
   if (misses.size() > kChunk) {
+    int64_t tp = trace::now_ns();
     auto vendors = proc_pci_vendors(root_);
+    trace::record("pci.proc_table", trace::now_ns() - tp);
     if (!vendors.empty()) {
       uint32_t amd = static_cast<uint32_t>(std::strtoul(kAmdVendorId, nullptr, 16));
       std::vector<size_t> amd_or_unknown;
@@ -194,15 +197,16 @@ std::vector<PCIDevice> SysfsAmdPCI::Devices() {
         // else: another vendor's function - identity stays "not relevant"
       }
       misses.swap(amd_or_unknown);
+      chunk = 2;  // ~6 reads per AMD function: a few functions per lane
     }
   }
   auto read_chunk = [&](size_t c) {
-    for (size_t k = c * kChunk; k < std::min(misses.size(), (c + 1) * kChunk); ++k) {
+    for (size_t k = c * chunk; k < std::min(misses.size(), (c + 1) * chunk); ++k) {
       auto& [addr, id] = next[misses[k]];
       id = read_identity(addr, fs::join(dir, addr), id.ino);
     }
   };
-  size_t chunks = (misses.size() + kChunk - 1) / kChunk;
+  size_t chunks = (misses.size() + chunk - 1) / chunk;
   if (chunks > 1)
     WorkerPool::instance().parallel_for(chunks, read_chunk);
   else if (chunks == 1)

@@ -39,8 +39,12 @@ int main() {
   bool changed = false;
   std::printf("DirListing read (open fd, getdents64 + compare) p50: %.1f us\n",
               p50(200, [&] { listing.read(dir, &changed); }));
+  std::printf("read /proc/bus/pci/devices p50: %.1f us\n",
+              p50(50, [&] { fs::read_file("/proc/bus/pci/devices", 4u << 20); }));
   sriov::SysfsAmdPCI pci("/");
+  trace::begin_cycle();
   std::printf("Devices() first: %.1f us\n", p50(1, [&] { pci.Devices(); }));
+  std::printf("first-scan phases: %s\n", trace::summary(0).c_str());
   auto devs = pci.Devices();
   std::printf("amd gpu functions: %zu\n", devs.size());
   std::printf("Devices() steady p50: %.1f us\n", p50(200, [&] { pci.Devices(); }));

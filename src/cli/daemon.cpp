@@ -119,49 +119,52 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
                         const config::Config& config, const lm::LabelerPtr& timestamp, bool write) {
   trace::begin_cycle();
   int64_t t0 = trace::now_ns();
-  // Work that does not depend on the device backend runs on a worker while
-  // the backend enumerates: first the node facts the device labeler needs
-  // after enumeration (machine type, file-backed versions), then the SR-IOV
-  // bus scan (the reference evaluates the vGPU labeler after the NVML
-  // labeler; only the merge order is observable).  The task never throws;
-  // an SR-IOV error is handed back and raised after the device labeler.
+  // Work that does not depend on the device backend runs on workers while
+  // the backend enumerates: the node facts the device labeler needs after
+  // enumeration (machine type, file-backed versions) and the SR-IOV bus scan
+  // (the reference evaluates the vGPU labeler after the NVML labeler; only
+  // the merge order is observable).  Whichever a worker has not started by
+  // the time it is needed runs on this thread instead (run_or_wait).  The
+  // tasks never throw; an SR-IOV error is handed back and raised after the
+  // device labeler.
   std::optional<std::string> version_root = manager.VersionFilesRoot();
   lm::NodeFacts facts;
   lm::Labels sriov_labels;
   std::exception_ptr sriov_error;
   int64_t facts_ns = 0, sriov_ns = 0;
-  auto worker = WorkerPool::instance().submit([&] {
+  auto facts_task = WorkerPool::instance().submit([&] {
     int64_t s0 = trace::now_ns();
     try {
       facts = lm::ReadNodeFacts(config, version_root);
     } catch (...) {
       facts = lm::NodeFacts{};  // fall back to the manager inside the labeler
     }
-    int64_t s1 = trace::now_ns();
-    facts_ns = s1 - s0;
+    facts_ns = trace::now_ns() - s0;
+  });
+  auto sriov_task = WorkerPool::instance().submit([&] {
+    int64_t s0 = trace::now_ns();
     try {
       sriov_labels = lm::NewSriovLabeler(sriov)->GetLabels();
     } catch (...) {
       sriov_error = std::current_exception();
     }
-    sriov_ns = trace::now_ns() - s1;
+    sriov_ns = trace::now_ns() - s0;
   });
-  bool joined = false;
-  auto join = [&]() -> const lm::NodeFacts& {
-    if (!joined) {
-      worker.wait();
-      joined = true;
-    }
+  auto join_facts = [&]() -> const lm::NodeFacts& {
+    facts_task.run_or_wait();
     return facts;
   };
   lm::LabelerPtr device;
   try {
-    device = GFD_WRAP("error creating device labeler", lm::NewDeviceLabeler(manager, config, join));
+    device = GFD_WRAP("error creating device labeler", lm::NewDeviceLabeler(manager, config, join_facts));
   } catch (...) {
-    join();
+    // Neither task may outlive this frame (they write its locals).
+    facts_task.cancel_or_wait();
+    sriov_task.cancel_or_wait();
     throw;
   }
-  join();
+  facts_task.cancel_or_wait();  // no devices: the labeler never needed them
+  sriov_task.run_or_wait();
   trace::record("facts(overlapped)", facts_ns);
   trace::record("sriov(overlapped)", sriov_ns);
   if (sriov_error) {

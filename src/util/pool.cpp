@@ -77,23 +77,29 @@ void WorkerPool::loop(Worker* w) {
   }
 }
 
+void WorkerPool::Task::State::run() {
+  std::exception_ptr err;
+  try {
+    fn();
+  } catch (...) {
+    err = std::current_exception();
+  }
+  fn = nullptr;  // release captures before publishing
+  std::lock_guard<std::mutex> g(mu);
+  error = err;
+  done = true;
+  cv.notify_all();
+}
+
 WorkerPool::Task WorkerPool::submit(std::function<void()> fn) {
   Task t;
   t.state_ = std::make_shared<Task::State>();
+  t.state_->fn = std::move(fn);
   auto st = t.state_;
   {
     std::lock_guard<std::mutex> g(mu_);
-    queue_.emplace_back([st, fn = std::move(fn)] {
-      std::exception_ptr err;
-      try {
-        fn();
-      } catch (...) {
-        err = std::current_exception();
-      }
-      std::lock_guard<std::mutex> g2(st->mu);
-      st->error = err;
-      st->done = true;
-      st->cv.notify_all();
+    queue_.emplace_back([st] {
+      if (!st->claimed.exchange(true)) st->run();  // else the submitter ran it
     });
     ensure_workers(queue_.size());
     wake_one();
@@ -106,6 +112,24 @@ void WorkerPool::Task::wait() {
   std::unique_lock<std::mutex> lk(state_->mu);
   state_->cv.wait(lk, [this] { return state_->done; });
   if (state_->error) std::rethrow_exception(state_->error);
+}
+
+void WorkerPool::Task::cancel_or_wait() {
+  if (!state_) return;
+  if (!state_->claimed.exchange(true)) {
+    std::lock_guard<std::mutex> g(state_->mu);
+    state_->fn = nullptr;
+    state_->done = true;
+    return;
+  }
+  std::unique_lock<std::mutex> lk(state_->mu);
+  state_->cv.wait(lk, [this] { return state_->done; });
+}
+
+void WorkerPool::Task::run_or_wait() {
+  if (!state_) return;
+  if (!state_->claimed.exchange(true)) state_->run();
+  wait();
 }
 
 void WorkerPool::parallel_for(size_t n, const std::function<void(size_t)>& fn, size_t max_parallel) {

@@ -11,6 +11,7 @@
 // so workers never steal SIGHUP/SIGTERM from the run loop's sigtimedwait.
 #pragma once
 
+#include <atomic>
 #include <condition_variable>
 #include <cstddef>
 #include <deque>
@@ -37,19 +38,30 @@ class WorkerPool {
    public:
     // Blocks until the task ran; rethrows its exception.
     void wait();
+    // Runs the task on the calling thread if no worker has started it yet,
+    // else waits for it; rethrows its exception.  A late worker wake-up
+    // (a core coming out of a deep idle state after the daemon's sleep)
+    // then costs the work itself, not the wake-up latency on top of it.
+    void run_or_wait();
+    // Drops the task if no thread has started it, else waits for it (its
+    // exception is discarded).  Afterwards fn is not running and never will.
+    void cancel_or_wait();
 
    private:
     friend class WorkerPool;
     struct State {
       std::mutex mu;
       std::condition_variable cv;
+      std::atomic<bool> claimed{false};  // a thread has started fn
       bool done = false;
       std::exception_ptr error;
+      std::function<void()> fn;
+      void run();  // claimed by the caller: run fn, publish the result
     };
     std::shared_ptr<State> state_;
   };
 
-  // Run fn on a worker.
+  // Run fn on a worker (or on the thread that calls run_or_wait first).
   Task submit(std::function<void()> fn);
   // Run fn(i) for i in [0, n): the calling thread takes part, at most
   // `max_parallel` (0 = unlimited) run concurrently.  Rethrows the first error.

@@ -77,3 +77,42 @@ TEST(Pool_NestedParallelForOnSaturatedPoolCompletes) {
   pool4.parallel_for(8, [&](size_t) { pool4.parallel_for(8, [&](size_t) { leaves++; }, 4); }, 8);
   EXPECT_EQ(leaves.load(), 64);
 }
+
+TEST(Pool_RunOrWaitRunsUnstartedTaskInline) {
+  // One worker, kept busy: a task queued behind it is run by the caller.
+  WorkerPool pool(1);
+  std::atomic<bool> release{false};
+  auto busy = pool.submit([&] {
+    while (!release.load()) std::this_thread::yield();
+  });
+  std::thread::id ran_on;
+  auto t = pool.submit([&] { ran_on = std::this_thread::get_id(); });
+  t.run_or_wait();
+  EXPECT_TRUE(ran_on == std::this_thread::get_id());
+  release = true;
+  busy.wait();
+  // Its exception reaches the caller either way.
+  auto bad = pool.submit([] { throw std::runtime_error("task failed"); });
+  EXPECT_THROW_MSG(bad.run_or_wait(), "task failed");
+}
+
+TEST(Pool_CancelOrWaitDropsUnstartedTask) {
+  WorkerPool pool(1);
+  std::atomic<bool> release{false};
+  auto busy = pool.submit([&] {
+    while (!release.load()) std::this_thread::yield();
+  });
+  std::atomic<int> ran{0};
+  auto t = pool.submit([&] { ran++; });
+  t.cancel_or_wait();
+  release = true;
+  busy.wait();
+  auto after = pool.submit([] {});
+  after.wait();  // the worker has drained the cancelled task by now
+  EXPECT_EQ(ran.load(), 0);
+  // A task already finished by a worker: cancel_or_wait returns at once.
+  auto done = pool.submit([&] { ran++; });
+  done.wait();
+  done.cancel_or_wait();
+  EXPECT_EQ(ran.load(), 1);
+}

@@ -4,6 +4,8 @@
 #include <time.h>
 
 #include <cerrno>
+#include <cstdlib>
+#include <functional>
 #include <cstdio>
 
 #include "info/version.h"
@@ -132,7 +134,7 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
   lm::Labels sriov_labels;
   std::exception_ptr sriov_error;
   int64_t facts_ns = 0, sriov_ns = 0;
-  auto facts_task = WorkerPool::instance().submit([&] {
+  std::function<void()> read_facts = [&] {
     int64_t s0 = trace::now_ns();
     try {
       facts = lm::ReadNodeFacts(config, version_root);
@@ -140,8 +142,8 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
       facts = lm::NodeFacts{};  // fall back to the manager inside the labeler
     }
     facts_ns = trace::now_ns() - s0;
-  });
-  auto sriov_task = WorkerPool::instance().submit([&] {
+  };
+  std::function<void()> scan_sriov = [&] {
     int64_t s0 = trace::now_ns();
     try {
       sriov_labels = lm::NewSriovLabeler(sriov)->GetLabels();
@@ -149,7 +151,23 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
       sriov_error = std::current_exception();
     }
     sriov_ns = trace::now_ns() - s0;
-  });
+  };
+  // Both on one worker, in that order: two workers measured slower (each
+  // task 1.5-4x longer on the second, colder core).  GFD_CYCLE_TASKS=split
+  // submits them separately (for A/B measurements).
+  static const bool split = [] {
+    const char* v = std::getenv("GFD_CYCLE_TASKS");
+    return v && std::string(v) == "split";
+  }();
+  WorkerPool::Task facts_task, sriov_task;
+  if (split) {
+    facts_task = WorkerPool::instance().submit(read_facts);
+    sriov_task = WorkerPool::instance().submit(scan_sriov);
+  } else {
+    auto seq = WorkerPool::instance().submit_sequence({read_facts, scan_sriov});
+    facts_task = seq[0];
+    sriov_task = seq[1];
+  }
   auto join_facts = [&]() -> const lm::NodeFacts& {
     facts_task.run_or_wait();
     return facts;

@@ -107,6 +107,26 @@ WorkerPool::Task WorkerPool::submit(std::function<void()> fn) {
   return t;
 }
 
+std::vector<WorkerPool::Task> WorkerPool::submit_sequence(std::vector<std::function<void()>> fns) {
+  std::vector<Task> tasks(fns.size());
+  std::vector<std::shared_ptr<Task::State>> states;
+  for (size_t i = 0; i < fns.size(); ++i) {
+    tasks[i].state_ = std::make_shared<Task::State>();
+    tasks[i].state_->fn = std::move(fns[i]);
+    states.push_back(tasks[i].state_);
+  }
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    queue_.emplace_back([states = std::move(states)] {
+      for (const auto& st : states)
+        if (!st->claimed.exchange(true)) st->run();
+    });
+    ensure_workers(queue_.size());
+    wake_one();
+  }
+  return tasks;
+}
+
 void WorkerPool::Task::wait() {
   if (!state_) return;
   std::unique_lock<std::mutex> lk(state_->mu);

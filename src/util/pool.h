@@ -63,6 +63,10 @@ class WorkerPool {
 
   // Run fn on a worker (or on the thread that calls run_or_wait first).
   Task submit(std::function<void()> fn);
+  // Run fns in order on ONE worker (same core, warm cache); each is still a
+  // Task of its own that the caller may run itself (run_or_wait) or drop
+  // (cancel_or_wait) if the worker has not reached it yet.
+  std::vector<Task> submit_sequence(std::vector<std::function<void()>> fns);
   // Run fn(i) for i in [0, n): the calling thread takes part, at most
   // `max_parallel` (0 = unlimited) run concurrently.  Rethrows the first error.
   // Safe to call from a pool task (nested): completes even if no worker is

@@ -28,7 +28,7 @@ namespace {
 Labels machine_type_labels(const std::string& path, std::string* warning) {
   std::string machine = "unknown";
   if (!path.empty()) {
-    auto r = fs::read_file(path, 4096);
+    auto r = fs::attrs().read(path, 4096);  // DMI: sysfs
     if (r.ok()) {
       machine = str::trim(r.data);
     } else {

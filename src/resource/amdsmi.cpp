@@ -253,7 +253,7 @@ bool is_generic_name(const std::string& s) { return s.empty() || s == "AMD Radeo
 // XCD count of a KFD node (num_xcc) - ~15 us versus ~140 us for
 // amdsmi_get_gpu_xcd_counter, which decodes the full gpu_metrics table.
 uint32_t kfd_num_xcc(const std::string& root, uint32_t node_id) {
-  auto r = fs::read_file(fs::join(root, "sys/class/kfd/kfd/topology/nodes/" + std::to_string(node_id) + "/properties"));
+  auto r = fs::attrs().read(fs::join(root, "sys/class/kfd/kfd/topology/nodes/" + std::to_string(node_id) + "/properties"));
   if (!r.ok()) return 0;
   static const char kKey[] = "\nnum_xcc ";
   auto pos = r.data.find(kKey);
@@ -286,7 +286,7 @@ void fix_market_name(AmdSmiLib& L, const std::string& root, ProcInfo& p) {
   if (!is_generic_name(p.market_name)) return;
   // The board FRU product name: amdgpu publishes it in sysfs (~5 us); the
   // amd-smi board-info call returns the same string for ~155 us.
-  auto v = fs::read_trimmed(fs::join(root, "sys/bus/pci/devices/" + p.bdf + "/product_name"));
+  auto v = fs::attrs().read_trimmed(fs::join(root, "sys/bus/pci/devices/" + p.bdf + "/product_name"));
   if (v && !is_generic_name(*v)) {
     p.market_name = *v;
   } else if (L.get_gpu_board_info) {
@@ -328,11 +328,11 @@ constexpr uint32_t kNoNode = 0xFFFFFFFFu;
 // partitioned or an attribute is missing; the caller then queries amd-smi.
 bool query_unpartitioned(AmdSmiLib& L, const std::string& root, ProcInfo& p, uint32_t* node_id) {
   std::string pci = fs::join(root, "sys/bus/pci/devices/" + p.bdf);
-  auto cp = AMDSMI_CALL("compute_partition(sysfs)", fs::read_trimmed(pci + "/current_compute_partition"));
+  auto cp = AMDSMI_CALL("compute_partition(sysfs)", fs::attrs().read_trimmed(pci + "/current_compute_partition"));
   if (!cp || *cp != "SPX") return false;
-  auto mp = AMDSMI_CALL("memory_partition(sysfs)", fs::read_trimmed(pci + "/current_memory_partition"));
+  auto mp = AMDSMI_CALL("memory_partition(sysfs)", fs::attrs().read_trimmed(pci + "/current_memory_partition"));
   if (!mp || mp->empty()) return false;
-  auto vram_s = AMDSMI_CALL("memory_total(sysfs)", fs::read_trimmed(pci + "/mem_info_vram_total"));
+  auto vram_s = AMDSMI_CALL("memory_total(sysfs)", fs::attrs().read_trimmed(pci + "/mem_info_vram_total"));
   auto vram = vram_s ? str::parse_uint(*vram_s) : std::nullopt;
   if (!vram || *vram == 0) return false;
   if (*node_id == kNoNode && !query_kfd(L, p, node_id)) return false;
@@ -384,7 +384,7 @@ void query_proc(AmdSmiLib& L, const std::string& root, ProcInfo& p) {
 // costs ~280 us per GPU per cycle (GFD_AMDSMI_CALL_TRACE on MI355X) versus
 // ~5 us here.
 int sysfs_xgmi_links(const std::string& root, const std::string& bdf) {
-  auto v = fs::read_trimmed(fs::join(root, "sys/bus/pci/devices/" + bdf + "/xgmi_num_links"));
+  auto v = fs::attrs().read_trimmed(fs::join(root, "sys/bus/pci/devices/" + bdf + "/xgmi_num_links"));
   if (!v) return -1;
   int total = 0;
   bool any = false;
@@ -421,7 +421,7 @@ void query_gpu_caps(AmdSmiLib& L, const ProcInfo& p, const std::string& root, Gp
   // Supported memory partition modes: world-readable in sysfs (~5 us);
   // the amd-smi partition-config call (~25 us) only as a fallback.
   if (auto v = AMDSMI_CALL("available_memory_partition(sysfs)",
-                           fs::read_trimmed(fs::join(root, "sys/bus/pci/devices/" + p.bdf + "/available_memory_partition")))) {
+                           fs::attrs().read_trimmed(fs::join(root, "sys/bus/pci/devices/" + p.bdf + "/available_memory_partition")))) {
     for (auto& m : str::split(*v, ','))
       if (!str::trim(m).empty()) x.available_memory.push_back(str::trim(m));
   } else if (L.get_gpu_memory_partition_config) {
@@ -443,7 +443,7 @@ void query_gpu_caps(AmdSmiLib& L, const ProcInfo& p, const std::string& root, Gp
   }
   if (x.available_compute.empty()) {
     auto v = AMDSMI_CALL("available_compute_partition(sysfs)",
-                         fs::read_trimmed(fs::join(root, "sys/bus/pci/devices/" + p.bdf + "/available_compute_partition")));
+                         fs::attrs().read_trimmed(fs::join(root, "sys/bus/pci/devices/" + p.bdf + "/available_compute_partition")));
     if (v)
       for (auto& m : str::split(*v, ','))
         if (!str::trim(m).empty()) x.available_compute.push_back(str::trim(m));
@@ -502,7 +502,7 @@ void AmdSmiManager::library_shutdown() {
 }
 
 std::string AmdSmiManager::read_generation() const {
-  return fs::read_trimmed(fs::join(opts_.root, "sys/class/kfd/kfd/topology/generation_id")).value_or("");
+  return fs::attrs().read_trimmed(fs::join(opts_.root, "sys/class/kfd/kfd/topology/generation_id")).value_or("");
 }
 
 void AmdSmiManager::Init() {
@@ -516,6 +516,7 @@ void AmdSmiManager::Init() {
     // invalidates every processor handle.
     std::string gen = read_generation();
     if (gen != generation_) {
+      fs::attrs().clear();  // KFD node paths of the old topology are gone
       library_shutdown();
       library_init();
       generation_ = gen;
@@ -624,14 +625,20 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
   // over threads makes each of them slower - measured 273 us sequential vs
   // 472 us split with amd-smi calls, and 2-3x slower sysfs reads (value
   // reads concurrent with the capability reads, profiles/README.md).
-  auto work = [&](Gpu& g) {
+  // One GPU's values and capabilities.  fast: only through the unpartitioned
+  // (attribute) path - returns false, having assigned nothing, if that path
+  // does not apply; otherwise every processor through the library.
+  auto work = [&](Gpu& g, bool fast) -> bool {
     try {
       int64_t t0 = trace::now_ns();
       auto& procs = *g.procs;
-      if (!(sysfs_values && procs.size() == 1 && query_unpartitioned(L, opts_.root, procs[0], &g.kfd_node)))
+      if (fast) {
+        if (procs.size() != 1 || !query_unpartitioned(L, opts_.root, procs[0], &g.kfd_node)) return false;
+      } else {
         for (auto& p : procs) query_proc(L, opts_.root, p);
-      std::sort(procs.begin(), procs.end(),
-                [](const ProcInfo& a, const ProcInfo& b) { return a.partition_id < b.partition_id; });
+        std::sort(procs.begin(), procs.end(),
+                  [](const ProcInfo& a, const ProcInfo& b) { return a.partition_id < b.partition_id; });
+      }
       int64_t t1 = trace::now_ns();
       const ProcInfo& first = procs.front();
       query_gpu_caps(L, first, opts_.root, g.extras);
@@ -642,17 +649,37 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
     } catch (...) {
       g.error = std::current_exception();
     }
+    return true;
   };
-  size_t threads = opts_.threads > 0 ? static_cast<size_t>(opts_.threads) : 8;
-  WorkerPool::instance().parallel_for(gpus.size(), [&](size_t i) { work(gpus[i]); }, threads);
-  // Phase times: the slowest GPU (items may have run on pool threads, whose
-  // trace records are their own).
+  // Unpartitioned GPUs on this thread, one after the other: ~5 us of
+  // attribute preads each on kept-open descriptors, which do not get faster
+  // on more cores (8 GPUs: 24 us on one thread, 29 us on eight -
+  // profiles/multi_gpu_read_probe.txt).  The rest - partitioned GPUs, tens
+  // of library calls each - are spread over the pool.
   int64_t proc_ns = 0, caps_ns = 0;
-  for (const auto& g : gpus) {
-    if (g.error) std::rethrow_exception(g.error);
-    proc_ns = std::max(proc_ns, g.proc_ns);
-    caps_ns = std::max(caps_ns, g.caps_ns);
+  std::vector<size_t> library_path;
+  for (size_t i = 0; i < gpus.size(); ++i) {
+    if (sysfs_values && work(gpus[i], true)) {
+      proc_ns += gpus[i].proc_ns;
+      caps_ns += gpus[i].caps_ns;
+    } else {
+      library_path.push_back(i);
+    }
   }
+  size_t threads = opts_.threads > 0 ? static_cast<size_t>(opts_.threads) : 8;
+  WorkerPool::instance().parallel_for(
+      library_path.size(), [&](size_t k) { work(gpus[library_path[k]], false); }, threads);
+  // Phase times: serial part summed, pooled part by its slowest GPU (items
+  // may have run on pool threads, whose trace records are their own).
+  int64_t pooled_proc = 0, pooled_caps = 0;
+  for (size_t k : library_path) {
+    pooled_proc = std::max(pooled_proc, gpus[k].proc_ns);
+    pooled_caps = std::max(pooled_caps, gpus[k].caps_ns);
+  }
+  proc_ns += pooled_proc;
+  caps_ns += pooled_caps;
+  for (const auto& g : gpus)
+    if (g.error) std::rethrow_exception(g.error);
   trace::record("amdsmi.proc", proc_ns);
   trace::record("amdsmi.extras", caps_ns);
   for (const auto& g : gpus) {

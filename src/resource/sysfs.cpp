@@ -129,7 +129,7 @@ std::string bdf_of(const KfdNode& n) {
 // passthrough; otherwise bare metal.
 std::string virtualization_mode(const std::string& pci, uint32_t device_id, bool in_vm) {
   if (is_mxgpu_vf(device_id) || fs::exists(fs::join(pci, "physfn"))) return "guest";
-  if (auto nv = fs::read_trimmed(fs::join(pci, "sriov_numvfs")); nv && str::parse_uint(*nv).value_or(0) > 0)
+  if (auto nv = fs::attrs().read_trimmed(fs::join(pci, "sriov_numvfs")); nv && str::parse_uint(*nv).value_or(0) > 0)
     return "host";
   return in_vm ? "passthrough" : "baremetal";
 }
@@ -169,7 +169,7 @@ void SysfsManager::Init() {
   // generation_id lives next to nodes/; when it is readable the topology is
   // there.  Otherwise list nodes/ (kernels without generation_id, or to get
   // the error to report).
-  generation_ = fs::read_trimmed(fs::join(opts_.root, "sys/class/kfd/kfd/topology/generation_id")).value_or("");
+  generation_ = fs::attrs().read_trimmed(fs::join(opts_.root, "sys/class/kfd/kfd/topology/generation_id")).value_or("");
   if (generation_.empty()) {
     int err = 0;
     fs::list_dir(topology_, &err);
@@ -207,18 +207,18 @@ static DevicePtr describe_gpu(const std::string& root, bool in_vm, int index, co
   info.device_id = static_cast<uint32_t>(first.device_id);
   info.uuid = amd_uuid(first.unique_id, static_cast<uint32_t>(first.device_id));
   info.gfx = gfx_target_from_kfd(first.gfx_target_version);
-  auto product = fs::read_trimmed(fs::join(pci, "product_name"));
+  auto product = fs::attrs().read_trimmed(fs::join(pci, "product_name"));
   info.name = product && !product->empty() ? *product : device_name(static_cast<uint32_t>(first.device_id));
-  info.compute_partition = fs::read_trimmed(fs::join(pci, "current_compute_partition")).value_or("");
-  info.memory_partition = fs::read_trimmed(fs::join(pci, "current_memory_partition")).value_or("");
-  info.available_compute_partitions = split_list(fs::read_trimmed(fs::join(pci, "available_compute_partition")).value_or(""));
-  info.available_memory_partitions = split_list(fs::read_trimmed(fs::join(pci, "available_memory_partition")).value_or(""));
-  if (auto x = fs::read_trimmed(fs::join(pci, "xgmi_num_links"))) info.xgmi_links = sum_links(*x);
+  info.compute_partition = fs::attrs().read_trimmed(fs::join(pci, "current_compute_partition")).value_or("");
+  info.memory_partition = fs::attrs().read_trimmed(fs::join(pci, "current_memory_partition")).value_or("");
+  info.available_compute_partitions = split_list(fs::attrs().read_trimmed(fs::join(pci, "available_compute_partition")).value_or(""));
+  info.available_memory_partitions = split_list(fs::attrs().read_trimmed(fs::join(pci, "available_memory_partition")).value_or(""));
+  if (auto x = fs::attrs().read_trimmed(fs::join(pci, "xgmi_num_links"))) info.xgmi_links = sum_links(*x);
   info.virtualization = virtualization_mode(pci, info.device_id, in_vm);
 
   bool partitioned = members.size() > 1 || (!info.compute_partition.empty() && info.compute_partition != "SPX");
   uint64_t vram = 0;
-  if (auto v = fs::read_trimmed(fs::join(pci, "mem_info_vram_total"))) vram = str::parse_uint(*v).value_or(0);
+  if (auto v = fs::attrs().read_trimmed(fs::join(pci, "mem_info_vram_total"))) vram = str::parse_uint(*v).value_or(0);
 
   // Per-partition HBM from each partition node's mem_banks (a list + read
   // per node; 8 of them in CPX), read in parallel.
@@ -318,6 +318,7 @@ std::vector<DevicePtr> SysfsManager::enumerate() {
   if (!generation_.empty() && generation_ == cached_generation_ && cached_) {
     topo = cached_;
   } else {
+    if (!cached_generation_.empty()) fs::attrs().clear();  // paths of the old topology
     topo = read_topology();
     cached_ = generation_.empty() ? nullptr : topo;
     cached_generation_ = generation_;
@@ -339,9 +340,14 @@ std::vector<DevicePtr> SysfsManager::enumerate() {
   }
   std::vector<DevicePtr> out(visible.size());
   trace::Span span("sysfs.gpus");
+  // Unpartitioned GPUs: ~10 attribute preads each, fastest on one thread
+  // (see AmdSmiManager::snapshot); partitioned ones also list and read each
+  // partition node's memory banks, and spread over the pool.
+  bool any_partitioned = false;
+  for (const auto& g : visible) any_partitioned |= g.members->size() > 1;
   WorkerPool::instance().parallel_for(
       visible.size(), [&](size_t i) { out[i] = describe_gpu(opts_.root, in_vm_, visible[i].index, *visible[i].bdf, *visible[i].members); },
-      8);
+      any_partitioned ? 8 : 1);
   return out;
 }
 

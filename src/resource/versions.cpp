@@ -30,7 +30,7 @@ std::optional<std::string> extract_version(const std::string& s) {
 }
 
 std::string host_driver_version(const std::string& root) {
-  if (auto v = fs::read_trimmed(fs::join(root, "sys/module/amdgpu/version")); v && !v->empty()) return *v;
+  if (auto v = fs::attrs().read_trimmed(fs::join(root, "sys/module/amdgpu/version")); v && !v->empty()) return *v;
   if (root != "/" && !root.empty()) {
     // Synthetic trees carry the kernel banner under proc/.
     if (auto v = fs::read_trimmed(fs::join(root, "proc/sys/kernel/osrelease")); v && !v->empty()) return *v;

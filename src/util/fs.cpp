@@ -3,6 +3,7 @@
 #include <dirent.h>
 #include <fcntl.h>
 #include <sys/stat.h>
+#include <sys/vfs.h>
 #include <sys/syscall.h>
 #include <unistd.h>
 
@@ -169,6 +170,100 @@ std::vector<std::pair<std::string, uint64_t>> DirListing::entries() const {
   }
   std::sort(out.begin(), out.end());
   return out;
+}
+
+namespace {
+
+constexpr long kSysfsMagic = 0x62656572;  // SYSFS_MAGIC
+constexpr size_t kMaxKeptOpen = 1024;
+
+// Whole file from offset 0 (pread: no file position involved).
+int pread_all(int fd, size_t max_bytes, std::string* out) {
+  out->clear();
+  char buf[8192];
+  off_t off = 0;
+  for (;;) {
+    ssize_t n = ::pread(fd, buf, sizeof(buf), off);
+    if (n < 0) {
+      if (errno == EINTR) continue;
+      return errno;
+    }
+    if (n == 0) return 0;
+    out->append(buf, static_cast<size_t>(n));
+    off += n;
+    if (out->size() >= max_bytes) {
+      out->resize(max_bytes);
+      return 0;
+    }
+  }
+}
+
+}  // namespace
+
+AttrReader::Fd::~Fd() { ::close(fd); }
+
+AttrReader::~AttrReader() { clear(); }
+
+void AttrReader::clear() {
+  std::lock_guard<std::mutex> g(mu_);
+  fds_.clear();
+}
+
+size_t AttrReader::open_count() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return fds_.size();
+}
+
+ReadResult AttrReader::read(const std::string& path, size_t max_bytes) {
+  ReadResult r;
+  std::shared_ptr<const Fd> kept;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = fds_.find(path);
+    if (it != fds_.end()) kept = it->second;
+  }
+  if (kept) {
+    if (pread_all(kept->fd, max_bytes, &r.data) == 0) return r;
+    // Removed since it was opened (ENODEV) or otherwise unusable: forget it
+    // and look the path up again.
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = fds_.find(path);
+    if (it != fds_.end() && it->second == kept) fds_.erase(it);
+  }
+  int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd < 0) {
+    r.err = errno;
+    return r;
+  }
+  if (int e = pread_all(fd, max_bytes, &r.data)) {
+    ::close(fd);
+    r.err = e;
+    r.data.clear();
+    return r;
+  }
+  struct statfs sfs;
+  bool keep = keep_all_ || (::fstatfs(fd, &sfs) == 0 && static_cast<long>(sfs.f_type) == kSysfsMagic);
+  if (keep) {
+    auto holder = std::make_shared<const Fd>(fd);
+    std::lock_guard<std::mutex> g(mu_);
+    if (fds_.size() >= kMaxKeptOpen) fds_.clear();
+    fds_.emplace(path, std::move(holder));  // if another thread kept one first, ours closes here
+    return r;
+  }
+  ::close(fd);
+  return r;
+}
+
+std::optional<std::string> AttrReader::read_trimmed(const std::string& path) {
+  auto r = read(path);
+  if (!r.ok()) return std::nullopt;
+  return str::trim(r.data);
+}
+
+AttrReader& attrs() {
+  // Leaked on purpose: pool threads may read attributes during exit.
+  static AttrReader* reader = new AttrReader();
+  return *reader;
 }
 
 std::string read_link(const std::string& path) {

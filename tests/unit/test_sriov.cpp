@@ -353,3 +353,38 @@ TEST(Sriov_ColdScanTakesVendorsFromProcTable) {
   EXPECT_THROW_MSG(ambiguous.Devices(), "unable to read PCI device vendor id for 0000:00:05.0");
   fs::remove_all(root);
 }
+
+TEST(Fs_AttrReaderKeepsOnlySysfsDescriptors) {
+  char d[] = "/tmp/gfd-attr-XXXXXX";
+  if (!mkdtemp(d)) throw std::runtime_error("mkdtemp");
+  std::string f = std::string(d) + "/attr";
+  put_file(f, "SPX\n");
+  // A regular file may be replaced under an open descriptor: never kept, and
+  // a replacement is seen.
+  fs::AttrReader plain;
+  EXPECT_EQ(plain.read_trimmed(f).value_or(""), std::string("SPX"));
+  EXPECT_EQ(plain.open_count(), static_cast<size_t>(0));
+  put_file(f, "CPX\n");
+  EXPECT_EQ(plain.read_trimmed(f).value_or(""), std::string("CPX"));
+  EXPECT_FALSE(plain.read_trimmed(std::string(d) + "/missing").has_value());
+  // Kept descriptors re-read from offset 0 every time (what kernfs turns
+  // into a fresh show() call): an in-place rewrite is seen.
+  fs::AttrReader kept;
+  kept.keep_all_for_testing(true);
+  EXPECT_EQ(kept.read_trimmed(f).value_or(""), std::string("CPX"));
+  EXPECT_EQ(kept.open_count(), static_cast<size_t>(1));
+  {
+    FILE* fp = std::fopen(f.c_str(), "r+");
+    std::fputs("DPX\n", fp);
+    std::fclose(fp);
+  }
+  EXPECT_EQ(kept.read_trimmed(f).value_or(""), std::string("DPX"));
+  EXPECT_EQ(kept.open_count(), static_cast<size_t>(1));
+  kept.clear();
+  EXPECT_EQ(kept.open_count(), static_cast<size_t>(0));
+  // Real sysfs (when present) is kept open.
+  fs::AttrReader sys;
+  if (sys.read_trimmed("/sys/kernel/mm/transparent_hugepage/enabled") || sys.read_trimmed("/sys/kernel/uevent_seqnum"))
+    EXPECT_EQ(sys.open_count(), static_cast<size_t>(1));
+  fs::remove_all(d);
+}

@@ -147,10 +147,21 @@ SysfsAmdPCI::Identity SysfsAmdPCI::read_identity(const std::string& addr, const 
 std::vector<PCIDevice> SysfsAmdPCI::Devices() {
   std::string dir = fs::join(root_, kPciDevicesRoot);
   int64_t t0 = trace::now_ns();
+  // The kernel's uevent sequence number goes up with every device added to
+  // or removed from the system - a PCI function, an SR-IOV VF included
+  // (device_add / device_del -> kobject_uevent; PCI devices pass the devices
+  // kset's uevent filter).  Read before the listing, so an event racing with
+  // this scan shows up as a new number next time.  Unchanged since the last
+  // scan: the bus listing is unchanged too, and is not read.
+  auto seqnum = fs::attrs().read_trimmed(fs::join(root_, "sys/kernel/uevent_seqnum"));
   bool changed = true;
-  int err = listing_.read(dir, &changed);
+  if (seqnum && !seqnum->empty() && *seqnum == seqnum_ && scanned_) {
+    changed = false;
+  } else {
+    int err = listing_.read(dir, &changed);
+    if (err != 0) throw Error("unable to read PCI bus devices: open " + dir + ": " + fs::errno_str(err));
+  }
   trace::record("pci.list", trace::now_ns() - t0);
-  if (err != 0) throw Error("unable to read PCI bus devices: open " + dir + ": " + fs::errno_str(err));
 
   // Merge the (sorted) listing with the (sorted) identity cache: entries
   // whose sysfs inode is unchanged reuse their identity, new or re-created
@@ -212,6 +223,8 @@ std::vector<PCIDevice> SysfsAmdPCI::Devices() {
   else if (chunks == 1)
     read_chunk(0);
   if (changed) cache_.swap(next);
+  scanned_ = true;
+  seqnum_ = seqnum.value_or("");
   int64_t t1 = trace::now_ns();
   trace::record("pci.identity", t1 - t0);
 

@@ -93,6 +93,8 @@ class AmdPCI {
 //     identity of a function (vendor, class, device ID) is kept per (address,
 //     sysfs inode) - a removed and re-added device gets a new inode and is
 //     re-read;
+//   * the listing itself is skipped while /sys/kernel/uevent_seqnum, which
+//     every device addition or removal increments, is unchanged;
 //   * the mutable SR-IOV state comes from the kernel's sysfs attributes
 //     (sriov_numvfs), which cost no PCI config cycles, and is re-read whenever
 //     the listing changed - enabling or disabling VFs adds or removes their
@@ -100,8 +102,10 @@ class AmdPCI {
 //   * configuration space (a 4 KiB read = ~1000 config cycles when
 //     privileged) is read only for functions whose SR-IOV state sysfs does not
 //     publish.
-// Measured on an 8-GPU MI355X host with 319 PCI functions: 2.5 ms first scan,
-// then ~60 us (list 30 us + cache merge 2 us + 8 NumVFs reads 26 us).
+// Measured on an 8-GPU MI355X host with 367 PCI functions: ~1.5 ms first
+// scan; then 15 us when the listing is read (one getdents64 pass) and ~1 us
+// when uevent_seqnum shows nothing was added or removed
+// (profiles/pci_scan_probe.txt).
 class SysfsAmdPCI : public AmdPCI {
  public:
   explicit SysfsAmdPCI(std::string root = "/") : root_(std::move(root)) {}
@@ -124,6 +128,8 @@ class SysfsAmdPCI : public AmdPCI {
   static Identity read_identity(const std::string& addr, const std::string& path, uint64_t ino);
   std::string root_;
   fs::DirListing listing_;
+  bool scanned_ = false;
+  std::string seqnum_;  // /sys/kernel/uevent_seqnum at the last scan
   std::vector<std::pair<std::string, Identity>> cache_;  // sorted by address
 };
 

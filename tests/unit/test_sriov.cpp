@@ -388,3 +388,26 @@ TEST(Fs_AttrReaderKeepsOnlySysfsDescriptors) {
     EXPECT_EQ(sys.open_count(), static_cast<size_t>(1));
   fs::remove_all(d);
 }
+
+TEST(Sriov_ListingSkippedWhileUeventSeqnumUnchanged) {
+  std::string root = pci_host(20, 0);
+  std::string dev = root + "/sys/bus/pci/devices/";
+  put_file(root + "/sys/kernel/uevent_seqnum", "1000\n");
+  SysfsAmdPCI pci(root);
+  EXPECT_EQ(pci.Devices().size(), static_cast<size_t>(5));
+  // A function appears without a uevent (impossible on a real kernel): the
+  // listing is not read again...
+  put_file(dev + "0000:e1:00.0/vendor", "0x1002\n");
+  put_file(dev + "0000:e1:00.0/class", "0x120000\n");
+  put_file(dev + "0000:e1:00.0/device", "0x75a3\n");
+  put_file(dev + "0000:e1:00.0/sriov_totalvfs", "0\n");
+  EXPECT_EQ(pci.Devices().size(), static_cast<size_t>(5));
+  // ... the uevent that device_add() sends makes the next scan see it.
+  put_file(root + "/sys/kernel/uevent_seqnum", "1001\n");
+  EXPECT_EQ(pci.Devices().size(), static_cast<size_t>(6));
+  // Without the counter every scan reads the listing.
+  fs::remove_all(root + "/sys/kernel/uevent_seqnum");
+  fs::remove_all(dev + "0000:e1:00.0");
+  EXPECT_EQ(pci.Devices().size(), static_cast<size_t>(5));
+  fs::remove_all(root);
+}

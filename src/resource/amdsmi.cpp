@@ -651,33 +651,33 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
     }
     return true;
   };
-  // Unpartitioned GPUs on this thread, one after the other: ~5 us of
-  // attribute preads each on kept-open descriptors, which do not get faster
-  // on more cores (8 GPUs: 24 us on one thread, 29 us on eight -
-  // profiles/multi_gpu_read_probe.txt).  The rest - partitioned GPUs, tens
-  // of library calls each - are spread over the pool.
-  int64_t proc_ns = 0, caps_ns = 0;
-  std::vector<size_t> library_path;
-  for (size_t i = 0; i < gpus.size(); ++i) {
-    if (sysfs_values && work(gpus[i], true)) {
-      proc_ns += gpus[i].proc_ns;
-      caps_ns += gpus[i].caps_ns;
-    } else {
-      library_path.push_back(i);
-    }
+  // Unpartitioned GPUs first: ~7 us of attribute preads and cached library
+  // lookups each.  Two GPUs per lane: on one thread a cycle after the
+  // daemon's sleep runs on a cold, down-clocked core (8 GPUs' reads: 170 us
+  // serial vs 36 us on four lanes), while back to back the pool only adds
+  // fan-out (26 us serial, 32 us on four lanes) - profiles/multi_gpu_read_probe.txt.
+  // The rest - partitioned GPUs, tens of library calls each - then go over
+  // the pool one per lane.
+  int64_t t_gpus = trace::now_ns();
+  std::vector<char> fast_ok(gpus.size(), 0);
+  if (sysfs_values) {
+    size_t lanes = opts_.threads > 0 ? static_cast<size_t>(opts_.threads) : std::min<size_t>(4, (gpus.size() + 1) / 2);
+    WorkerPool::instance().parallel_for(gpus.size(), [&](size_t i) { fast_ok[i] = work(gpus[i], true); }, lanes);
   }
+  std::vector<size_t> library_path;
+  for (size_t i = 0; i < gpus.size(); ++i)
+    if (!fast_ok[i]) library_path.push_back(i);
   size_t threads = opts_.threads > 0 ? static_cast<size_t>(opts_.threads) : 8;
   WorkerPool::instance().parallel_for(
       library_path.size(), [&](size_t k) { work(gpus[library_path[k]], false); }, threads);
-  // Phase times: serial part summed, pooled part by its slowest GPU (items
-  // may have run on pool threads, whose trace records are their own).
-  int64_t pooled_proc = 0, pooled_caps = 0;
-  for (size_t k : library_path) {
-    pooled_proc = std::max(pooled_proc, gpus[k].proc_ns);
-    pooled_caps = std::max(pooled_caps, gpus[k].caps_ns);
+  trace::record("amdsmi.gpus", trace::now_ns() - t_gpus);
+  // Per-GPU phase times: the slowest GPU (items may have run on pool
+  // threads, whose trace records are their own).
+  int64_t proc_ns = 0, caps_ns = 0;
+  for (const auto& g : gpus) {
+    proc_ns = std::max(proc_ns, g.proc_ns);
+    caps_ns = std::max(caps_ns, g.caps_ns);
   }
-  proc_ns += pooled_proc;
-  caps_ns += pooled_caps;
   for (const auto& g : gpus)
     if (g.error) std::rethrow_exception(g.error);
   trace::record("amdsmi.proc", proc_ns);

@@ -340,14 +340,15 @@ std::vector<DevicePtr> SysfsManager::enumerate() {
   }
   std::vector<DevicePtr> out(visible.size());
   trace::Span span("sysfs.gpus");
-  // Unpartitioned GPUs: ~10 attribute preads each, fastest on one thread
-  // (see AmdSmiManager::snapshot); partitioned ones also list and read each
-  // partition node's memory banks, and spread over the pool.
+  // Unpartitioned GPUs: ~10 attribute preads each, two GPUs per lane (see
+  // AmdSmiManager::snapshot); partitioned ones also list and read each
+  // partition node's memory banks, one GPU per lane.
   bool any_partitioned = false;
   for (const auto& g : visible) any_partitioned |= g.members->size() > 1;
+  size_t lanes = any_partitioned ? 8 : std::min<size_t>(4, (visible.size() + 1) / 2);
   WorkerPool::instance().parallel_for(
       visible.size(), [&](size_t i) { out[i] = describe_gpu(opts_.root, in_vm_, visible[i].index, *visible[i].bdf, *visible[i].members); },
-      any_partitioned ? 8 : 1);
+      lanes);
   return out;
 }
 

@@ -8,6 +8,8 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <ctime>
+#include <type_traits>
 #include <chrono>
 #include <cstdio>
 #include <string>
@@ -53,12 +55,17 @@ int main() {
   }
   // Per attribute: 8 GPUs on 8 lanes vs on one thread, and the pool's own
   // fan-out cost (empty items).
+  // Median of f's duration, or of f's return value if it measures itself.
   auto p50 = [](auto&& f, int iters) {
     std::vector<double> t;
     for (int it = 0; it < iters; ++it) {
       double a = now_us();
-      f();
-      t.push_back(now_us() - a);
+      if constexpr (std::is_same_v<decltype(f()), double>) {
+        t.push_back(f());
+      } else {
+        f();
+        t.push_back(now_us() - a);
+      }
     }
     std::sort(t.begin(), t.end());
     return t[t.size() / 2];
@@ -88,14 +95,30 @@ int main() {
       char buf[4096];
       for (int fd : fds[i]) (void)!::pread(fd, buf, sizeof(buf), 0);
     };
-    std::printf("kept-open fds + pread: 1 GPU %.1f us", p50([&] { pread_gpu(0); }, 500));
+    std::printf("kept-open fds + pread: 1 GPU %.1f us\n", p50([&] { pread_gpu(0); }, 500));
     if (gpus.size() >= 8) {
-      std::printf(" | 8 GPUs serial %.1f us | 8 GPUs on 8 lanes %.1f us | on 2 lanes %.1f us",
-                  p50([&] { for (size_t i = 0; i < 8; ++i) pread_gpu(i); }, 500),
-                  p50([&] { WorkerPool::instance().parallel_for(8, pread_gpu, 8); }, 500),
-                  p50([&] { WorkerPool::instance().parallel_for(8, pread_gpu, 2); }, 500));
+      // Lanes sweep for 8 GPUs, back to back and with a 2 ms idle gap before
+      // each sample (the daemon sleeps between cycles: workers park, cores idle).
+      for (bool gap : {false, true}) {
+        std::printf("8 GPUs, kept-open fds + pread, %s:", gap ? "2 ms idle before each" : "back to back");
+        for (size_t lanes : {1, 2, 4, 8}) {
+          double v = p50([&] {
+            if (gap) {
+              struct timespec ts{0, 2000000};
+              nanosleep(&ts, nullptr);
+            }
+            double a = now_us();
+            if (lanes == 1)
+              for (size_t i = 0; i < 8; ++i) pread_gpu(i);
+            else
+              WorkerPool::instance().parallel_for(8, pread_gpu, lanes);
+            return now_us() - a;
+          }, 400);
+          std::printf("  %zu lane(s) %.1f us", lanes, v);
+        }
+        std::printf("\n");
+      }
     }
-    std::printf("\n");
     for (auto& v : fds)
       for (int fd : v) ::close(fd);
   }

@@ -619,14 +619,12 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
   }
   const bool sysfs_values = sysfs_values_enabled();
 
-  // Query every processor; parallel across physical GPUs on multi-GPU nodes,
-  // sequential within one GPU: amdgpu serialises a device's queries on its
-  // own locks (amd-smi adds a per-device mutex), so splitting one GPU's reads
-  // over threads makes each of them slower - measured 273 us sequential vs
-  // 472 us split with amd-smi calls, and 2-3x slower sysfs reads (value
-  // reads concurrent with the capability reads, profiles/README.md).
-  // One GPU's values and capabilities.  fast: only through the unpartitioned
-  // (attribute) path - returns false, having assigned nothing, if that path
+  // One GPU's values and capabilities, always on one thread: amdgpu
+  // serialises a device's queries on its own locks (amd-smi adds a
+  // per-device mutex), so splitting one GPU's reads over threads makes each
+  // of them slower - measured 273 us sequential vs 472 us split with amd-smi
+  // calls, and 2-3x slower sysfs reads (profiles/README.md).  fast: only
+  // through the unpartitioned (attribute) path - returns false if that path
   // does not apply; otherwise every processor through the library.
   auto work = [&](Gpu& g, bool fast) -> bool {
     try {

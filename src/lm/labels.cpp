@@ -20,6 +20,13 @@ class FixedLabeler : public Labeler {
  public:
   explicit FixedLabeler(Labels l) : labels_(std::move(l)) {}
   Labels GetLabels() override { return labels_; }
+  void AppendTo(Labels& out) override {
+    if (out.empty()) {
+      out = labels_;
+      return;
+    }
+    for (const auto& kv : labels_) out[kv.first] = kv.second;
+  }
 
  private:
   Labels labels_;
@@ -30,17 +37,18 @@ class ListLabeler : public Labeler {
   explicit ListLabeler(std::vector<LabelerPtr> l) : labelers_(std::move(l)) {}
   Labels GetLabels() override {
     Labels all;
+    AppendTo(all);
+    return all;
+  }
+  void AppendTo(Labels& out) override {
     for (const auto& l : labelers_) {
       if (!l) continue;
-      Labels part;
       try {
-        part = l->GetLabels();
+        l->AppendTo(out);
       } catch (const std::exception& e) {
         throw Error(std::string("error generating labels: ") + e.what());
       }
-      for (auto& kv : part) all[kv.first] = std::move(kv.second);
     }
-    return all;
   }
 
  private:

@@ -26,6 +26,11 @@ class Labeler {
  public:
   virtual ~Labeler() = default;
   virtual Labels GetLabels() = 0;
+  // Adds this labeler's labels to `out` (overriding same keys) - what a
+  // merge does with each of its labelers, without an intermediate map.
+  virtual void AppendTo(Labels& out) {
+    for (auto& kv : GetLabels()) out[kv.first] = std::move(kv.second);
+  }
 };
 using LabelerPtr = std::shared_ptr<Labeler>;
 

@@ -37,8 +37,14 @@ Labels ResourceLabeler::replicas_label() const {
 
 Labels ResourceLabeler::base_labels(int count, const std::vector<std::string>& parts) const {
   Labels l = product_label(parts);
-  for (auto& kv : count_label(count)) l[kv.first] = kv.second;
-  for (auto& kv : replicas_label()) l[kv.first] = kv.second;
+  update(l, "count", std::to_string(count));
+  int replicas = 1;
+  if (sharing_disabled()) {
+    replicas = 0;
+  } else if (const auto* r = replication_info(); r && r->replicas > 1) {
+    replicas = r->replicas;
+  }
+  update(l, "replicas", std::to_string(replicas));
   return l;
 }
 
@@ -82,7 +88,7 @@ Labels NewGPUResourceLabels(const config::Config* config, const Device& device, 
 
   Labels l = rl.base_labels(count, {model});
   if (memory != 0) rl.update(l, "memory", std::to_string(memory));
-  for (auto& kv : arch) l[kv.first] = kv.second;
+  l.merge(arch);  // disjoint keys
   const auto& info = device.Info();
   if (info.compute_units) rl.update(l, "compute-units", std::to_string(info.compute_units));
   if (info.xcds) rl.update(l, "xcds", std::to_string(info.xcds));

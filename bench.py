@@ -154,6 +154,9 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--backend", default="auto", help="auto | amdsmi | sysfs | synthetic")
     ap.add_argument("--no-extras", action="store_true", help="skip the secondary measurements")
+    ap.add_argument("--sysfs-root", default=None,
+                    help="with --backend sysfs: read this root instead of / (tools/hybrid_root.py builds one that "
+                         "shows every GPU of a shared host)")
     a = ap.parse_args()
 
     # Bind amd-smi to the system libdrm before anything imports PyTorch (which
@@ -196,6 +199,7 @@ def main() -> int:
             synth.make_mi355x_node(root, n_gpus=n, seed=1234)
         elif backend == "sysfs":
             hardware = True
+            root = a.sysfs_root
     backend = dist.broadcast_obj(backend)
     hardware = dist.broadcast_obj(hardware)
 
@@ -260,6 +264,7 @@ def main() -> int:
             "vs_baseline": None,
             "dtype": "n/a",
             "data": ("real MI355X via amd-smi (live driver queries every step)" if backend == "amdsmi"
+                     else f"real MI355X via KFD sysfs under {root}" if backend == "sysfs" and root
                      else "real MI355X via KFD sysfs" if backend == "sysfs"
                      else f"synthetic {n}-GPU MI355X sysfs tree (random device IDs), no GPU available"),
             "config": {

@@ -659,13 +659,13 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
   int64_t t_gpus = trace::now_ns();
   std::vector<char> fast_ok(gpus.size(), 0);
   if (sysfs_values) {
-    size_t lanes = opts_.threads > 0 ? static_cast<size_t>(opts_.threads) : std::min<size_t>(4, (gpus.size() + 1) / 2);
+    size_t lanes = opts_.threads > 0 ? static_cast<size_t>(opts_.threads) : gpu_lanes(gpus.size(), true);
     WorkerPool::instance().parallel_for(gpus.size(), [&](size_t i) { fast_ok[i] = work(gpus[i], true); }, lanes);
   }
   std::vector<size_t> library_path;
   for (size_t i = 0; i < gpus.size(); ++i)
     if (!fast_ok[i]) library_path.push_back(i);
-  size_t threads = opts_.threads > 0 ? static_cast<size_t>(opts_.threads) : 8;
+  size_t threads = opts_.threads > 0 ? static_cast<size_t>(opts_.threads) : gpu_lanes(library_path.size(), false);
   WorkerPool::instance().parallel_for(
       library_path.size(), [&](size_t k) { work(gpus[library_path[k]], false); }, threads);
   trace::record("amdsmi.gpus", trace::now_ns() - t_gpus);

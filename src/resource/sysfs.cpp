@@ -127,8 +127,8 @@ std::string bdf_of(const KfdNode& n) {
 // container can see: an SR-IOV virtual function runs as a guest; a physical
 // function with VFs enabled is the host; a whole GPU inside a VM is
 // passthrough; otherwise bare metal.
-std::string virtualization_mode(const std::string& pci, uint32_t device_id, bool in_vm) {
-  if (is_mxgpu_vf(device_id) || fs::exists(fs::join(pci, "physfn"))) return "guest";
+std::string virtualization_mode(const std::string& pci, uint32_t device_id, bool in_vm, bool has_physfn) {
+  if (is_mxgpu_vf(device_id) || has_physfn) return "guest";
   if (auto nv = fs::attrs().read_trimmed(fs::join(pci, "sriov_numvfs")); nv && str::parse_uint(*nv).value_or(0) > 0)
     return "host";
   return in_vm ? "passthrough" : "baremetal";
@@ -196,7 +196,7 @@ std::vector<DevicePtr> SysfsManager::GetDevices() {
 
 // One physical GPU (and its partitions) from its KFD nodes and PCI attributes.
 static DevicePtr describe_gpu(const std::string& root, bool in_vm, int index, const std::string& bdf,
-                              const std::vector<const KfdNode*>& members) {
+                              const std::vector<const KfdNode*>& members, bool has_physfn) {
   const KfdNode& first = *members.front();
   std::string pci = fs::join(root, "sys/bus/pci/devices/" + bdf);
 
@@ -214,7 +214,7 @@ static DevicePtr describe_gpu(const std::string& root, bool in_vm, int index, co
   info.available_compute_partitions = split_list(fs::attrs().read_trimmed(fs::join(pci, "available_compute_partition")).value_or(""));
   info.available_memory_partitions = split_list(fs::attrs().read_trimmed(fs::join(pci, "available_memory_partition")).value_or(""));
   if (auto x = fs::attrs().read_trimmed(fs::join(pci, "xgmi_num_links"))) info.xgmi_links = sum_links(*x);
-  info.virtualization = virtualization_mode(pci, info.device_id, in_vm);
+  info.virtualization = virtualization_mode(pci, info.device_id, in_vm, has_physfn);
 
   bool partitioned = members.size() > 1 || (!info.compute_partition.empty() && info.compute_partition != "SPX");
   uint64_t vram = 0;
@@ -275,6 +275,9 @@ static DevicePtr describe_gpu(const std::string& root, bool in_vm, int index, co
 struct SysfsManager::Topology {
   std::vector<KfdNode> nodes;                              // accessible GPU nodes, by node id
   std::map<std::string, std::vector<const KfdNode*>> groups;  // by BDF (ordered)
+  // A `physfn` link (the function is an SR-IOV VF), fixed when the PCI
+  // function is created - looked up here, not with a path walk per cycle.
+  std::map<std::string, bool> has_physfn;
 };
 
 std::shared_ptr<const SysfsManager::Topology> SysfsManager::read_topology() const {
@@ -310,6 +313,8 @@ std::shared_ptr<const SysfsManager::Topology> SysfsManager::read_topology() cons
 
   // 2. Group partitions by PCI location (partitions share the parent's BDF).
   for (const auto& n : topo->nodes) topo->groups[bdf_of(n)].push_back(&n);
+  for (const auto& g : topo->groups)
+    topo->has_physfn[g.first] = fs::exists(fs::join(opts_.root, "sys/bus/pci/devices/" + g.first + "/physfn"));
   return topo;
 }
 
@@ -345,9 +350,10 @@ std::vector<DevicePtr> SysfsManager::enumerate() {
   // partition node's memory banks, one GPU per lane.
   bool any_partitioned = false;
   for (const auto& g : visible) any_partitioned |= g.members->size() > 1;
-  size_t lanes = any_partitioned ? 8 : std::min<size_t>(4, (visible.size() + 1) / 2);
+  size_t lanes = gpu_lanes(visible.size(), !any_partitioned);
   WorkerPool::instance().parallel_for(
-      visible.size(), [&](size_t i) { out[i] = describe_gpu(opts_.root, in_vm_, visible[i].index, *visible[i].bdf, *visible[i].members); },
+      visible.size(), [&](size_t i) { out[i] = describe_gpu(opts_.root, in_vm_, visible[i].index, *visible[i].bdf, *visible[i].members,
+                                                              topo->has_physfn.at(*visible[i].bdf)); },
       lanes);
   return out;
 }

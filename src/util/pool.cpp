@@ -2,6 +2,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstdlib>
 
 namespace gfd {
 
@@ -202,6 +203,15 @@ void WorkerPool::parallel_for(size_t n, const std::function<void(size_t)>& fn, s
   std::unique_lock<std::mutex> lk(sh->mu);
   sh->cv.wait(lk, [&] { return sh->done == sh->n; });
   if (sh->error) std::rethrow_exception(sh->error);
+}
+
+size_t gpu_lanes(size_t n_gpus, bool light) {
+  static const size_t forced = [] {
+    const char* v = std::getenv("GFD_GPU_LANES");
+    return v && *v ? static_cast<size_t>(std::strtoul(v, nullptr, 10)) : size_t{0};
+  }();
+  if (forced) return forced;
+  return light ? std::min<size_t>(4, (n_gpus + 1) / 2) : 8;
 }
 
 }  // namespace gfd

@@ -95,4 +95,12 @@ class WorkerPool {
   bool stop_ = false;
 };
 
+// Lanes for per-GPU work in one cycle.  light: a few attribute preads per
+// GPU (two GPUs per lane, at most four: a cycle after the daemon's sleep runs
+// on cold cores, where one thread is 4-5x slower than four, while back to
+// back the fan-out costs a little - profiles/multi_gpu_read_probe.txt);
+// otherwise (tens of library calls per GPU) one GPU per lane.
+// GFD_GPU_LANES=N overrides both (measurements).
+size_t gpu_lanes(size_t n_gpus, bool light);
+
 }  // namespace gfd

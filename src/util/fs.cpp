@@ -205,12 +205,12 @@ AttrReader::Fd::~Fd() { ::close(fd); }
 AttrReader::~AttrReader() { clear(); }
 
 void AttrReader::clear() {
-  std::lock_guard<std::mutex> g(mu_);
+  std::unique_lock<std::shared_mutex> g(mu_);
   fds_.clear();
 }
 
 size_t AttrReader::open_count() const {
-  std::lock_guard<std::mutex> g(mu_);
+  std::shared_lock<std::shared_mutex> g(mu_);
   return fds_.size();
 }
 
@@ -218,7 +218,7 @@ ReadResult AttrReader::read(const std::string& path, size_t max_bytes) {
   ReadResult r;
   std::shared_ptr<const Fd> kept;
   {
-    std::lock_guard<std::mutex> g(mu_);
+    std::shared_lock<std::shared_mutex> g(mu_);
     auto it = fds_.find(path);
     if (it != fds_.end()) kept = it->second;
   }
@@ -226,7 +226,7 @@ ReadResult AttrReader::read(const std::string& path, size_t max_bytes) {
     if (pread_all(kept->fd, max_bytes, &r.data) == 0) return r;
     // Removed since it was opened (ENODEV) or otherwise unusable: forget it
     // and look the path up again.
-    std::lock_guard<std::mutex> g(mu_);
+    std::unique_lock<std::shared_mutex> g(mu_);
     auto it = fds_.find(path);
     if (it != fds_.end() && it->second == kept) fds_.erase(it);
   }
@@ -245,7 +245,7 @@ ReadResult AttrReader::read(const std::string& path, size_t max_bytes) {
   bool keep = keep_all_ || (::fstatfs(fd, &sfs) == 0 && static_cast<long>(sfs.f_type) == kSysfsMagic);
   if (keep) {
     auto holder = std::make_shared<const Fd>(fd);
-    std::lock_guard<std::mutex> g(mu_);
+    std::unique_lock<std::shared_mutex> g(mu_);
     if (fds_.size() >= kMaxKeptOpen) fds_.clear();
     fds_.emplace(path, std::move(holder));  // if another thread kept one first, ours closes here
     return r;

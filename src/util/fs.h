@@ -6,6 +6,7 @@
 #include <cstdint>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <optional>
 #include <string>
 #include <unordered_map>
@@ -98,7 +99,9 @@ class AttrReader {
     ~Fd();
     int fd;
   };
-  mutable std::mutex mu_;
+  // Lookups (every read) share the lock; only opening and dropping a
+  // descriptor take it exclusively, so per-GPU lanes do not queue on it.
+  mutable std::shared_mutex mu_;
   std::unordered_map<std::string, std::shared_ptr<const Fd>> fds_;
   bool keep_all_ = false;
 };

@@ -153,9 +153,12 @@ std::vector<PCIDevice> SysfsAmdPCI::Devices() {
   // kset's uevent filter).  Read before the listing, so an event racing with
   // this scan shows up as a new number next time.  Unchanged since the last
   // scan: the bus listing is unchanged too, and is not read.
+  // A booted kernel has sent thousands of uevents; "0" would be an emulated
+  // sysfs that never counts, and is not trusted.
   auto seqnum = fs::attrs().read_trimmed(fs::join(root_, "sys/kernel/uevent_seqnum"));
+  if (seqnum && (seqnum->empty() || *seqnum == "0")) seqnum.reset();
   bool changed = true;
-  if (seqnum && !seqnum->empty() && *seqnum == seqnum_ && scanned_) {
+  if (seqnum && *seqnum == seqnum_ && scanned_) {
     changed = false;
   } else {
     int err = listing_.read(dir, &changed);

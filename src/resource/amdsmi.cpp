@@ -326,7 +326,8 @@ constexpr uint32_t kNoNode = 0xFFFFFFFFu;
 // ~4 us each.  `node_id` is the session-cached KFD node (kNoNode = not yet
 // known: queried and returned through it).  Returns false when the GPU is
 // partitioned or an attribute is missing; the caller then queries amd-smi.
-bool query_unpartitioned(AmdSmiLib& L, const std::string& root, ProcInfo& p, uint32_t* node_id) {
+bool query_unpartitioned(AmdSmiLib& L, const std::string& root, ProcInfo& p, AmdSmiManager::KfdNodeFacts* kfd) {
+  uint32_t* node_id = &kfd->node_id;
   std::string pci = fs::join(root, "sys/bus/pci/devices/" + p.bdf);
   auto cp = AMDSMI_CALL("compute_partition(sysfs)", fs::attrs().read_trimmed(pci + "/current_compute_partition"));
   if (!cp || *cp != "SPX") return false;
@@ -340,7 +341,8 @@ bool query_unpartitioned(AmdSmiLib& L, const std::string& root, ProcInfo& p, uin
   p.compute_partition = *cp;
   p.memory_partition = *mp;
   p.vram = *vram;
-  if (*node_id != kNoNode) p.xcds = AMDSMI_CALL("kfd_num_xcc(sysfs)", kfd_num_xcc(root, *node_id));
+  if (kfd->num_xcc == 0 && *node_id != kNoNode) kfd->num_xcc = AMDSMI_CALL("kfd_num_xcc(sysfs)", kfd_num_xcc(root, *node_id));
+  p.xcds = kfd->num_xcc;
   if (p.xcds == 0 && L.get_gpu_xcd_counter) {
     uint16_t x = 0;
     if (L.get_gpu_xcd_counter(p.h, &x) == AMDSMI_STATUS_SUCCESS) p.xcds = x;
@@ -603,7 +605,7 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
     GpuExtras extras;
     std::exception_ptr error;
     int64_t proc_ns = 0, caps_ns = 0;
-    uint32_t kfd_node = kNoNode;  // session cache entry (unpartitioned GPUs)
+    KfdNodeFacts kfd;  // session cache entry (unpartitioned GPUs)
   };
   std::vector<Gpu> gpus;
   int index = -1;
@@ -614,7 +616,7 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
       auto v = virt_mode_.find(bdf);
       if (v != virt_mode_.end()) gpus.back().extras.virtualization = v->second;
       auto k = kfd_node_.find(bdf);
-      if (k != kfd_node_.end()) gpus.back().kfd_node = k->second;
+      if (k != kfd_node_.end()) gpus.back().kfd = k->second;
     }
   }
   const bool sysfs_values = sysfs_values_enabled();
@@ -631,7 +633,7 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
       int64_t t0 = trace::now_ns();
       auto& procs = *g.procs;
       if (fast) {
-        if (procs.size() != 1 || !query_unpartitioned(L, opts_.root, procs[0], &g.kfd_node)) return false;
+        if (procs.size() != 1 || !query_unpartitioned(L, opts_.root, procs[0], &g.kfd)) return false;
       } else {
         for (auto& p : procs) query_proc(L, opts_.root, p);
         std::sort(procs.begin(), procs.end(),
@@ -682,7 +684,7 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
   trace::record("amdsmi.extras", caps_ns);
   for (const auto& g : gpus) {
     if (!g.extras.virtualization.empty()) virt_mode_[g.bdf] = g.extras.virtualization;
-    if (g.kfd_node != kNoNode) kfd_node_[g.bdf] = g.kfd_node;
+    if (g.kfd.node_id != kNoNode) kfd_node_[g.bdf] = g.kfd;
   }
 
   std::vector<DevicePtr> out;

@@ -24,6 +24,7 @@
 //     share a PCI address; they are regrouped into parent GPUs by BDF.
 #pragma once
 
+#include <cstdint>
 #include <map>
 #include <memory>
 #include <string>
@@ -61,6 +62,12 @@ class AmdSmiManager : public Manager {
   // Number of amdsmi_init calls made by this manager (tests / benchmarks).
   int init_count() const { return init_count_; }
 
+  // Per-session facts of an unpartitioned GPU's KFD node (see kfd_node_).
+  struct KfdNodeFacts {
+    uint32_t node_id = 0xFFFFFFFFu;
+    uint32_t num_xcc = 0;
+  };
+
  private:
   std::vector<DevicePtr> snapshot();
   void library_init();
@@ -81,13 +88,16 @@ class AmdSmiManager : public Manager {
   // session, which clears this.  Saves ~100 us per GPU per cycle (the most
   // expensive amd-smi call left on the hot path, profiles/).
   std::map<std::string, std::string> virt_mode_;
-  // KFD topology node of each unpartitioned GPU (by BDF) for the lifetime of
-  // one session: node ids only change with the topology generation, which
-  // re-initialises the session and clears this.  The per-cycle values of an
-  // unpartitioned GPU (VRAM, compute/memory partition, XCD count) are then
-  // read from the amdgpu/KFD sysfs attributes amd-smi itself reads, ~4 us
-  // each instead of 11-18 us per library call.
-  std::map<std::string, uint32_t> kfd_node_;
+  // KFD topology node of each unpartitioned GPU (by BDF) and its XCD count
+  // (num_xcc) for the lifetime of one session: KFD rebuilds its topology and
+  // bumps the generation whenever a node changes (a partition switch changes
+  // num_xcc), and a new generation re-initialises the session, which clears
+  // this - the same rule the sysfs backend applies to node properties.  The
+  // per-cycle values of an unpartitioned GPU (VRAM, compute/memory
+  // partition) are read from the amdgpu attributes amd-smi itself reads,
+  // ~1 us each through kept-open descriptors instead of 11-18 us per
+  // library call.
+  std::map<std::string, KfdNodeFacts> kfd_node_;
 };
 
 }  // namespace gfd::resource

@@ -49,7 +49,7 @@ std::optional<RuntimeVersion> rocm_version(const std::string& root) {
     candidates.push_back(fs::join(rp, ".info/version"));
   if (!synthetic) candidates.push_back("/opt/rocm/.info/version");
   for (const auto& c : candidates) {
-    auto v = fs::read_trimmed(c);
+    auto v = fs::attrs().read_checked_trimmed(c);
     if (!v) continue;
     auto ver = extract_version(*v);
     if (!ver) continue;

@@ -207,11 +207,12 @@ AttrReader::~AttrReader() { clear(); }
 void AttrReader::clear() {
   std::unique_lock<std::shared_mutex> g(mu_);
   fds_.clear();
+  checked_.clear();
 }
 
 size_t AttrReader::open_count() const {
   std::shared_lock<std::shared_mutex> g(mu_);
-  return fds_.size();
+  return fds_.size() + checked_.size();
 }
 
 ReadResult AttrReader::read(const std::string& path, size_t max_bytes) {
@@ -252,6 +253,48 @@ ReadResult AttrReader::read(const std::string& path, size_t max_bytes) {
   }
   ::close(fd);
   return r;
+}
+
+ReadResult AttrReader::read_checked(const std::string& path, size_t max_bytes) {
+  ReadResult r;
+  struct stat st;
+  if (::stat(path.c_str(), &st) != 0) {
+    r.err = errno;
+    std::unique_lock<std::shared_mutex> g(mu_);
+    checked_.erase(path);
+    return r;
+  }
+  std::shared_ptr<const Fd> kept;
+  {
+    std::shared_lock<std::shared_mutex> g(mu_);
+    auto it = checked_.find(path);
+    if (it != checked_.end() && it->second.dev == static_cast<uint64_t>(st.st_dev) &&
+        it->second.ino == static_cast<uint64_t>(st.st_ino))
+      kept = it->second.fd;
+  }
+  if (kept && pread_all(kept->fd, max_bytes, &r.data) == 0) return r;
+  int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd < 0) {
+    r.err = errno;
+    return r;
+  }
+  auto holder = std::make_shared<const Fd>(fd);
+  struct stat fst;
+  if (int e = pread_all(fd, max_bytes, &r.data); e != 0 || ::fstat(fd, &fst) != 0) {
+    r.err = e ? e : errno;
+    r.data.clear();
+    return r;
+  }
+  std::unique_lock<std::shared_mutex> g(mu_);
+  if (checked_.size() >= kMaxKeptOpen) checked_.clear();
+  checked_[path] = Checked{std::move(holder), static_cast<uint64_t>(fst.st_dev), static_cast<uint64_t>(fst.st_ino)};
+  return r;
+}
+
+std::optional<std::string> AttrReader::read_checked_trimmed(const std::string& path) {
+  auto r = read_checked(path);
+  if (!r.ok()) return std::nullopt;
+  return str::trim(r.data);
 }
 
 std::optional<std::string> AttrReader::read_trimmed(const std::string& path) {

@@ -82,6 +82,12 @@ class AttrReader {
   AttrReader& operator=(const AttrReader&) = delete;
   ReadResult read(const std::string& path, size_t max_bytes = 64 * 1024);
   std::optional<std::string> read_trimmed(const std::string& path);
+  // A regular file that may be replaced (e.g. a package's version file):
+  // kept open too, but a stat() of the path confirms it is still the same
+  // file (device + inode) before every pread - cheaper than open/read/close,
+  // and a replaced or removed file is seen at once.
+  ReadResult read_checked(const std::string& path, size_t max_bytes = 64 * 1024);
+  std::optional<std::string> read_checked_trimmed(const std::string& path);
   // Close every kept descriptor (e.g. when the topology generation changed
   // and some paths will never be read again).
   void clear();
@@ -103,6 +109,11 @@ class AttrReader {
   // descriptor take it exclusively, so per-GPU lanes do not queue on it.
   mutable std::shared_mutex mu_;
   std::unordered_map<std::string, std::shared_ptr<const Fd>> fds_;
+  struct Checked {
+    std::shared_ptr<const Fd> fd;
+    uint64_t dev = 0, ino = 0;
+  };
+  std::unordered_map<std::string, Checked> checked_;
   bool keep_all_ = false;
 };
 

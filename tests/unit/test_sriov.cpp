@@ -411,3 +411,26 @@ TEST(Sriov_ListingSkippedWhileUeventSeqnumUnchanged) {
   EXPECT_EQ(pci.Devices().size(), static_cast<size_t>(5));
   fs::remove_all(root);
 }
+
+TEST(Fs_AttrReaderCheckedFollowsReplacedFiles) {
+  char d[] = "/tmp/gfd-checked-XXXXXX";
+  if (!mkdtemp(d)) throw std::runtime_error("mkdtemp");
+  std::string f = std::string(d) + "/version";
+  put_file(f, "7.2.0\n");
+  fs::AttrReader r;
+  EXPECT_EQ(r.read_checked_trimmed(f).value_or(""), std::string("7.2.0"));
+  EXPECT_EQ(r.open_count(), static_cast<size_t>(1));
+  EXPECT_EQ(r.read_checked_trimmed(f).value_or(""), std::string("7.2.0"));
+  put_file(f, "7.3.1\n");  // replaced (rename over it): a new inode
+  EXPECT_EQ(r.read_checked_trimmed(f).value_or(""), std::string("7.3.1"));
+  {
+    FILE* fp = std::fopen(f.c_str(), "r+");  // rewritten in place
+    std::fputs("7.4.0\n", fp);
+    std::fclose(fp);
+  }
+  EXPECT_EQ(r.read_checked_trimmed(f).value_or(""), std::string("7.4.0"));
+  fs::remove_all(f);
+  EXPECT_FALSE(r.read_checked_trimmed(f).has_value());
+  EXPECT_EQ(r.open_count(), static_cast<size_t>(0));
+  fs::remove_all(d);
+}

@@ -7,9 +7,14 @@ One "step" is one full labeling cycle of the daemon in its default
 configuration: enumerate the node through the backend (amd-smi on a GPU
 box), build every label (version, partition, xGMI, resources, SR-IOV PCI
 scan) and atomically rewrite the NFD feature file.  Nothing is cached across
-steps except what the daemon itself keeps (the loaded library and, in the
-default persistent amd-smi session, the initialised handle table); every
-device fact is re-queried from the driver each step.
+steps except what the daemon itself keeps between its cycles, listed with
+the reason each is safe in docs/ARCHITECTURE.md ("What is kept between
+cycles"): the loaded library, the persistent amd-smi session's handles and
+the facts fixed until the KFD topology generation changes (virtualization
+mode, KFD node id and XCD count), open descriptors of sysfs attributes, and
+the PCI bus listing while no device was added or removed.  Every other
+device value - memory, partition modes, xGMI links, partition
+capabilities, versions, machine type - is read from the driver each step.
 
 The label set of every step is checked for correctness (count == N GPUs,
 gfx950/cdna4 arch, MI355 product, HBM size) before timing is reported.

@@ -599,9 +599,9 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
 
   // Apply the visible-device filter on physical GPUs (index = BDF order).
   struct Gpu {
-    int index;
+    int index = 0;
     std::string bdf;
-    std::vector<ProcInfo>* procs;
+    std::vector<ProcInfo>* procs = nullptr;
     GpuExtras extras;
     std::exception_ptr error;
     int64_t proc_ns = 0, caps_ns = 0;
@@ -612,7 +612,11 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
   for (auto& [bdf, procs] : groups) {
     ++index;
     if (opts_.filter.matches(index, bdf)) {
-      gpus.push_back(Gpu{index, bdf, &procs, {}, {}});
+      Gpu g;
+      g.index = index;
+      g.bdf = bdf;
+      g.procs = &procs;
+      gpus.push_back(std::move(g));
       auto v = virt_mode_.find(bdf);
       if (v != virt_mode_.end()) gpus.back().extras.virtualization = v->second;
       auto k = kfd_node_.find(bdf);

@@ -204,3 +204,31 @@ def test_devices_match_amd_smi_cli(amdsmi_devices, sysfs_devices):
             assert d["xgmi_links"] == sum(1 for x in ports[d["bdf"]] if x == "U")
             if d["compute_partition"] == "SPX":
                 assert d["compute_units"] == s["asic"]["num_compute_units"]
+
+
+def test_attribute_descriptors_kept_open_and_stable(native):
+    """Per-cycle sysfs attributes are read through descriptors kept open
+    across cycles (pread at offset 0 re-runs the driver's show()): after a
+    few cycles the process holds descriptors on the GPU's amdgpu attributes,
+    their number does not grow, and the labels do not change."""
+    s = native.Session(["--backend=amdsmi", "--no-timestamp", "--output-file="])
+    first = s.cycle(False)["labels"]
+
+    def sysfs_fds():
+        out = []
+        for fd in os.listdir("/proc/self/fd"):
+            try:
+                target = os.readlink(f"/proc/self/fd/{fd}")
+            except OSError:
+                continue
+            if target.startswith("/sys/"):
+                out.append(target)
+        return sorted(out)
+
+    before = sysfs_fds()
+    for _ in range(50):
+        assert s.cycle(False)["labels"] == first
+    after = sysfs_fds()
+    assert any(t.endswith("/current_compute_partition") for t in after), after
+    assert any(t.endswith("/mem_info_vram_total") for t in after), after
+    assert len(after) == len(before), (before, after)

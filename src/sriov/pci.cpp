@@ -178,7 +178,9 @@ std::vector<PCIDevice> SysfsAmdPCI::Devices() {
     for (auto& [addr, ino] : entries) {
       while (hit != cache_.end() && hit->first < addr) ++hit;
       if (hit != cache_.end() && hit->first == addr && hit->second.ino == ino && ino != 0) {
-        next.emplace_back(std::move(addr), std::move(hit->second));
+        // Copied, not moved: if an identity read below fails, cache_ must
+        // still be intact for the next scan.
+        next.emplace_back(std::move(addr), hit->second);
         next.back().second.sriov_numvfs = -1;  // re-read below
       } else {
         misses.push_back(next.size());
@@ -221,10 +223,15 @@ std::vector<PCIDevice> SysfsAmdPCI::Devices() {
     }
   };
   size_t chunks = (misses.size() + chunk - 1) / chunk;
-  if (chunks > 1)
-    WorkerPool::instance().parallel_for(chunks, read_chunk);
-  else if (chunks == 1)
-    read_chunk(0);
+  try {
+    if (chunks > 1)
+      WorkerPool::instance().parallel_for(chunks, read_chunk);
+    else if (chunks == 1)
+      read_chunk(0);
+  } catch (...) {
+    listing_.reset();  // the next scan must see this listing as changed again
+    throw;
+  }
   if (changed) cache_.swap(next);
   scanned_ = true;
   seqnum_ = seqnum.value_or("");

@@ -52,6 +52,11 @@ class DirListing {
   int read(const std::string& path, bool* changed);
   // Entries of the last read, without . and .., sorted by name.
   std::vector<std::pair<std::string, uint64_t>> entries() const;
+  // Forget the last listing: the next read reports a change.
+  void reset() {
+    raw_.clear();
+    prev_.clear();
+  }
 
  private:
   int read_raw();

@@ -434,3 +434,24 @@ TEST(Fs_AttrReaderCheckedFollowsReplacedFiles) {
   EXPECT_EQ(r.open_count(), static_cast<size_t>(0));
   fs::remove_all(d);
 }
+
+TEST(Sriov_FailedScanLeavesStateForTheNextOne) {
+  std::string root = pci_host(20, 0);
+  std::string dev = root + "/sys/bus/pci/devices/";
+  SysfsAmdPCI pci(root);
+  EXPECT_EQ(pci.Devices().size(), static_cast<size_t>(5));
+  // A new function whose vendor cannot be read yet: the scan fails ...
+  fs::mkdir_all(dev + "0000:e1:00.0/vendor");
+  put_file(dev + "0000:e1:00.0/class", "0x120000\n");
+  put_file(dev + "0000:e1:00.0/device", "0x75a3\n");
+  put_file(dev + "0000:e1:00.0/sriov_totalvfs", "0\n");
+  EXPECT_THROW_MSG(pci.Devices(), "unable to read PCI device vendor id for 0000:e1:00.0");
+  // ... and the next one, over the same listing, reads it again and keeps
+  // the identities it already had.
+  fs::remove_all(dev + "0000:e1:00.0/vendor");
+  put_file(dev + "0000:e1:00.0/vendor", "0x1002\n");
+  auto devs = pci.Devices();
+  EXPECT_EQ(devs.size(), static_cast<size_t>(6));
+  for (const auto& d : devs) EXPECT_EQ(d.device, std::string("0x75a3"));
+  fs::remove_all(root);
+}

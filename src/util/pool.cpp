@@ -141,6 +141,7 @@ void WorkerPool::Task::cancel_or_wait() {
     std::lock_guard<std::mutex> g(state_->mu);
     state_->fn = nullptr;
     state_->done = true;
+    state_->cv.notify_all();
     return;
   }
   std::unique_lock<std::mutex> lk(state_->mu);

@@ -92,9 +92,12 @@ def test_helm_chart(native):
 
 
 def test_helm_env_names_are_daemon_flags(native):
-    text = (CHART / "templates" / "daemonset.yml").read_text()
-    names = set(re.findall(r"name: (GFD_[A-Z_]+)", text))
-    assert names and names <= _env_vars(native)
+    # The DaemonSet takes its env list from the gfd-amd.env helper.
+    assert 'include "gfd-amd.env"' in (CHART / "templates" / "daemonset.yml").read_text()
+    text = (CHART / "templates" / "_helpers.tpl").read_text()
+    names = set(re.findall(r'"(GFD_[A-Z_]+)"', text)) | set(re.findall(r"name: (GFD_[A-Z_]+)", text))
+    assert {"GFD_MIG_STRATEGY", "GFD_SLEEP_INTERVAL", "GFD_FAIL_ON_INIT_ERROR"} <= names
+    assert names <= _env_vars(native)
 
 
 def test_dockerfile(native):

@@ -191,9 +191,9 @@ void WorkerPool::parallel_for(size_t n, const std::function<void(size_t)>& fn, s
       if (++sh->done == sh->n) sh->cv.notify_all();
     }
   };
-  // Enqueue every helper lane under one lock and wake the workers with one
-  // futex call: per-lane submit+notify_one staggers the 8th lane's start by
-  // several wake-up latencies on an 8-GPU cycle.
+  // Enqueue every helper lane and wake its worker under one acquisition of
+  // the pool lock: per-lane submit (lock, enqueue, notify, unlock) staggers
+  // the 8th lane's start by several wake-up latencies on an 8-GPU cycle.
   {
     std::lock_guard<std::mutex> g(mu_);
     for (size_t l = 1; l < lanes; ++l) queue_.emplace_back(body);

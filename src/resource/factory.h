@@ -5,8 +5,10 @@
 //   amd-smi loadable            -> AmdSmiManager   (NVML analogue)
 //   else KFD topology present   -> SysfsManager    (Tegra/CUDA analogue)
 //   else                        -> NullManager
-// When both are present amd-smi wins and the KFD path is only a fallback,
-// mirroring "NVML + Tegra -> Tegra disabled" (factory.go:53-62).
+// When both are present amd-smi is preferred and the KFD path takes over if
+// amd-smi fails to initialise (PreferenceManager); the reference instead
+// disables the second backend ("NVML + Tegra -> Tegra disabled",
+// factory.go:53-62).
 // Explicit values: amdsmi | sysfs | null | mock (with --mock-file).
 #pragma once
 

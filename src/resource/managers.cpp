@@ -25,6 +25,31 @@ void FallbackManager::Init() {
   }
 }
 
+PreferenceManager::PreferenceManager(std::vector<ManagerPtr> candidates) : candidates_(std::move(candidates)) {
+  if (candidates_.empty()) throw Error("PreferenceManager needs at least one manager");
+  current_ = candidates_.front();
+}
+
+void PreferenceManager::Init() {
+  // Init runs once per labeling cycle: start from the manager in use, so a
+  // candidate that failed is not retried before the next reload.
+  std::string errors;
+  for (size_t i = chosen_; i < candidates_.size(); ++i) {
+    try {
+      candidates_[i]->Init();
+      bool switched = i != chosen_;
+      current_ = candidates_[i];
+      chosen_ = i;
+      if (switched) log::printf("Using the %s manager", current_->Name().c_str());
+      return;
+    } catch (const std::exception& e) {
+      log::printf("Warning: %s manager failed to initialize: %s", candidates_[i]->Name().c_str(), e.what());
+      errors += (errors.empty() ? "" : "; ") + candidates_[i]->Name() + ": " + e.what();
+    }
+  }
+  throw Error("no resource manager could be initialized (" + errors + ")");
+}
+
 ManagerPtr with_config(ManagerPtr m, const config::Config& c) {
   if (c.fail_on_init_error()) return m;
   return std::make_shared<FallbackManager>(std::move(m));

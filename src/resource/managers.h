@@ -47,6 +47,33 @@ class FallbackManager : public Manager {
   bool fell_back_ = false;
 };
 
+// `--backend=auto` on a node with both amd-smi and a KFD topology: the
+// candidates in order of preference (amd-smi, then KFD sysfs).  Init keeps
+// the first one whose Init succeeds - an amd-smi library that cannot talk to
+// the driver (version skew, no /dev/kfd in the container) still leaves the
+// node labelled from sysfs - and the choice sticks until the manager is
+// rebuilt (SIGHUP reload).  Init fails only when every candidate failed.
+// (The reference simply disables its second backend on such nodes,
+// internal/resource/factory.go:55-59.)
+class PreferenceManager : public Manager {
+ public:
+  explicit PreferenceManager(std::vector<ManagerPtr> candidates);
+  void Init() override;
+  void Shutdown() override { current_->Shutdown(); }
+  std::vector<DevicePtr> GetDevices() override { return current_->GetDevices(); }
+  std::string GetDriverVersion() override { return current_->GetDriverVersion(); }
+  RuntimeVersion GetRuntimeVersion() override { return current_->GetRuntimeVersion(); }
+  std::string Name() const override { return current_->Name(); }
+  std::optional<std::string> VersionFilesRoot() const override { return current_->VersionFilesRoot(); }
+  // Index of the candidate in use (0 until an Init fell through).
+  size_t chosen() const { return chosen_; }
+
+ private:
+  std::vector<ManagerPtr> candidates_;
+  ManagerPtr current_;
+  size_t chosen_ = 0;
+};
+
 // Wrap `m` in a FallbackManager unless failOnInitError is set.
 ManagerPtr with_config(ManagerPtr m, const config::Config& c);
 

@@ -13,7 +13,9 @@
 //                             (processor type, BDF, ASIC info) busy-waits N us
 //                             holding that GPU's lock (amd-smi serialises per
 //                             device), to model multi-GPU scaling of the backend
-// Counters are exposed for assertions (fake_amdsmi_init_calls, ...).
+// Counters are exposed for assertions (fake_amdsmi_init_calls, ...).  The
+// spec can also come from the GFD_FAKE_AMDSMI_SPEC environment variable
+// ('|' separates lines), read when the library is loaded.
 #include <amd_smi/amdsmi.h>
 
 #include <cstdint>
@@ -397,3 +399,17 @@ amdsmi_status_t amdsmi_get_lib_version(amdsmi_version_t* v) {
 }
 
 }  // extern "C"
+
+namespace {
+// A process that cannot call fake_amdsmi_configure (the daemon binary under a
+// Python test) describes the node in GFD_FAKE_AMDSMI_SPEC instead, with '|'
+// or newlines between lines.
+__attribute__((constructor)) void configure_from_env() {
+  const char* spec = std::getenv("GFD_FAKE_AMDSMI_SPEC");
+  if (!spec || !*spec) return;
+  std::string text(spec);
+  for (char& ch : text)
+    if (ch == '|') ch = '\n';
+  fake_amdsmi_configure(text.c_str());
+}
+}  // namespace

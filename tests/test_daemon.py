@@ -259,3 +259,45 @@ def test_write_failure_is_an_error(binary, tmp_path):
         assert cp.returncode == 1 and "error writing file" in cp.stderr
     finally:
         ro.chmod(0o700)
+
+
+def _fake_amdsmi_env(spec: str) -> dict:
+    import gpu_feature_discovery_amd as gfd
+
+    lib = gfd.BUILD_DIR / "libfake_amdsmi.so"
+    if not lib.exists():
+        pytest.skip("libfake_amdsmi.so not built")
+    return {"GFD_AMDSMI_LIBRARY": str(lib), "GFD_FAKE_AMDSMI_SPEC": spec}
+
+
+def test_auto_backend_uses_sysfs_when_amdsmi_fails_to_initialise(binary, tmp_path, mi355x_node):
+    """amd-smi loads but amdsmi_init fails (DRIVER_NOT_LOADED): on a node
+    with a KFD topology the auto backend labels from sysfs instead of failing
+    (PreferenceManager; the reference has no second backend to try)."""
+    root = mi355x_node(n_gpus=2)
+    out = tmp_path / "gfd"
+    cp = run_daemon(binary, "--oneshot", "--backend=auto", f"--sysfs-root={root}", f"--output-file={out}",
+                    env=_fake_amdsmi_env("init_status=34"), check=True)
+    labels = golden.parse_labels(out.read_text())
+    assert labels["amd.com/gpu.count"] == "2"
+    assert labels["amd.com/gpu.product"].startswith("AMD-Instinct-MI355")
+    assert "amdsmi(persistent) manager failed to initialize" in cp.stderr
+    assert "Using the sysfs manager" in cp.stderr
+
+
+def test_auto_backend_prefers_amdsmi(binary, tmp_path, mi355x_node):
+    root = mi355x_node(n_gpus=2)
+    out = tmp_path / "gfd"
+    spec = "bdf=0000:d9:00.0;mode=SPX;parts=1;cus=256;xcds=8;vram_mib=294896;links=7;virt=1"
+    cp = run_daemon(binary, "--oneshot", "--backend=auto", f"--sysfs-root={root}", f"--output-file={out}",
+                    env=_fake_amdsmi_env(spec), check=True)
+    labels = golden.parse_labels(out.read_text())
+    assert labels["amd.com/gpu.count"] == "1"  # the fake's one GPU, not the tree's two
+    assert "failed to initialize" not in cp.stderr
+
+
+def test_auto_backend_without_kfd_topology_still_fails_on_init_error(binary, tmp_path):
+    cp = run_daemon(binary, "--oneshot", "--backend=auto", f"--sysfs-root={tmp_path}", "--output-file=",
+                    env=_fake_amdsmi_env("init_status=34"))
+    assert cp.returncode == 1
+    assert "amdsmi_init failed" in cp.stderr

@@ -15,6 +15,7 @@
 #include "config/config.h"
 #include "lm/resource.h"
 #include "resource/amdsmi.h"
+#include "resource/factory.h"
 #include "test.h"
 #include "util/fs.h"
 
@@ -300,6 +301,27 @@ TEST(AmdSmiFake_InitFailureSurfaces) {
   std::string root = temp_root();
   AmdSmiManager m(opts(root, true));
   EXPECT_THROW_MSG(m.Init(), "amdsmi_init failed: AMDSMI_STATUS_DRIVER_NOT_LOADED");
+  fs::remove_all(root);
+}
+
+TEST(AmdSmiFake_AutoBackendFallsBackToSysfsWhenInitFails) {
+  REQUIRE_FAKE();
+  fake().configure("init_status=34\n");
+  std::string root = temp_root();
+  fs::mkdir_all(root + "/sys/class/kfd/kfd/topology/nodes");
+  set_generation(root, "1");
+  config::Config c;
+  c.flags.gfd.backend = "auto";
+  c.flags.gfd.sysfs_root = root;
+  int i0 = fake().init_calls();
+  auto m = get_manager(c);
+  EXPECT_EQ(m->Name(), std::string("amdsmi(persistent)"));
+  m->Init();
+  EXPECT_EQ(m->Name(), std::string("sysfs"));
+  EXPECT_EQ(m->GetDevices().size(), static_cast<size_t>(0));
+  m->Shutdown();
+  m->Init();
+  EXPECT_EQ(fake().init_calls() - i0, 1);  // amd-smi is not retried every cycle
   fs::remove_all(root);
 }
 

@@ -281,6 +281,46 @@ TEST(Factory_FailOnInitErrorWrapsInFallback) {
   EXPECT_EQ(new_manager(c)->Name(), std::string("null"));
 }
 
+TEST(Preference_FirstManagerThatInitialisesIsKeptUntilRebuilt) {
+  auto a = std::make_shared<MockManager>();
+  a->with_error_on_init("no driver");
+  auto b = std::make_shared<MockManager>(std::vector<DevicePtr>{new_full_gpu()});
+  PreferenceManager p({a, b});
+  p.Init();
+  EXPECT_EQ(p.chosen(), static_cast<size_t>(1));
+  EXPECT_EQ(p.GetDevices().size(), static_cast<size_t>(1));
+  p.Shutdown();
+  // Init runs every cycle; the failed candidate is not retried.
+  p.Init();
+  EXPECT_EQ(a->init_calls, 1);
+  EXPECT_EQ(b->init_calls, 2);
+  EXPECT_EQ(b->shutdown_calls, 1);
+}
+
+TEST(Preference_PreferredManagerUsedWhenItInitialises) {
+  auto a = std::make_shared<MockManager>(std::vector<DevicePtr>{new_full_gpu(), new_full_gpu()});
+  auto b = std::make_shared<MockManager>();
+  PreferenceManager p({a, b});
+  p.Init();
+  EXPECT_EQ(p.chosen(), static_cast<size_t>(0));
+  EXPECT_EQ(p.GetDevices().size(), static_cast<size_t>(2));
+  EXPECT_EQ(b->init_calls, 0);
+}
+
+TEST(Preference_EveryCandidateFailingIsAnInitError) {
+  auto a = std::make_shared<MockManager>();
+  a->with_error_on_init("no driver");
+  auto b = std::make_shared<MockManager>();
+  b->with_error_on_init("no topology");
+  auto p = std::make_shared<PreferenceManager>(std::vector<ManagerPtr>{a, b});
+  EXPECT_THROW_MSG(p->Init(), "mock: no driver; mock: no topology");
+  // Without failOnInitError the daemon then labels with the Null manager.
+  FallbackManager f(p);
+  f.Init();
+  EXPECT_TRUE(f.fell_back());
+  EXPECT_EQ(f.Name(), std::string("fallback(null)"));
+}
+
 TEST(AmdSmi_InitFailsCleanlyWithoutDriver) {
   // In the CPU container libamd_smi loads but there is no amdgpu driver:
   // amdsmi_init returns DRIVER_NOT_LOADED, which must surface as an Init error.

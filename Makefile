@@ -43,8 +43,15 @@ coverage:
 	cmake -S . -B build-cov -G Ninja -DCMAKE_BUILD_TYPE=Debug -DGFD_BUILD_PYTHON=OFF \
 	  -DCMAKE_CXX_FLAGS="--coverage" -DCMAKE_EXE_LINKER_FLAGS="--coverage"
 	cmake --build build-cov -j $(JOBS)
-	GFD_AMDSMI_LIBRARY=build-cov/libfake_amdsmi.so ./build-cov/gfd_unit_tests
-	gcov -o build-cov/CMakeFiles/gfdcore.dir/src -r src/*/*.cpp > /dev/null 2>&1 || true
+	find build-cov -name '*.gcda' -delete
+	./build-cov/gfd_unit_tests > /dev/null
+	GFD_AMDSMI_LIBRARY=build-cov/libfake_amdsmi.so ./build-cov/gfd_unit_tests > /dev/null
+	# The daemon binary under the Python end-to-end tests adds its own counts.
+	GFD_BINARY=$(CURDIR)/build-cov/gpu-feature-discovery $(PYTHON) -m pytest tests -q -m "not gpu" -p no:cacheprovider
+	@for f in src/*/*.cpp; do gcov -n -o build-cov/CMakeFiles/gfdcore.dir/$$f.o $$f 2>/dev/null | \
+	  grep -A1 "^File '.*$$f'" | tail -1 | sed "s|Lines executed:|$$f |"; done | \
+	  awk '{split($$2, p, "%"); n = $$4; hit += p[1] * n / 100; tot += n; print} \
+	       END {printf "TOTAL %.1f%% of %d lines\n", 100 * hit / tot, tot}'
 
 bench: build
 	$(PYTHON) bench.py

@@ -1,5 +1,6 @@
 // Labeler unit tests.  Ports of internal/lm/resource_test.go:27-304 and
 // internal/lm/nvml_test.go:11-77, re-expressed for the amd.com schema.
+#include <fcntl.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -342,6 +343,32 @@ TEST(WriteToFile_AtomicWithMode0644) {
 
 TEST(WriteToFile_UnwritableDirectoryErrors) {
   EXPECT_THROW_MSG(lm::write_to_file({{"k", "v"}}, "/proc/gfd-cannot-write/here/gfd"), "error atomically writing file");
+}
+
+TEST(WriteToFile_RenameFailureLeavesNoTemporaries) {
+  char dir[] = "/tmp/gfd-write-XXXXXX";
+  EXPECT_TRUE(mkdtemp(dir) != nullptr);
+  // The output path is a non-empty directory: rename(2) refuses it.
+  std::string path = std::string(dir) + "/gfd";
+  fs::mkdir_all(path + "/keep");
+  EXPECT_THROW_MSG(lm::write_to_file({{"k", "v"}}, path), "error moving temporary file to");
+  EXPECT_FALSE(fs::exists(std::string(dir) + "/gfd-tmp"));
+  EXPECT_TRUE(fs::is_dir(path + "/keep"));
+  fs::remove_all(dir);
+}
+
+TEST(WriteToFile_RecoversFromABlockedTemporaryDirectory) {
+  char dir[] = "/tmp/gfd-write-XXXXXX";
+  EXPECT_TRUE(mkdtemp(dir) != nullptr);
+  std::string path = std::string(dir) + "/gfd";
+  // A regular file where gfd-tmp/ belongs: that cycle fails and clears it,
+  // the next one writes.
+  EXPECT_TRUE(::close(::open((std::string(dir) + "/gfd-tmp").c_str(), O_CREAT | O_WRONLY, 0644)) == 0);
+  EXPECT_THROW_MSG(lm::write_to_file({{"k", "v"}}, path), "fail to create temporary output file");
+  EXPECT_FALSE(fs::exists(std::string(dir) + "/gfd-tmp"));
+  lm::write_to_file({{"k", "v"}}, path);
+  EXPECT_EQ(fs::read_file(path).data, std::string("k=v\n"));
+  fs::remove_all(dir);
 }
 
 TEST(SanitizeLabelValue) {

@@ -9,6 +9,7 @@
 #include "util/fs.h"
 #include "util/strings.h"
 
+#include <sys/wait.h>
 #include <unistd.h>
 
 #include <cstdio>
@@ -387,6 +388,35 @@ TEST(Fs_AttrReaderKeepsOnlySysfsDescriptors) {
   if (sys.read_trimmed("/sys/kernel/mm/transparent_hugepage/enabled") || sys.read_trimmed("/sys/kernel/uevent_seqnum"))
     EXPECT_EQ(sys.open_count(), static_cast<size_t>(1));
   fs::remove_all(d);
+}
+
+TEST(Fs_AttrReaderDropsADescriptorThatStopsReading) {
+  // The CPU-side analogue of a sysfs attribute whose device went away (reads
+  // on the kept descriptor fail with ENODEV): a /proc file of a process that
+  // has been reaped fails with ESRCH.  The descriptor is dropped and the path
+  // looked up again, which then fails too.
+  int pipefd[2];
+  EXPECT_TRUE(::pipe(pipefd) == 0);
+  pid_t pid = ::fork();
+  if (pid == 0) {
+    char c;
+    ::close(pipefd[1]);
+    while (::read(pipefd[0], &c, 1) > 0) {
+    }
+    ::_exit(0);
+  }
+  ::close(pipefd[0]);
+  std::string path = "/proc/" + std::to_string(pid) + "/stat";
+  fs::AttrReader r;
+  r.keep_all_for_testing(true);
+  EXPECT_TRUE(r.read_trimmed(path).has_value());
+  EXPECT_EQ(r.open_count(), static_cast<size_t>(1));
+  ::close(pipefd[1]);  // the child sees EOF and exits
+  int status = 0;
+  EXPECT_EQ(::waitpid(pid, &status, 0), pid);
+  auto gone = r.read(path);
+  EXPECT_FALSE(gone.ok());
+  EXPECT_EQ(r.open_count(), static_cast<size_t>(0));
 }
 
 TEST(Sriov_ListingSkippedWhileUeventSeqnumUnchanged) {

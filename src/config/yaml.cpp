@@ -217,7 +217,11 @@ class Parser {
     throw Error("yaml: line " + std::to_string(no) + ": " + msg);
   }
 
-  static std::string strip_comment(const std::string& s) {
+  // Remove comments outside quoted scalars.  `s` may span lines (flow
+  // collections gathered over several lines): quote state carries across
+  // line breaks and a comment ends at the next one.
+  static std::string strip_comment(const std::string& in) {
+    std::string s = in;
     bool sq = false, dq = false;
     for (size_t i = 0; i < s.size(); ++i) {
       char c = s[i];
@@ -234,12 +238,15 @@ class Parser {
           else
             sq = false;
         }
-      } else if (c == '"' && (i == 0 || strchr(" \t[{,:", s[i - 1]))) {
+      } else if (c == '"' && (i == 0 || strchr(" \t\n[{,:", s[i - 1]))) {
         dq = true;
-      } else if (c == '\'' && (i == 0 || strchr(" \t[{,:", s[i - 1]))) {
+      } else if (c == '\'' && (i == 0 || strchr(" \t\n[{,:", s[i - 1]))) {
         sq = true;
-      } else if (c == '#' && (i == 0 || s[i - 1] == ' ' || s[i - 1] == '\t')) {
-        return s.substr(0, i);
+      } else if (c == '#' && (i == 0 || s[i - 1] == ' ' || s[i - 1] == '\t' || s[i - 1] == '\n')) {
+        size_t nl = s.find('\n', i);
+        if (nl == std::string::npos) return s.substr(0, i);
+        s.erase(i, nl - i);
+        --i;  // the loop's ++i lands on the line break
       }
     }
     return s;
@@ -302,8 +309,14 @@ class Parser {
     size_t i = 0;
     std::string key;
     if (s[0] == '"' || s[0] == '\'') {
+      // An implicit key is on one line: a quote still open at the end of the
+      // line starts a (multi-line) quoted value instead.
       size_t end;
-      key = parse_quoted(s, 0, &end, lineno);
+      try {
+        key = parse_quoted(s, 0, &end, lineno);
+      } catch (const Error&) {
+        return std::nullopt;
+      }
       i = end;
       while (i < s.size() && s[i] == ' ') ++i;
       if (i >= s.size() || s[i] != ':') return std::nullopt;
@@ -319,6 +332,28 @@ class Parser {
       }
     }
     return std::nullopt;
+  }
+
+  // Line folding inside a quoted scalar, at the line break s[i]: trailing
+  // blanks before it and leading blanks after each break are dropped; one
+  // break becomes a space, n+1 breaks (n empty lines) become n newlines.
+  // Returns the index of the first character of the continuation.
+  static size_t fold_line_break(const std::string& s, size_t i, std::string& out) {
+    while (!out.empty() && (out.back() == ' ' || out.back() == '\t')) out.pop_back();
+    size_t empties = 0;
+    size_t j = i + 1;
+    for (;;) {
+      while (j < s.size() && (s[j] == ' ' || s[j] == '\t')) ++j;
+      if (j < s.size() && s[j] == '\n') {
+        ++empties;
+        ++j;
+        continue;
+      }
+      break;
+    }
+    if (empties == 0) out.push_back(' ');
+    else out.append(empties, '\n');
+    return j;
   }
 
   // Parse a quoted scalar starting at s[pos]; *end is set past the closing quote.
@@ -339,17 +374,7 @@ class Parser {
           return out;
         }
         if (c == '\n') {
-          // Line folding: newline + leading spaces -> single space.
-          while (!out.empty() && out.back() == ' ') out.pop_back();
-          size_t j = i + 1;
-          while (j < s.size() && (s[j] == ' ' || s[j] == '\t')) ++j;
-          if (j < s.size() && s[j] == '\n') {
-            out.push_back('\n');
-            i = j;
-            continue;
-          }
-          out.push_back(' ');
-          i = j;
+          i = fold_line_break(s, i, out);
           continue;
         }
         out.push_back(c);
@@ -362,16 +387,7 @@ class Parser {
         return out;
       }
       if (c == '\n') {
-        while (!out.empty() && out.back() == ' ') out.pop_back();
-        size_t j = i + 1;
-        while (j < s.size() && (s[j] == ' ' || s[j] == '\t')) ++j;
-        if (j < s.size() && s[j] == '\n') {
-          out.push_back('\n');
-          i = j;
-          continue;
-        }
-        out.push_back(' ');
-        i = j;
+        i = fold_line_break(s, i, out);
         continue;
       }
       if (c == '\\') {
@@ -463,18 +479,17 @@ class Parser {
         if (is_key && c == ':') break;
         ++i;
       }
-      // Fold internal newlines.
+      // Line breaks fold (one space, or a newline per empty line); blanks
+      // inside a line are content.
       std::string t = str::trim(s.substr(start, i - start));
       std::string out;
-      bool sp = false;
-      for (char c : t) {
-        if (c == '\n' || c == '\r' || c == '\t' || c == ' ') {
-          sp = true;
+      for (size_t k = 0; k < t.size();) {
+        if (t[k] == '\n') {
+          k = fold_line_break(t, k, out);
           continue;
         }
-        if (sp && !out.empty()) out.push_back(' ');
-        sp = false;
-        out.push_back(c);
+        if (t[k] != '\r') out.push_back(t[k]);
+        ++k;
       }
       return out;
     }
@@ -576,10 +591,13 @@ class Parser {
   // Collect flow text starting with `first` (content of line idx-1) plus as
   // many following lines as needed to balance brackets.  Advances idx.
   std::string gather_flow(const std::string& first, size_t& idx, int lineno) {
+    std::string raw = first;
     std::string buf = first;
+    // A quote opens a quoted scalar only where a flow node starts (after
+    // '[', '{', ',' or ": "); inside a plain scalar ("[0']") it is text.
     auto balanced = [](const std::string& t) {
       int depth = 0;
-      bool sq = false, dq = false;
+      bool sq = false, dq = false, node_start = true;
       for (size_t i = 0; i < t.size(); ++i) {
         char c = t[i];
         if (dq) {
@@ -590,19 +608,23 @@ class Parser {
           continue;
         }
         if (sq) {
-          if (c == '\'') sq = false;
+          if (c == '\'') sq = false;  // '' re-opens on the next character
           continue;
         }
-        if (c == '"') dq = true;
-        else if (c == '\'') sq = true;
+        if (c == ' ' || c == '\t' || c == '\n') continue;
+        if (node_start && c == '"') dq = true;
+        else if (node_start && c == '\'') sq = true;
         else if (c == '[' || c == '{') ++depth;
         else if (c == ']' || c == '}') --depth;
+        node_start = c == '[' || c == '{' || c == ',' ||
+                     (c == ':' && (i + 1 >= t.size() || t[i + 1] == ' ' || t[i + 1] == '\t' || t[i + 1] == '\n'));
       }
       return depth <= 0 && !sq && !dq;
     };
     while (!balanced(buf)) {
       if (idx >= lines_.size()) fail_no(lineno, "did not find expected end of flow collection");
-      buf += "\n" + str::trim(strip_comment(lines_[idx].raw));
+      raw += "\n" + str::trim(lines_[idx].raw);
+      buf = strip_comment(raw);
       ++idx;
     }
     return buf;
@@ -654,21 +676,33 @@ class Parser {
       ++trailing;
     }
     std::string out;
-    for (size_t k = 0; k < raw.size(); ++k) {
-      if (k > 0) {
-        if (literal) {
-          out.push_back('\n');
-        } else {
-          // Folded: single newline between non-empty, non-indented lines -> space.
-          bool prev_more = !raw[k - 1].empty() && (raw[k - 1][0] == ' ' || raw[k - 1][0] == '\t');
-          bool cur_more = !raw[k].empty() && (raw[k][0] == ' ' || raw[k][0] == '\t');
-          if (raw[k].empty() || raw[k - 1].empty() || prev_more || cur_more)
-            out.push_back('\n');
-          else
-            out.push_back(' ');
-        }
+    if (literal) {
+      for (size_t k = 0; k < raw.size(); ++k) {
+        if (k > 0) out.push_back('\n');
+        out += raw[k];
       }
-      out += raw[k];
+    } else {
+      // Folded: the break between two lines at the block's indentation
+      // becomes a space, and when n empty lines separate them the first
+      // break is dropped (n newlines).  Around a more-indented line every
+      // break is kept.  Leading empty lines are newlines.
+      auto more = [](const std::string& l) { return !l.empty() && (l[0] == ' ' || l[0] == '\t'); };
+      size_t k = 0;
+      while (k < raw.size() && raw[k].empty()) {
+        out.push_back('\n');
+        ++k;
+      }
+      while (k < raw.size()) {
+        out += raw[k];
+        size_t m = k + 1;
+        while (m < raw.size() && raw[m].empty()) ++m;
+        if (m >= raw.size()) break;  // trailing empties were taken off above
+        size_t empties = m - k - 1;
+        if (more(raw[k]) || more(raw[m])) out.append(empties + 1, '\n');
+        else if (empties == 0) out.push_back(' ');
+        else out.append(empties, '\n');
+        k = m;
+      }
     }
     if (!raw.empty()) {
       if (chomp == 'c') out.push_back('\n');

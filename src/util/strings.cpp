@@ -2,6 +2,7 @@
 
 #include <algorithm>
 #include <cerrno>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -120,7 +121,11 @@ std::optional<double> parse_float(std::string_view sv) {
   errno = 0;
   char* end = nullptr;
   double v = strtod(s.c_str(), &end);
-  if (errno != 0 || end != s.c_str() + s.size()) return std::nullopt;
+  if (end != s.c_str() + s.size()) return std::nullopt;
+  // Like Go's strconv.ParseFloat: overflow is an error, underflow (a
+  // subnormal or zero result, also ERANGE for strtod) is not.
+  if (errno == ERANGE && std::isinf(v)) return std::nullopt;
+  if (errno != 0 && errno != ERANGE) return std::nullopt;
   return v;
 }
 

@@ -16,6 +16,14 @@ TEST(Yaml_Yaml11Booleans) {
   EXPECT_EQ(to_json(n), std::string("{\"a\":true,\"b\":false,\"c\":true,\"d\":false}"));
 }
 
+TEST(Yaml_GoYamlV2Resolution) {
+  // Where go-yaml v2 (the reference's reader) and PyYAML disagree the native
+  // reader follows go-yaml: y/n are booleans, an exponent needs no dot, and
+  // an underflowing float is a (subnormal) number, not a string.
+  Node n = parse("a: y\nb: n\nc: 1e3\nd: 1.1125369292536007e-308\ne: 1e999x\n");
+  EXPECT_EQ(to_json(n), std::string("{\"a\":true,\"b\":false,\"c\":1000,\"d\":1.1125369292536007e-308,\"e\":\"1e999x\"}"));
+}
+
 TEST(Yaml_NestedAndComments) {
   Node n = parse("# header\nversion: v1 # trailing\nflags:\n  migStrategy: single\n  gfd:\n    oneshot: true\n\n    sleepInterval: 30s\n");
   EXPECT_EQ(to_json(n), std::string("{\"version\":\"v1\",\"flags\":{\"migStrategy\":\"single\",\"gfd\":{\"oneshot\":true,\"sleepInterval\":\"30s\"}}}"));

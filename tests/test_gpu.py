@@ -84,12 +84,27 @@ def test_daemon_oneshot_matches_regex_golden(binary, tmp_path):
     out = tmp_path / "gfd"
     cp = run_daemon(binary, "--oneshot", f"--output-file={out}", "--trace-timing", check=True, timeout=120)
     assert "Detected amd-smi platform" in cp.stderr
+    assert "Using amd-smi manager" in cp.stderr and "failed to initialize" not in cp.stderr
     text = out.read_text()
     golden.check_regex_golden(text, TESTS / "expected-output.txt", select=lambda ln: "sriov" not in ln)
     labels = golden.parse_labels(text)
     assert labels["amd.com/gpu.arch"] == "gfx950"
     assert labels["amd.com/gpu.family"] == "cdna4"
     assert labels["amd.com/gpu.compute-units"] == "256"
+
+
+def test_auto_backend_falls_back_to_sysfs_on_hardware(binary, tmp_path):
+    """An amd-smi library that loads but cannot initialise (the scriptable
+    fake, told to fail amdsmi_init) on a real node: the auto backend labels
+    the GPU from the KFD topology instead, with the same label set."""
+    fake = REPO / "build" / "libfake_amdsmi.so"
+    out = tmp_path / "gfd"
+    cp = run_daemon(binary, "--oneshot", f"--output-file={out}", check=True, timeout=60,
+                    env={"GFD_AMDSMI_LIBRARY": str(fake), "GFD_FAKE_AMDSMI_SPEC": "init_status=34"})
+    assert "Using the sysfs manager" in cp.stderr
+    text = out.read_text()
+    golden.check_regex_golden(text, TESTS / "expected-output.txt", select=lambda ln: "sriov" not in ln)
+    assert golden.parse_labels(text)["amd.com/gpu.arch"] == "gfx950"
 
 
 def test_daemon_sysfs_backend_oneshot(binary, tmp_path):

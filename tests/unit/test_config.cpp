@@ -95,6 +95,24 @@ TEST(Config_TimeSlicingValidation) {
                    "unsupported type for device");
 }
 
+TEST(Config_PartitionDeviceRefs) {
+  auto devices = [](const std::string& items) {
+    return parse_config_text("sharing:\n  timeSlicing:\n    resources:\n    - name: gpu\n      replicas: 2\n"
+                             "      devices:\n" + items)
+        .sharing.time_slicing.resources[0]
+        .devices.list;
+  };
+  EXPECT_EQ(devices("      - PARTITION-GPU-3aff75a3-0000-1000-807c-178b7c5e4d5c/3\n"
+                    "      - PARTITION-3aff75a3-0000-1000-807c-178b7c5e4d5c/0\n      - \"1:7\"\n")
+                .size(),
+            static_cast<size_t>(3));
+  EXPECT_THROW_MSG(devices("      - PARTITION-nope/1\n"), "unsupported type for device");
+  EXPECT_THROW_MSG(devices("      - PARTITION-GPU-3aff75a3-0000-1000-807c-178b7c5e4d5c/x\n"), "unsupported type for device");
+  EXPECT_THROW_MSG(devices("      - \"1:x\"\n"), "unsupported type for device");
+  EXPECT_THROW_MSG(devices("      - GPU-3aff75a3\n"), "unsupported type for device");
+  EXPECT_THROW_MSG(devices("      - -1\n"), "unsupported type for device");
+}
+
 TEST(Config_DeviceRefsAcceptUuids) {
   Config c = parse_config_text(
       "sharing:\n  timeSlicing:\n    resources:\n    - name: gpu\n      replicas: 2\n      devices:\n"

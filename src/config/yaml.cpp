@@ -3,6 +3,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <optional>
 
 #include "util/error.h"
@@ -209,6 +210,8 @@ class Parser {
 
  private:
   std::vector<Line> lines_;
+  // Anchored nodes by name (&name), for aliases (*name) later in the document.
+  std::map<std::string, Node> anchors_;
 
   [[noreturn]] static void fail(const Line& l, const std::string& msg) {
     throw Error("yaml: line " + std::to_string(l.no) + ": " + msg);
@@ -445,11 +448,84 @@ class Parser {
     fail_no(lineno, "found unexpected end of stream while scanning a quoted scalar");
   }
 
+  // ---- Anchors, aliases and tags (go-yaml v2 resolves the same set).
+
+  static const Node& alias(const std::map<std::string, Node>& anchors, const std::string& name, int lineno) {
+    auto it = anchors.find(name);
+    if (it == anchors.end()) fail_no(lineno, "unknown anchor '" + name + "' referenced");
+    return it->second;
+  }
+
+  static void check_anchor_name(const std::string& name, int lineno) {
+    if (name.empty()) fail_no(lineno, "did not find expected alphabetic or numeric character");
+  }
+
+  // Apply a tag to a parsed value.  `plain` is the untouched text of a plain
+  // scalar (has_plain false for quoted/flow/block values).  !!str and the
+  // non-specific "!" turn a plain scalar into a string as written.
+  static Node apply_tag(const std::string& tag, Node v, bool has_plain, const std::string& plain, int lineno) {
+    auto bad = [&](const char* what) -> Node {
+      fail_no(lineno, std::string("cannot decode ") + what + " as " + tag);
+    };
+    if (tag == "!" || tag == "!!str") {
+      if (has_plain) return Node::string(plain);
+      if (v.kind() == Node::Kind::String) return v;
+      if (v.is_null()) return Node::string("");
+      if (v.kind() == Node::Kind::Bool) return Node::string(v.as_bool() ? "true" : "false");
+      if (v.kind() == Node::Kind::Int) return Node::string(std::to_string(v.as_int()));
+      if (v.kind() == Node::Kind::Float) return Node::string(v.text());
+      return bad(v.kind_name().c_str());
+    }
+    // A quoted scalar under a scalar tag is resolved from its content.
+    if (v.kind() == Node::Kind::String && !has_plain &&
+        (tag == "!!int" || tag == "!!float" || tag == "!!bool" || tag == "!!null"))
+      v = resolve_plain(v.text());
+    if (tag == "!!int") return v.kind() == Node::Kind::Int ? v : bad(v.kind_name().c_str());
+    if (tag == "!!float") {
+      if (v.kind() == Node::Kind::Int) return Node::floating(static_cast<double>(v.as_int()));
+      return v.kind() == Node::Kind::Float ? v : bad(v.kind_name().c_str());
+    }
+    if (tag == "!!bool") return v.kind() == Node::Kind::Bool ? v : bad(v.kind_name().c_str());
+    if (tag == "!!null") return v.is_null() ? v : bad(v.kind_name().c_str());
+    if (tag == "!!map") return v.is_map() ? v : bad(v.kind_name().c_str());
+    if (tag == "!!seq") return v.is_seq() ? v : bad(v.kind_name().c_str());
+    fail_no(lineno, "unsupported tag " + tag);
+  }
+
+  // "<<" entries: keys of the merged mapping(s) that the mapping does not
+  // set itself; with a sequence of mappings the earlier one wins.
+  static void apply_merges(Node& m, const std::vector<Node>& merges, int lineno) {
+    for (const Node& src : merges) {
+      std::vector<const Node*> maps;
+      if (src.is_map()) {
+        maps.push_back(&src);
+      } else if (src.is_seq()) {
+        for (const Node& item : src.items()) {
+          if (!item.is_map()) fail_no(lineno, "map merge requires map or sequence of maps as the value");
+          maps.push_back(&item);
+        }
+      } else {
+        fail_no(lineno, "map merge requires map or sequence of maps as the value");
+      }
+      for (const Node* mp : maps)
+        for (const auto& kv : mp->entries())
+          if (!m.get(kv.first)) m.set(kv.first, kv.second);
+    }
+  }
+
   // ---- Flow parsing over a joined text buffer.
   struct Flow {
     const std::string& s;
     size_t i;
     int lineno;
+    std::map<std::string, Node>* anchors;
+
+    // Anchor or tag name: up to a blank or a flow indicator.
+    std::string token() {
+      size_t start = i;
+      while (i < s.size() && !strchr(" \t\n\r,[]{}", s[i])) ++i;
+      return s.substr(start, i - start);
+    }
 
     [[noreturn]] void err(const std::string& m) const { fail_no(lineno, m); }
     void ws() {
@@ -467,8 +543,37 @@ class Parser {
         i = end;
         return Node::string(v);
       }
-      if (c == '&' || c == '*' || c == '!') err("anchors, aliases and tags are not supported");
+      if (c == '&') {
+        ++i;
+        std::string name = token();
+        check_anchor_name(name, lineno);
+        Node v = value_or_null();
+        (*anchors)[name] = v;
+        return v;
+      }
+      if (c == '*') {
+        ++i;
+        std::string name = token();
+        check_anchor_name(name, lineno);
+        return alias(*anchors, name, lineno);
+      }
+      if (c == '!') {
+        std::string tag = token();
+        ws();
+        bool plain_next = i < s.size() && !strchr("[{\"'&*!,]}", s[i]);
+        if (plain_next) {
+          std::string text = plain_text(false);
+          return apply_tag(tag, resolve_plain(text), true, text, lineno);
+        }
+        return apply_tag(tag, value_or_null(), false, "", lineno);
+      }
       return Node(plain(false));
+    }
+    // A value that may be empty (before ',', ']' or '}').
+    Node value_or_null() {
+      ws();
+      if (i >= s.size() || s[i] == ',' || s[i] == ']' || s[i] == '}') return Node::null();
+      return value();
     }
     std::string plain_text(bool is_key) {
       size_t start = i;
@@ -553,14 +658,17 @@ class Parser {
     }
     Node mapping() {
       Node n = Node::map();
+      std::vector<Node> merges;
       ++i;  // {
       for (;;) {
         ws();
         if (i >= s.size()) err("did not find expected ',' or '}'");
         if (s[i] == '}') {
           ++i;
+          apply_merges(n, merges, lineno);
           return n;
         }
+        bool quoted_key = s[i] == '"' || s[i] == '\'';
         std::string k = key();
         ws();
         Node v;
@@ -572,7 +680,10 @@ class Parser {
           else
             v = value();
         }
-        n.set(k, std::move(v));
+        if (k == "<<" && !quoted_key)
+          merges.push_back(std::move(v));
+        else
+          n.set(k, std::move(v));
         ws();
         if (i >= s.size()) err("did not find expected ',' or '}'");
         if (s[i] == ',') {
@@ -581,6 +692,7 @@ class Parser {
         }
         if (s[i] == '}') {
           ++i;
+          apply_merges(n, merges, lineno);
           return n;
         }
         err("did not find expected ',' or '}'");
@@ -631,7 +743,7 @@ class Parser {
   }
 
   Node parse_flow_text(const std::string& text, int lineno) {
-    Flow f{text, 0, lineno};
+    Flow f{text, 0, lineno, &anchors_};
     Node n = f.value();
     f.ws();
     if (f.i != text.size()) fail_no(lineno, "unexpected trailing content after flow collection");
@@ -761,8 +873,32 @@ class Parser {
       }
     }
     if (c == '|' || c == '>') return parse_block_scalar(rest, idx, parent_indent, lineno);
-    if (c == '&' || c == '*' || c == '!') fail_no(lineno, "anchors, aliases and tags are not supported");
-    // Plain scalar, possibly continued on more-indented lines.
+    if (c == '&' || c == '*' || c == '!') {
+      size_t sp = rest.find_first_of(" \t");
+      std::string name = rest.substr(c == '!' ? 0 : 1, sp == std::string::npos ? std::string::npos : sp - (c == '!' ? 0 : 1));
+      std::string after = sp == std::string::npos ? std::string() : str::trim(rest.substr(sp));
+      if (c == '*') {
+        check_anchor_name(name, lineno);
+        if (!after.empty()) fail_no(lineno, "unexpected content after alias *" + name);
+        return alias(anchors_, name, lineno);
+      }
+      if (c == '&') {
+        check_anchor_name(name, lineno);
+        Node v = parse_inline_value(after, idx, parent_indent, is_map_value);
+        anchors_[name] = v;
+        return v;
+      }
+      if (!after.empty() && !strchr("[{\"'|>&*!", after[0])) {
+        std::string text = gather_plain(after, idx, parent_indent);
+        return apply_tag(name, resolve_plain(text), true, text, lineno);
+      }
+      return apply_tag(name, parse_inline_value(after, idx, parent_indent, is_map_value), false, "", lineno);
+    }
+    return resolve_plain(gather_plain(rest, idx, parent_indent));
+  }
+
+  // Plain scalar text starting with `rest`, continued on more-indented lines.
+  std::string gather_plain(const std::string& rest, size_t& idx, int parent_indent) {
     std::string text = rest;
     for (;;) {
       size_t j = next_content(idx);
@@ -772,7 +908,7 @@ class Parser {
       text += " " + l.content;
       idx = j + 1;
     }
-    return resolve_plain(text);
+    return text;
   }
 
   Node parse_block(size_t& idx, int indent) {
@@ -791,6 +927,8 @@ class Parser {
 
   Node parse_map(size_t& idx, int indent) {
     Node m = Node::map();
+    std::vector<Node> merges;
+    int merge_line = 0;
     for (;;) {
       idx = next_content(idx);
       if (idx >= lines_.size()) break;
@@ -801,12 +939,19 @@ class Parser {
       auto kv = split_key(l.content, l.no);
       if (!kv) fail(l, "could not find expected ':'");
       if (kv->first.size() >= 2 && (kv->first[0] == '&' || kv->first[0] == '*' || kv->first[0] == '!'))
-        fail(l, "anchors, aliases and tags are not supported");
-      if (kv->first == "<<") fail(l, "merge keys are not supported");
+        fail(l, "anchors, aliases and tags on mapping keys are not supported");
+      int no = l.no;
+      bool merge = kv->first == "<<" && l.content[0] == '<';
       ++idx;
       Node v = parse_inline_value(kv->second, idx, indent, true);
-      m.set(kv->first, std::move(v));
+      if (merge) {
+        merges.emplace_back(std::move(v));
+        merge_line = no;
+      } else {
+        m.set(kv->first, std::move(v));
+      }
     }
+    apply_merges(m, merges, merge_line);
     return m;
   }
 

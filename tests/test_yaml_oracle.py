@@ -6,9 +6,9 @@ The reference reads its config file with sigs.k8s.io/yaml (go-yaml v2, YAML
 octal, and null; where go-yaml v2 and PyYAML differ the test follows go-yaml:
 ``y``/``n`` are booleans and ``1e3`` is a float there, so generated strings
 that would hit those rules are kept out of the comparison (the native reader's
-handling of them is pinned in tests/unit/test_config.cpp).  Anchors, tags and
-complex keys are rejected by the native reader with an error and are not
-generated.
+handling of them is pinned in tests/unit/test_yaml.cpp).  Shared subtrees
+make PyYAML emit anchors and aliases.  Complex keys and !!binary are rejected
+by the native reader with an error and are not generated.
 """
 
 from __future__ import annotations
@@ -51,6 +51,20 @@ def _same(a, b) -> bool:
 @settings(max_examples=300, deadline=None)
 @given(doc=st.dictionaries(_keys, _docs, min_size=1, max_size=6), flow=st.booleans(), width=st.sampled_from([10, 20, 80]))
 def test_native_reader_matches_pyyaml(native, doc, flow, width):
+    _check(native, doc, flow, width)
+
+
+@settings(max_examples=150, deadline=None)
+@given(shared=st.one_of(st.lists(_docs, min_size=1, max_size=3), st.dictionaries(_keys, _docs, min_size=1, max_size=3)),
+       keys=st.lists(_keys, min_size=2, max_size=4, unique=True), flow=st.booleans())
+def test_anchors_and_aliases_match_pyyaml(native, shared, keys, flow):
+    # The same object under several keys: PyYAML anchors the first and
+    # aliases the rest.
+    doc = {k: (shared if i % 2 == 0 else [shared, {"x": shared}]) for i, k in enumerate(keys)}
+    _check(native, doc, flow, 80)
+
+
+def _check(native, doc, flow, width):
     text = yaml.safe_dump(doc, default_flow_style=flow, width=width, allow_unicode=True, sort_keys=False)
     expected = yaml.safe_load(text)
     got = native.parse_yaml(text)
@@ -74,6 +88,14 @@ def test_native_reader_matches_pyyaml(native, doc, flow, width):
     ("{0  0: null}\n", {"0  0": None}),               # blanks inside a flow plain scalar
     ('{a: "x\\\n    #"}\n', {"a": "x#"}),           # '#' on a quoted continuation line
     ("a: 1.1125369292536007e-308\n", {"a": 1.1125369292536007e-308}),  # subnormal float
+    # Anchors, aliases, merge keys, standard tags.
+    ("base: &b\n  x: 1\n  y: 2\nc:\n  <<: *b\n  y: 3\n", {"base": {"x": 1, "y": 2}, "c": {"x": 1, "y": 3}}),
+    ("d:\n  <<: [{a: 1}, {a: 2, b: 3}]\n  c: 4\n", {"d": {"a": 1, "b": 3, "c": 4}}),
+    ("{a: &x {p: 1}, b: *x, c: {<<: *x, q: 2}}\n", {"a": {"p": 1}, "b": {"p": 1}, "c": {"p": 1, "q": 2}}),
+    ("- &a\n  x: 1\n- *a\n", [{"x": 1}, {"x": 1}]),
+    ("a: &x\n- 1\n- 2\nb: *x\n", {"a": [1, 2], "b": [1, 2]}),
+    ("a: !!str 1\nb: !!str 0x10\nd: !!float 3\ne: !!str\nf: !!int '3'\nt: !!str 1.50\n",
+     {"a": "1", "b": "0x10", "d": 3.0, "e": "", "f": 3, "t": "1.50"}),
 ])
 def test_pinned_cases(native, text, expected):
     assert native.parse_yaml(text) == expected

@@ -67,10 +67,22 @@ TEST(Yaml_DuplicateKeysLastWins) {
   EXPECT_EQ(n.get("a")->as_int(), static_cast<int64_t>(2));
 }
 
+TEST(Yaml_AnchorsAliasesMergeKeys) {
+  Node n = parse("defaults: &d\n  replicas: 2\n  rename: x\nres:\n- <<: *d\n  name: gpu\n- *d\n");
+  EXPECT_EQ(to_json(n), std::string("{\"defaults\":{\"replicas\":2,\"rename\":\"x\"},\"res\":[{\"name\":\"gpu\","
+                                    "\"replicas\":2,\"rename\":\"x\"},{\"replicas\":2,\"rename\":\"x\"}]}"));
+  // A quoted "<<" is an ordinary key.
+  EXPECT_EQ(to_json(parse("\"<<\": 1\n")), std::string("{\"<<\":1}"));
+}
+
 TEST(Yaml_Errors) {
   EXPECT_THROW_MSG(parse("a: 1\n  b: 2\n"), "line 2");
   EXPECT_THROW_MSG(parse("a: [1, 2\n"), "flow");
-  EXPECT_THROW_MSG(parse("a: &anchor 1\n"), "anchors");
+  EXPECT_THROW_MSG(parse("a: *missing\n"), "unknown anchor 'missing'");
+  EXPECT_THROW_MSG(parse("a: !!binary aGk=\n"), "unsupported tag !!binary");
+  EXPECT_THROW_MSG(parse("a: !!int x\n"), "cannot decode string as !!int");
+  EXPECT_THROW_MSG(parse("a:\n  <<: 1\n"), "map merge requires map");
+  EXPECT_THROW_MSG(parse("&k a: 1\n"), "mapping keys are not supported");
   EXPECT_THROW_MSG(parse("a: 1\n---\nb: 2\n"), "multiple YAML documents");
   EXPECT_THROW_MSG(parse("a: \"unterminated\n"), "quoted scalar");
   EXPECT_THROW_MSG(parse("\ta: 1\n"), "tab");

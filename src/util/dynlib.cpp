@@ -6,21 +6,6 @@ namespace gfd {
 
 DynLib::~DynLib() { close(); }
 
-DynLib::DynLib(DynLib&& o) noexcept : handle_(o.handle_), path_(std::move(o.path_)), error_(std::move(o.error_)) {
-  o.handle_ = nullptr;
-}
-
-DynLib& DynLib::operator=(DynLib&& o) noexcept {
-  if (this != &o) {
-    close();
-    handle_ = o.handle_;
-    path_ = std::move(o.path_);
-    error_ = std::move(o.error_);
-    o.handle_ = nullptr;
-  }
-  return *this;
-}
-
 bool DynLib::open(const std::vector<std::string>& candidates) {
   close();
   for (const auto& c : candidates) {

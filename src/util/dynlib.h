@@ -4,7 +4,7 @@
 // reference drives far too often — go-nvlib re-dlopens libnvidia-ml on every
 // IsMigCapable/IsMigEnabled call (nvlib/device/device.go:55-88, :327-338).
 // Here a library is opened once per process and its symbols are resolved
-// once into a function table (see resource/amdsmi_lib.h).
+// once into a function table (AmdSmiLib in resource/amdsmi.cpp).
 #pragma once
 
 #include <string>
@@ -18,8 +18,6 @@ class DynLib {
   ~DynLib();
   DynLib(const DynLib&) = delete;
   DynLib& operator=(const DynLib&) = delete;
-  DynLib(DynLib&& o) noexcept;
-  DynLib& operator=(DynLib&& o) noexcept;
 
   // Try each candidate path in order (RTLD_LAZY | RTLD_LOCAL).  Returns false
   // and records the last dlerror() if none loads.

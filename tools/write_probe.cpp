@@ -58,6 +58,29 @@ int main(int argc, char** argv) {
     lm::write_file_atomically(path, contents, 0644);
     whole.add(now_us() - h);
   }
-  for (Acc* x : {&mk, &st, &wr, &ch, &cl, &rn, &whole}) x->print();
+  // Variants: descriptor-relative calls on kept-open directory fds (no path
+  // walk), and a temporary in the target directory itself (same-directory
+  // rename; NFD would see the temporary, so for comparison only).
+  Acc rel{"dirfd-relative"}, same{"same-dir"};
+  int tmpfd = ::open(tmp_dir.c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC);
+  int outfd = ::open(dir.c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC);
+  std::string base = fs::basename(path);
+  for (int i = 0; i < 300; ++i) {
+    double a = now_us();
+    std::string name = "gfd-" + std::to_string(i);
+    int fd = ::openat(tmpfd, name.c_str(), O_WRONLY | O_CREAT | O_EXCL | O_CLOEXEC, 0644);
+    if (fd < 0 || ::write(fd, contents.data(), contents.size()) < 0) return 1;
+    ::close(fd);
+    ::renameat(tmpfd, name.c_str(), outfd, base.c_str());
+    rel.add(now_us() - a);
+    double b = now_us();
+    std::string dot = dir + "/.gfd-" + std::to_string(i);
+    fd = ::open(dot.c_str(), O_WRONLY | O_CREAT | O_EXCL | O_CLOEXEC, 0644);
+    if (fd < 0 || ::write(fd, contents.data(), contents.size()) < 0) return 1;
+    ::close(fd);
+    ::rename(dot.c_str(), path.c_str());
+    same.add(now_us() - b);
+  }
+  for (Acc* x : {&mk, &st, &wr, &ch, &cl, &rn, &whole, &rel, &same}) x->print();
   return 0;
 }

@@ -20,14 +20,6 @@ std::optional<std::string> lookup_env(const std::string& name, const std::map<st
   return std::string(v);
 }
 
-std::string type_name(FlagType t) {
-  switch (t) {
-    case FlagType::Bool: return "bool";
-    case FlagType::Duration: return "duration";
-    default: return "string";
-  }
-}
-
 void validate(const FlagDef& d, const std::string& v, const std::string& source) {
   if (d.type == FlagType::Bool && !str::parse_bool(v))
     throw UsageError("could not parse \"" + v + "\" as bool value from " + source + " for flag " + d.name +
@@ -158,14 +150,6 @@ Nanos Context::Duration(const std::string& name) const {
   }
 }
 
-std::vector<std::string> Context::Names(const std::string& name) const {
-  const FlagDef* d = find(name);
-  if (!d) return {};
-  std::vector<std::string> out{d->name};
-  out.insert(out.end(), d->aliases.begin(), d->aliases.end());
-  return out;
-}
-
 std::vector<FlagDef> gfd_flags() {
   using T = FlagType;
   return {
@@ -216,7 +200,6 @@ std::string help_text(const std::vector<FlagDef>& defs, const std::string& app_n
     std::vector<std::string> envs;
     for (const auto& e : d.env_vars) envs.push_back("$" + e);
     if (!envs.empty()) line += " [" + str::join(envs, ", ") + "]";
-    (void)type_name;
     out += line + "\n";
   }
   out += "   --help, -h\tshow help\n";

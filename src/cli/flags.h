@@ -57,8 +57,6 @@ class Context {
   std::string String(const std::string& name) const;
   bool Bool(const std::string& name) const;
   Nanos Duration(const std::string& name) const;
-  // Names (canonical + aliases) of a flag.
-  std::vector<std::string> Names(const std::string& name) const;
   const std::vector<FlagDef>& defs() const { return defs_; }
 
  private:

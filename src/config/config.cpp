@@ -36,9 +36,7 @@ std::string new_resource_name(const std::string& in) {
   if (n.size() > kMaxResourceNameLength)
     throw Error(str::format("fully-qualified resource name must be %zu characters or less: %s", kMaxResourceNameLength,
                             n.c_str()));
-  auto [prefix, name] = split_resource_name(n);
-  (void)prefix;
-  if (!is_dns1123_subdomain(name))
+  if (!is_dns1123_subdomain(split_resource_name(n).second))
     throw Error("incorrect format for resource name '" + n +
                 "': [a lowercase RFC 1123 subdomain must consist of lower case alphanumeric characters, '-' or '.', "
                 "and must start and end with an alphanumeric character]");
@@ -80,12 +78,12 @@ int to_int(const Node& n, const std::string& path) {
 }
 
 // Duration: a Go duration string or a number of nanoseconds (duration.go:36-53).
-std::optional<Nanos> opt_duration(const Node* n, const std::string& path) {
+// The reference's error names no field (duration.go:50), so neither does this.
+std::optional<Nanos> opt_duration(const Node* n, const std::string& /*path*/) {
   if (!n || n->is_null()) return std::nullopt;
   if (n->kind() == Node::Kind::Int) return static_cast<Nanos>(n->as_int());
   if (n->kind() == Node::Kind::Float) return static_cast<Nanos>(n->as_float());
   if (n->kind() == Node::Kind::String) return parse_duration(n->text());
-  (void)path;
   throw Error("invalid duration");
 }
 

@@ -78,7 +78,7 @@ int to_int(const Node& n, const std::string& path) {
 }
 
 // Duration: a Go duration string or a number of nanoseconds (duration.go:36-53).
-// The reference's error names no field (duration.go:50), so neither does this.
+// The reference's error names no field (vendored api/config/v1/duration.go:51).
 std::optional<Nanos> opt_duration(const Node* n, const std::string& /*path*/) {
   if (!n || n->is_null()) return std::nullopt;
   if (n->kind() == Node::Kind::Int) return static_cast<Nanos>(n->as_int());

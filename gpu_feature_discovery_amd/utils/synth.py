@@ -6,7 +6,11 @@ MI355X pool (verified by tools/probe_box.sh; see profiles/hw_probe.md):
 
 * ``sys/class/kfd/kfd/topology/nodes/N/properties`` and ``mem_banks`` - one
   node per CPU socket, then one node per GPU (SPX) or per compute partition
-  (DPX/QPX/CPX: 2/4/8 nodes sharing the GPU's PCI location),
+  (DPX/QPX/CPX: 2/4/8 nodes).  A partition node's ``location_id`` follows
+  ``NodeSpec.partition_layout``: ``"function"`` (upstream amdgpu on GC
+  9.4.3-class parts ORs the partition index into the PCI function bits, so
+  partition k of ``bb:00.0`` reports ``bb:00.k``) or ``"shared"`` (older
+  kernels: every partition reports the parent's location),
 * ``sys/bus/pci/devices/<bdf>/...`` - product name, partition modes, VRAM,
   xGMI link table, SR-IOV attributes, configuration space,
 * ``sys/module/amdgpu/version``, ``sys/class/dmi/id/product_name``.
@@ -53,6 +57,9 @@ class GpuSpec:
     # True: this GPU is an SR-IOV virtual function handed to a guest VM (VF
     # device ID, no SR-IOV capability of its own, no physfn link).
     vf: bool = False
+    # Partition indices whose KFD nodes the container may read (None: all),
+    # e.g. [3] for a pod that was allocated one CPX partition.
+    visible_partitions: list[int] | None = None
 
 
 @dataclass
@@ -66,6 +73,8 @@ class NodeSpec:
     seed: int = 0
     hive_size: int = 8  # GPUs per xGMI hive (MI355X platforms: 8)
     hypervisor: bool = False  # CPU "hypervisor" flag (running inside a VM)
+    partition_layout: str = "function"  # "function" | "shared" (see module docstring)
+    rocm_version_file: bool = True  # write opt/rocm/.info/version
 
 
 def _write(path: Path, text: str | bytes) -> None:
@@ -158,7 +167,10 @@ def make_node(root: str | os.PathLike, spec: NodeSpec) -> Path:
     topo = root / "sys/class/kfd/kfd/topology"
     _write(topo / "generation_id", "1\n")
     _write(root / "sys/module/amdgpu/version", spec.driver_version + "\n")
-    _write(root / "opt/rocm/.info/version", spec.rocm_version + "\n")
+    if spec.partition_layout not in ("function", "shared"):
+        raise ValueError(f"unknown partition_layout {spec.partition_layout!r}")
+    if spec.rocm_version_file:
+        _write(root / "opt/rocm/.info/version", spec.rocm_version + "\n")
     _write(root / "sys/class/dmi/id/product_name", spec.machine + "\n")
     flags = "fpu vme de pse tsc msr pae mce cx8 apic sep mtrr" + (" hypervisor" if spec.hypervisor else "") + " lahf_lm"
     _write(root / "proc/cpuinfo", "processor\t: 0\nvendor_id\t: AuthenticAMD\nmodel name\t: AMD EPYC 9575F 64-Core "
@@ -186,12 +198,14 @@ def make_node(root: str | os.PathLike, spec: NodeSpec) -> Path:
         node_mem = g.vram_bytes // parts
         for p in range(parts):
             ndir = topo / f"nodes/{node}"
-            if g.hidden:
+            # kfd_topology.c: location_id = pci_dev_id | xcp node id.
+            node_location = location | p if spec.partition_layout == "function" and parts > 1 else location
+            if g.hidden or (g.visible_partitions is not None and p not in g.visible_partitions):
                 # Unreadable: the kernel returns EPERM; a directory named
                 # `properties` makes every read fail the same way (EISDIR).
                 (ndir / "properties").mkdir(parents=True, exist_ok=True)
             else:
-                _write(ndir / "properties", _kfd_properties(g, parts, location, render, unique, xcc))
+                _write(ndir / "properties", _kfd_properties(g, parts, node_location, render, unique, xcc))
                 _write(ndir / "mem_banks/0/properties", f"heap_type 1\nsize_in_bytes {node_mem}\nflags 0\nwidth 8192\n")
                 _write(ndir / "gpu_id", f"{rng.randint(1000, 65535)}\n")
             node += 1

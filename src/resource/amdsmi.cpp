@@ -10,6 +10,7 @@
 #include <mutex>
 
 #include "resource/pci_ids.h"
+#include "resource/physical.h"
 #include "resource/versions.h"
 #include "util/dynlib.h"
 #include "util/error.h"
@@ -174,7 +175,9 @@ bool is_stale(amdsmi_status_t st) { return st == AMDSMI_STATUS_NOT_INIT || st ==
 // Raw per-processor facts (one amd-smi processor = a GPU or a partition).
 struct ProcInfo {
   amdsmi_processor_handle h = nullptr;
-  std::string bdf;
+  std::string bdf;      // as amd-smi reports it (a partition's may carry its index)
+  std::string gpu_bdf;  // parent PCI function of its physical GPU (GPU-wide attributes)
+  bool identified = false;  // query_identity ran this cycle
   std::string market_name;
   uint32_t vendor_id = 0;
   uint32_t device_id = 0;
@@ -264,6 +267,7 @@ uint32_t kfd_num_xcc(const std::string& root, uint32_t node_id) {
 // Identity of a processor from its ASIC info (the library caches it after
 // the first call: ~2 us).
 void query_identity(AmdSmiLib& L, ProcInfo& p) {
+  if (p.identified) return;
   amdsmi_asic_info_t asic;
   std::memset(&asic, 0, sizeof(asic));
   amdsmi_status_t st = AMDSMI_CALL("asic_info", L.get_gpu_asic_info(p.h, &asic));
@@ -280,13 +284,14 @@ void query_identity(AmdSmiLib& L, ProcInfo& p) {
   if (serial_hex.size() > 2 && serial_hex[0] == '0' && (serial_hex[1] == 'x' || serial_hex[1] == 'X'))
     serial_hex.erase(0, 2);
   if (auto serial = str::parse_uint(serial_hex, 16)) p.uuid = amd_uuid(*serial, p.device_id);
+  p.identified = true;
 }
 
 void fix_market_name(AmdSmiLib& L, const std::string& root, ProcInfo& p) {
   if (!is_generic_name(p.market_name)) return;
   // The board FRU product name: amdgpu publishes it in sysfs (~5 us); the
   // amd-smi board-info call returns the same string for ~155 us.
-  auto v = fs::attrs().read_trimmed(fs::join(root, "sys/bus/pci/devices/" + p.bdf + "/product_name"));
+  auto v = fs::attrs().read_trimmed(fs::join(root, "sys/bus/pci/devices/" + p.gpu_bdf + "/product_name"));
   if (v && !is_generic_name(*v)) {
     p.market_name = *v;
   } else if (L.get_gpu_board_info) {
@@ -328,7 +333,7 @@ constexpr uint32_t kNoNode = 0xFFFFFFFFu;
 // partitioned or an attribute is missing; the caller then queries amd-smi.
 bool query_unpartitioned(AmdSmiLib& L, const std::string& root, ProcInfo& p, AmdSmiManager::KfdNodeFacts* kfd) {
   uint32_t* node_id = &kfd->node_id;
-  std::string pci = fs::join(root, "sys/bus/pci/devices/" + p.bdf);
+  std::string pci = fs::join(root, "sys/bus/pci/devices/" + p.gpu_bdf);
   auto cp = AMDSMI_CALL("compute_partition(sysfs)", fs::attrs().read_trimmed(pci + "/current_compute_partition"));
   if (!cp || *cp != "SPX") return false;
   auto mp = AMDSMI_CALL("memory_partition(sysfs)", fs::attrs().read_trimmed(pci + "/current_memory_partition"));
@@ -403,7 +408,7 @@ int sysfs_xgmi_links(const std::string& root, const std::string& bdf) {
 // GPU-level capabilities: xGMI links, virtualization mode, supported
 // partition modes.  Any processor handle of the GPU will do.
 void query_gpu_caps(AmdSmiLib& L, const ProcInfo& p, const std::string& root, GpuExtras& x) {
-  x.xgmi_links = AMDSMI_CALL("xgmi_num_links(sysfs)", sysfs_xgmi_links(root, p.bdf));
+  x.xgmi_links = AMDSMI_CALL("xgmi_num_links(sysfs)", sysfs_xgmi_links(root, p.gpu_bdf));
   if (x.xgmi_links < 0 && L.get_gpu_xgmi_link_status) {
     amdsmi_xgmi_link_status_t ls;
     std::memset(&ls, 0, sizeof(ls));
@@ -423,7 +428,7 @@ void query_gpu_caps(AmdSmiLib& L, const ProcInfo& p, const std::string& root, Gp
   // Supported memory partition modes: world-readable in sysfs (~5 us);
   // the amd-smi partition-config call (~25 us) only as a fallback.
   if (auto v = AMDSMI_CALL("available_memory_partition(sysfs)",
-                           fs::attrs().read_trimmed(fs::join(root, "sys/bus/pci/devices/" + p.bdf + "/available_memory_partition")))) {
+                           fs::attrs().read_trimmed(fs::join(root, "sys/bus/pci/devices/" + p.gpu_bdf + "/available_memory_partition")))) {
     for (auto& m : str::split(*v, ','))
       if (!str::trim(m).empty()) x.available_memory.push_back(str::trim(m));
   } else if (L.get_gpu_memory_partition_config) {
@@ -445,7 +450,7 @@ void query_gpu_caps(AmdSmiLib& L, const ProcInfo& p, const std::string& root, Gp
   }
   if (x.available_compute.empty()) {
     auto v = AMDSMI_CALL("available_compute_partition(sysfs)",
-                         fs::attrs().read_trimmed(fs::join(root, "sys/bus/pci/devices/" + p.bdf + "/available_compute_partition")));
+                         fs::attrs().read_trimmed(fs::join(root, "sys/bus/pci/devices/" + p.gpu_bdf + "/available_compute_partition")));
     if (v)
       for (auto& m : str::split(*v, ','))
         if (!str::trim(m).empty()) x.available_compute.push_back(str::trim(m));
@@ -494,6 +499,7 @@ void AmdSmiManager::library_init() {
   lib_initialized_ = true;
   virt_mode_.clear();
   kfd_node_.clear();
+  parent_bdf_.clear();
   ++init_count_;
 }
 
@@ -569,8 +575,10 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
     sockets.resize(ns);
   }
 
-  // Collect GPU processors, grouped by PCI address.
-  std::map<std::string, std::vector<ProcInfo>> groups;
+  // Collect GPU processors by PCI slot (domain:bus:device - amd-smi's own
+  // socket id, the same for every partition of a GPU under both KFD
+  // location layouts; resource/physical.h).
+  std::map<std::string, std::vector<ProcInfo>> slots;
   for (auto s : sockets) {
     uint32_t np = 0;
     st = L.get_processor_handles(s, &np, nullptr);
@@ -591,13 +599,47 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
       ProcInfo p;
       p.h = h;
       p.bdf = format_bdf(b);
-      groups[p.bdf].push_back(p);
+      slots[bdf_slot(p.bdf)].push_back(p);
     }
   }
 
+  // Split slots into physical GPUs.  One processor: a GPU (the hot path, no
+  // further calls).  Several: the partitions of one GPU when they share the
+  // ASIC serial and the family puts partitions on one slot; otherwise
+  // distinct GPUs that happen to share a slot (e.g. ARI virtual functions).
+  std::vector<std::vector<ProcInfo>> physical;
+  for (auto& [slot, procs] : slots) {
+    if (procs.size() == 1) {
+      physical.push_back(std::move(procs));
+      continue;
+    }
+    std::map<std::string, std::vector<ProcInfo>> by_gpu;
+    for (auto& p : procs) {
+      query_identity(L, p);
+      bool partitions = partition_index_in_function_bits(gfx_target_from_amdsmi(p.gfx));
+      by_gpu[partitions ? "serial:" + p.uuid : "bdf:" + p.bdf].push_back(std::move(p));
+    }
+    for (auto& [key, members] : by_gpu) physical.push_back(std::move(members));
+  }
+  // Parent PCI function of each GPU, resolved once per session.
+  for (auto& procs : physical) {
+    std::vector<std::string> bdfs;
+    for (const auto& p : procs) bdfs.push_back(p.bdf);
+    std::string key = str::join(bdfs, ",");
+    auto it = parent_bdf_.find(key);
+    if (it == parent_bdf_.end()) {
+      uint32_t device_id = 0;
+      if (procs.size() > 1) device_id = procs.front().device_id;  // identified above
+      it = parent_bdf_.emplace(key, resolve_parent_bdf(opts_.root, bdfs, device_id)).first;
+    }
+    for (auto& p : procs) p.gpu_bdf = it->second;
+  }
+  std::sort(physical.begin(), physical.end(),
+            [](const std::vector<ProcInfo>& a, const std::vector<ProcInfo>& b) { return a[0].gpu_bdf < b[0].gpu_bdf; });
+
   trace::record("amdsmi.handles", trace::now_ns() - handles_t0);
 
-  // Apply the visible-device filter on physical GPUs (index = BDF order).
+  // Apply the visible-device filter on physical GPUs (index = parent BDF order).
   struct Gpu {
     int index = 0;
     std::string bdf;
@@ -608,14 +650,13 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
     KfdNodeFacts kfd;  // session cache entry (unpartitioned GPUs)
   };
   std::vector<Gpu> gpus;
-  int index = -1;
-  for (auto& [bdf, procs] : groups) {
-    ++index;
-    if (opts_.filter.matches(index, bdf)) {
+  for (size_t i = 0; i < physical.size(); ++i) {
+    const std::string& bdf = physical[i][0].gpu_bdf;
+    if (opts_.filter.matches(static_cast<int>(i), bdf)) {
       Gpu g;
-      g.index = index;
+      g.index = static_cast<int>(i);
       g.bdf = bdf;
-      g.procs = &procs;
+      g.procs = &physical[i];
       gpus.push_back(std::move(g));
       auto v = virt_mode_.find(bdf);
       if (v != virt_mode_.end()) gpus.back().extras.virtualization = v->second;
@@ -720,7 +761,7 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
       if (!partitioned) continue;
       DeviceInfo pi;
       pi.partition_id = static_cast<int>(p.partition_id);
-      pi.bdf = g.bdf;
+      pi.bdf = p.bdf;
       pi.uuid = p.uuid;
       pi.vendor_id = p.vendor_id;
       pi.device_id = p.device_id;

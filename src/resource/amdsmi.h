@@ -20,8 +20,10 @@
 //   * an unpartitioned (SPX) GPU's per-cycle values come straight from the
 //     sysfs attributes the library would read for them (GFD_AMDSMI_SYSFS=0
 //     turns this off); partitioned GPUs are queried through amd-smi.
-//   * compute partitions (DPX/QPX/CPX) are separate amd-smi processors that
-//     share a PCI address; they are regrouped into parent GPUs by BDF.
+//   * compute partitions (DPX/QPX/CPX) are separate amd-smi processors on
+//     one PCI slot (their function bits may carry the partition index); they
+//     are regrouped into parent GPUs by slot and ASIC serial
+//     (resource/physical.h).
 #pragma once
 
 #include <cstdint>
@@ -98,6 +100,10 @@ class AmdSmiManager : public Manager {
   // ~1 us each through kept-open descriptors instead of 11-18 us per
   // library call.
   std::map<std::string, KfdNodeFacts> kfd_node_;
+  // Parent PCI function of each physical GPU (key: its processors' BDFs),
+  // for the lifetime of one session: processor addresses and PCI functions
+  // only change with a driver reload or partition switch, which re-initialise.
+  std::map<std::string, std::string> parent_bdf_;
 };
 
 }  // namespace gfd::resource

@@ -1,0 +1,37 @@
+#include "resource/physical.h"
+
+#include <algorithm>
+
+#include "util/fs.h"
+#include "util/strings.h"
+
+namespace gfd::resource {
+
+bool partition_index_in_function_bits(const GfxTarget& t) { return t.major == 9 && t.minor >= 4; }
+
+std::string bdf_slot(const std::string& bdf) {
+  auto dot = bdf.rfind('.');
+  return dot == std::string::npos ? bdf : bdf.substr(0, dot);
+}
+
+std::string resolve_parent_bdf(const std::string& root, std::vector<std::string> member_bdfs, uint32_t device_id) {
+  if (member_bdfs.empty()) return "";
+  std::sort(member_bdfs.begin(), member_bdfs.end());
+  member_bdfs.erase(std::unique(member_bdfs.begin(), member_bdfs.end()), member_bdfs.end());
+  std::vector<std::string> candidates = member_bdfs;
+  std::string fn0 = bdf_slot(member_bdfs.front()) + ".0";
+  if (std::find(candidates.begin(), candidates.end(), fn0) == candidates.end()) candidates.push_back(fn0);
+  for (const auto& c : candidates) {
+    // Read once per topology (callers cache the result), so a plain read.
+    auto dev = fs::read_trimmed(fs::join(root, "sys/bus/pci/devices/" + c + "/device"));
+    if (!dev) continue;
+    std::string hex = *dev;
+    if (hex.size() > 2 && hex[0] == '0' && (hex[1] == 'x' || hex[1] == 'X')) hex.erase(0, 2);
+    auto id = str::parse_uint(hex, 16);
+    if (!id) continue;
+    if (device_id == 0 || *id == device_id) return c;
+  }
+  return member_bdfs.front();
+}
+
+}  // namespace gfd::resource

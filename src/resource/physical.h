@@ -1,0 +1,49 @@
+// Physical-GPU identity of KFD nodes and amd-smi processors.
+//
+// Reference analogue: the MIG parent/child walk (internal/mig/mig.go:41-124,
+// internal/resource/nvml-mig-device.go:27-134, go-nvlib
+// nvlib/device/device.go:91-118), where NVML hands out MIG devices as
+// children of their parent's handle.  Neither amd-smi nor KFD has such a
+// parent link for compute partitions (XCPs): each partition is a KFD node /
+// amd-smi processor of its own, so the backends regroup them.
+//
+// What identifies the physical GPU of a partition (upstream amdgpu,
+// kfd_topology.c): on GC 9.4.3-class parts (gfx94x, gfx950) KFD sets
+//     location_id = pci_dev_id(parent) | xcp node_id
+// i.e. partition k of a GPU at dddd:bb:00.0 reports dddd:bb:00.k, and
+// amd-smi (which takes its BDF from the KFD node) reports the same.  Older
+// kernels report the parent's location for every partition.  Domain, bus
+// and device number (amd-smi's own "socket id") and the ASIC serial
+// (KFD unique_id, amd-smi asic_serial) are the same for every partition
+// under both layouts, so they are the grouping key; the function bits are
+// ignored for partition-capable families only.  The parent PCI function -
+// where amdgpu publishes the GPU-wide attributes (current_compute_partition,
+// mem_info_vram_total, xgmi_num_links, ...) - is then the lowest member
+// address that is a PCI function of the same device ID (partition 0 reports
+// it exactly), else the address with the function bits cleared.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "resource/types.h"
+
+namespace gfd::resource {
+
+// True for ASIC families whose partitions carry their index in the PCI
+// function bits (gfx 9.4.x, 9.5.x: MI300, MI325, MI350/MI355).
+bool partition_index_in_function_bits(const GfxTarget& t);
+
+// "dddd:bb:dd.f" -> "dddd:bb:dd" (amd-smi's socket id of the function).
+std::string bdf_slot(const std::string& bdf);
+
+// Parent PCI function of a physical GPU whose members (partitions, or the
+// GPU itself) report `member_bdfs`.  `device_id` 0 accepts any device.
+// Candidates: the member addresses in ascending order, then the slot's
+// function 0; the first with <root>/sys/bus/pci/devices/<bdf>/device equal
+// to `device_id` wins.  Without a readable PCI tree (or no match) the lowest
+// member address is returned.
+std::string resolve_parent_bdf(const std::string& root, std::vector<std::string> member_bdfs, uint32_t device_id);
+
+}  // namespace gfd::resource

@@ -3,8 +3,10 @@
 #include <algorithm>
 #include <cerrno>
 #include <map>
+#include <tuple>
 
 #include "resource/pci_ids.h"
+#include "resource/physical.h"
 #include "resource/versions.h"
 #include "util/error.h"
 #include "util/fs.h"
@@ -195,6 +197,8 @@ std::vector<DevicePtr> SysfsManager::GetDevices() {
 }
 
 // One physical GPU (and its partitions) from its KFD nodes and PCI attributes.
+// `bdf` is the parent PCI function (see resource/physical.h): every GPU-wide
+// attribute is read there, whichever addresses the partitions report.
 static DevicePtr describe_gpu(const std::string& root, bool in_vm, int index, const std::string& bdf,
                               const std::vector<const KfdNode*>& members, bool has_physfn) {
   const KfdNode& first = *members.front();
@@ -240,7 +244,7 @@ static DevicePtr describe_gpu(const std::string& root, bool in_vm, int index, co
     if (!partitioned) continue;
     DeviceInfo pi;
     pi.partition_id = static_cast<int>(p);
-    pi.bdf = bdf;
+    pi.bdf = bdf_of(n);
     pi.vendor_id = info.vendor_id;
     pi.device_id = info.device_id;
     pi.compute_units = pcus;
@@ -273,11 +277,15 @@ static DevicePtr describe_gpu(const std::string& root, bool in_vm, int index, co
 }
 
 struct SysfsManager::Topology {
-  std::vector<KfdNode> nodes;                              // accessible GPU nodes, by node id
-  std::map<std::string, std::vector<const KfdNode*>> groups;  // by BDF (ordered)
-  // A `physfn` link (the function is an SR-IOV VF), fixed when the PCI
-  // function is created - looked up here, not with a path walk per cycle.
-  std::map<std::string, bool> has_physfn;
+  std::vector<KfdNode> nodes;  // accessible GPU nodes, by node id
+  struct Gpu {
+    std::string bdf;                       // parent PCI function
+    std::vector<const KfdNode*> members;   // its partitions' nodes, by node id
+    // A `physfn` link (the function is an SR-IOV VF), fixed when the PCI
+    // function is created - looked up here, not with a path walk per cycle.
+    bool has_physfn = false;
+  };
+  std::vector<Gpu> gpus;  // ordered by parent BDF (the enumeration index)
 };
 
 std::shared_ptr<const SysfsManager::Topology> SysfsManager::read_topology() const {
@@ -311,10 +319,31 @@ std::shared_ptr<const SysfsManager::Topology> SysfsManager::read_topology() cons
     if (usable[i]) topo->nodes.push_back(std::move(nodes[i]));
   std::sort(topo->nodes.begin(), topo->nodes.end(), [](const KfdNode& a, const KfdNode& b) { return a.id < b.id; });
 
-  // 2. Group partitions by PCI location (partitions share the parent's BDF).
-  for (const auto& n : topo->nodes) topo->groups[bdf_of(n)].push_back(&n);
-  for (const auto& g : topo->groups)
-    topo->has_physfn[g.first] = fs::exists(fs::join(opts_.root, "sys/bus/pci/devices/" + g.first + "/physfn"));
+  // 2. Group partitions by physical GPU: (domain, location, unique_id), with
+  //    the PCI function bits - where partition-capable parts put the
+  //    partition index - masked (resource/physical.h).
+  struct Key {
+    uint64_t domain, location, unique_id;
+    bool operator<(const Key& o) const {
+      return std::tie(domain, location, unique_id) < std::tie(o.domain, o.location, o.unique_id);
+    }
+  };
+  std::map<Key, std::vector<const KfdNode*>> groups;
+  for (const auto& n : topo->nodes) {
+    bool masked = partition_index_in_function_bits(gfx_target_from_kfd(n.gfx_target_version));
+    groups[Key{n.domain, masked ? (n.location_id & ~uint64_t{7}) : n.location_id, n.unique_id}].push_back(&n);
+  }
+  for (auto& [key, members] : groups) {
+    std::vector<std::string> bdfs;
+    for (const auto* n : members) bdfs.push_back(bdf_of(*n));
+    Topology::Gpu g;
+    g.bdf = resolve_parent_bdf(opts_.root, bdfs, static_cast<uint32_t>(members.front()->device_id));
+    g.members = std::move(members);
+    g.has_physfn = fs::exists(fs::join(opts_.root, "sys/bus/pci/devices/" + g.bdf + "/physfn"));
+    topo->gpus.push_back(std::move(g));
+  }
+  std::sort(topo->gpus.begin(), topo->gpus.end(),
+            [](const Topology::Gpu& a, const Topology::Gpu& b) { return a.bdf < b.bdf; });
   return topo;
 }
 
@@ -328,32 +357,27 @@ std::vector<DevicePtr> SysfsManager::enumerate() {
     cached_ = generation_.empty() ? nullptr : topo;
     cached_generation_ = generation_;
   }
-  const auto& groups = topo->groups;
 
   // 3. Describe each visible physical GPU (~10 sysfs reads each), in
   //    parallel across GPUs.
-  struct Gpu {
-    int index;
-    const std::string* bdf;
-    const std::vector<const KfdNode*>* members;
-  };
-  std::vector<Gpu> visible;
-  int index = -1;
-  for (const auto& [bdf, members] : groups) {
-    ++index;
-    if (opts_.filter.matches(index, bdf)) visible.push_back(Gpu{index, &bdf, &members});
-  }
+  std::vector<std::pair<int, const Topology::Gpu*>> visible;
+  for (size_t i = 0; i < topo->gpus.size(); ++i)
+    if (opts_.filter.matches(static_cast<int>(i), topo->gpus[i].bdf))
+      visible.emplace_back(static_cast<int>(i), &topo->gpus[i]);
   std::vector<DevicePtr> out(visible.size());
   trace::Span span("sysfs.gpus");
   // Unpartitioned GPUs: ~10 attribute preads each, two GPUs per lane (see
   // AmdSmiManager::snapshot); partitioned ones also list and read each
   // partition node's memory banks, one GPU per lane.
   bool any_partitioned = false;
-  for (const auto& g : visible) any_partitioned |= g.members->size() > 1;
+  for (const auto& v : visible) any_partitioned |= v.second->members.size() > 1;
   size_t lanes = gpu_lanes(visible.size(), !any_partitioned);
   WorkerPool::instance().parallel_for(
-      visible.size(), [&](size_t i) { out[i] = describe_gpu(opts_.root, in_vm_, visible[i].index, *visible[i].bdf, *visible[i].members,
-                                                              topo->has_physfn.at(*visible[i].bdf)); },
+      visible.size(),
+      [&](size_t i) {
+        const Topology::Gpu& g = *visible[i].second;
+        out[i] = describe_gpu(opts_.root, in_vm_, visible[i].first, g.bdf, g.members, g.has_physfn);
+      },
       lanes);
   return out;
 }

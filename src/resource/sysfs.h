@@ -48,7 +48,7 @@ class SysfsManager : public Manager {
   // Enumerate without the Init/Shutdown protocol (used by GetDevices).
   std::vector<DevicePtr> enumerate();
 
-  // GPU nodes of one KFD topology generation, grouped by PCI address.
+  // GPU nodes of one KFD topology generation, grouped by physical GPU.
   struct Topology;
 
  private:

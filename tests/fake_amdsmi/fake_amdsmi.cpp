@@ -3,12 +3,21 @@
 //
 // The node is described by fake_amdsmi_configure(spec), one GPU per line:
 //   bdf=0000:23:00.0;mode=CPX;parts=8;name=AMD Instinct MI355 OAM;cus=32;xcds=1;vram_mib=36862;links=7;virt=1
+// (optional per GPU: serial=<hex asic serial>; visible=3,5 - only those
+// partitions are reported, like a pod allocated part of a GPU)
 // plus optional global lines:
 //   init_status=34            amdsmi_init returns this status
 //   stale_after=N             after N successful queries, queries return NOT_INIT until re-init
 //   fail=<function>:<status>  that amd-smi function returns <status> for
 //                             every device (repeatable), e.g.
 //                             fail=amdsmi_get_gpu_memory_total:2
+//   partition_bdf=function    partition p of a GPU at dddd:bb:dd.0 reports
+//                             function p (upstream amdgpu on GC 9.4.3-class
+//                             parts; the default) - or `shared`: every
+//                             partition reports the parent's BDF (older kernels)
+//   sockets=slot              one socket per PCI slot, i.e. per physical GPU
+//                             (what amd-smi does; the default) - or `one`: a
+//                             single socket holding every processor
 //   latency_us=N              every device query except handle-table lookups
 //                             (processor type, BDF, ASIC info) busy-waits N us
 //                             holding that GPU's lock (amd-smi serialises per
@@ -19,8 +28,10 @@
 #include <amd_smi/amdsmi.h>
 
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <map>
@@ -34,6 +45,7 @@ namespace {
 
 struct Proc {
   std::string bdf;
+  std::string gpu;  // BDF of the physical GPU (its per-device lock)
   uint64_t domain = 0;
   uint32_t bus = 0, dev = 0, fn = 0;
   std::string mode = "SPX";
@@ -46,6 +58,7 @@ struct Proc {
   uint64_t vram = 309220868096ULL;
   int links = 7;
   int virt = AMDSMI_VIRTUALIZATION_MODE_BAREMETAL;
+  std::string serial;  // asic_serial ("" = derived from the bus)
 };
 
 struct State {
@@ -62,6 +75,9 @@ struct State {
   long latency_us = 0;
   std::map<std::string, std::unique_ptr<std::mutex>> device_mu;  // by BDF
   std::map<std::string, int> fail;                               // function -> status
+  bool partition_fn = true;   // partition_bdf=function
+  bool socket_per_slot = true;  // sockets=slot
+  std::vector<std::vector<uint32_t>> sockets;  // processor indices per socket
 };
 
 State& S() {
@@ -106,7 +122,7 @@ amdsmi_status_t check(amdsmi_processor_handle h, Proc** out, bool cheap = false,
     auto f = s.fail.find(fn);
     if (f != s.fail.end()) return static_cast<amdsmi_status_t>(f->second);
     latency = s.latency_us;
-    if (latency > 0 && !cheap) dev = s.device_mu[(*out)->bdf].get();
+    if (latency > 0 && !cheap) dev = s.device_mu[(*out)->gpu].get();
   }
   if (dev) {
     // Like amd-smi's per-device mutex around its sysfs/ioctl work.
@@ -138,6 +154,9 @@ int fake_amdsmi_configure(const char* spec) {
   s.fail.clear();
   s.queries = 0;
   s.stale = false;
+  s.partition_fn = true;
+  s.socket_per_slot = true;
+  s.sockets.clear();
   std::istringstream in(spec);
   std::string line;
   while (std::getline(in, line)) {
@@ -156,12 +175,21 @@ int fake_amdsmi_configure(const char* spec) {
       s.fail[line.substr(5, colon - 5)] = std::atoi(line.c_str() + colon + 1);
       continue;
     }
+    if (line.rfind("partition_bdf=", 0) == 0) {
+      s.partition_fn = line.substr(14) == "function";
+      continue;
+    }
+    if (line.rfind("sockets=", 0) == 0) {
+      s.socket_per_slot = line.substr(8) == "slot";
+      continue;
+    }
     if (line.rfind("latency_us=", 0) == 0) {
       s.latency_us = std::atol(line.c_str() + 11);
       continue;
     }
     Proc base;
     int parts = 1;
+    std::vector<int> visible;  // partitions the process may see (empty: all)
     // key=value pairs separated by ';' (values may contain spaces).
     std::vector<std::pair<std::string, std::string>> kv;
     std::istringstream fields(line);
@@ -184,14 +212,40 @@ int fake_amdsmi_configure(const char* spec) {
       else if (k == "vram_mib") base.vram = std::strtoull(v.c_str(), nullptr, 10) << 20;
       else if (k == "links") base.links = std::atoi(v.c_str());
       else if (k == "virt") base.virt = std::atoi(v.c_str());
+      else if (k == "serial") base.serial = v;
+      else if (k == "visible") {
+        std::istringstream ids(v);
+        std::string id;
+        while (std::getline(ids, id, ',')) visible.push_back(std::atoi(id.c_str()));
+      }
     }
     // Enumerate partitions in reverse to prove the backend orders them.
     for (int p = parts - 1; p >= 0; --p) {
+      if (!visible.empty() && std::find(visible.begin(), visible.end(), p) == visible.end()) continue;
       Proc q = base;
+      q.gpu = base.bdf;
       q.partition_id = static_cast<uint32_t>(p);
-      if (!s.device_mu.count(q.bdf)) s.device_mu[q.bdf] = std::make_unique<std::mutex>();
+      if (parts > 1 && s.partition_fn) {
+        // kfd_topology.c: location_id = pci_dev_id | xcp node id.
+        q.fn = base.fn | static_cast<uint32_t>(p);
+        char buf[32];
+        snprintf(buf, sizeof(buf), "%04llx:%02x:%02x.%x", static_cast<unsigned long long>(q.domain), q.bus, q.dev, q.fn);
+        q.bdf = buf;
+      }
+      if (!s.device_mu.count(base.bdf)) s.device_mu[base.bdf] = std::make_unique<std::mutex>();
       s.procs.push_back(q);
     }
+  }
+  // amd-smi's socket id is domain:bus:device (one socket per physical GPU).
+  std::map<std::string, size_t> slot_socket;
+  for (uint32_t i = 0; i < s.procs.size(); ++i) {
+    std::string slot = s.socket_per_slot ? s.procs[i].bdf.substr(0, s.procs[i].bdf.rfind('.')) : "";
+    auto it = slot_socket.find(slot);
+    if (it == slot_socket.end()) {
+      it = slot_socket.emplace(slot, s.sockets.size()).first;
+      s.sockets.emplace_back();
+    }
+    s.sockets[it->second].push_back(i);
   }
   return 0;
 }
@@ -233,17 +287,23 @@ amdsmi_status_t amdsmi_status_code_to_string(amdsmi_status_t status, const char*
 amdsmi_status_t amdsmi_get_socket_handles(uint32_t* count, amdsmi_socket_handle* handles) {
   auto& s = S();
   if (!s.initialized) return AMDSMI_STATUS_NOT_INIT;
-  if (handles && *count >= 1) handles[0] = reinterpret_cast<amdsmi_socket_handle>(1);
-  *count = 1;
+  uint32_t n = static_cast<uint32_t>(s.sockets.size());
+  if (handles)
+    for (uint32_t i = 0; i < n && i < *count; ++i) handles[i] = reinterpret_cast<amdsmi_socket_handle>(uintptr_t(i + 1));
+  *count = n;
   return AMDSMI_STATUS_SUCCESS;
 }
 
-amdsmi_status_t amdsmi_get_processor_handles(amdsmi_socket_handle, uint32_t* count, amdsmi_processor_handle* handles) {
+amdsmi_status_t amdsmi_get_processor_handles(amdsmi_socket_handle sock, uint32_t* count, amdsmi_processor_handle* handles) {
   auto& s = S();
   if (!s.initialized) return AMDSMI_STATUS_NOT_INIT;
-  uint32_t n = static_cast<uint32_t>(s.procs.size());
+  uintptr_t si = reinterpret_cast<uintptr_t>(sock);
+  if (si == 0 || si > s.sockets.size()) return AMDSMI_STATUS_INVAL;
+  const auto& members = s.sockets[si - 1];
+  uint32_t n = static_cast<uint32_t>(members.size());
   if (handles)
-    for (uint32_t i = 0; i < n && i < *count; ++i) handles[i] = reinterpret_cast<amdsmi_processor_handle>(uintptr_t(i + 1));
+    for (uint32_t i = 0; i < n && i < *count; ++i)
+      handles[i] = reinterpret_cast<amdsmi_processor_handle>(uintptr_t(members[i] + 1));
   *count = n;
   return AMDSMI_STATUS_SUCCESS;
 }
@@ -278,7 +338,8 @@ amdsmi_status_t amdsmi_get_gpu_asic_info(amdsmi_processor_handle h, amdsmi_asic_
   // A 64-bit hex serial, here derived from the bus (the real library's
   // spelling of the prefix varies; both forms are exercised).
   copy(a->asic_serial, sizeof(a->asic_serial),
-       std::string(p->bus & 0x10 ? "0x" : "") + "3A7C178B7C5E" + std::string(p->bdf.substr(5, 2)) + "5C");
+       !p->serial.empty() ? p->serial
+                          : std::string(p->bus & 0x10 ? "0x" : "") + "3A7C178B7C5E" + p->gpu.substr(5, 2) + "5C");
   return AMDSMI_STATUS_SUCCESS;
 }
 

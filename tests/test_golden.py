@@ -152,8 +152,17 @@ def test_synthetic_spx_matches_regex_golden(binary, tmp_path):
     golden.check_regex_golden(text, TESTS / "expected-output.txt")
 
 
-def test_synthetic_cpx_single(binary, tmp_path):
-    root = synth.make_mi355x_node(tmp_path / "root", n_gpus=8, compute_partition="CPX", seed=5)
+# Partition layouts: current kernels report partition k of a GPU at bb:00.0
+# as bb:00.k in its KFD location_id (kfd_topology.c ORs the XCP node id in);
+# older ones give every partition the parent's location.  Both must produce
+# the same labels (resource/physical.h).
+LAYOUTS = ["function", "shared"]
+
+
+@pytest.mark.parametrize("layout", LAYOUTS)
+def test_synthetic_cpx_single(binary, tmp_path, layout):
+    root = synth.make_mi355x_node(tmp_path / "root", n_gpus=8, compute_partition="CPX", seed=5,
+                                  partition_layout=layout)
     text = _oneshot(binary, tmp_path, "--backend=sysfs", "--mig-strategy=single", sysfs_root=str(root))
     golden.check_byte_golden(text, GOLDEN / "synthetic-cpx-single.txt", UPDATE)
     labels = golden.parse_labels(text)
@@ -162,14 +171,73 @@ def test_synthetic_cpx_single(binary, tmp_path):
     assert labels["amd.com/gpu.compute-units"] == "32"
 
 
-def test_synthetic_dpx_nps2_mixed(binary, tmp_path):
+@pytest.mark.parametrize("layout", LAYOUTS)
+def test_synthetic_dpx_nps2_mixed(binary, tmp_path, layout):
     root = synth.make_mi355x_node(tmp_path / "root", n_gpus=4, compute_partition="DPX", memory_partition="NPS2",
-                                  seed=6)
+                                  seed=6, partition_layout=layout)
     text = _oneshot(binary, tmp_path, "--backend=sysfs", "--mig-strategy=mixed", sysfs_root=str(root))
     golden.check_byte_golden(text, GOLDEN / "synthetic-dpx-nps2-mixed.txt", UPDATE)
     labels = golden.parse_labels(text)
     assert labels["amd.com/partition-dpx.4xcd.144gb.count"] == "8"
     assert labels["amd.com/partition-dpx.4xcd.144gb.memory-partition"] == "NPS2"
+
+
+@pytest.mark.parametrize("layout", LAYOUTS)
+def test_two_gpu_cpx_single_and_mixed(binary, tmp_path, layout):
+    """Round-1 review reproduction: 2 GPUs in CPX, partition addresses with
+    the index in the function bits, must count 16 partitions, not 16 GPUs."""
+    root = synth.make_mi355x_node(tmp_path / "root", n_gpus=2, compute_partition="CPX", seed=11,
+                                  partition_layout=layout)
+    single = golden.parse_labels(_oneshot(binary, tmp_path, "--backend=sysfs", "--mig-strategy=single",
+                                          sysfs_root=str(root)))
+    assert single["amd.com/gpu.count"] == "16"
+    assert single["amd.com/gpu.product"] == "AMD-Instinct-MI355-OAM-PARTITION-cpx.1xcd.36gb"
+    assert single["amd.com/gpu.compute-partition"] == "CPX"
+    assert single["amd.com/gpu.xgmi.links"] == "7"
+    mixed = golden.parse_labels(_oneshot(binary, tmp_path, "--backend=sysfs", "--mig-strategy=mixed",
+                                         sysfs_root=str(root)))
+    assert mixed["amd.com/partition-cpx.1xcd.36gb.count"] == "16"
+    assert mixed["amd.com/gpu.count"] == "2"
+    assert mixed["amd.com/gpu.memory"] == str(synth.MI355X_VRAM_BYTES >> 20)
+    assert mixed["amd.com/gpu.compute-partition"] == "CPX"
+
+
+@pytest.mark.parametrize("layout", LAYOUTS)
+def test_one_visible_cpx_partition(binary, tmp_path, layout):
+    """A pod allocated one CPX partition: its KFD node reports bb:00.3 (not a
+    PCI function); the GPU-wide attributes come from bb:00.0."""
+    spec = synth.NodeSpec(gpus=[synth.GpuSpec(compute_partition="CPX", visible_partitions=[3])],
+                          partition_layout=layout, seed=12)
+    root = str(synth.make_node(tmp_path / "root", spec))
+    labels = golden.parse_labels(_oneshot(binary, tmp_path, "--backend=sysfs", "--mig-strategy=single",
+                                          sysfs_root=root))
+    assert labels["amd.com/gpu.count"] == "1"
+    assert labels["amd.com/gpu.product"] == "AMD-Instinct-MI355-OAM-PARTITION-cpx.1xcd.36gb"
+    assert labels["amd.com/gpu.compute-partition"] == "CPX"
+    assert labels["amd.com/gpu.memory-partition"] == "NPS1"
+    assert labels["amd.com/gpu.partition.capable"] == "true"
+
+
+def test_partitions_of_other_families_keep_exact_addresses(binary, tmp_path):
+    """Function-bit masking applies to partition-capable families (gfx94x,
+    gfx950) only: two gfx90a GPUs that are functions of one slot stay two GPUs."""
+    gpus = [synth.GpuSpec(gfx_target_version=90010, product_name="AMD Instinct MI250X", cus=104, xcds=1)
+            for _ in range(2)]
+    root = synth.make_node(tmp_path / "root", synth.NodeSpec(gpus=gpus, seed=13))
+    kfd = root / "sys/class/kfd/kfd/topology/nodes"
+    # Move the second GPU onto function 1 of the first GPU's slot.
+    props = [kfd / d / "properties" for d in sorted(os.listdir(kfd), key=int)]
+    gpu_props = [p for p in props if "simd_count 0\n" not in p.read_text()]
+    first_loc = int(next(ln.split()[1] for ln in gpu_props[0].read_text().splitlines() if ln.startswith("location_id")))
+    text = gpu_props[1].read_text()
+    old_loc = next(ln for ln in text.splitlines() if ln.startswith("location_id"))
+    text = text.replace(old_loc, f"location_id {first_loc | 1}")
+    # ... and with the same (e.g. unreported) unique_id, so only the address tells them apart.
+    first_uid = next(ln for ln in gpu_props[0].read_text().splitlines() if ln.startswith("unique_id"))
+    old_uid = next(ln for ln in text.splitlines() if ln.startswith("unique_id"))
+    gpu_props[1].write_text(text.replace(old_uid, first_uid))
+    labels = golden.parse_labels(_oneshot(binary, tmp_path, "--backend=sysfs", sysfs_root=str(root)))
+    assert labels["amd.com/gpu.count"] == "2"
 
 
 def test_synthetic_sriov_pf(binary, tmp_path):

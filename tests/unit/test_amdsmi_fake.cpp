@@ -4,7 +4,8 @@
 // runs them in a separate process); otherwise they return immediately.
 //
 // They cover what the pool cannot exercise on real hardware: compute-
-// partitioned GPUs (CPX regrouping by PCI address, partition ordering),
+// partitioned GPUs (CPX regrouping into physical GPUs under both partition
+// address layouts, partition ordering),
 // the persistent session's re-initialisation rules, stale handles and the
 // market-name fallback.
 #include <dlfcn.h>
@@ -369,6 +370,131 @@ TEST(AmdSmiFake_SingleStrategyOverCpxNode) {
   EXPECT_EQ(l["amd.com/gpu.memory"], std::string("36862"));
   EXPECT_EQ(l["amd.com/gpu.compute-units"], std::string("32"));
   EXPECT_EQ(l["amd.com/partition.strategy"], std::string("single"));
+  fs::remove_all(root);
+}
+
+// ---- Partition layouts (resource/physical.h) --------------------------------
+// Current kernels put the partition index in the PCI function bits of each
+// partition's address (kfd_topology.c ORs the XCP node id into location_id);
+// older ones give every partition the parent's address.  amd-smi groups
+// processors into one socket per domain:bus:device; `sockets=one` checks the
+// backend does not depend on that.  Every combination must label the same.
+
+namespace {
+const char* kLayouts[][2] = {{"partition_bdf=function", "sockets=slot"},
+                             {"partition_bdf=function", "sockets=one"},
+                             {"partition_bdf=shared", "sockets=slot"},
+                             {"partition_bdf=shared", "sockets=one"}};
+
+std::string with_layout(const char* const layout[2], const std::string& gpus) {
+  return std::string(layout[0]) + "\n" + layout[1] + "\n" + gpus;
+}
+
+lm::Labels strategy_labels(const std::string& spec, const std::string& strategy, const std::string& root) {
+  fake().configure(spec.c_str());
+  AmdSmiManager m(opts(root, false));
+  config::Config c;
+  c.flags.mig_strategy = strategy;
+  m.Init();
+  auto l = lm::NewResourceLabeler(m, c)->GetLabels();
+  m.Shutdown();
+  return l;
+}
+
+const std::string kTwoCpx =
+    "bdf=0000:23:00.0;mode=CPX;parts=8;cus=32;xcds=1;vram_mib=36862\n"
+    "bdf=0000:24:00.0;mode=CPX;parts=8;cus=32;xcds=1;vram_mib=36862\n";
+}  // namespace
+
+TEST(AmdSmiFake_CpxSingleAndMixedUnderEveryLayout) {
+  REQUIRE_FAKE();
+  std::string root = temp_root();
+  for (const auto& layout : kLayouts) {
+    auto single = strategy_labels(with_layout(layout, kTwoCpx), "single", root);
+    EXPECT_EQ(single["amd.com/gpu.count"], std::string("16"));
+    EXPECT_EQ(single["amd.com/gpu.product"], std::string("AMD-Instinct-MI355-OAM-PARTITION-cpx.1xcd.36gb"));
+    EXPECT_EQ(single["amd.com/gpu.memory"], std::string("36862"));
+    auto mixed = strategy_labels(with_layout(layout, kTwoCpx), "mixed", root);
+    EXPECT_EQ(mixed["amd.com/partition-cpx.1xcd.36gb.count"], std::string("16"));
+    EXPECT_EQ(mixed["amd.com/gpu.count"], std::string("2"));
+    EXPECT_EQ(mixed["amd.com/gpu.replicas"], std::string("0"));
+  }
+  fs::remove_all(root);
+}
+
+TEST(AmdSmiFake_PartitionAddressesAndParent) {
+  REQUIRE_FAKE();
+  fake().configure(("partition_bdf=function\n" + kTwoCpx).c_str());
+  std::string root = temp_root();
+  AmdSmiManager m(opts(root, false));
+  m.Init();
+  auto devs = m.GetDevices();
+  EXPECT_EQ(devs.size(), static_cast<size_t>(2));
+  EXPECT_EQ(devs[0]->Info().bdf, std::string("0000:23:00.0"));
+  EXPECT_EQ(devs[1]->Info().bdf, std::string("0000:24:00.0"));
+  auto parts = devs[1]->GetPartitions();
+  EXPECT_EQ(parts.size(), static_cast<size_t>(8));
+  for (size_t i = 0; i < parts.size(); ++i) {
+    EXPECT_EQ(parts[i]->Info().partition_id, static_cast<int>(i));
+    EXPECT_EQ(parts[i]->Info().bdf, "0000:24:00." + std::to_string(i));
+    EXPECT_EQ(parts[i]->GetParent().get(), devs[1].get());
+  }
+  m.Shutdown();
+  fs::remove_all(root);
+}
+
+TEST(AmdSmiFake_OnePartitionVisibleReadsParentAttributes) {
+  REQUIRE_FAKE();
+  // A pod allocated partition 3 of a CPX GPU: the one processor reports
+  // 0000:23:00.3, which is not a PCI function; the GPU-wide attributes live
+  // on 0000:23:00.0.
+  std::string root = temp_root();
+  std::string pci = root + "/sys/bus/pci/devices/0000:23:00.0";
+  fs::mkdir_all(pci);
+  lm::write_file_atomically(pci + "/device", "0x75a3\n", 0644);
+  lm::write_file_atomically(pci + "/xgmi_num_links", "01 01 01 00 01 01 01 01\n", 0644);
+  lm::write_file_atomically(pci + "/available_memory_partition", "NPS1, NPS2, NPS4\n", 0644);
+  fake().configure("partition_bdf=function\nbdf=0000:23:00.0;mode=CPX;parts=8;cus=32;xcds=1;vram_mib=36862;visible=3\n");
+  AmdSmiManager m(opts(root, false));
+  m.Init();
+  auto devs = m.GetDevices();
+  EXPECT_EQ(devs.size(), static_cast<size_t>(1));
+  EXPECT_EQ(devs[0]->Info().bdf, std::string("0000:23:00.0"));
+  EXPECT_TRUE(devs[0]->IsPartitioned());
+  EXPECT_EQ(devs[0]->Info().xgmi_links, 7);
+  EXPECT_EQ(devs[0]->Info().available_memory_partitions, (std::vector<std::string>{"NPS1", "NPS2", "NPS4"}));
+  auto parts = devs[0]->GetPartitions();
+  EXPECT_EQ(parts.size(), static_cast<size_t>(1));
+  EXPECT_EQ(parts[0]->Info().partition_id, 3);
+  EXPECT_EQ(parts[0]->Info().bdf, std::string("0000:23:00.3"));
+  m.Shutdown();
+  config::Config c;
+  c.flags.mig_strategy = "single";
+  m.Init();
+  auto l = lm::NewResourceLabeler(m, c)->GetLabels();
+  m.Shutdown();
+  EXPECT_EQ(l["amd.com/gpu.count"], std::string("1"));
+  EXPECT_EQ(l["amd.com/gpu.product"], std::string("AMD-Instinct-MI355-OAM-PARTITION-cpx.1xcd.36gb"));
+  fs::remove_all(root);
+}
+
+TEST(AmdSmiFake_DistinctGpusOnOneSlotStaySeparate) {
+  REQUIRE_FAKE();
+  // Two SR-IOV virtual functions a guest sees on one slot (ARI): different
+  // ASIC serials, so two GPUs, not one GPU with two partitions.
+  fake().configure(
+      "bdf=0000:05:00.0;mode=SPX;parts=1;serial=0x1111222233334444\n"
+      "bdf=0000:05:00.1;mode=SPX;parts=1;serial=0x5555666677778888\n");
+  std::string root = temp_root();
+  AmdSmiManager m(opts(root, false));
+  m.Init();
+  auto devs = m.GetDevices();
+  EXPECT_EQ(devs.size(), static_cast<size_t>(2));
+  EXPECT_FALSE(devs[0]->IsPartitioned());
+  EXPECT_FALSE(devs[1]->IsPartitioned());
+  EXPECT_EQ(devs[0]->Info().bdf, std::string("0000:05:00.0"));
+  EXPECT_EQ(devs[1]->Info().bdf, std::string("0000:05:00.1"));
+  m.Shutdown();
   fs::remove_all(root);
 }
 

@@ -69,4 +69,8 @@ Daemon flags as GFD_* environment variables, one per value that is set
 - name: GFD_CONFIG_FILE
   value: /etc/gfd/config.yaml
 {{- end }}
+{{- if .Values.hostOpt.enabled }}
+- name: GFD_HOST_ROOT
+  value: /host
+{{- end }}
 {{- end -}}

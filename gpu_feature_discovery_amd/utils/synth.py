@@ -236,6 +236,13 @@ def make_node(root: str | os.PathLike, spec: NodeSpec) -> Path:
             _write(d / "sriov_totalvfs", f"{sriov.get('total', 1)}\n")
             _write(d / "sriov_numvfs", f"{sriov.get('num', 0)}\n")
         _write(d / "config", config_space(device_id, g.sriov, 4096 if spec.privileged else 64))
+        if spec.privileged:
+            # Per-partition resources of the current mode (amdgpu_xcp.c); mode
+            # 0400 on real nodes, so only a privileged reader sees them.
+            # Illustrative counts: 4 decoders / 32 JPEG engines per GPU.
+            for res, total in (("xcc", g.xcds), ("dma", 16), ("dec", 4), ("jpeg", 32)):
+                _write(d / f"compute_partition_config/{res}/num_inst", f"{max(1, total // parts)}\n")
+                _write(d / f"compute_partition_config/{res}/num_shared", f"{max(1, parts // total)}\n")
         for v in range(sriov.get("num", 0)):
             vf_bdf = f"0000:{bus:02x}:00.{v + 1}"
             vd = root / "sys/bus/pci/devices" / vf_bdf

@@ -42,6 +42,8 @@ void update_from_cli_flags(config::Flags& f, const Context& ctx) {
   str_field(g.machine_type_file, "machine-type-file");
   str_field(g.backend, "backend");
   str_field(g.sysfs_root, "sysfs-root");
+  str_field(g.host_root, "host-root");
+  str_field(g.rocm_version_file, "rocm-version-file");
   str_field(g.visible_devices, "visible-devices");
   str_field(g.amdsmi_session, "amdsmi-session");
   str_field(g.mock_file, "mock-file");
@@ -129,7 +131,7 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
   // the time it is needed runs on this thread instead (run_or_wait).  The
   // tasks never throw; an SR-IOV error is handed back and raised after the
   // device labeler.
-  std::optional<std::string> version_root = manager.VersionFilesRoot();
+  std::optional<resource::VersionSources> version_files = manager.VersionFiles();
   lm::NodeFacts facts;
   lm::Labels sriov_labels;
   std::exception_ptr sriov_error;
@@ -137,7 +139,7 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
   std::function<void()> read_facts = [&] {
     int64_t s0 = trace::now_ns();
     try {
-      facts = lm::ReadNodeFacts(config, version_root);
+      facts = lm::ReadNodeFacts(config, version_files);
     } catch (...) {
       facts = lm::NodeFacts{};  // fall back to the manager inside the labeler
     }
@@ -255,6 +257,17 @@ bool run(resource::Manager& manager, const std::shared_ptr<sriov::Interface>& sr
   }
 }
 
+namespace {
+// Process-level timeline for --trace-timing (a oneshot Job's latency is
+// mostly outside the labeling cycle: process start, backend selection and
+// library loading, teardown).  Absolute CLOCK_MONOTONIC milliseconds, so a
+// parent that timed the spawn can attribute the rest.
+struct ProcessTimeline {
+  bool enabled = false;
+  int64_t main_ns = 0, configured_ns = 0, manager_ns = 0, run_done_ns = 0;
+} g_timeline;
+}  // namespace
+
 void start(const Context& ctx, SignalWatcher& sigs) {
   for (;;) {
     log::printf("Loading configuration.");
@@ -266,12 +279,19 @@ void start(const Context& ctx, SignalWatcher& sigs) {
     }
     config::disable_resource_renaming(c);
     log::printf("\nRunning with config:\n%s", config::to_json(c).c_str());
+    g_timeline.enabled = c.trace_timing();
+    if (!g_timeline.configured_ns) g_timeline.configured_ns = trace::now_ns();
 
-    resource::ManagerPtr manager = resource::new_manager(c);
-    auto sriov = sriov::new_sriov_lib(c.sysfs_root());
+    bool restart;
+    {
+      resource::ManagerPtr manager = resource::new_manager(c);
+      auto sriov = sriov::new_sriov_lib(c.sysfs_root());
+      if (!g_timeline.manager_ns) g_timeline.manager_ns = trace::now_ns();
 
-    log::printf("Start running");
-    bool restart = run(*manager, sriov, c, &sigs);
+      log::printf("Start running");
+      restart = run(*manager, sriov, c, &sigs);
+      g_timeline.run_done_ns = trace::now_ns();
+    }  // the manager (and a persistent amd-smi session) is released here
     if (!restart) return;
   }
 }
@@ -297,6 +317,7 @@ int gfd_main(int argc, char** argv) {
     printf("%s version %s\n", app.c_str(), info::version_string().c_str());
     return 0;
   }
+  g_timeline.main_ns = trace::now_ns();
   int rc = 0;
   {
     log::printf("Starting OS watcher.");
@@ -309,6 +330,14 @@ int gfd_main(int argc, char** argv) {
       return 1;
     }
     log::printf("Exiting");
+  }
+  if (g_timeline.enabled) {
+    int64_t end = trace::now_ns();
+    auto ms = [](int64_t ns) { return static_cast<double>(ns) / 1e6; };
+    log::printf("Process timing: main_at=%.3fms config=%.3fms backend_select=%.3fms run=%.3fms teardown=%.3fms",
+                ms(g_timeline.main_ns), ms(g_timeline.configured_ns - g_timeline.main_ns),
+                ms(g_timeline.manager_ns - g_timeline.configured_ns), ms(g_timeline.run_done_ns - g_timeline.manager_ns),
+                ms(end - g_timeline.run_done_ns));
   }
   return rc;
 }

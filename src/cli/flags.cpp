@@ -171,6 +171,11 @@ std::vector<FlagDef> gfd_flags() {
        "device backend: auto (amd-smi, else KFD sysfs, else none) | amdsmi | sysfs | null | mock"},
       {"sysfs-root", {}, T::String, "/", {"GFD_SYSFS_ROOT"},
        "root prefix for sysfs/procfs reads (synthetic trees for testing)"},
+      {"host-root", {}, T::String, "", {"GFD_HOST_ROOT"},
+       "where the host's filesystem (at least /opt) is mounted in the container: the ROCm runtime version is\n\t\t"
+       "read from <host-root>/opt/rocm/.info/version, following the host's absolute symlinks (empty: this root)"},
+      {"rocm-version-file", {}, T::String, "", {"GFD_ROCM_VERSION_FILE"},
+       "read the ROCm runtime version from this file (e.g. a mounted /opt/rocm/.info/version); an error if unreadable"},
       {"visible-devices", {}, T::String, "", {"GFD_VISIBLE_DEVICES"},
        "restrict labeling to these physical GPUs: indices, ranges or PCI addresses (\"0,2-3\"); empty = all"},
       {"amdsmi-session", {}, T::String, "persistent", {"GFD_AMDSMI_SESSION"},

@@ -227,6 +227,8 @@ GFDFlags decode_gfd_flags(const Node& n) {
   g.machine_type_file = opt_string(n.get("machineTypeFile"), "Config.flags.gfd.machineTypeFile");
   g.backend = opt_string(n.get("backend"), "Config.flags.gfd.backend");
   g.sysfs_root = opt_string(n.get("sysfsRoot"), "Config.flags.gfd.sysfsRoot");
+  g.host_root = opt_string(n.get("hostRoot"), "Config.flags.gfd.hostRoot");
+  g.rocm_version_file = opt_string(n.get("rocmVersionFile"), "Config.flags.gfd.rocmVersionFile");
   g.visible_devices = opt_string(n.get("visibleDevices"), "Config.flags.gfd.visibleDevices");
   g.mock_file = opt_string(n.get("mockFile"), "Config.flags.gfd.mockFile");
   g.amdsmi_session = opt_string(n.get("amdsmiSession"), "Config.flags.gfd.amdsmiSession");
@@ -336,6 +338,8 @@ Node to_node(const Config& c) {
   gfd.set("machineTypeFile", opt_node(g.machine_type_file));
   gfd.set("backend", opt_node(g.backend));
   gfd.set("sysfsRoot", opt_node(g.sysfs_root));
+  gfd.set("hostRoot", opt_node(g.host_root));
+  gfd.set("rocmVersionFile", opt_node(g.rocm_version_file));
   gfd.set("visibleDevices", opt_node(g.visible_devices));
   if (g.mock_file && !g.mock_file->empty()) gfd.set("mockFile", Node::string(*g.mock_file));
   gfd.set("amdsmiSession", opt_node(g.amdsmi_session));

@@ -95,6 +95,8 @@ struct GFDFlags {
   // AMD extensions.
   std::optional<std::string> backend;          // auto | amdsmi | sysfs | null | mock
   std::optional<std::string> sysfs_root;       // root prefix for /sys reads
+  std::optional<std::string> host_root;        // host filesystem mount (node-true ROCm version)
+  std::optional<std::string> rocm_version_file;  // explicit ROCm .info/version file
   std::optional<std::string> visible_devices;  // "" = all; "0,2-3" or BDFs
   std::optional<std::string> mock_file;        // device fixture for backend=mock
   std::optional<std::string> amdsmi_session;   // per-cycle | persistent
@@ -125,6 +127,8 @@ struct Config {
   std::string machine_type_file() const { return flags.gfd.machine_type_file.value_or(kDefaultMachineTypeFile); }
   std::string backend() const { return flags.gfd.backend.value_or("auto"); }
   std::string sysfs_root() const { return flags.gfd.sysfs_root.value_or("/"); }
+  std::string host_root() const { return flags.gfd.host_root.value_or(""); }
+  std::string rocm_version_file() const { return flags.gfd.rocm_version_file.value_or(""); }
   std::string visible_devices() const { return flags.gfd.visible_devices.value_or(""); }
   std::string mock_file() const { return flags.gfd.mock_file.value_or(""); }
   std::string amdsmi_session() const { return flags.gfd.amdsmi_session.value_or("persistent"); }

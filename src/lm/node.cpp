@@ -1,5 +1,6 @@
 #include "lm/node.h"
 
+#include <atomic>
 #include <ctime>
 #include <map>
 
@@ -40,21 +41,32 @@ Labels machine_type_labels(const std::string& path, std::string* warning) {
 }
 
 // nvml.go:75-106: the driver version is fetched and checked before the
-// runtime version is asked for.
+// runtime version is asked for.  A node without a ROCm release (nullopt:
+// driver-only hosts whose workloads bring ROCm in their images) gets the
+// driver labels only; failing to read a source that should be there (an
+// explicitly configured version file) is an error, as in the reference.
 template <typename DriverFn, typename RuntimeFn>
 LabelerPtr version_labeler(DriverFn&& get_driver, RuntimeFn&& get_runtime) {
   std::string driver = GFD_WRAP("error getting driver version", get_driver());
   auto parts = str::split(driver, '.');
   if (parts.size() > 3 || parts.size() < 2)
     throw Error("error getting driver version: Version \"" + driver + "\" does not match format \"X.Y[.Z]\"");
-  resource::RuntimeVersion rt = GFD_WRAP("error getting ROCm runtime version", get_runtime());
-  return from_labels(Labels{
+  std::optional<resource::RuntimeVersion> rt = GFD_WRAP("error getting ROCm runtime version", get_runtime());
+  Labels l{
       {keys::kDriverMajor, parts[0]},
       {keys::kDriverMinor, parts[1]},
       {keys::kDriverRev, parts.size() > 2 ? parts[2] : ""},
-      {keys::kRuntimeMajor, std::to_string(rt.major)},
-      {keys::kRuntimeMinor, std::to_string(rt.minor)},
-  });
+  };
+  if (rt) {
+    l[keys::kRuntimeMajor] = std::to_string(rt->major);
+    l[keys::kRuntimeMinor] = std::to_string(rt->minor);
+  } else {
+    static std::atomic<bool> warned{false};
+    if (!warned.exchange(true))
+      log::printf("WARNING: no ROCm release found on the node; omitting the rocm.runtime labels "
+                  "(in a pod, mount the host's /opt and set --host-root)");
+  }
+  return from_labels(std::move(l));
 }
 
 }  // namespace
@@ -70,14 +82,14 @@ LabelerPtr NewVersionLabeler(resource::Manager& manager) {
   return version_labeler([&] { return manager.GetDriverVersion(); }, [&] { return manager.GetRuntimeVersion(); });
 }
 
-NodeFacts ReadNodeFacts(const config::Config& config, const std::optional<std::string>& version_files_root) {
+NodeFacts ReadNodeFacts(const config::Config& config, const std::optional<resource::VersionSources>& version_files) {
   NodeFacts f;
   f.machine = machine_type_labels(config.machine_type_file(), &f.machine_warning);
-  if (version_files_root) {
+  if (version_files) {
     f.have_versions = true;
-    f.driver_version = resource::driver_version(*version_files_root);
+    f.driver_version = resource::driver_version(version_files->root);
     try {
-      f.runtime_version = resource::runtime_version(*version_files_root);
+      f.runtime_version = resource::rocm_version(*version_files);
     } catch (const std::exception& e) {
       f.runtime_error = e.what();
     }
@@ -221,8 +233,8 @@ LabelerPtr NewDeviceLabeler(resource::Manager& manager, const config::Config& co
     version = GFD_WRAP("failed to construct version labeler",
                        version_labeler([&] { return pre->driver_version; },
                                        [&] {
-                                         if (!pre->runtime_version) throw Error(pre->runtime_error);
-                                         return *pre->runtime_version;
+                                         if (!pre->runtime_error.empty()) throw Error(pre->runtime_error);
+                                         return pre->runtime_version;
                                        }));
   } else {
     version = GFD_WRAP("failed to construct version labeler", NewVersionLabeler(manager));

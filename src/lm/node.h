@@ -44,17 +44,17 @@ LabelerPtr NewSriovLabeler(std::shared_ptr<sriov::Interface> lib);
 
 // Node facts that need no device context: the DMI machine type and, for
 // managers whose version queries are plain file reads
-// (Manager::VersionFilesRoot), the driver and ROCm versions.  The daemon
+// (Manager::VersionFiles), the driver and ROCm versions.  The daemon
 // reads them on a worker while the backend enumerates the GPUs.
 struct NodeFacts {
   Labels machine;               // amd.com/gpu.machine
   std::string machine_warning;  // logged when the labels are used
   bool have_versions = false;
   std::string driver_version;
-  std::optional<resource::RuntimeVersion> runtime_version;
-  std::string runtime_error;  // when runtime_version is unset
+  std::optional<resource::RuntimeVersion> runtime_version;  // nullopt: no ROCm on the node
+  std::string runtime_error;  // a configured version source failed
 };
-NodeFacts ReadNodeFacts(const config::Config& config, const std::optional<std::string>& version_files_root);
+NodeFacts ReadNodeFacts(const config::Config& config, const std::optional<resource::VersionSources>& version_files);
 
 // The device labeler (NewNVMLLabeler analogue, nvml.go:29-72): Init, defer
 // Shutdown, enumerate, and build every device-derived labeler eagerly inside

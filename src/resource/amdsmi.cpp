@@ -69,8 +69,6 @@ class AmdSmiLib {
   GFD_AMDSMI_FN(get_gpu_compute_partition, amdsmi_processor_handle, char*, uint32_t);
   GFD_AMDSMI_FN(get_gpu_memory_partition, amdsmi_processor_handle, char*, uint32_t);
   GFD_AMDSMI_FN(get_gpu_memory_partition_config, amdsmi_processor_handle, amdsmi_memory_partition_config_t*);
-  GFD_AMDSMI_FN(get_gpu_accelerator_partition_profile, amdsmi_processor_handle,
-                amdsmi_accelerator_partition_profile_t*, uint32_t*);
   GFD_AMDSMI_FN(get_gpu_accelerator_partition_profile_config, amdsmi_processor_handle,
                 amdsmi_accelerator_partition_profile_config_t*);
   GFD_AMDSMI_FN(get_gpu_xgmi_link_status, amdsmi_processor_handle, amdsmi_xgmi_link_status_t*);
@@ -120,7 +118,6 @@ class AmdSmiLib {
     lib_.bind("amdsmi_get_gpu_compute_partition", get_gpu_compute_partition);
     lib_.bind("amdsmi_get_gpu_memory_partition", get_gpu_memory_partition);
     lib_.bind("amdsmi_get_gpu_memory_partition_config", get_gpu_memory_partition_config);
-    lib_.bind("amdsmi_get_gpu_accelerator_partition_profile", get_gpu_accelerator_partition_profile);
     lib_.bind("amdsmi_get_gpu_accelerator_partition_profile_config", get_gpu_accelerator_partition_profile_config);
     lib_.bind("amdsmi_get_gpu_xgmi_link_status", get_gpu_xgmi_link_status);
     lib_.bind("amdsmi_get_gpu_virtualization_mode", get_gpu_virtualization_mode);
@@ -186,6 +183,7 @@ struct ProcInfo {
   uint64_t vram = 0;
   uint32_t partition_id = 0;
   uint32_t xcds = 0;
+  int sdma = -1;  // KFD node num_sdma_engines (-1: node unknown)
   std::string compute_partition;
   std::string memory_partition;
   std::string uuid;
@@ -197,7 +195,7 @@ struct GpuExtras {
   std::string virtualization;
   std::vector<std::string> available_memory;
   std::vector<std::string> available_compute;
-  Attributes engines;  // engines.* from the accelerator partition profile
+  Attributes engines;  // engines.* of each partition (partition_engine_counts)
 };
 
 const char* virt_name(amdsmi_virtualization_mode_t m) {
@@ -253,16 +251,29 @@ auto timed(const char* name, F&& f) -> decltype(f()) {
 // observed on the MI355X pool.
 bool is_generic_name(const std::string& s) { return s.empty() || s == "AMD Radeon Graphics" || s == "N/A"; }
 
-// XCD count of a KFD node (num_xcc) - ~15 us versus ~140 us for
-// amdsmi_get_gpu_xcd_counter, which decodes the full gpu_metrics table.
-uint32_t kfd_num_xcc(const std::string& root, uint32_t node_id) {
+// XCD and SDMA-engine counts of a KFD node (num_xcc, num_sdma_engines) -
+// ~15 us versus ~140 us for amdsmi_get_gpu_xcd_counter, which decodes the
+// full gpu_metrics table.  Zero / -1 when the node cannot be read.
+struct KfdCounts {
+  uint32_t num_xcc = 0;
+  int num_sdma = -1;
+};
+KfdCounts kfd_counts(const std::string& root, uint32_t node_id) {
+  KfdCounts c;
   auto r = fs::attrs().read(fs::join(root, "sys/class/kfd/kfd/topology/nodes/" + std::to_string(node_id) + "/properties"));
-  if (!r.ok()) return 0;
-  static const char kKey[] = "\nnum_xcc ";
-  auto pos = r.data.find(kKey);
-  if (pos == std::string::npos) return 0;
-  return static_cast<uint32_t>(strtoul(r.data.c_str() + pos + sizeof(kKey) - 1, nullptr, 10));
+  if (!r.ok()) return c;
+  auto field = [&](const char* key, size_t len) -> std::optional<unsigned long> {
+    auto pos = r.data.find(key);
+    if (pos == std::string::npos) return std::nullopt;
+    return strtoul(r.data.c_str() + pos + len, nullptr, 10);
+  };
+  static const char kXcc[] = "\nnum_xcc ";
+  static const char kSdma[] = "\nnum_sdma_engines ";
+  if (auto v = field(kXcc, sizeof(kXcc) - 1)) c.num_xcc = static_cast<uint32_t>(*v);
+  if (auto v = field(kSdma, sizeof(kSdma) - 1)) c.num_sdma = static_cast<int>(*v);
+  return c;
 }
+uint32_t kfd_num_xcc(const std::string& root, uint32_t node_id) { return kfd_counts(root, node_id).num_xcc; }
 
 // Identity of a processor from its ASIC info (the library caches it after
 // the first call: ~2 us).
@@ -366,7 +377,11 @@ void query_proc(AmdSmiLib& L, const std::string& root, ProcInfo& p) {
 
   uint32_t node_id = kNoNode;
   query_kfd(L, p, &node_id);
-  if (node_id != kNoNode) p.xcds = AMDSMI_CALL("kfd_num_xcc(sysfs)", kfd_num_xcc(root, node_id));
+  if (node_id != kNoNode) {
+    KfdCounts c = AMDSMI_CALL("kfd_counts(sysfs)", kfd_counts(root, node_id));
+    p.xcds = c.num_xcc;
+    p.sdma = c.num_sdma;
+  }
   char buf[64];
   if (L.get_gpu_compute_partition) {
     std::memset(buf, 0, sizeof(buf));
@@ -457,21 +472,6 @@ void query_gpu_caps(AmdSmiLib& L, const ProcInfo& p, const std::string& root, Gp
   }
 }
 
-// Per-partition engine counts (only meaningful when partitioned).
-void query_partition_engines(AmdSmiLib& L, const ProcInfo& p, GpuExtras& x) {
-  if (L.get_gpu_accelerator_partition_profile) {
-    amdsmi_accelerator_partition_profile_t prof;
-    std::memset(&prof, 0, sizeof(prof));
-    uint32_t ids[AMDSMI_MAX_ACCELERATOR_PARTITIONS] = {0};
-    if (L.get_gpu_accelerator_partition_profile(p.h, &prof, ids) == AMDSMI_STATUS_SUCCESS && prof.num_resources > 0) {
-      // resources[partition][resource-type] holds instance counts.
-      static const char* kNames[] = {"engines.xcc", "engines.encoder", "engines.decoder", "engines.dma", "engines.jpeg"};
-      for (uint32_t r = 0; r < prof.num_resources && r < AMDSMI_ACCELERATOR_MAX; ++r)
-        if (r != AMDSMI_ACCELERATOR_XCC) x.engines[kNames[r]] = std::to_string(prof.resources[0][r]);
-    }
-  }
-}
-
 std::string format_bdf(const amdsmi_bdf_t& b) {
   return str::format("%04llx:%02x:%02x.%x", static_cast<unsigned long long>(b.domain_number),
                      static_cast<unsigned>(b.bus_number), static_cast<unsigned>(b.device_number),
@@ -484,7 +484,7 @@ std::string format_bdf(const amdsmi_bdf_t& b) {
 // ---------------------------------------------------------------------------
 // AmdSmiManager
 
-AmdSmiManager::AmdSmiManager(AmdSmiOptions opts) : opts_(std::move(opts)) {}
+AmdSmiManager::AmdSmiManager(AmdSmiOptions opts) : opts_(std::move(opts)) { opts_.versions.root = opts_.root; }
 
 AmdSmiManager::~AmdSmiManager() {
   if (lib_initialized_) library_shutdown();
@@ -688,7 +688,7 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
       const ProcInfo& first = procs.front();
       query_gpu_caps(L, first, opts_.root, g.extras);
       if (procs.size() > 1 || (!first.compute_partition.empty() && first.compute_partition != "SPX"))
-        query_partition_engines(L, first, g.extras);
+        g.extras.engines = AMDSMI_CALL("partition_engines(sysfs)", partition_engine_counts(opts_.root, first.gpu_bdf));
       g.proc_ns = t1 - t0;
       g.caps_ns = trace::now_ns() - t1;
     } catch (...) {
@@ -771,14 +771,8 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
       pi.compute_partition = p.compute_partition;
       pi.memory_partition = p.memory_partition;
       pi.name = partition_profile_name(pi.compute_partition, pi.xcds, pi.memory_mib);
-      pi.attributes = {
-          {"memory", std::to_string(pi.memory_mib)},
-          {"compute-units", std::to_string(pi.compute_units)},
-          {"xcds", std::to_string(pi.xcds)},
-      };
-      for (const auto& kv : g.extras.engines) pi.attributes[kv.first] = kv.second;
-      if (!pi.compute_partition.empty()) pi.attributes["compute-partition"] = pi.compute_partition;
-      if (!pi.memory_partition.empty()) pi.attributes["memory-partition"] = pi.memory_partition;
+      pi.attributes = partition_attributes(pi.memory_mib, pi.compute_units, pi.xcds, p.sdma, g.extras.engines,
+                                           pi.compute_partition, pi.memory_partition);
       parts.push_back(SnapshotDevice::partition(std::move(pi)));
     }
     info.memory_mib = mem >> 20;
@@ -800,6 +794,6 @@ std::string AmdSmiManager::GetDriverVersion() {
   return driver_version(opts_.root);
 }
 
-RuntimeVersion AmdSmiManager::GetRuntimeVersion() { return runtime_version(opts_.root); }
+std::optional<RuntimeVersion> AmdSmiManager::GetRuntimeVersion() { return rocm_version(opts_.versions); }
 
 }  // namespace gfd::resource

@@ -42,6 +42,7 @@ struct AmdSmiOptions {
   std::string root = "/";       // for the KFD generation check / sysfs hints
   DeviceFilter filter;
   int threads = 0;              // 0 = auto (one per physical GPU, max 8)
+  VersionSources versions;  // its root is `root`
 };
 
 // Process-wide handle to libamd_smi (opened on first use).
@@ -57,9 +58,9 @@ class AmdSmiManager : public Manager {
   void Shutdown() override;
   std::vector<DevicePtr> GetDevices() override;
   std::string GetDriverVersion() override;
-  RuntimeVersion GetRuntimeVersion() override;
+  std::optional<RuntimeVersion> GetRuntimeVersion() override;
   std::string Name() const override { return opts_.persistent ? "amdsmi(persistent)" : "amdsmi"; }
-  std::optional<std::string> VersionFilesRoot() const override { return opts_.root; }
+  std::optional<VersionSources> VersionFiles() const override { return opts_.versions; }
 
   // Number of amdsmi_init calls made by this manager (tests / benchmarks).
   int init_count() const { return init_count_; }

@@ -14,6 +14,14 @@ namespace gfd::resource {
 
 namespace {
 
+VersionSources version_sources(const config::Config& c) {
+  VersionSources v;
+  v.root = c.sysfs_root();
+  v.host_root = c.host_root();
+  v.rocm_version_file = c.rocm_version_file();
+  return v;
+}
+
 AmdSmiOptions amdsmi_options(const config::Config& c) {
   AmdSmiOptions o;
   std::string mode = c.amdsmi_session();
@@ -26,6 +34,7 @@ AmdSmiOptions amdsmi_options(const config::Config& c) {
   }
   o.root = c.sysfs_root();
   o.filter = DeviceFilter::parse(c.visible_devices());
+  o.versions = version_sources(c);
   if (const char* t = std::getenv("GFD_AMDSMI_THREADS"); t && *t) o.threads = static_cast<int>(str::parse_uint(t).value_or(0));
   return o;
 }
@@ -34,6 +43,7 @@ SysfsOptions sysfs_options(const config::Config& c) {
   SysfsOptions o;
   o.root = c.sysfs_root();
   o.filter = DeviceFilter::parse(c.visible_devices());
+  o.versions = version_sources(c);
   return o;
 }
 
@@ -45,12 +55,16 @@ bool log_with_reason(bool is, const std::string& reason, std::string tag) {
 
 // Startup observability: the runtime and driver versions the
 // hardware backends will label with.
-void log_versions(const std::string& root) {
-  auto rv = rocm_version(root);
-  std::string drv = host_driver_version(root);
-  log::printf("ROCm runtime %s, amdgpu driver %s",
-              rv ? (std::to_string(rv->major) + "." + std::to_string(rv->minor)).c_str() : "not found",
-              extract_version(drv).value_or(drv).c_str());
+void log_versions(const config::Config& c) {
+  std::string source, rocm = "not found";
+  try {
+    if (auto rv = rocm_version(version_sources(c), &source))
+      rocm = std::to_string(rv->major) + "." + std::to_string(rv->minor) + " (" + source + ")";
+  } catch (const std::exception& e) {
+    rocm = e.what();
+  }
+  std::string drv = host_driver_version(c.sysfs_root());
+  log::printf("ROCm runtime %s, amdgpu driver %s", rocm.c_str(), extract_version(drv).value_or(drv).c_str());
 }
 
 }  // namespace
@@ -68,20 +82,32 @@ ManagerPtr get_manager(const config::Config& c) {
   }
   if (backend == "sysfs") {
     log::printf("Using sysfs (KFD topology) manager");
-    log_versions(c.sysfs_root());
+    log_versions(c);
     return std::make_shared<SysfsManager>(sysfs_options(c));
   }
   if (backend == "amdsmi") {
     log::printf("Using amd-smi manager");
-    log_versions(c.sysfs_root());
+    log_versions(c);
     return std::make_shared<AmdSmiManager>(amdsmi_options(c));
   }
   if (backend != "auto") throw Error("unknown backend '" + backend + "' (expected auto, amdsmi, sysfs, null or mock)");
 
   std::string why;
+  if (c.oneshot()) {
+    // Job mode labels once and exits, so amd-smi's ~25 ms amdsmi_init (it
+    // parses all of /proc/cpuinfo, profiles/amdsmi_init_profile.txt) would be
+    // most of the process's life.  The KFD topology answers the same
+    // questions with the same values (tests/test_gpu.py checks the two label
+    // files are byte-identical), so a Job reads it and never loads amd-smi.
+    if (log_with_reason(has_kfd_topology(c.sysfs_root(), &why), why, "KFD")) {
+      log_versions(c);
+      log::printf("Using sysfs (KFD topology) manager (oneshot: amd-smi not loaded)");
+      return std::make_shared<SysfsManager>(sysfs_options(c));
+    }
+  }
   bool has_smi = log_with_reason(has_amdsmi(&why), why, "amd-smi");
   bool has_kfd = log_with_reason(has_kfd_topology(c.sysfs_root(), &why), why, "KFD");
-  if (has_smi || has_kfd) log_versions(c.sysfs_root());
+  if (has_smi || has_kfd) log_versions(c);
   if (has_smi && has_kfd) {
     log::printf("Using amd-smi manager, KFD sysfs manager if amd-smi fails to initialize");
     return std::make_shared<PreferenceManager>(std::vector<ManagerPtr>{

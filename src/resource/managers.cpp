@@ -11,7 +11,7 @@ namespace gfd::resource {
 // Null / Fallback
 
 std::string NullManager::GetDriverVersion() { throw Error("GetDriverVersion is unsupported"); }
-RuntimeVersion NullManager::GetRuntimeVersion() { throw Error("GetRuntimeVersion is unsupported"); }
+std::optional<RuntimeVersion> NullManager::GetRuntimeVersion() { throw Error("GetRuntimeVersion is unsupported"); }
 
 FallbackManager::FallbackManager(ManagerPtr wraps) : current_(std::move(wraps)) {}
 
@@ -78,7 +78,7 @@ std::string MockManager::GetDriverVersion() {
   return driver_version;
 }
 
-RuntimeVersion MockManager::GetRuntimeVersion() {
+std::optional<RuntimeVersion> MockManager::GetRuntimeVersion() {
   if (runtime_error) throw Error(*runtime_error);
   return runtime_version;
 }
@@ -245,7 +245,9 @@ std::shared_ptr<MockManager> mock_manager_from_node(const yaml::Node& root) {
   if (const Node* e = root.get("driverVersionError"); e && !e->is_null()) m->driver_error = e->text();
   if (const Node* e = root.get("runtimeVersionError"); e && !e->is_null()) m->runtime_error = e->text();
   m->driver_version = scalar_or(root.get("driverVersion"), m->driver_version);
-  if (const Node* rv = root.get("runtimeVersion"); rv && !rv->is_null()) {
+  if (const Node* rv = root.get("runtimeVersion"); rv && !rv->is_null() && rv->text().empty()) {
+    m->runtime_version = std::nullopt;  // runtimeVersion: "" - a node without ROCm
+  } else if (rv && !rv->is_null()) {
     auto parts = str::split(rv->text(), '.');
     auto maj = parts.size() > 0 ? str::parse_uint(parts[0]) : std::nullopt;
     auto min = parts.size() > 1 ? str::parse_uint(parts[1]) : std::optional<uint64_t>(0);

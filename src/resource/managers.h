@@ -24,7 +24,7 @@ class NullManager : public Manager {
   void Shutdown() override {}
   std::vector<DevicePtr> GetDevices() override { return {}; }
   std::string GetDriverVersion() override;
-  RuntimeVersion GetRuntimeVersion() override;
+  std::optional<RuntimeVersion> GetRuntimeVersion() override;
   std::string Name() const override { return "null"; }
 };
 
@@ -37,9 +37,9 @@ class FallbackManager : public Manager {
   void Shutdown() override { current_->Shutdown(); }
   std::vector<DevicePtr> GetDevices() override { return current_->GetDevices(); }
   std::string GetDriverVersion() override { return current_->GetDriverVersion(); }
-  RuntimeVersion GetRuntimeVersion() override { return current_->GetRuntimeVersion(); }
+  std::optional<RuntimeVersion> GetRuntimeVersion() override { return current_->GetRuntimeVersion(); }
   std::string Name() const override { return "fallback(" + current_->Name() + ")"; }
-  std::optional<std::string> VersionFilesRoot() const override { return current_->VersionFilesRoot(); }
+  std::optional<VersionSources> VersionFiles() const override { return current_->VersionFiles(); }
   bool fell_back() const { return fell_back_; }
 
  private:
@@ -62,9 +62,9 @@ class PreferenceManager : public Manager {
   void Shutdown() override { current_->Shutdown(); }
   std::vector<DevicePtr> GetDevices() override { return current_->GetDevices(); }
   std::string GetDriverVersion() override { return current_->GetDriverVersion(); }
-  RuntimeVersion GetRuntimeVersion() override { return current_->GetRuntimeVersion(); }
+  std::optional<RuntimeVersion> GetRuntimeVersion() override { return current_->GetRuntimeVersion(); }
   std::string Name() const override { return current_->Name(); }
-  std::optional<std::string> VersionFilesRoot() const override { return current_->VersionFilesRoot(); }
+  std::optional<VersionSources> VersionFiles() const override { return current_->VersionFiles(); }
   // Index of the candidate in use (0 until an Init fell through).
   size_t chosen() const { return chosen_; }
 
@@ -88,7 +88,7 @@ class MockManager : public Manager {
   void Shutdown() override;
   std::vector<DevicePtr> GetDevices() override;
   std::string GetDriverVersion() override;
-  RuntimeVersion GetRuntimeVersion() override;
+  std::optional<RuntimeVersion> GetRuntimeVersion() override;
   std::string Name() const override { return "mock"; }
 
   MockManager& with_error_on_init(std::string msg);
@@ -101,7 +101,7 @@ class MockManager : public Manager {
   std::optional<std::string> driver_error;
   std::optional<std::string> runtime_error;
   std::string driver_version = "6.12.12";
-  RuntimeVersion runtime_version{7, 2};
+  std::optional<RuntimeVersion> runtime_version = RuntimeVersion{7, 2};  // nullopt: no ROCm on the node
 
   int init_calls = 0;
   int shutdown_calls = 0;

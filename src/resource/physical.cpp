@@ -34,4 +34,29 @@ std::string resolve_parent_bdf(const std::string& root, std::vector<std::string>
   return member_bdfs.front();
 }
 
+Attributes partition_engine_counts(const std::string& root, const std::string& parent_bdf) {
+  static const std::pair<const char*, const char*> kEngines[] = {{"dec", "engines.decoder"}, {"jpeg", "engines.jpeg"}};
+  Attributes out;
+  std::string cfg = fs::join(root, "sys/bus/pci/devices/" + parent_bdf + "/compute_partition_config");
+  for (const auto& [res, label] : kEngines) {
+    auto v = fs::attrs().read_trimmed(cfg + "/" + res + "/num_inst");
+    if (!v) continue;
+    if (auto n = str::parse_uint(*v)) out[label] = std::to_string(*n);
+  }
+  return out;
+}
+
+Attributes partition_attributes(uint64_t memory_mib, uint32_t compute_units, uint32_t xcds, int sdma,
+                                const Attributes& engines, const std::string& compute_partition,
+                                const std::string& memory_partition) {
+  Attributes a = engines;
+  a["memory"] = std::to_string(memory_mib);
+  a["compute-units"] = std::to_string(compute_units);
+  a["xcds"] = std::to_string(xcds);
+  if (sdma >= 0) a["engines.dma"] = std::to_string(sdma);
+  if (!compute_partition.empty()) a["compute-partition"] = compute_partition;
+  if (!memory_partition.empty()) a["memory-partition"] = memory_partition;
+  return a;
+}
+
 }  // namespace gfd::resource

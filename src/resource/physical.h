@@ -46,4 +46,19 @@ std::string bdf_slot(const std::string& bdf);
 // member address is returned.
 std::string resolve_parent_bdf(const std::string& root, std::vector<std::string> member_bdfs, uint32_t device_id);
 
+// Engine counts per partition that amdgpu publishes for the current compute
+// partition mode under the parent function
+// (compute_partition_config/{dec,jpeg}/num_inst -> engines.decoder,
+// engines.jpeg; mode 0400 on current kernels, so a non-root pod sees none).
+// amd-smi's accelerator-partition profile reports the same files and is
+// refused to non-root callers the same way (profiles/hw_probe.md).
+Attributes partition_engine_counts(const std::string& root, const std::string& parent_bdf);
+
+// The attribute set of one compute partition - built here so that both
+// backends label a partition identically.  `sdma` is the partition's KFD
+// node num_sdma_engines (-1: unknown, omitted).
+Attributes partition_attributes(uint64_t memory_mib, uint32_t compute_units, uint32_t xcds, int sdma,
+                                const Attributes& engines, const std::string& compute_partition,
+                                const std::string& memory_partition);
+
 }  // namespace gfd::resource

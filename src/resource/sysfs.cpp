@@ -163,6 +163,7 @@ bool has_kfd_topology(const std::string& root, std::string* reason) {
 }
 
 SysfsManager::SysfsManager(SysfsOptions opts) : opts_(std::move(opts)) {
+  opts_.versions.root = opts_.root;
   topology_ = fs::join(opts_.root, kTopology);
   in_vm_ = running_in_vm(opts_.root);
 }
@@ -233,6 +234,8 @@ static DevicePtr describe_gpu(const std::string& root, bool in_vm, int index, co
       part_mem[p] = n.local_mem_size ? n.local_mem_size : node_memory_bytes(n.dir);
     });
 
+  Attributes engines;
+  if (partitioned) engines = partition_engine_counts(root, bdf);
   std::vector<std::shared_ptr<SnapshotDevice>> parts;
   uint32_t cus = 0, xcds = 0;
   uint64_t part_mem_sum = 0;
@@ -255,14 +258,8 @@ static DevicePtr describe_gpu(const std::string& root, bool in_vm, int index, co
     pi.compute_partition = info.compute_partition;
     pi.memory_partition = info.memory_partition;
     pi.name = partition_profile_name(pi.compute_partition, pi.xcds, pi.memory_mib);
-    pi.attributes = {
-        {"memory", std::to_string(pi.memory_mib)},
-        {"compute-units", std::to_string(pcus)},
-        {"xcds", std::to_string(pi.xcds)},
-        {"engines.dma", std::to_string(n.num_sdma_engines)},
-    };
-    if (!pi.compute_partition.empty()) pi.attributes["compute-partition"] = pi.compute_partition;
-    if (!pi.memory_partition.empty()) pi.attributes["memory-partition"] = pi.memory_partition;
+    pi.attributes = partition_attributes(pi.memory_mib, pcus, pi.xcds, static_cast<int>(n.num_sdma_engines), engines,
+                                         pi.compute_partition, pi.memory_partition);
     parts.push_back(SnapshotDevice::partition(std::move(pi)));
   }
   info.compute_units = cus;
@@ -384,6 +381,6 @@ std::vector<DevicePtr> SysfsManager::enumerate() {
 
 std::string SysfsManager::GetDriverVersion() { return driver_version(opts_.root); }
 
-RuntimeVersion SysfsManager::GetRuntimeVersion() { return runtime_version(opts_.root); }
+std::optional<RuntimeVersion> SysfsManager::GetRuntimeVersion() { return rocm_version(opts_.versions); }
 
 }  // namespace gfd::resource

@@ -32,6 +32,7 @@ namespace gfd::resource {
 struct SysfsOptions {
   std::string root = "/";
   DeviceFilter filter;
+  VersionSources versions;  // its root is `root`
 };
 
 class SysfsManager : public Manager {
@@ -41,9 +42,9 @@ class SysfsManager : public Manager {
   void Shutdown() override;
   std::vector<DevicePtr> GetDevices() override;
   std::string GetDriverVersion() override;
-  RuntimeVersion GetRuntimeVersion() override;
+  std::optional<RuntimeVersion> GetRuntimeVersion() override;
   std::string Name() const override { return "sysfs"; }
-  std::optional<std::string> VersionFilesRoot() const override { return opts_.root; }
+  std::optional<VersionSources> VersionFiles() const override { return opts_.versions; }
 
   // Enumerate without the Init/Shutdown protocol (used by GetDevices).
   std::vector<DevicePtr> enumerate();

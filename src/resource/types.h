@@ -149,8 +149,16 @@ struct RuntimeVersion {
   unsigned minor = 0;
 };
 
+// Where the node's driver and ROCm versions are read from (resource/versions.h).
+struct VersionSources {
+  std::string root = "/";         // sysfs root (synthetic trees in tests)
+  std::string host_root;          // host filesystem mount point ("" = none)
+  std::string rocm_version_file;  // explicit ROCm version file ("" = discover)
+};
+
 // Reference: resource.Manager (types.go:22-28).  GetCudaDriverVersion maps
-// to GetRuntimeVersion (installed ROCm major/minor).
+// to GetRuntimeVersion (the node's ROCm major/minor; nullopt when the node
+// has no ROCm release installed).
 class Manager {
  public:
   virtual ~Manager() = default;
@@ -158,13 +166,13 @@ class Manager {
   virtual void Shutdown() = 0;
   virtual std::vector<DevicePtr> GetDevices() = 0;
   virtual std::string GetDriverVersion() = 0;
-  virtual RuntimeVersion GetRuntimeVersion() = 0;
+  virtual std::optional<RuntimeVersion> GetRuntimeVersion() = 0;
   virtual std::string Name() const = 0;
   // For managers whose version queries are plain reads of node files
-  // (resource::driver_version / runtime_version under this root) and touch
+  // (resource::driver_version / rocm_version from these sources) and touch
   // no manager state: the daemon then reads them on a worker, overlapped
   // with enumeration.  nullopt: ask the manager, inside the Init window.
-  virtual std::optional<std::string> VersionFilesRoot() const { return std::nullopt; }
+  virtual std::optional<VersionSources> VersionFiles() const { return std::nullopt; }
 };
 
 using ManagerPtr = std::shared_ptr<Manager>;

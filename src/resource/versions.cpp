@@ -3,6 +3,7 @@
 #include <sys/utsname.h>
 
 #include <cstdlib>
+#include <tuple>
 
 #include "util/error.h"
 #include "util/fs.h"
@@ -40,37 +41,72 @@ std::string host_driver_version(const std::string& root) {
   return "";
 }
 
-std::optional<RuntimeVersion> rocm_version(const std::string& root) {
-  std::vector<std::string> candidates;
-  // A synthetic root is authoritative (deterministic test trees).
-  bool synthetic = !root.empty() && root != "/";
-  if (synthetic) candidates.push_back(fs::join(root, "opt/rocm/.info/version"));
-  if (const char* rp = std::getenv("ROCM_PATH"); rp && *rp && !synthetic)
-    candidates.push_back(fs::join(rp, ".info/version"));
-  if (!synthetic) candidates.push_back("/opt/rocm/.info/version");
-  for (const auto& c : candidates) {
-    auto v = fs::attrs().read_checked_trimmed(c);
-    if (!v) continue;
-    auto ver = extract_version(*v);
-    if (!ver) continue;
-    auto parts = str::split(*ver, '.');
-    auto maj = str::parse_uint(parts[0]);
-    auto min = str::parse_uint(parts[1]);
-    if (maj && min) return RuntimeVersion{static_cast<unsigned>(*maj), static_cast<unsigned>(*min)};
+std::optional<RuntimeVersion> parse_runtime_version(const std::string& text) {
+  auto ver = extract_version(text);
+  if (!ver) return std::nullopt;
+  auto parts = str::split(*ver, '.');
+  auto maj = str::parse_uint(parts[0]);
+  auto min = str::parse_uint(parts[1]);
+  if (!maj || !min) return std::nullopt;
+  return RuntimeVersion{static_cast<unsigned>(*maj), static_cast<unsigned>(*min)};
+}
+
+namespace {
+
+std::optional<RuntimeVersion> read_version_file(const std::string& path) {
+  auto v = fs::attrs().read_checked_trimmed(path);
+  if (!v) return std::nullopt;
+  return parse_runtime_version(*v);
+}
+
+// Highest <host_root>/opt/rocm-X.Y.Z/.info/version (versioned installs).
+std::optional<RuntimeVersion> newest_versioned_install(const std::string& host_root, std::string* source) {
+  std::optional<RuntimeVersion> best;
+  for (const auto& name : fs::list_dir(fs::join(host_root, "opt"))) {
+    if (name.rfind("rocm-", 0) != 0) continue;
+    std::string path = fs::resolve_in_root(host_root, "opt/" + name + "/.info/version");
+    if (path.empty()) continue;
+    auto v = read_version_file(path);
+    if (v && (!best || std::tie(v->major, v->minor) > std::tie(best->major, best->minor))) {
+      best = v;
+      if (source) *source = path;
+    }
   }
-  return std::nullopt;
+  return best;
+}
+
+}  // namespace
+
+std::optional<RuntimeVersion> rocm_version(const VersionSources& s, std::string* source) {
+  auto from = [&](const std::string& path) -> std::optional<RuntimeVersion> {
+    auto v = read_version_file(path);
+    if (v && source) *source = path;
+    return v;
+  };
+  if (!s.rocm_version_file.empty()) {
+    auto text = fs::attrs().read_checked_trimmed(s.rocm_version_file);
+    if (!text) throw Error("unable to read the ROCm version file " + s.rocm_version_file);
+    auto v = parse_runtime_version(*text);
+    if (!v) throw Error("ROCm version file " + s.rocm_version_file + " holds \"" + *text + "\", not X.Y[.Z]");
+    if (source) *source = s.rocm_version_file;
+    return v;
+  }
+  if (!s.host_root.empty()) {
+    std::string path = fs::resolve_in_root(s.host_root, "opt/rocm/.info/version");
+    if (!path.empty())
+      if (auto v = from(path)) return v;
+    return newest_versioned_install(s.host_root, source);
+  }
+  if (!s.root.empty() && s.root != "/") return from(fs::join(s.root, "opt/rocm/.info/version"));
+  if (const char* rp = std::getenv("ROCM_PATH"); rp && *rp)
+    if (auto v = from(fs::join(rp, ".info/version"))) return v;
+  return from("/opt/rocm/.info/version");
 }
 
 std::string driver_version(const std::string& root) {
   std::string raw = host_driver_version(root);
   auto v = extract_version(raw);
   return v ? *v : raw;
-}
-
-RuntimeVersion runtime_version(const std::string& root) {
-  auto v = rocm_version(root);
-  if (!v) throw Error("unable to determine the ROCm version (no .info/version under $ROCM_PATH or /opt/rocm)");
-  return *v;
 }
 
 }  // namespace gfd::resource

@@ -316,6 +316,43 @@ std::string read_link(const std::string& path) {
   return std::string(buf, static_cast<size_t>(n));
 }
 
+std::string resolve_in_root(const std::string& root, const std::string& rel) {
+  std::vector<std::string> todo;  // components still to walk, in reverse order
+  auto push_path = [&](const std::string& p) {
+    auto parts = str::split(p, '/');
+    for (auto it = parts.rbegin(); it != parts.rend(); ++it)
+      if (!it->empty() && *it != ".") todo.push_back(*it);
+  };
+  push_path(rel);
+  std::vector<std::string> cur;
+  int links = 0;
+  auto path_of = [&](const std::vector<std::string>& comps) {
+    std::string p = root.empty() ? "/" : root;
+    for (const auto& c : comps) p = join(p, c);
+    return p;
+  };
+  while (!todo.empty()) {
+    std::string c = std::move(todo.back());
+    todo.pop_back();
+    if (c == "..") {
+      if (!cur.empty()) cur.pop_back();
+      continue;
+    }
+    cur.push_back(c);
+    std::string p = path_of(cur);
+    struct stat st;
+    if (::lstat(p.c_str(), &st) != 0) return {};
+    if (!S_ISLNK(st.st_mode)) continue;
+    if (++links > 40) return {};
+    std::string target = read_link(p);
+    if (target.empty()) return {};
+    cur.pop_back();
+    if (target.front() == '/') cur.clear();
+    push_path(target);
+  }
+  return path_of(cur);
+}
+
 std::string real_basename(const std::string& path) {
   char buf[PATH_MAX];
   if (!::realpath(path.c_str(), buf)) return {};

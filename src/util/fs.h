@@ -129,6 +129,13 @@ AttrReader& attrs();
 std::string read_link(const std::string& path);
 // Final path component of realpath(path), or empty.
 std::string real_basename(const std::string& path);
+// Resolve `rel` under `root` the way a process chrooted at `root` would:
+// component by component, following symlinks, with absolute link targets
+// re-rooted under `root` (a host's /opt/rocm -> /opt/rocm-7.2.0 seen through
+// a mount of the host's /opt at /host/opt).  ".." never leaves `root`.
+// Returns the resolved path under `root`, or "" if a component does not
+// exist or links nest deeper than 40.
+std::string resolve_in_root(const std::string& root, const std::string& rel);
 
 std::string join(const std::string& a, const std::string& b);
 std::string dirname(const std::string& path);

@@ -4,7 +4,8 @@
 // The node is described by fake_amdsmi_configure(spec), one GPU per line:
 //   bdf=0000:23:00.0;mode=CPX;parts=8;name=AMD Instinct MI355 OAM;cus=32;xcds=1;vram_mib=36862;links=7;virt=1
 // (optional per GPU: serial=<hex asic serial>; visible=3,5 - only those
-// partitions are reported, like a pod allocated part of a GPU)
+// partitions are reported, like a pod allocated part of a GPU; kfd_base=N -
+// partition p is KFD topology node N+p, else no KFD node is reported)
 // plus optional global lines:
 //   init_status=34            amdsmi_init returns this status
 //   stale_after=N             after N successful queries, queries return NOT_INIT until re-init
@@ -59,6 +60,7 @@ struct Proc {
   int links = 7;
   int virt = AMDSMI_VIRTUALIZATION_MODE_BAREMETAL;
   std::string serial;  // asic_serial ("" = derived from the bus)
+  uint32_t kfd_node = 0xFFFFFFFFu;  // KFD topology node (kfd_base + partition)
 };
 
 struct State {
@@ -213,6 +215,7 @@ int fake_amdsmi_configure(const char* spec) {
       else if (k == "links") base.links = std::atoi(v.c_str());
       else if (k == "virt") base.virt = std::atoi(v.c_str());
       else if (k == "serial") base.serial = v;
+      else if (k == "kfd_base") base.kfd_node = static_cast<uint32_t>(std::atoi(v.c_str()));
       else if (k == "visible") {
         std::istringstream ids(v);
         std::string id;
@@ -225,6 +228,7 @@ int fake_amdsmi_configure(const char* spec) {
       Proc q = base;
       q.gpu = base.bdf;
       q.partition_id = static_cast<uint32_t>(p);
+      if (base.kfd_node != 0xFFFFFFFFu) q.kfd_node = base.kfd_node + static_cast<uint32_t>(p);
       if (parts > 1 && s.partition_fn) {
         // kfd_topology.c: location_id = pci_dev_id | xcp node id.
         q.fn = base.fn | static_cast<uint32_t>(p);
@@ -363,7 +367,7 @@ amdsmi_status_t amdsmi_get_gpu_kfd_info(amdsmi_processor_handle h, amdsmi_kfd_in
   if (auto st = check(h, &p)) return st;
   std::memset(k, 0, sizeof(*k));
   k->kfd_id = 1000;
-  k->node_id = 0xFFFFFFFFu;  // no KFD node: the backend falls back to xcd_counter
+  k->node_id = p->kfd_node;  // default none: the backend falls back to xcd_counter
   k->current_partition_id = p->partition_id;
   return AMDSMI_STATUS_SUCCESS;
 }

@@ -1,0 +1,109 @@
+"""Both hardware backends label the same node identically.
+
+On the MI355X pool this is checked on a real (SPX) GPU
+(tests/test_gpu.py::test_label_sets_identical_across_backends).  Compute
+partitions cannot be switched there, so partitioned nodes are checked here:
+a synthetic sysfs tree read by the KFD-sysfs backend, and the scriptable
+fake amd-smi configured with the same GPUs (same PCI addresses, partition
+layout, KFD nodes) read by the amd-smi backend over the same tree - the
+labels must be byte-identical, under both partition address layouts and
+with and without the root-only partition resource files.
+"""
+
+from __future__ import annotations
+
+from pathlib import Path
+
+import pytest
+
+from conftest import run_daemon
+from gpu_feature_discovery_amd import BUILD_DIR
+from gpu_feature_discovery_amd.utils import golden, synth
+
+FAKE = BUILD_DIR / "libfake_amdsmi.so"
+
+
+def _fake_spec(root: Path, spec: synth.NodeSpec) -> str:
+    """amd-smi's view of the synthetic node: one line per readable GPU."""
+    lines = [f"partition_bdf={spec.partition_layout}", "sockets=slot"]
+    kfd = root / "sys/class/kfd/kfd/topology/nodes"
+    node = spec.cpu_sockets
+    gpu_bdfs = sorted(p.name for p in (root / "sys/bus/pci/devices").iterdir()
+                      if (p / "current_compute_partition").exists())
+    # make_node assigns buses in GPU order; recover each GPU's address from
+    # its first partition node's location_id.
+    for g in spec.gpus:
+        parts = synth.PARTITIONS_PER_MODE[g.compute_partition]
+        first = None
+        for p in range(parts):
+            props = kfd / str(node + p) / "properties"
+            if props.is_file():
+                first = first or props
+        if g.hidden or first is None:
+            node += parts
+            continue
+        loc = int(next(ln.split()[1] for ln in first.read_text().splitlines() if ln.startswith("location_id")))
+        bdf = f"0000:{loc >> 8:02x}:00.0"
+        assert bdf in gpu_bdfs
+        fields = [f"bdf={bdf}", f"mode={g.compute_partition}", f"nps={g.memory_partition}", f"parts={parts}",
+                  f"name={g.product_name}", f"cus={g.cus // parts}", f"xcds={g.xcds // parts}",
+                  f"vram_mib={(g.vram_bytes // parts) >> 20}", f"kfd_base={node}"]
+        if g.visible_partitions is not None:
+            fields.append("visible=" + ",".join(map(str, g.visible_partitions)))
+        lines.append(";".join(fields))
+        node += parts
+    return "\n".join(lines)
+
+
+CASES = {
+    "spx": dict(mode="SPX", nps="NPS1", strategy="none", n=2),
+    "cpx-single": dict(mode="CPX", nps="NPS1", strategy="single", n=2),
+    "cpx-mixed": dict(mode="CPX", nps="NPS1", strategy="mixed", n=2),
+    "dpx-nps2-mixed": dict(mode="DPX", nps="NPS2", strategy="mixed", n=2),
+    "qpx-single": dict(mode="QPX", nps="NPS1", strategy="single", n=1),
+}
+
+
+@pytest.mark.skipif(not FAKE.exists(), reason="libfake_amdsmi.so not built")
+@pytest.mark.parametrize("privileged", [False, True], ids=["pod", "privileged"])
+@pytest.mark.parametrize("layout", ["function", "shared"])
+@pytest.mark.parametrize("case", list(CASES))
+def test_amdsmi_and_sysfs_backends_label_identically(binary, tmp_path, case, layout, privileged):
+    c = CASES[case]
+    spec = synth.NodeSpec(gpus=[synth.GpuSpec(compute_partition=c["mode"], memory_partition=c["nps"])
+                                for _ in range(c["n"])],
+                          partition_layout=layout, privileged=privileged, seed=21)
+    root = synth.make_node(tmp_path / "root", spec)
+    outs = {}
+    for backend in ("sysfs", "amdsmi"):
+        out = tmp_path / f"gfd-{backend}"
+        env = {"GFD_AMDSMI_LIBRARY": str(FAKE), "GFD_FAKE_AMDSMI_SPEC": _fake_spec(root, spec).replace("\n", "|")}
+        run_daemon(binary, "--oneshot", "--no-timestamp", f"--backend={backend}", f"--sysfs-root={root}",
+                   f"--machine-type-file={root}/sys/class/dmi/id/product_name", f"--mig-strategy={c['strategy']}",
+                   f"--output-file={out}", env=env, check=True)
+        outs[backend] = out.read_text()
+    assert outs["amdsmi"] == outs["sysfs"]
+    labels = golden.parse_labels(outs["sysfs"])
+    if c["mode"] != "SPX":
+        key = "amd.com/gpu" if c["strategy"] == "single" else next(
+            k.rsplit(".", 1)[0] for k in labels if k.startswith("amd.com/partition-") and k.endswith(".count"))
+        assert (f"{key}.engines.decoder" in labels) == privileged
+        assert f"{key}.engines.dma" in labels
+
+
+@pytest.mark.skipif(not FAKE.exists(), reason="libfake_amdsmi.so not built")
+@pytest.mark.parametrize("layout", ["function", "shared"])
+def test_backends_agree_on_one_visible_partition(binary, tmp_path, layout):
+    spec = synth.NodeSpec(gpus=[synth.GpuSpec(compute_partition="CPX", visible_partitions=[5])],
+                          partition_layout=layout, seed=22)
+    root = synth.make_node(tmp_path / "root", spec)
+    outs = {}
+    for backend in ("sysfs", "amdsmi"):
+        out = tmp_path / f"gfd-{backend}"
+        env = {"GFD_AMDSMI_LIBRARY": str(FAKE), "GFD_FAKE_AMDSMI_SPEC": _fake_spec(root, spec).replace("\n", "|")}
+        run_daemon(binary, "--oneshot", "--no-timestamp", f"--backend={backend}", f"--sysfs-root={root}",
+                   f"--machine-type-file={root}/sys/class/dmi/id/product_name", "--mig-strategy=single",
+                   f"--output-file={out}", env=env, check=True)
+        outs[backend] = out.read_text()
+    assert outs["amdsmi"] == outs["sysfs"]
+    assert golden.parse_labels(outs["sysfs"])["amd.com/gpu.count"] == "1"

@@ -270,30 +270,58 @@ def _fake_amdsmi_env(spec: str) -> dict:
     return {"GFD_AMDSMI_LIBRARY": str(lib), "GFD_FAKE_AMDSMI_SPEC": spec}
 
 
+def _first_cycle(binary, out, *args, env=None):
+    """Daemon (loop) mode: start it, read the feature file of its first
+    cycle, stop it with SIGTERM; returns (labels, stderr)."""
+    e = {k: v for k, v in os.environ.items() if not k.startswith("GFD_")}
+    e.update(env or {})
+    p = subprocess.Popen([binary, "--sleep-interval=30s", f"--output-file={out}", *args], env=e,
+                         stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+    try:
+        deadline = time.monotonic() + 20
+        while not out.exists() and time.monotonic() < deadline and p.poll() is None:
+            time.sleep(0.01)
+        text = out.read_text() if out.exists() else ""
+    finally:
+        p.send_signal(signal.SIGTERM)
+        _, err = p.communicate(timeout=20)
+    return golden.parse_labels(text), err
+
+
 def test_auto_backend_uses_sysfs_when_amdsmi_fails_to_initialise(binary, tmp_path, mi355x_node):
     """amd-smi loads but amdsmi_init fails (DRIVER_NOT_LOADED): on a node
     with a KFD topology the auto backend labels from sysfs instead of failing
     (PreferenceManager; the reference has no second backend to try)."""
     root = mi355x_node(n_gpus=2)
-    out = tmp_path / "gfd"
-    cp = run_daemon(binary, "--oneshot", "--backend=auto", f"--sysfs-root={root}", f"--output-file={out}",
-                    env=_fake_amdsmi_env("init_status=34"), check=True)
-    labels = golden.parse_labels(out.read_text())
+    labels, err = _first_cycle(binary, tmp_path / "gfd", "--backend=auto", f"--sysfs-root={root}",
+                               env=_fake_amdsmi_env("init_status=34"))
     assert labels["amd.com/gpu.count"] == "2"
     assert labels["amd.com/gpu.product"].startswith("AMD-Instinct-MI355")
-    assert "amdsmi(persistent) manager failed to initialize" in cp.stderr
-    assert "Using the sysfs manager" in cp.stderr
+    assert "amdsmi(persistent) manager failed to initialize" in err
+    assert "Using the sysfs manager" in err
 
 
 def test_auto_backend_prefers_amdsmi(binary, tmp_path, mi355x_node):
+    root = mi355x_node(n_gpus=2)
+    spec = "bdf=0000:d9:00.0;mode=SPX;parts=1;cus=256;xcds=8;vram_mib=294896;links=7;virt=1"
+    labels, err = _first_cycle(binary, tmp_path / "gfd", "--backend=auto", f"--sysfs-root={root}",
+                               env=_fake_amdsmi_env(spec))
+    assert labels["amd.com/gpu.count"] == "1"  # the fake's one GPU, not the tree's two
+    assert "failed to initialize" not in err
+
+
+def test_auto_backend_oneshot_reads_kfd_without_loading_amdsmi(binary, tmp_path, mi355x_node):
+    """Job mode: a KFD topology answers everything, so amd-smi (and its
+    ~25 ms amdsmi_init) is never loaded - not even to probe it."""
     root = mi355x_node(n_gpus=2)
     out = tmp_path / "gfd"
     spec = "bdf=0000:d9:00.0;mode=SPX;parts=1;cus=256;xcds=8;vram_mib=294896;links=7;virt=1"
     cp = run_daemon(binary, "--oneshot", "--backend=auto", f"--sysfs-root={root}", f"--output-file={out}",
                     env=_fake_amdsmi_env(spec), check=True)
     labels = golden.parse_labels(out.read_text())
-    assert labels["amd.com/gpu.count"] == "1"  # the fake's one GPU, not the tree's two
-    assert "failed to initialize" not in cp.stderr
+    assert labels["amd.com/gpu.count"] == "2"  # the tree's two GPUs
+    assert "oneshot: amd-smi not loaded" in cp.stderr
+    assert "amd-smi platform" not in cp.stderr
 
 
 def test_auto_backend_without_kfd_topology_still_fails_on_init_error(binary, tmp_path):

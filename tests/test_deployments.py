@@ -52,10 +52,21 @@ def test_static_daemonsets(native, name, strategy):
     assert env["GFD_MIG_STRATEGY"] == strategy
     assert set(env) <= _env_vars(native)
     mounts = {m["mountPath"] for m in c["volumeMounts"]}
-    assert {"/etc/kubernetes/node-feature-discovery/features.d", "/sys"} <= mounts
+    assert {"/etc/kubernetes/node-feature-discovery/features.d", "/sys", "/host/opt"} <= mounts
+    _check_host_opt(spec, c)
+    assert env["GFD_HOST_ROOT"] == "/host"
     terms = spec["affinity"]["nodeAffinity"]["requiredDuringSchedulingIgnoredDuringExecution"]["nodeSelectorTerms"]
     keys = {e["key"] for t in terms for e in t["matchExpressions"]}
     assert "feature.node.kubernetes.io/pci-1002.present" in keys
+
+
+def _check_host_opt(spec, container):
+    """The node's ROCm release comes from the host's /opt (read-only), which
+    --host-root=/host points the daemon at - never from the image."""
+    vols = {v["name"]: v for v in spec["volumes"]}
+    assert vols["host-opt"]["hostPath"]["path"] == "/opt"
+    (m,) = [m for m in container["volumeMounts"] if m["name"] == "host-opt"]
+    assert m["mountPath"] == "/host/opt" and m["readOnly"] is True
 
 
 def test_job_template(native):
@@ -63,8 +74,10 @@ def test_job_template(native):
     spec = job["spec"]["template"]["spec"]
     assert spec["nodeName"] == "NODE_NAME"
     assert spec["restartPolicy"] == "Never"
-    assert "--oneshot" in spec["containers"][0]["args"]
+    args = spec["containers"][0]["args"]
+    assert "--oneshot" in args and "--backend=auto" in args and "--host-root=/host" in args
     assert spec["containers"][0]["image"].endswith(":" + _version())
+    _check_host_opt(spec, spec["containers"][0])
 
 
 def test_nfd_manifest(native):
@@ -104,3 +117,13 @@ def test_dockerfile(native):
     text = (DEPLOY / "container" / "Dockerfile").read_text()
     assert 'ENTRYPOINT ["/usr/bin/gpu-feature-discovery"]' in text
     assert "gfd_unit_tests" in text  # the build stage runs the unit tests
+    # The image must not carry a ROCm version of its own (node-true labels).
+    assert not re.search(r"^COPY .*\.info/version", text, re.M)
+
+
+def test_helm_mounts_host_opt(native):
+    text = (CHART / "templates" / "daemonset.yml").read_text()
+    assert "mountPath: /host/opt, readOnly: true" in text
+    values = native.parse_yaml((CHART / "values.yaml").read_text())
+    assert values["hostOpt"] == {"enabled": True, "path": "/opt"}
+    assert "GFD_HOST_ROOT" in (CHART / "templates" / "_helpers.tpl").read_text()

@@ -294,3 +294,57 @@ def test_synthetic_passthrough_vm(binary, tmp_path):
     labels = golden.parse_labels(_oneshot(binary, tmp_path, "--backend=sysfs", sysfs_root=str(root)))
     assert labels["amd.com/gpu.virtualization-mode"] == "passthrough"
     assert not any("sriov" in k for k in labels)
+
+
+# ---- Node-true ROCm version (--host-root / --rocm-version-file) --------------
+
+def _host(tmp_path, version: str | None, link: str = "/opt/rocm-{v}"):
+    host = tmp_path / "host"
+    (host / "opt").mkdir(parents=True)
+    if version:
+        d = host / f"opt/rocm-{version}/.info"
+        d.mkdir(parents=True)
+        (d / "version").write_text(version + "-57\n")
+        (host / "opt/rocm").symlink_to(link.format(v=version))
+    return host
+
+
+def test_host_root_labels_the_nodes_rocm_not_the_images(binary, tmp_path):
+    """The pod's own tree says 7.2 (what an image would carry); the host's
+    /opt/rocm -> /opt/rocm-6.4.1 (an absolute link, re-rooted under the mount)
+    says 6.4: the labels describe the node."""
+    root = synth.make_mi355x_node(tmp_path / "root", n_gpus=1, rocm_version="7.2.0")
+    host = _host(tmp_path, "6.4.1")
+    labels = golden.parse_labels(_oneshot(binary, tmp_path, "--backend=sysfs", f"--host-root={host}",
+                                          sysfs_root=str(root)))
+    assert (labels["amd.com/rocm.runtime.major"], labels["amd.com/rocm.runtime.minor"]) == ("6", "4")
+
+
+def test_driver_only_host_gets_no_runtime_labels(binary, tmp_path):
+    root = synth.make_mi355x_node(tmp_path / "root", n_gpus=1, rocm_version="7.2.0")
+    host = _host(tmp_path, None)
+    out = tmp_path / "gfd"
+    cp = run_daemon_checked(binary, tmp_path, root, f"--host-root={host}", out=out)
+    labels = golden.parse_labels(out.read_text())
+    assert "amd.com/rocm.runtime.major" not in labels
+    assert labels["amd.com/driver.major"] == "6"
+    assert "no ROCm release found on the node" in cp.stderr
+
+
+def test_explicit_rocm_version_file(binary, tmp_path):
+    root = synth.make_mi355x_node(tmp_path / "root", n_gpus=1, rocm_version="7.2.0")
+    f = tmp_path / "version"
+    f.write_text("6.3.3\n")
+    labels = golden.parse_labels(_oneshot(binary, tmp_path, "--backend=sysfs", f"--rocm-version-file={f}",
+                                          sysfs_root=str(root)))
+    assert labels["amd.com/rocm.runtime.minor"] == "3"
+    cp = run_daemon(binary, "--oneshot", "--backend=sysfs", f"--sysfs-root={root}", "--output-file=",
+                    f"--rocm-version-file={tmp_path / 'missing'}")
+    assert cp.returncode == 1
+    assert "unable to read the ROCm version file" in cp.stderr
+
+
+def run_daemon_checked(binary, tmp_path, root, *args, out):
+    return run_daemon(binary, "--oneshot", "--no-timestamp", "--backend=sysfs", f"--sysfs-root={root}",
+                      f"--machine-type-file={root}/sys/class/dmi/id/product_name", f"--output-file={out}", *args,
+                      check=True)

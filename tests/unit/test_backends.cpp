@@ -144,8 +144,8 @@ TEST(Sysfs_EnumeratesSpxAndCpxGpus) {
   EXPECT_EQ(spx.Info().compute_partition, std::string("SPX"));
   EXPECT_EQ(spx.Info().available_memory_partitions, (std::vector<std::string>{"NPS1", "NPS2"}));
   EXPECT_EQ(m.GetDriverVersion(), std::string("6.12.12"));
-  EXPECT_EQ(m.GetRuntimeVersion().major, 7u);
-  EXPECT_EQ(m.GetRuntimeVersion().minor, 2u);
+  EXPECT_EQ(m.GetRuntimeVersion()->major, 7u);
+  EXPECT_EQ(m.GetRuntimeVersion()->minor, 2u);
   m.Shutdown();
 }
 
@@ -230,6 +230,96 @@ TEST(Versions_Extract) {
   EXPECT_FALSE(extract_version("no version here 7").has_value());
 }
 
+// ---- Node-true ROCm version (resource/versions.h) ----
+
+namespace {
+std::string mktemp_dir() {
+  char d[] = "/tmp/gfd-rocm-XXXXXX";
+  if (!mkdtemp(d)) throw std::runtime_error("mkdtemp");
+  return d;
+}
+void link(const std::string& target, const std::string& path) {
+  fs::mkdir_all(fs::dirname(path));
+  EXPECT_EQ(symlink(target.c_str(), path.c_str()), 0);
+}
+}  // namespace
+
+TEST(ResolveInRoot_FollowsHostSymlinksUnderTheMount) {
+  std::string host = mktemp_dir();
+  put(host + "/opt/rocm-6.4.1/.info/version", "6.4.1-120\n");
+  link("/opt/rocm-6.4.1", host + "/opt/rocm");         // absolute: re-rooted
+  link("rocm-6.4.1", host + "/opt/rocm-rel");          // relative
+  link("../opt/./rocm", host + "/usr/rocm-up");        // .. and . through another link
+  EXPECT_EQ(fs::resolve_in_root(host, "opt/rocm/.info/version"), host + "/opt/rocm-6.4.1/.info/version");
+  EXPECT_EQ(fs::resolve_in_root(host, "/opt/rocm-rel/.info/version"), host + "/opt/rocm-6.4.1/.info/version");
+  EXPECT_EQ(fs::resolve_in_root(host, "usr/rocm-up/.info/version"), host + "/opt/rocm-6.4.1/.info/version");
+  EXPECT_EQ(fs::resolve_in_root(host, "../../../opt/rocm/.info/version"), host + "/opt/rocm-6.4.1/.info/version");
+  EXPECT_EQ(fs::resolve_in_root(host, "opt/missing/.info/version"), std::string());
+  link("/loop-b", host + "/loop-a");
+  link("/loop-a", host + "/loop-b");
+  EXPECT_EQ(fs::resolve_in_root(host, "loop-a/x"), std::string());
+  fs::remove_all(host);
+}
+
+TEST(RocmVersion_HostRootWinsOverTheImage) {
+  std::string image = mktemp_dir(), host = mktemp_dir();
+  put(image + "/opt/rocm/.info/version", "7.2.0\n");  // the container image's own
+  put(host + "/opt/rocm-6.4.1/.info/version", "6.4.1-120\n");
+  link("/opt/rocm-6.4.1", host + "/opt/rocm");
+  VersionSources s;
+  s.root = image;
+  std::string source;
+  EXPECT_EQ(rocm_version(s)->major, 7u);  // without a host root: this root
+  s.host_root = host;
+  auto v = rocm_version(s, &source);
+  EXPECT_TRUE(v.has_value());
+  EXPECT_EQ(v->major, 6u);
+  EXPECT_EQ(v->minor, 4u);
+  EXPECT_EQ(source, host + "/opt/rocm-6.4.1/.info/version");
+  fs::remove_all(image);
+  fs::remove_all(host);
+}
+
+TEST(RocmVersion_AlternativesLinkOutsideTheMountUsesNewestInstall) {
+  std::string host = mktemp_dir();
+  put(host + "/opt/rocm-6.4.1/.info/version", "6.4.1\n");
+  put(host + "/opt/rocm-7.0.2/.info/version", "7.0.2\n");
+  put(host + "/opt/rocm-7.10.0/.info/version", "7.10.0\n");  // numeric, not lexical, order
+  link("/etc/alternatives/rocm", host + "/opt/rocm");  // /etc is not mounted
+  VersionSources s;
+  s.host_root = host;
+  auto v = rocm_version(s);
+  EXPECT_TRUE(v.has_value());
+  EXPECT_EQ(v->major, 7u);
+  EXPECT_EQ(v->minor, 10u);
+  fs::remove_all(host);
+}
+
+TEST(RocmVersion_DriverOnlyHostHasNone) {
+  std::string image = mktemp_dir(), host = mktemp_dir();
+  put(image + "/opt/rocm/.info/version", "7.2.0\n");
+  fs::mkdir_all(host + "/opt/containerd");
+  VersionSources s;
+  s.root = image;
+  s.host_root = host;
+  EXPECT_FALSE(rocm_version(s).has_value());  // never the image's version
+  fs::remove_all(image);
+  fs::remove_all(host);
+}
+
+TEST(RocmVersion_ExplicitFileMustBeReadable) {
+  std::string d = mktemp_dir();
+  VersionSources s;
+  s.rocm_version_file = d + "/version";
+  EXPECT_THROW_MSG(rocm_version(s), "unable to read the ROCm version file");
+  put(d + "/version", "not a version\n");
+  EXPECT_THROW_MSG(rocm_version(s), "not X.Y[.Z]");
+  put(d + "/version", "6.3.3\n");
+  s.host_root = "/nonexistent";  // the explicit file wins
+  EXPECT_EQ(rocm_version(s)->minor, 3u);
+  fs::remove_all(d);
+}
+
 TEST(MockFixture_Loads) {
   auto m = mock_manager_from_node(yaml::parse(R"(
 driverVersion: 6.8.5
@@ -250,7 +340,7 @@ devices:
 )"));
   EXPECT_EQ(m->devices.size(), static_cast<size_t>(2));
   EXPECT_EQ(m->driver_version, std::string("6.8.5"));
-  EXPECT_EQ(m->runtime_version.minor, 4u);
+  EXPECT_EQ(m->runtime_version->minor, 4u);
   EXPECT_TRUE(m->devices[0]->IsPartitionCapable());
   EXPECT_EQ(m->devices[0]->GetGfxTarget().name(), std::string("gfx942"));
   EXPECT_EQ(m->devices[1]->GetPartitions()[0]->GetAttributes().at("memory"), std::string("24576"));

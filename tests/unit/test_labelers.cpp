@@ -266,18 +266,28 @@ TEST(NodeFacts_PrefetchedVersionsMatchManager) {
   lm::write_file_atomically(root + "/sys/module/amdgpu/version", "6.12.12\n", 0644);
   config::Config c;
   c.flags.gfd.machine_type_file = root + "/missing-dmi";
-  lm::NodeFacts f = lm::ReadNodeFacts(c, root);
+  resource::VersionSources src;
+  src.root = root;
+  lm::NodeFacts f = lm::ReadNodeFacts(c, src);
   EXPECT_TRUE(f.have_versions);
   EXPECT_EQ(f.driver_version, std::string("6.12.12"));
   EXPECT_FALSE(f.runtime_version.has_value());  // no opt/rocm/.info/version in this root
+  EXPECT_TRUE(f.runtime_error.empty());         // ... which is not an error: no ROCm on the node
   EXPECT_EQ(f.machine, (Labels{{"amd.com/gpu.machine", "unknown"}}));
   EXPECT_TRUE(f.machine_warning.find("error getting machine type") != std::string::npos);
   resource::MockManager m({resource::new_full_gpu()});
+  auto no_rocm = lm::NewDeviceLabeler(m, c, [&]() -> const lm::NodeFacts& { return f; })->GetLabels();
+  EXPECT_EQ(no_rocm["amd.com/driver.major"], std::string("6"));
+  EXPECT_EQ(no_rocm.count("amd.com/rocm.runtime.major"), static_cast<size_t>(0));
+  // An explicitly configured version file that cannot be read is an error.
+  resource::VersionSources bad = src;
+  bad.rocm_version_file = root + "/nope";
+  f = lm::ReadNodeFacts(c, bad);
   EXPECT_THROW_MSG(lm::NewDeviceLabeler(m, c, [&]() -> const lm::NodeFacts& { return f; }),
-                   "error getting ROCm runtime version: unable to determine the ROCm version");
+                   "error getting ROCm runtime version: unable to read the ROCm version file");
   fs::mkdir_all(root + "/opt/rocm/.info");
   lm::write_file_atomically(root + "/opt/rocm/.info/version", "7.2.0-43\n", 0644);
-  f = lm::ReadNodeFacts(c, root);
+  f = lm::ReadNodeFacts(c, src);
   auto l = lm::NewDeviceLabeler(m, c, [&]() -> const lm::NodeFacts& { return f; })->GetLabels();
   EXPECT_EQ(l["amd.com/driver.minor"], std::string("12"));
   EXPECT_EQ(l["amd.com/rocm.runtime.major"], std::string("7"));

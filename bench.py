@@ -26,7 +26,13 @@ and the MAX wall time over ranks is reported.  Scaling is "weak": the work
 per visible GPU is fixed and total work grows with N.
 
 Without a usable GPU (CPU container) the benchmark runs the KFD-sysfs backend
-over a synthetic N-GPU MI355X tree and says so in "data".
+over a synthetic N-GPU MI355X tree and says so in "data"; with
+GFD_AMDSMI_LIBRARY pointing at the test double (build/libfake_amdsmi.so) it
+rehearses the amd-smi path on CPU.
+
+Besides the headline (back-to-back cycles) the JSON carries the deployed
+daemon's first cycle, its cycles 1 s apart on idle cores (cold_cycle), the
+Job-mode process from spawn to exit, and per-phase p50s of the timed steps.
 """
 
 from __future__ import annotations
@@ -115,18 +121,25 @@ def _time_variant(args: list[str], steps: int, warmup: int) -> dict:
             "mean_ms": round(statistics.fmean(ms), 4), "backend": r["backend"]}
 
 
-def _daemon_loop(binary: str, args: list[str], cycles: int) -> dict:
+def _daemon_loop(binary: str, args: list[str], cycles: int, interval: str = "2ms",
+                 env: dict | None = None) -> dict:
     """The production path: the daemon binary in loop mode, timing every
-    cycle itself (--trace-timing), stopped with SIGTERM."""
+    cycle itself (--trace-timing), stopped with SIGTERM.  With a long
+    `interval` every cycle after the first starts on idle, down-clocked
+    cores - what a deployed DaemonSet (60 s between cycles) sees."""
     import signal
 
-    p = subprocess.Popen([binary, "--sleep-interval=2ms", "--trace-timing", *args], stdout=subprocess.DEVNULL,
-                         stderr=subprocess.PIPE, text=True)
-    totals = []
+    p = subprocess.Popen([binary, f"--sleep-interval={interval}", "--trace-timing", *args], stdout=subprocess.DEVNULL,
+                         stderr=subprocess.PIPE, text=True, env={**os.environ, **(env or {})})
+    totals, phases = [], {}
     try:
         for line in p.stderr:
             if "Timing:" in line:
-                totals.append(float(line.rsplit("total=", 1)[1].strip().rstrip("ms")))
+                fields = dict(kv.split("=", 1) for kv in line.split("Timing:", 1)[1].split())
+                totals.append(float(fields["total"].rstrip("ms")))
+                if len(totals) > 1:
+                    for k, v in fields.items():
+                        phases.setdefault(k, []).append(float(v.rstrip("ms")))
                 if len(totals) >= cycles:
                     break
     finally:
@@ -136,20 +149,29 @@ def _daemon_loop(binary: str, args: list[str], cycles: int) -> dict:
         except subprocess.TimeoutExpired:
             p.kill()
     steady = totals[1:] or totals
-    return {"first_cycle_ms": round(totals[0], 3) if totals else None,
+    return {"interval": interval, "first_cycle_ms": round(totals[0], 3) if totals else None,
             "p50_ms": round(_percentile(steady, 0.5), 4), "p90_ms": round(_percentile(steady, 0.9), 4),
-            "cycles": len(totals)}
+            "cycles": len(totals),
+            "phases_p50_ms": {k: round(_percentile(v, 0.5), 4) for k, v in phases.items() if k != "total"}}
 
 
 def _cold_process(binary: str, args: list[str], runs: int) -> dict:
-    """Oneshot Job mode: fork+exec the daemon binary per label file."""
+    """Oneshot Job mode: fork+exec the daemon binary per label file (the
+    whole process: start, backend selection, one cycle, exit)."""
     ms = []
     for _ in range(runs):
         t0 = time.perf_counter_ns()
         subprocess.run([binary, "--oneshot", *args], check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
                        timeout=60)
         ms.append((time.perf_counter_ns() - t0) / 1e6)
-    return {"p50_ms": round(_percentile(ms, 0.5), 3), "p90_ms": round(_percentile(ms, 0.9), 3), "runs": runs}
+    return {"p50_ms": round(_percentile(ms, 0.5), 3), "p90_ms": round(_percentile(ms, 0.9), 3), "runs": runs,
+            "args": " ".join(a for a in args if not a.startswith(("--output-file", "--sysfs-root", "--machine")))}
+
+
+def _fake_amdsmi() -> str | None:
+    """GFD_AMDSMI_LIBRARY pointing at the test double: a CPU rehearsal."""
+    lib = os.environ.get("GFD_AMDSMI_LIBRARY", "")
+    return lib if "fake" in os.path.basename(lib) else None
 
 
 def main() -> int:
@@ -159,6 +181,8 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--backend", default="auto", help="auto | amdsmi | sysfs | synthetic")
     ap.add_argument("--no-extras", action="store_true", help="skip the secondary measurements")
+    ap.add_argument("--cold-cycles", type=int, default=env_int("GFD_BENCH_COLD_CYCLES", 8),
+                    help="daemon cycles 1 s apart for the cold-cycle measurement (0: skip)")
     ap.add_argument("--sysfs-root", default=None,
                     help="with --backend sysfs: read this root instead of / (tools/hybrid_root.py builds one that "
                          "shows every GPU of a shared host)")
@@ -233,29 +257,48 @@ def main() -> int:
     if dist.rank == 0:
         p50 = _percentile(ms, 0.5)
         backend_name = session.backend
-        phases = {name: round(v, 4) for name, v in session.cycle(write=True).phases_ms}
+        phases = {name: round(_percentile(v, 0.5), 4) for name, v in session.bench_phases().items()}
         # Release the persistent amd-smi session before measuring variants
         # that must pay amdsmi_init themselves.
         del session
         gc.collect()
-        extras = {"phases_ms": phases}
+        extras: dict = {}
+        cold, first_cycle = None, None
+        fake = _fake_amdsmi()
         if not a.no_extras:
             sess_backend = "sysfs" if backend == "synthetic" else backend
+            loop_args = _session_args(sess_backend, n, out, root, [])
             try:
                 binary = str(gfd.binary_path())
                 runs = max(5, min(30, a.steps // 10))
-                extras["daemon_loop"] = _daemon_loop(binary, _session_args(sess_backend, n, out, root, []),
-                                                     max(20, min(a.steps, 300)))
+                extras["daemon_loop"] = _daemon_loop(binary, loop_args, max(20, min(a.steps, 300)))
+                first_cycle = extras["daemon_loop"]["first_cycle_ms"]
+                # Deployed cadence: cycles after >= 1 s of idle (the daemon
+                # sleeps 60 s), each starting on cold, down-clocked cores.
+                if a.cold_cycles > 1:
+                    cold = _daemon_loop(binary, loop_args, a.cold_cycles, interval="1s")
+                    extras["cold_cycle_inline_tasks"] = _daemon_loop(binary, loop_args, a.cold_cycles, interval="1s",
+                                                                    env={"GFD_CYCLE_TASKS": "inline"})
                 if backend == "amdsmi":
                     extras["amdsmi_per_cycle_session"] = _time_variant(
                         _session_args("amdsmi", n, out, None, ["--amdsmi-session=per-cycle"]), max(10, a.steps // 10), 2)
                     extras["sysfs_backend"] = _time_variant(_session_args("sysfs", n, out, None, []), a.steps, a.warmup)
-                extras["oneshot_process"] = _cold_process(binary, _session_args(sess_backend, n, out, root, []), runs)
+                # Job mode as deployed (the Job template: --backend=auto),
+                # the whole process from spawn to exit.
+                extras["oneshot_process"] = _cold_process(binary, _session_args("auto", n, out, root, []), runs)
                 if backend == "amdsmi":
-                    extras["oneshot_process_sysfs"] = _cold_process(binary, _session_args("sysfs", n, out, None, []),
-                                                                    runs)
+                    extras["oneshot_process_amdsmi"] = _cold_process(binary, _session_args("amdsmi", n, out, None, []),
+                                                                     runs)
             except (FileNotFoundError, subprocess.SubprocessError, ValueError) as e:
                 extras["error"] = str(e)
+        if backend == "amdsmi" and fake:
+            data = f"CPU rehearsal: fake amd-smi library ({os.path.basename(fake)}), {n} scripted MI355X GPU(s)"
+        elif backend == "amdsmi":
+            data = "real MI355X via amd-smi (live driver queries every step)"
+        elif backend == "sysfs":
+            data = f"real MI355X via KFD sysfs under {root}" if root else "real MI355X via KFD sysfs"
+        else:
+            data = f"synthetic {n}-GPU MI355X sysfs tree (random device IDs), no GPU available"
         result = {
             "metric": METRIC,
             "value": round(p50, 4),
@@ -268,10 +311,7 @@ def main() -> int:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "n/a",
-            "data": ("real MI355X via amd-smi (live driver queries every step)" if backend == "amdsmi"
-                     else f"real MI355X via KFD sysfs under {root}" if backend == "sysfs" and root
-                     else "real MI355X via KFD sysfs" if backend == "sysfs"
-                     else f"synthetic {n}-GPU MI355X sysfs tree (random device IDs), no GPU available"),
+            "data": data,
             "config": {
                 "model": f"{n}xMI355X SPX/NPS1 node, amd.com label set",
                 "global_batch": n,
@@ -282,6 +322,14 @@ def main() -> int:
             },
             "p90_ms": round(_percentile(ms, 0.9), 4),
             "mean_ms": round(statistics.fmean(ms), 4) if ms else None,
+            # Per-phase p50 over the K timed steps: what an N-GPU cycle
+            # spends where (the scaling curve's explanation).
+            "phases_p50_ms": phases,
+            # The deployed daemon's first cycle (library init included) and
+            # its cycles after an idle second (see _daemon_loop).
+            "first_cycle_ms": first_cycle,
+            "cold_cycle": cold,
+            "oneshot_process_p50_ms": extras.get("oneshot_process", {}).get("p50_ms"),
             "labels_ok": labels_ok,
             "label_problems": problems,
             "n_labels": len(labels),

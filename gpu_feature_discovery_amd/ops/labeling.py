@@ -60,6 +60,10 @@ class Labeler:
         loop (no Python between cycles); returns per-cycle milliseconds."""
         return [ns / 1e6 for ns in self._session.bench(steps, warmup, write)]
 
+    def bench_phases(self) -> dict[str, list[float]]:
+        """Per-phase milliseconds of the last ``bench`` call's timed cycles."""
+        return {name: [ns / 1e6 for ns in v] for name, v in self._session.bench_phases().items()}
+
 
 def label_once(args: Sequence[str] = ()) -> CycleResult:
     """Labels of one cycle, without writing the output file."""

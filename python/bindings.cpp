@@ -121,18 +121,21 @@ class Session {
   }
 
   // Tight loop in native code: `warmup` untimed cycles, then `steps` timed
-  // cycles; returns per-cycle wall time in ns.
+  // cycles; returns per-cycle wall time in ns.  The timed cycles' phase
+  // times are kept for bench_phases().
   std::vector<int64_t> bench(int steps, int warmup, bool write) {
     std::vector<int64_t> out;
     out.reserve(static_cast<size_t>(steps));
     py::gil_scoped_release nogil;
     bool was_quiet = log::set_quiet(true);
+    phases_.clear();
     try {
       for (int i = 0; i < warmup; ++i) cli::label_cycle(*manager_, sriov_, config_, timestamp_, write);
       for (int i = 0; i < steps; ++i) {
         int64_t t0 = trace::now_ns();
-        cli::label_cycle(*manager_, sriov_, config_, timestamp_, write);
+        cli::CycleResult r = cli::label_cycle(*manager_, sriov_, config_, timestamp_, write);
         out.push_back(trace::now_ns() - t0);
+        for (const auto& [name, ns] : r.phases) phases_[name].push_back(ns);
       }
     } catch (...) {
       log::set_quiet(was_quiet);
@@ -156,6 +159,9 @@ class Session {
     return l;
   }
 
+  // Per-phase times (ns) of the last bench()'s timed cycles.
+  std::map<std::string, std::vector<int64_t>> bench_phases() const { return phases_; }
+
   std::string backend() const { return manager_->Name(); }
   std::string config_json() const { return config::to_json(config_); }
 
@@ -170,6 +176,7 @@ class Session {
   resource::ManagerPtr manager_;
   std::shared_ptr<sriov::Interface> sriov_;
   lm::LabelerPtr timestamp_;
+  std::map<std::string, std::vector<int64_t>> phases_;
 };
 
 }  // namespace
@@ -206,6 +213,7 @@ PYBIND11_MODULE(_gfd, m) {
            py::arg("args") = std::vector<std::string>{}, py::arg("env") = py::none())
       .def("cycle", &Session::cycle, py::arg("write") = true)
       .def("bench", &Session::bench, py::arg("steps"), py::arg("warmup") = 0, py::arg("write") = true)
+      .def("bench_phases", &Session::bench_phases)
       .def("devices", &Session::devices)
       .def("run_loop", &Session::run_loop)
       .def_property_readonly("backend", &Session::backend)

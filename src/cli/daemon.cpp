@@ -156,22 +156,31 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
   };
   // Both on one worker, in that order: two workers measured slower (each
   // task 1.5-4x longer on the second, colder core).  GFD_CYCLE_TASKS=split
-  // submits them separately (for A/B measurements).
-  static const bool split = [] {
+  // submits them separately, =inline runs both on this thread (facts when
+  // the labeler needs them, the scan after it) - for A/B measurements.
+  enum class Tasks { sequence, split, inline_ };
+  static const Tasks mode = [] {
     const char* v = std::getenv("GFD_CYCLE_TASKS");
-    return v && std::string(v) == "split";
+    std::string m = v ? v : "";
+    return m == "split" ? Tasks::split : m == "inline" ? Tasks::inline_ : Tasks::sequence;
   }();
   WorkerPool::Task facts_task, sriov_task;
-  if (split) {
+  bool facts_done = false;
+  if (mode == Tasks::split) {
     facts_task = WorkerPool::instance().submit(read_facts);
     sriov_task = WorkerPool::instance().submit(scan_sriov);
-  } else {
+  } else if (mode == Tasks::sequence) {
     auto seq = WorkerPool::instance().submit_sequence({read_facts, scan_sriov});
     facts_task = seq[0];
     sriov_task = seq[1];
   }
   auto join_facts = [&]() -> const lm::NodeFacts& {
-    facts_task.run_or_wait();
+    if (mode != Tasks::inline_) {
+      facts_task.run_or_wait();
+    } else if (!facts_done) {
+      read_facts();
+      facts_done = true;
+    }
     return facts;
   };
   lm::LabelerPtr device;
@@ -179,12 +188,18 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
     device = GFD_WRAP("error creating device labeler", lm::NewDeviceLabeler(manager, config, join_facts));
   } catch (...) {
     // Neither task may outlive this frame (they write its locals).
-    facts_task.cancel_or_wait();
-    sriov_task.cancel_or_wait();
+    if (mode != Tasks::inline_) {
+      facts_task.cancel_or_wait();
+      sriov_task.cancel_or_wait();
+    }
     throw;
   }
-  facts_task.cancel_or_wait();  // no devices: the labeler never needed them
-  sriov_task.run_or_wait();
+  if (mode != Tasks::inline_) {
+    facts_task.cancel_or_wait();  // no devices: the labeler never needed them
+    sriov_task.run_or_wait();
+  } else {
+    scan_sriov();
+  }
   trace::record("facts(overlapped)", facts_ns);
   trace::record("sriov(overlapped)", sriov_ns);
   if (sriov_error) {

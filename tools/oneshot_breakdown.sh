@@ -32,7 +32,7 @@ for name, cmd in [("/bin/true", ["/bin/true"]),
 PY
   for b in null sysfs auto amdsmi; do
     echo "## --oneshot --backend=$b --trace-timing"
-    timeout -k 5 60 "$bin" --oneshot --backend=$b --trace-timing -o "$out/gfd" 2>&1 | grep -E "Timing|Using|Detected" || exit 1
+    timeout -k 5 60 "$bin" --oneshot --backend=$b --trace-timing -o "$out/gfd" 2>&1 | grep -iE "timing:|Using|Detected" || exit 1
   done
   echo "## LD_DEBUG=statistics --version"
   LD_DEBUG=statistics timeout -k 5 30 "$bin" --version 2>&1 | grep -E "time|relocations" | head -12

@@ -32,8 +32,8 @@ def _free_port() -> int:
 
 
 def test_single_process_contract():
-    cp = subprocess.run([sys.executable, "bench.py", "--steps", "30", "--warmup", "3", "--backend", "synthetic"],
-                        capture_output=True, text=True, timeout=300, cwd=str(REPO))
+    cp = subprocess.run([sys.executable, "bench.py", "--steps", "30", "--warmup", "3", "--backend", "synthetic",
+                         "--cold-cycles", "2"], capture_output=True, text=True, timeout=300, cwd=str(REPO))
     assert cp.returncode == 0, cp.stderr[-3000:]
     lines = _json_lines(cp.stdout)
     assert len(lines) == 1
@@ -45,8 +45,13 @@ def test_single_process_contract():
     assert r["labels_ok"] is True, r["label_problems"]
     assert "synthetic" in r["data"]
     assert 0 < r["value"] < 50
-    assert {"init", "enumerate", "label", "write"} <= set(r["extras"]["phases_ms"])
+    assert {"init", "enumerate", "label", "write"} <= set(r["phases_p50_ms"])
     assert r["extras"]["oneshot_process"]["p50_ms"] > 0
+    assert "--backend=auto" in r["extras"]["oneshot_process"]["args"]  # the Job template's backend
+    assert r["oneshot_process_p50_ms"] == r["extras"]["oneshot_process"]["p50_ms"]
+    assert r["first_cycle_ms"] > 0
+    assert r["cold_cycle"]["interval"] == "1s" and r["cold_cycle"]["cycles"] == 2
+    assert r["cold_cycle"]["p50_ms"] > 0 and "write" in r["cold_cycle"]["phases_p50_ms"]
 
 
 @pytest.mark.parametrize("n", [2, 4, 8])
@@ -71,3 +76,41 @@ def test_two_ranks_gloo():
     assert r["n_gpus"] == 2 and r["labels_ok"] is True
     assert "2 rank(s)" in r["config"]["parallelism"]
     assert r["ms_per_step"] > 0
+
+
+def test_driver_n8_command_over_fake_amdsmi(tmp_path):
+    """The exact command the driver runs for the 8-GPU scaling point
+    (torch.distributed.run, 8 ranks, 127.0.0.1), rehearsed on CPU: rank 0
+    labels 8 MI355X GPUs through the amd-smi backend over the scriptable fake
+    library (gloo for the barriers).  Checks the JSON contract and the 8-GPU
+    label set: gpu.count=8 and the per-GPU xGMI links (7)."""
+    import os
+
+    fake = REPO / "build" / "libfake_amdsmi.so"
+    if not fake.exists():
+        pytest.skip("libfake_amdsmi.so not built")
+    spec = "|".join(f"bdf=0000:{0x10 + 0x10 * i:02x}:00.0;mode=SPX;parts=1;cus=256;xcds=8;vram_mib=294896;links=7"
+                    for i in range(8))
+    env = {**os.environ, "GFD_AMDSMI_LIBRARY": str(fake), "GFD_FAKE_AMDSMI_SPEC": spec, "GFD_BENCH_COLD_CYCLES": "2",
+           "OMP_NUM_THREADS": "1"}
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "8", "--steps", "20", "--warmup", "2"]
+    cp = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd=str(REPO), env=env)
+    assert cp.returncode == 0, cp.stderr[-3000:]
+    lines = _json_lines(cp.stdout)
+    assert len(lines) == 1, cp.stdout  # rank 0 only
+    r = lines[0]
+    assert REQUIRED <= set(r)
+    assert r["n_gpus"] == 8 and r["steps"] == 20 and r["warmup"] == 2
+    assert r["labels_ok"] is True, r["label_problems"]
+    assert r["config"]["backend"] == "amdsmi(persistent)"
+    assert "8 rank(s)" in r["config"]["parallelism"] and r["config"]["global_batch"] == 8
+    assert "fake amd-smi" in r["data"]
+    assert {"amdsmi.snapshot", "enumerate", "write"} <= set(r["phases_p50_ms"])
+    assert r["cold_cycle"]["cycles"] == 2
+    out = subprocess.run([str(REPO / "build" / "gpu-feature-discovery"), "--oneshot", "--backend=amdsmi",
+                          "--output-file=", "--no-timestamp"], capture_output=True, text=True, timeout=60, env=env)
+    labels = dict(ln.split("=", 1) for ln in out.stdout.splitlines())
+    assert labels["amd.com/gpu.count"] == "8"
+    assert labels["amd.com/gpu.xgmi.links"] == "7"

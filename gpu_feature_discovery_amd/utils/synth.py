@@ -2,7 +2,7 @@
 
 Builds the subset of ``/sys`` (plus ``/opt/rocm/.info/version``) that the
 daemon's KFD-sysfs backend and SR-IOV scanner read, laid out exactly like the
-MI355X pool (verified by tools/probe_box.sh; see profiles/hw_probe.md):
+MI355X pool (verified by tools/hw_probe.sh; see profiles/hw_probe.md):
 
 * ``sys/class/kfd/kfd/topology/nodes/N/properties`` and ``mem_banks`` - one
   node per CPU socket, then one node per GPU (SPX) or per compute partition

@@ -38,13 +38,7 @@ Labels ResourceLabeler::replicas_label() const {
 Labels ResourceLabeler::base_labels(int count, const std::vector<std::string>& parts) const {
   Labels l = product_label(parts);
   update(l, "count", std::to_string(count));
-  int replicas = 1;
-  if (sharing_disabled()) {
-    replicas = 0;
-  } else if (const auto* r = replication_info(); r && r->replicas > 1) {
-    replicas = r->replicas;
-  }
-  update(l, "replicas", std::to_string(replicas));
+  l.merge(replicas_label());  // disjoint keys
   return l;
 }
 
@@ -137,14 +131,14 @@ Labels new_gpu_labels(resource::Manager& manager, const config::Config& config) 
   if (auto it = by_partitioned.find(true); it != by_partitioned.end()) {
     for (const auto& d : it->second) {
       std::string name = GFD_WRAP("error getting device name", d->GetName());
-      partitioned.emplace(name, d);
+      partitioned[name] = d;  // the last device of a model represents it (map assignment, mig-strategy.go:132)
       counts[name]++;
     }
   }
   if (auto it = by_partitioned.find(false); it != by_partitioned.end()) {
     for (const auto& d : it->second) {
       std::string name = GFD_WRAP("error getting device name", d->GetName());
-      full.emplace(name, d);
+      full[name] = d;  // mig-strategy.go:142
       counts[name]++;
     }
   }

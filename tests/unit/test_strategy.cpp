@@ -214,3 +214,18 @@ TEST(DeviceInfo_IsPartitionedErrorPropagates) {
   partition::DeviceInfo di(m);
   EXPECT_THROW_MSG(di.GetDevicesMap(), "driver gone");
 }
+
+// Several GPUs of one model: the reference keeps the LAST device of each
+// name in a map (mig-strategy.go:129-142), so its memory is what the labels
+// report when same-named GPUs differ (e.g. after a RAS page retirement).
+TEST(StrategyNone_LastDeviceOfAModelRepresentsIt) {
+  auto a = new_full_gpu();
+  auto b = new_full_gpu();
+  a->mutable_info().memory_mib = 294896;
+  b->mutable_info().memory_mib = 294880;  // 16 MiB retired
+  Labels l = resource_labels({a, b}, strategy_config("none"));
+  EXPECT_EQ(l["amd.com/gpu.count"], std::string("2"));
+  EXPECT_EQ(l["amd.com/gpu.memory"], std::string("294880"));
+  l = resource_labels({b, a}, strategy_config("none"));
+  EXPECT_EQ(l["amd.com/gpu.memory"], std::string("294896"));
+}

@@ -75,6 +75,7 @@ class NodeSpec:
     hypervisor: bool = False  # CPU "hypervisor" flag (running inside a VM)
     partition_layout: str = "function"  # "function" | "shared" (see module docstring)
     rocm_version_file: bool = True  # write opt/rocm/.info/version
+    gim_version: str | None = None  # SR-IOV host driver (GIM) loaded: sys/module/gim/version
 
 
 def _write(path: Path, text: str | bytes) -> None:
@@ -167,6 +168,8 @@ def make_node(root: str | os.PathLike, spec: NodeSpec) -> Path:
     topo = root / "sys/class/kfd/kfd/topology"
     _write(topo / "generation_id", "1\n")
     _write(root / "sys/module/amdgpu/version", spec.driver_version + "\n")
+    if spec.gim_version:
+        _write(root / "sys/module/gim/version", spec.gim_version + "\n")
     if spec.partition_layout not in ("function", "shared"):
         raise ValueError(f"unknown partition_layout {spec.partition_layout!r}")
     if spec.rocm_version_file:

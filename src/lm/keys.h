@@ -37,6 +37,7 @@ inline constexpr const char* kSriovPresent = "amd.com/sriov.present";
 inline constexpr const char* kSriovRole = "amd.com/sriov.role";
 inline constexpr const char* kSriovNumVfs = "amd.com/sriov.num-vfs";
 inline constexpr const char* kSriovTotalVfs = "amd.com/sriov.total-vfs";
+inline constexpr const char* kSriovHostDriverVersion = "amd.com/sriov.host-driver-version";
 
 // Full-GPU resource and the prefix of per-profile partition resources.
 inline constexpr const char* kFullGpuResource = "amd.com/gpu";

@@ -173,6 +173,8 @@ class SriovLabeler : public Labeler {
     if (any_pf) {
       l[keys::kSriovTotalVfs] = std::to_string(total);
       l[keys::kSriovNumVfs] = std::to_string(num);
+      // vgpu.go:44-52 labels the host driver; an MxGPU host's is GIM.
+      if (auto v = lib_->HostDriverVersion()) l[keys::kSriovHostDriverVersion] = sanitize_label_value(*v);
     }
     return l;
   }

@@ -81,6 +81,13 @@ std::vector<Function> Lib::Devices() {
   return out;
 }
 
+std::optional<std::string> Lib::HostDriverVersion() {
+  if (root_.empty()) return std::nullopt;
+  auto v = fs::attrs().read_trimmed(fs::join(root_, "sys/module/gim/version"));
+  if (!v || v->empty()) return std::nullopt;
+  return v;
+}
+
 namespace {
 class EmptyLib : public Interface {
  public:
@@ -89,7 +96,7 @@ class EmptyLib : public Interface {
 }  // namespace
 
 std::shared_ptr<Interface> new_sriov_lib(const std::string& root) {
-  return std::make_shared<Lib>(std::make_shared<SysfsAmdPCI>(root));
+  return std::make_shared<Lib>(std::make_shared<SysfsAmdPCI>(root), root);
 }
 
 std::shared_ptr<Interface> new_mock_sriov() { return std::make_shared<Lib>(std::make_shared<MockAmdPCI>()); }

@@ -13,8 +13,13 @@
 //   * a physical function with VFs enabled (SR-IOV extended capability
 //     NumVFs > 0, or sysfs sriov_numvfs > 0 when the extended config space is
 //     not readable by an unprivileged pod).
-// The guest cannot read the host (GIM) driver version from config space, so
-// the info carries role and VF counts instead of host driver strings.
+// The host driver of an MxGPU host is GIM (the SR-IOV "GPU-IOV module"); its
+// version is the analogue of the reference's vgpu.host-driver-version and is
+// read from the module's sysfs entry on the host.  A guest has no view of it:
+// AMD puts no host-driver record in the VF's config space (NVIDIA's vGPU
+// vendor capability has one), the PF2VF message amdgpu receives carries no
+// host driver version, and amd-smi reports only the guest's own driver - so
+// on guests that label is absent (docs/PARITY.md, "parity unpinned").
 #pragma once
 
 #include <memory>
@@ -64,17 +69,23 @@ class Interface {
  public:
   virtual ~Interface() = default;
   virtual std::vector<Function> Devices() = 0;
+  // Version of the SR-IOV host driver (GIM) loaded on this node; nullopt
+  // when it is not (bare metal, amdgpu-only hosts, guests).
+  virtual std::optional<std::string> HostDriverVersion() { return std::nullopt; }
 };
 
 class Lib : public Interface {
  public:
-  explicit Lib(std::shared_ptr<AmdPCI> pci) : pci_(std::move(pci)) {}
+  explicit Lib(std::shared_ptr<AmdPCI> pci, std::string root = "") : pci_(std::move(pci)), root_(std::move(root)) {}
   std::vector<Function> Devices() override;
+  // <root>/sys/module/gim/version (no root: not looked up).
+  std::optional<std::string> HostDriverVersion() override;
   // Classifies one PCI function; nullopt if it is not SR-IOV relevant.
   static std::optional<Info> Classify(const PCIDevice& d);
 
  private:
   std::shared_ptr<AmdPCI> pci_;
+  std::string root_;
 };
 
 std::shared_ptr<Interface> new_sriov_lib(const std::string& root);

@@ -254,6 +254,22 @@ def test_synthetic_sriov_pf(binary, tmp_path):
     golden.check_byte_golden(text, GOLDEN / "synthetic-sriov.txt", UPDATE)
 
 
+def test_sriov_host_driver_version_on_gim_host(binary, tmp_path):
+    """vgpu.go:44-52 labels the host driver version; on an MxGPU host that is
+    the GIM module's version.  A guest cannot see it (no host-driver record
+    in the VF's config space): the label is absent there."""
+    spec = synth.NodeSpec(gpus=[synth.GpuSpec(sriov={"total": 8, "num": 4})], gim_version="8.1.0.K", seed=7)
+    root = synth.make_node(tmp_path / "root", spec)
+    labels = golden.parse_labels(_oneshot(binary, tmp_path, "--backend=sysfs", sysfs_root=str(root)))
+    assert labels["amd.com/sriov.role"] == "pf"
+    assert labels["amd.com/sriov.host-driver-version"] == "8.1.0.K"
+    guest = synth.NodeSpec(gpus=[synth.GpuSpec(vf=True)], hypervisor=True, gim_version="8.1.0.K", seed=9)
+    root = synth.make_node(tmp_path / "guest", guest)
+    labels = golden.parse_labels(_oneshot(binary, tmp_path, "--backend=sysfs", sysfs_root=str(root)))
+    assert labels["amd.com/sriov.role"] == "vf"
+    assert "amd.com/sriov.host-driver-version" not in labels
+
+
 def test_synthetic_sriov_privileged_config_space(binary, tmp_path):
     spec = synth.NodeSpec(gpus=[synth.GpuSpec(sriov={"total": 8, "num": 2})], privileged=True, seed=8)
     root = synth.make_node(tmp_path / "root", spec)

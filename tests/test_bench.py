@@ -64,6 +64,7 @@ def test_synthetic_scaling_labels(n):
 
 
 def test_two_ranks_gloo():
+    pytest.importorskip("torch")  # ranks are launched with torch.distributed.run
     port = _free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2", "--steps", "10", "--warmup", "2",
@@ -86,6 +87,7 @@ def test_driver_n8_command_over_fake_amdsmi(tmp_path):
     label set: gpu.count=8 and the per-GPU xGMI links (7)."""
     import os
 
+    pytest.importorskip("torch")  # ranks are launched with torch.distributed.run
     fake = REPO / "build" / "libfake_amdsmi.so"
     if not fake.exists():
         pytest.skip("libfake_amdsmi.so not built")

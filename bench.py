@@ -266,8 +266,9 @@ def main() -> int:
         cold, first_cycle = None, None
         fake = _fake_amdsmi()
         if not a.no_extras:
-            sess_backend = "sysfs" if backend == "synthetic" else backend
-            loop_args = _session_args(sess_backend, n, out, root, [])
+            # The daemon as the DaemonSet runs it: --backend=auto (amd-smi,
+            # initialised in the background while KFD labels the first cycle).
+            loop_args = _session_args("auto", n, out, root, [])
             try:
                 binary = str(gfd.binary_path())
                 runs = max(5, min(30, a.steps // 10))

@@ -108,6 +108,12 @@ ManagerPtr get_manager(const config::Config& c) {
   bool has_smi = log_with_reason(has_amdsmi(&why), why, "amd-smi");
   bool has_kfd = log_with_reason(has_kfd_topology(c.sysfs_root(), &why), why, "KFD");
   if (has_smi || has_kfd) log_versions(c);
+  if (has_smi && has_kfd && c.amdsmi_session() == "persistent") {
+    log::printf("Using amd-smi manager (initialized in the background), KFD sysfs manager until then "
+                "or if amd-smi fails to initialize");
+    return std::make_shared<WarmStartManager>(std::make_shared<AmdSmiManager>(amdsmi_options(c)),
+                                              std::make_shared<SysfsManager>(sysfs_options(c)));
+  }
   if (has_smi && has_kfd) {
     log::printf("Using amd-smi manager, KFD sysfs manager if amd-smi fails to initialize");
     return std::make_shared<PreferenceManager>(std::vector<ManagerPtr>{

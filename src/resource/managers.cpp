@@ -4,6 +4,7 @@
 #include "util/fs.h"
 #include "util/log.h"
 #include "util/strings.h"
+#include "util/trace.h"
 
 namespace gfd::resource {
 
@@ -48,6 +49,60 @@ void PreferenceManager::Init() {
     }
   }
   throw Error("no resource manager could be initialized (" + errors + ")");
+}
+
+WarmStartManager::WarmStartManager(ManagerPtr preferred, ManagerPtr quick)
+    : preferred_(std::move(preferred)), quick_(std::move(quick)), current_(quick_) {}
+
+WarmStartManager::~WarmStartManager() {
+  if (warmer_.joinable()) warmer_.join();
+}
+
+void WarmStartManager::fall_back(const std::string& why) {
+  log::printf("Warning: %s manager failed to initialize: %s", preferred_->Name().c_str(), why.c_str());
+  log::printf("Using the %s manager", quick_->Name().c_str());
+  state_ = State::quick_only;
+  current_ = quick_;
+}
+
+void WarmStartManager::Init() {
+  if (state_ == State::cold) {
+    // A persistent session stays initialised after Shutdown: the warmer
+    // opens it, and the cycle that switches over finds it ready.
+    warmer_ = std::thread([this] {
+      int64_t t0 = trace::now_ns();
+      try {
+        preferred_->Init();
+        preferred_->Shutdown();
+      } catch (const std::exception& e) {
+        warm_error_ = e.what();
+      }
+      warm_ns_ = trace::now_ns() - t0;
+      warm_done_.store(true, std::memory_order_release);
+    });
+    state_ = State::warming;
+    log::printf("Initializing the %s manager in the background; labeling from the %s manager meanwhile",
+                preferred_->Name().c_str(), quick_->Name().c_str());
+  } else if (state_ == State::warming && warm_done_.load(std::memory_order_acquire)) {
+    warmer_.join();
+    if (!warm_error_.empty()) {
+      fall_back(warm_error_);
+    } else {
+      log::printf("Using the %s manager (initialized in the background in %.1f ms)", preferred_->Name().c_str(),
+                  static_cast<double>(warm_ns_) / 1e6);
+      state_ = State::preferred;
+      current_ = preferred_;
+    }
+  }
+  if (state_ == State::preferred) {
+    try {
+      preferred_->Init();
+      return;
+    } catch (const std::exception& e) {
+      fall_back(e.what());
+    }
+  }
+  quick_->Init();
 }
 
 ManagerPtr with_config(ManagerPtr m, const config::Config& c) {

@@ -12,6 +12,9 @@
 #include <vector>
 
 #include "config/config.h"
+#include <atomic>
+#include <thread>
+
 #include "config/yaml.h"
 #include "resource/types.h"
 
@@ -72,6 +75,42 @@ class PreferenceManager : public Manager {
   std::vector<ManagerPtr> candidates_;
   ManagerPtr current_;
   size_t chosen_ = 0;
+};
+
+// `--backend=auto` in daemon mode on a node with both amd-smi and a KFD
+// topology, amd-smi session persistent.  amd-smi's first amdsmi_init costs
+// ~25 ms (it parses all of /proc/cpuinfo, profiles/amdsmi_init_profile.txt)
+// while the KFD topology answers the same questions with byte-identical
+// labels (tests/test_gpu.py).  So the first cycle is labelled from KFD while
+// the preferred manager initialises on a background thread; the first cycle
+// that finds it ready switches to it for good.  If its initialisation
+// failed - or it fails later - the quick manager keeps serving until the
+// manager is rebuilt (SIGHUP), as with PreferenceManager.  Switching happens
+// only in Init, between cycles.
+class WarmStartManager : public Manager {
+ public:
+  WarmStartManager(ManagerPtr preferred, ManagerPtr quick);
+  ~WarmStartManager() override;  // waits for a background initialisation
+  void Init() override;
+  void Shutdown() override { current_->Shutdown(); }
+  std::vector<DevicePtr> GetDevices() override { return current_->GetDevices(); }
+  std::string GetDriverVersion() override { return current_->GetDriverVersion(); }
+  std::optional<RuntimeVersion> GetRuntimeVersion() override { return current_->GetRuntimeVersion(); }
+  std::string Name() const override { return current_->Name(); }
+  std::optional<VersionSources> VersionFiles() const override { return current_->VersionFiles(); }
+  // The preferred manager is the one in use.
+  bool warmed() const { return state_ == State::preferred; }
+
+ private:
+  enum class State { cold, warming, preferred, quick_only };
+  void fall_back(const std::string& why);
+
+  ManagerPtr preferred_, quick_, current_;
+  State state_ = State::cold;
+  std::thread warmer_;
+  std::atomic<bool> warm_done_{false};
+  std::string warm_error_;  // set by the warmer before warm_done_
+  int64_t warm_ns_ = 0;
 };
 
 // Wrap `m` in a FallbackManager unless failOnInitError is set.

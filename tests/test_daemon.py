@@ -270,44 +270,56 @@ def _fake_amdsmi_env(spec: str) -> dict:
     return {"GFD_AMDSMI_LIBRARY": str(lib), "GFD_FAKE_AMDSMI_SPEC": spec}
 
 
-def _first_cycle(binary, out, *args, env=None):
-    """Daemon (loop) mode: start it, read the feature file of its first
-    cycle, stop it with SIGTERM; returns (labels, stderr)."""
+def _loop_until(binary, out, *args, env=None, until="Writing labels to output file", timeout=30):
+    """Daemon (loop) mode: start it, wait for a log line containing `until`
+    and the feature file written after it, stop it with SIGTERM; returns
+    (labels, stderr)."""
     e = {k: v for k, v in os.environ.items() if not k.startswith("GFD_")}
     e.update(env or {})
-    p = subprocess.Popen([binary, "--sleep-interval=30s", f"--output-file={out}", *args], env=e,
+    p = subprocess.Popen([binary, "--sleep-interval=20ms", f"--output-file={out}", *args], env=e,
                          stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+    seen, err = False, []
     try:
-        deadline = time.monotonic() + 20
-        while not out.exists() and time.monotonic() < deadline and p.poll() is None:
-            time.sleep(0.01)
+        deadline = time.monotonic() + timeout
+        for line in p.stderr:
+            err.append(line)
+            seen = seen or until in line
+            # The file is complete once the cycle that logged this line ends.
+            if seen and "Sleeping for" in line:
+                break
+            if time.monotonic() > deadline:
+                break
         text = out.read_text() if out.exists() else ""
     finally:
         p.send_signal(signal.SIGTERM)
-        _, err = p.communicate(timeout=20)
-    return golden.parse_labels(text), err
+        _, rest = p.communicate(timeout=20)
+        err.append(rest or "")
+    assert seen, "".join(err)[-3000:]
+    return golden.parse_labels(text), "".join(err)
 
 
 def test_auto_backend_uses_sysfs_when_amdsmi_fails_to_initialise(binary, tmp_path, mi355x_node):
     """amd-smi loads but amdsmi_init fails (DRIVER_NOT_LOADED): on a node
-    with a KFD topology the auto backend labels from sysfs instead of failing
-    (PreferenceManager; the reference has no second backend to try)."""
+    with a KFD topology the auto backend keeps labelling from sysfs instead
+    of failing (the reference has no second backend to try)."""
     root = mi355x_node(n_gpus=2)
-    labels, err = _first_cycle(binary, tmp_path / "gfd", "--backend=auto", f"--sysfs-root={root}",
-                               env=_fake_amdsmi_env("init_status=34"))
+    labels, err = _loop_until(binary, tmp_path / "gfd", "--backend=auto", f"--sysfs-root={root}",
+                              env=_fake_amdsmi_env("init_status=34"), until="Using the sysfs manager")
     assert labels["amd.com/gpu.count"] == "2"
     assert labels["amd.com/gpu.product"].startswith("AMD-Instinct-MI355")
     assert "amdsmi(persistent) manager failed to initialize" in err
-    assert "Using the sysfs manager" in err
 
 
 def test_auto_backend_prefers_amdsmi(binary, tmp_path, mi355x_node):
+    """Daemon mode: the first cycle is labelled from KFD while amd-smi
+    initialises in the background; once it is ready amd-smi takes over."""
     root = mi355x_node(n_gpus=2)
     spec = "bdf=0000:d9:00.0;mode=SPX;parts=1;cus=256;xcds=8;vram_mib=294896;links=7;virt=1"
-    labels, err = _first_cycle(binary, tmp_path / "gfd", "--backend=auto", f"--sysfs-root={root}",
-                               env=_fake_amdsmi_env(spec))
+    labels, err = _loop_until(binary, tmp_path / "gfd", "--backend=auto", f"--sysfs-root={root}",
+                              env=_fake_amdsmi_env(spec), until="Using the amdsmi(persistent) manager")
     assert labels["amd.com/gpu.count"] == "1"  # the fake's one GPU, not the tree's two
     assert "failed to initialize" not in err
+    assert "labeling from the sysfs manager meanwhile" in err
 
 
 def test_auto_backend_oneshot_reads_kfd_without_loading_amdsmi(binary, tmp_path, mi355x_node):

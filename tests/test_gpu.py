@@ -119,31 +119,63 @@ def test_oneshot_auto_skips_amdsmi_with_identical_labels(binary, tmp_path):
     assert statistics.median(walls) < 10.0, walls
 
 
+def _daemon_files(binary, tmp_path, env_extra=None, until="", timeout=60):
+    """Run the daemon loop (20 ms sleeps; the timestamp is fixed per run) and collect the
+    feature file after every cycle until a log line containing `until` has
+    been seen and one more cycle completed; returns (files, stderr)."""
+    import signal
+    import time
+
+    out = tmp_path / "gfd"
+    env = {k: v for k, v in os.environ.items() if not k.startswith("GFD_")}
+    env.update(env_extra or {})
+    p = subprocess.Popen([binary, "--sleep-interval=20ms", f"--output-file={out}"], env=env,
+                         stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+    files, err, seen = [], [], False
+    try:
+        deadline = time.monotonic() + timeout
+        for line in p.stderr:
+            err.append(line)
+            if "Sleeping for" in line:
+                files.append(out.read_text())
+                if seen:
+                    break
+            seen = seen or (until in line)
+            if time.monotonic() > deadline:
+                break
+    finally:
+        p.send_signal(signal.SIGTERM)
+        _, rest = p.communicate(timeout=30)
+        err.append(rest or "")
+    return files, "".join(err)
+
+
 def test_auto_backend_falls_back_to_sysfs_on_hardware(binary, tmp_path):
     """An amd-smi library that loads but cannot initialise (the scriptable
     fake, told to fail amdsmi_init) on a real node: the auto backend of the
     daemon loop labels the GPU from the KFD topology instead, with the same
     label set."""
-    import signal
-    import time
-
     fake = REPO / "build" / "libfake_amdsmi.so"
-    out = tmp_path / "gfd"
-    env = {k: v for k, v in os.environ.items() if not k.startswith("GFD_")}
-    env.update({"GFD_AMDSMI_LIBRARY": str(fake), "GFD_FAKE_AMDSMI_SPEC": "init_status=34"})
-    p = subprocess.Popen([binary, "--sleep-interval=30s", f"--output-file={out}"], env=env,
-                         stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
-    try:
-        deadline = time.monotonic() + 60
-        while not out.exists() and time.monotonic() < deadline and p.poll() is None:
-            time.sleep(0.01)
-        text = out.read_text()
-    finally:
-        p.send_signal(signal.SIGTERM)
-        _, err = p.communicate(timeout=30)
-    assert "Using the sysfs manager" in err
-    golden.check_regex_golden(text, TESTS / "expected-output.txt", select=lambda ln: "sriov" not in ln)
-    assert golden.parse_labels(text)["amd.com/gpu.arch"] == "gfx950"
+    files, err = _daemon_files(binary, tmp_path, {"GFD_AMDSMI_LIBRARY": str(fake),
+                                                  "GFD_FAKE_AMDSMI_SPEC": "init_status=34"},
+                               until="Using the sysfs manager")
+    assert "Using the sysfs manager" in err, err[-3000:]
+    golden.check_regex_golden(files[-1], TESTS / "expected-output.txt", select=lambda ln: "sriov" not in ln)
+    assert golden.parse_labels(files[-1])["amd.com/gpu.arch"] == "gfx950"
+
+
+def test_daemon_first_cycle_from_kfd_then_amdsmi_with_identical_labels(binary, tmp_path):
+    """Daemon mode, --backend=auto on a real MI355X: the first cycle is
+    labelled from the KFD topology while amd-smi initialises in the
+    background (~25 ms); then amd-smi takes over.  Every feature file of the
+    run - before and after the switch - is the same."""
+    files, err = _daemon_files(binary, tmp_path, until="Using the amdsmi(persistent) manager")
+    assert "labeling from the sysfs manager meanwhile" in err, err[-3000:]
+    assert "Using the amdsmi(persistent) manager (initialized in the background" in err, err[-3000:]
+    assert "failed to initialize" not in err
+    assert len(files) >= 2
+    assert all(f == files[0] for f in files), files
+    golden.check_regex_golden(files[0], TESTS / "expected-output.txt", select=lambda ln: "sriov" not in ln)
 
 
 def test_daemon_sysfs_backend_oneshot(binary, tmp_path):

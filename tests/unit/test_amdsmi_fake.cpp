@@ -316,14 +316,40 @@ TEST(AmdSmiFake_AutoBackendFallsBackToSysfsWhenInitFails) {
   c.flags.gfd.backend = "auto";
   c.flags.gfd.sysfs_root = root;
   int i0 = fake().init_calls();
-  auto m = get_manager(c);
-  EXPECT_EQ(m->Name(), std::string("amdsmi(persistent)"));
-  m->Init();
-  EXPECT_EQ(m->Name(), std::string("sysfs"));
-  EXPECT_EQ(m->GetDevices().size(), static_cast<size_t>(0));
-  m->Shutdown();
-  m->Init();
+  auto m = get_manager(c);  // daemon mode: amd-smi initialises in the background
+  for (int i = 0; i < 200; ++i) {
+    m->Init();
+    EXPECT_EQ(m->Name(), std::string("sysfs"));
+    EXPECT_EQ(m->GetDevices().size(), static_cast<size_t>(0));
+    m->Shutdown();
+    usleep(1000);
+  }
   EXPECT_EQ(fake().init_calls() - i0, 1);  // amd-smi is not retried every cycle
+  fs::remove_all(root);
+}
+
+TEST(AmdSmiFake_AutoBackendSwitchesToAmdsmiOnceInitialised) {
+  REQUIRE_FAKE();
+  fake().configure(kTwoGpus);
+  std::string root = temp_root();
+  fs::mkdir_all(root + "/sys/class/kfd/kfd/topology/nodes");  // a KFD topology without GPUs
+  set_generation(root, "1");
+  config::Config c;
+  c.flags.gfd.backend = "auto";
+  c.flags.gfd.sysfs_root = root;
+  auto m = get_manager(c);
+  m->Init();
+  EXPECT_EQ(m->Name(), std::string("sysfs"));  // the first cycle does not wait for amdsmi_init
+  m->Shutdown();
+  size_t n = 0;
+  for (int i = 0; i < 2000 && n == 0; ++i) {
+    usleep(1000);
+    m->Init();
+    n = m->GetDevices().size();
+    m->Shutdown();
+  }
+  EXPECT_EQ(n, static_cast<size_t>(2));  // the fake's GPUs: amd-smi took over
+  EXPECT_EQ(m->Name(), std::string("amdsmi(persistent)"));
   fs::remove_all(root);
 }
 

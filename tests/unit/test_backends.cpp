@@ -411,6 +411,81 @@ TEST(Preference_EveryCandidateFailingIsAnInitError) {
   EXPECT_EQ(f.Name(), std::string("fallback(null)"));
 }
 
+namespace {
+// Cycles (Init, GetDevices, Shutdown) until the preferred manager is in use
+// or 2 s passed; returns the device counts seen.
+std::vector<size_t> cycle_until_warm(WarmStartManager& w) {
+  std::vector<size_t> seen;
+  for (int i = 0; i < 2000 && !w.warmed(); ++i) {
+    w.Init();
+    seen.push_back(w.GetDevices().size());
+    w.Shutdown();
+    usleep(1000);
+  }
+  return seen;
+}
+}  // namespace
+
+TEST(WarmStart_FirstCycleFromQuickThenPreferred) {
+  auto smi = std::make_shared<MockManager>(std::vector<DevicePtr>{new_full_gpu(), new_full_gpu()});
+  auto kfd = std::make_shared<MockManager>(std::vector<DevicePtr>{new_full_gpu()});
+  WarmStartManager w(smi, kfd);
+  auto seen = cycle_until_warm(w);
+  EXPECT_TRUE(w.warmed());
+  EXPECT_EQ(seen.front(), static_cast<size_t>(1));  // the first cycle: the quick manager
+  w.Init();
+  EXPECT_EQ(w.GetDevices().size(), static_cast<size_t>(2));
+  w.Shutdown();
+  int kfd_inits = kfd->init_calls;
+  w.Init();  // switched for good
+  w.Shutdown();
+  EXPECT_EQ(kfd->init_calls, kfd_inits);
+  EXPECT_EQ(smi->init_calls, 4);  // the warmer, the cycle that switched, 2 more
+}
+
+TEST(WarmStart_PreferredFailingInTheBackgroundKeepsQuick) {
+  auto smi = std::make_shared<MockManager>();
+  smi->with_error_on_init("no driver");
+  auto kfd = std::make_shared<MockManager>(std::vector<DevicePtr>{new_full_gpu()});
+  WarmStartManager w(smi, kfd);
+  for (int i = 0; i < 50; ++i) {
+    w.Init();
+    EXPECT_EQ(w.GetDevices().size(), static_cast<size_t>(1));
+    w.Shutdown();
+    usleep(1000);
+  }
+  EXPECT_FALSE(w.warmed());
+  EXPECT_EQ(smi->init_calls, 1);  // tried once, in the background; never retried
+}
+
+TEST(WarmStart_PreferredFailingLaterFallsBackForGood) {
+  auto smi = std::make_shared<MockManager>(std::vector<DevicePtr>{new_full_gpu(), new_full_gpu()});
+  auto kfd = std::make_shared<MockManager>(std::vector<DevicePtr>{new_full_gpu()});
+  WarmStartManager w(smi, kfd);
+  cycle_until_warm(w);
+  EXPECT_TRUE(w.warmed());
+  smi->with_error_on_init("driver reloaded");
+  w.Init();
+  EXPECT_EQ(w.GetDevices().size(), static_cast<size_t>(1));
+  w.Shutdown();
+  EXPECT_FALSE(w.warmed());
+  int smi_inits = smi->init_calls;
+  w.Init();
+  w.Shutdown();
+  EXPECT_EQ(smi->init_calls, smi_inits);
+}
+
+TEST(WarmStart_DestructorWaitsForTheWarmer) {
+  auto smi = std::make_shared<MockManager>();
+  auto kfd = std::make_shared<MockManager>();
+  {
+    WarmStartManager w(smi, kfd);
+    w.Init();
+    w.Shutdown();
+  }  // must not leave a running thread behind (TSan / std::terminate)
+  EXPECT_EQ(smi->init_calls, 1);
+}
+
 TEST(AmdSmi_InitFailsCleanlyWithoutDriver) {
   // In the CPU container libamd_smi loads but there is no amdgpu driver:
   // amdsmi_init returns DRIVER_NOT_LOADED, which must surface as an Init error.

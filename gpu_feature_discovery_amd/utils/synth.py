@@ -268,3 +268,40 @@ def make_mi355x_node(root: str | os.PathLike, n_gpus: int = 8, compute_partition
     gpus = [GpuSpec(compute_partition=compute_partition, memory_partition=memory_partition,
                     hidden=i >= n_gpus - hidden) for i in range(n_gpus)]
     return make_node(root, NodeSpec(gpus=gpus, seed=seed, **kwargs))
+
+
+def fake_amdsmi_spec(root: str | os.PathLike, spec: NodeSpec, latency_us: int = 0) -> str:
+    """The scriptable fake amd-smi (tests/fake_amdsmi) configured as amd-smi
+    would see the node ``make_node(root, spec)`` built: same PCI addresses,
+    partition layout and KFD nodes, one line per readable GPU."""
+    root = Path(root)
+    lines = [f"partition_bdf={spec.partition_layout}", "sockets=slot"]
+    if latency_us:
+        lines.append(f"latency_us={latency_us}")
+    kfd = root / "sys/class/kfd/kfd/topology/nodes"
+    node = spec.cpu_sockets
+    gpu_bdfs = sorted(p.name for p in (root / "sys/bus/pci/devices").iterdir()
+                      if (p / "current_compute_partition").exists())
+    # make_node assigns buses in GPU order; recover each GPU's address from
+    # its first partition node's location_id.
+    for g in spec.gpus:
+        parts = PARTITIONS_PER_MODE[g.compute_partition]
+        first = None
+        for p in range(parts):
+            props = kfd / str(node + p) / "properties"
+            if props.is_file():
+                first = first or props
+        if g.hidden or first is None:
+            node += parts
+            continue
+        loc = int(next(ln.split()[1] for ln in first.read_text().splitlines() if ln.startswith("location_id")))
+        bdf = f"0000:{loc >> 8:02x}:00.0"
+        assert bdf in gpu_bdfs
+        fields = [f"bdf={bdf}", f"mode={g.compute_partition}", f"nps={g.memory_partition}", f"parts={parts}",
+                  f"name={g.product_name}", f"cus={g.cus // parts}", f"xcds={g.xcds // parts}",
+                  f"vram_mib={(g.vram_bytes // parts) >> 20}", f"kfd_base={node}"]
+        if g.visible_partitions is not None:
+            fields.append("visible=" + ",".join(map(str, g.visible_partitions)))
+        lines.append(";".join(fields))
+        node += parts
+    return "\n".join(lines)

@@ -367,6 +367,50 @@ bool query_unpartitioned(AmdSmiLib& L, const std::string& root, ProcInfo& p, Amd
   return true;
 }
 
+// The processors of one partitioned GPU (DPX/QPX/CPX, or the partitions of
+// it this container may see): per cycle, the compute and memory partition
+// modes from the parent function's amdgpu attributes (shared by every
+// partition) and each processor's ASIC info; per session (`facts`, aligned
+// with `procs`; node_id kNoNode = not known yet) each partition's KFD node
+// (amdsmi_get_gpu_kfd_info) and from it the partition id, XCD/SDMA counts
+// and memory.  Returns false when the parent reports SPX or an attribute or
+// node is missing; the caller then queries every value through amd-smi.
+bool query_partitioned(AmdSmiLib& L, const std::string& root, std::vector<ProcInfo>& procs,
+                       std::vector<AmdSmiManager::PartitionFacts>& facts) {
+  std::string pci = fs::join(root, "sys/bus/pci/devices/" + procs.front().gpu_bdf);
+  auto cp = AMDSMI_CALL("compute_partition(sysfs)", fs::attrs().read_trimmed(pci + "/current_compute_partition"));
+  if (!cp || cp->empty() || *cp == "SPX") return false;
+  auto mp = AMDSMI_CALL("memory_partition(sysfs)", fs::attrs().read_trimmed(pci + "/current_memory_partition"));
+  if (!mp || mp->empty()) return false;
+  for (size_t i = 0; i < procs.size(); ++i) {
+    ProcInfo& p = procs[i];
+    AmdSmiManager::PartitionFacts& f = facts[i];
+    if (f.node_id == kNoNode) {
+      uint32_t node = kNoNode;
+      if (!query_kfd(L, p, &node) || node == kNoNode) return false;
+      KfdCounts c = AMDSMI_CALL("kfd_counts(sysfs)", kfd_counts(root, node));
+      uint64_t mem = kfd_node_memory_bytes(fs::join(root, "sys/class/kfd/kfd/topology/nodes/" + std::to_string(node)));
+      if (c.num_xcc == 0 || mem == 0) return false;
+      f.handle = p.h;
+      f.node_id = node;
+      f.partition_id = p.partition_id;
+      f.num_xcc = c.num_xcc;
+      f.sdma = c.num_sdma;
+      f.mem_bytes = mem;
+    }
+    query_identity(L, p);
+    p.partition_id = f.partition_id;
+    p.xcds = f.num_xcc;
+    p.sdma = f.sdma;
+    p.vram = f.mem_bytes;
+    p.compute_partition = *cp;
+    p.memory_partition = *mp;
+  }
+  fix_market_name(L, root, procs.front());
+  for (auto& p : procs) p.market_name = procs.front().market_name;
+  return true;
+}
+
 // Every value through amd-smi (partitioned GPUs, or sysfs values disabled).
 void query_proc(AmdSmiLib& L, const std::string& root, ProcInfo& p) {
   query_identity(L, p);
@@ -499,6 +543,7 @@ void AmdSmiManager::library_init() {
   lib_initialized_ = true;
   virt_mode_.clear();
   kfd_node_.clear();
+  partition_facts_.clear();
   parent_bdf_.clear();
   ++init_count_;
 }
@@ -648,6 +693,7 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
     std::exception_ptr error;
     int64_t proc_ns = 0, caps_ns = 0;
     KfdNodeFacts kfd;  // session cache entry (unpartitioned GPUs)
+    std::vector<PartitionFacts> parts;  // session cache entries (partitioned GPUs), aligned with procs
   };
   std::vector<Gpu> gpus;
   for (size_t i = 0; i < physical.size(); ++i) {
@@ -662,6 +708,10 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
       if (v != virt_mode_.end()) gpus.back().extras.virtualization = v->second;
       auto k = kfd_node_.find(bdf);
       if (k != kfd_node_.end()) gpus.back().kfd = k->second;
+      for (const auto& p : physical[i]) {
+        auto f = partition_facts_.find(p.h);
+        gpus.back().parts.push_back(f != partition_facts_.end() ? f->second : PartitionFacts{});
+      }
     }
   }
   const bool sysfs_values = sysfs_values_enabled();
@@ -678,7 +728,10 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
       int64_t t0 = trace::now_ns();
       auto& procs = *g.procs;
       if (fast) {
-        if (procs.size() != 1 || !query_unpartitioned(L, opts_.root, procs[0], &g.kfd)) return false;
+        bool done = procs.size() == 1 && query_unpartitioned(L, opts_.root, procs[0], &g.kfd);
+        if (!done && !query_partitioned(L, opts_.root, procs, g.parts)) return false;
+        std::sort(procs.begin(), procs.end(),
+                  [](const ProcInfo& a, const ProcInfo& b) { return a.partition_id < b.partition_id; });
       } else {
         for (auto& p : procs) query_proc(L, opts_.root, p);
         std::sort(procs.begin(), procs.end(),
@@ -696,25 +749,32 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
     }
     return true;
   };
-  // Unpartitioned GPUs first: ~7 us of attribute preads and cached library
-  // lookups each.  Two GPUs per lane: on one thread a cycle after the
-  // daemon's sleep runs on a cold, down-clocked core (8 GPUs' reads: 170 us
-  // serial vs 36 us on four lanes), while back to back the pool only adds
-  // fan-out (26 us serial, 32 us on four lanes) - profiles/multi_gpu_read_probe.txt.
-  // The rest - partitioned GPUs, tens of library calls each - then go over
-  // the pool one per lane.
+  // One pass over the GPUs; each tries the attribute path first (SPX: ~7 us
+  // of preads and cached library lookups; partitioned: two preads plus the
+  // session-cached partition facts) and falls back to library calls in the
+  // same lane.  (Two passes - all attribute attempts, then the library
+  // fallbacks - left the second pass's helper lanes queued behind the first
+  // pass's, so its items ran mostly serially on the caller: 8 GPUs 0.94 ms
+  // instead of 0.22 ms over the latency-modelled fake.)  Lanes: two GPUs per
+  // lane while every GPU took the attribute path last cycle - on one thread
+  // a cycle after the daemon's sleep runs on a cold, down-clocked core
+  // (8 GPUs' reads: 170 us serial vs 36 us on four lanes), while back to back
+  // the pool only adds fan-out (26 us serial, 32 us on four lanes) -
+  // profiles/multi_gpu_read_probe.txt; one GPU per lane otherwise.
   int64_t t_gpus = trace::now_ns();
   std::vector<char> fast_ok(gpus.size(), 0);
-  if (sysfs_values) {
-    size_t lanes = opts_.threads > 0 ? static_cast<size_t>(opts_.threads) : gpu_lanes(gpus.size(), true);
-    WorkerPool::instance().parallel_for(gpus.size(), [&](size_t i) { fast_ok[i] = work(gpus[i], true); }, lanes);
-  }
-  std::vector<size_t> library_path;
-  for (size_t i = 0; i < gpus.size(); ++i)
-    if (!fast_ok[i]) library_path.push_back(i);
-  size_t threads = opts_.threads > 0 ? static_cast<size_t>(opts_.threads) : gpu_lanes(library_path.size(), false);
+  size_t lanes = opts_.threads > 0 ? static_cast<size_t>(opts_.threads) : gpu_lanes(gpus.size(), all_fast_);
   WorkerPool::instance().parallel_for(
-      library_path.size(), [&](size_t k) { work(gpus[library_path[k]], false); }, threads);
+      gpus.size(),
+      [&](size_t i) {
+        if (sysfs_values && work(gpus[i], true)) {
+          fast_ok[i] = 1;
+          return;
+        }
+        work(gpus[i], false);
+      },
+      lanes);
+  all_fast_ = std::all_of(fast_ok.begin(), fast_ok.end(), [](char c) { return c != 0; });
   trace::record("amdsmi.gpus", trace::now_ns() - t_gpus);
   // Per-GPU phase times: the slowest GPU (items may have run on pool
   // threads, whose trace records are their own).
@@ -730,6 +790,8 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
   for (const auto& g : gpus) {
     if (!g.extras.virtualization.empty()) virt_mode_[g.bdf] = g.extras.virtualization;
     if (g.kfd.node_id != kNoNode) kfd_node_[g.bdf] = g.kfd;
+    for (const auto& f : g.parts)
+      if (f.node_id != kNoNode) partition_facts_[f.handle] = f;
   }
 
   std::vector<DevicePtr> out;

@@ -70,6 +70,15 @@ class AmdSmiManager : public Manager {
     uint32_t node_id = 0xFFFFFFFFu;
     uint32_t num_xcc = 0;
   };
+  // Per-session facts of one compute partition (see partition_facts_).
+  struct PartitionFacts {
+    void* handle = nullptr;        // amd-smi processor handle
+    uint32_t node_id = 0xFFFFFFFFu;  // KFD node (0xFFFFFFFF: not known yet)
+    uint32_t partition_id = 0;
+    uint32_t num_xcc = 0;
+    int sdma = -1;
+    uint64_t mem_bytes = 0;
+  };
 
  private:
   std::vector<DevicePtr> snapshot();
@@ -101,10 +110,20 @@ class AmdSmiManager : public Manager {
   // ~1 us each through kept-open descriptors instead of 11-18 us per
   // library call.
   std::map<std::string, KfdNodeFacts> kfd_node_;
+  // The same for each compute partition of a partitioned GPU (by processor
+  // handle): its KFD node, partition id, XCD and SDMA counts and its share
+  // of HBM, all fixed until a partition/NPS switch - which rebuilds the KFD
+  // topology, bumps its generation and re-initialises the session.  The
+  // partition modes themselves are read from the parent's amdgpu
+  // attributes every cycle (two reads per GPU, not two library calls per
+  // partition).
+  std::map<void*, PartitionFacts> partition_facts_;
   // Parent PCI function of each physical GPU (key: its processors' BDFs),
   // for the lifetime of one session: processor addresses and PCI functions
   // only change with a driver reload or partition switch, which re-initialise.
   std::map<std::string, std::string> parent_bdf_;
+  // Every GPU took the attribute path in the last snapshot (lane sizing).
+  bool all_fast_ = false;
 };
 
 }  // namespace gfd::resource

@@ -34,6 +34,25 @@ std::string resolve_parent_bdf(const std::string& root, std::vector<std::string>
   return member_bdfs.front();
 }
 
+uint64_t kfd_node_memory_bytes(const std::string& node_dir) {
+  uint64_t total = 0;
+  std::string banks = fs::join(node_dir, "mem_banks");
+  for (const auto& b : fs::list_dir(banks)) {
+    auto r = fs::read_file(fs::join(banks, b + "/properties"));
+    if (!r.ok()) continue;
+    uint64_t heap = 0, size = 0;
+    for (const auto& line : str::split(r.data, '\n')) {
+      auto kv = str::split_n(line, ' ', 2);
+      if (kv.size() != 2) continue;
+      if (kv[0] == "heap_type") heap = str::parse_uint(kv[1]).value_or(0);
+      if (kv[0] == "size_in_bytes") size = str::parse_uint(kv[1]).value_or(0);
+    }
+    // HSA_HEAPTYPE_FRAME_BUFFER_PUBLIC (1) / _PRIVATE (2): device-local HBM.
+    if (heap == 1 || heap == 2) total += size;
+  }
+  return total;
+}
+
 Attributes partition_engine_counts(const std::string& root, const std::string& parent_bdf) {
   static const std::pair<const char*, const char*> kEngines[] = {{"dec", "engines.decoder"}, {"jpeg", "engines.jpeg"}};
   Attributes out;

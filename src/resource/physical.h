@@ -46,6 +46,12 @@ std::string bdf_slot(const std::string& bdf);
 // member address is returned.
 std::string resolve_parent_bdf(const std::string& root, std::vector<std::string> member_bdfs, uint32_t device_id);
 
+// Device-local memory (bytes) of a KFD topology node: the sum of its
+// frame-buffer memory banks (mem_banks/N/properties, heap types 1 and 2).
+// For a partition node that is the partition's share of HBM
+// (KFD_XCP_MEMORY_SIZE); 0 if unreadable.
+uint64_t kfd_node_memory_bytes(const std::string& node_dir);
+
 // Engine counts per partition that amdgpu publishes for the current compute
 // partition mode under the parent function
 // (compute_partition_config/{dec,jpeg}/num_inst -> engines.decoder,

@@ -35,6 +35,7 @@ struct KfdNode {
   uint64_t drm_render_minor = 0;
   uint64_t num_sdma_engines = 0;
   uint64_t local_mem_size = 0;
+  uint64_t mem_bytes = 0;  // device-local memory of the node (mem_banks), read with the properties
   std::string dir;
 };
 
@@ -70,25 +71,6 @@ void parse_properties(const std::string& text, KfdNode& n) {
     }
     pos = eol + 1;
   }
-}
-
-uint64_t node_memory_bytes(const std::string& node_dir) {
-  uint64_t total = 0;
-  std::string banks = fs::join(node_dir, "mem_banks");
-  for (const auto& b : fs::list_dir(banks)) {
-    auto r = fs::read_file(fs::join(banks, b + "/properties"));
-    if (!r.ok()) continue;
-    uint64_t heap = 0, size = 0;
-    for (const auto& line : str::split(r.data, '\n')) {
-      auto kv = str::split_n(line, ' ', 2);
-      if (kv.size() != 2) continue;
-      if (kv[0] == "heap_type") heap = str::parse_uint(kv[1]).value_or(0);
-      if (kv[0] == "size_in_bytes") size = str::parse_uint(kv[1]).value_or(0);
-    }
-    // HSA_HEAPTYPE_FRAME_BUFFER_PUBLIC (1) / _PRIVATE (2): device-local HBM.
-    if (heap == 1 || heap == 2) total += size;
-  }
-  return total;
 }
 
 std::vector<std::string> split_list(const std::string& s) {
@@ -225,14 +207,9 @@ static DevicePtr describe_gpu(const std::string& root, bool in_vm, int index, co
   uint64_t vram = 0;
   if (auto v = fs::attrs().read_trimmed(fs::join(pci, "mem_info_vram_total"))) vram = str::parse_uint(*v).value_or(0);
 
-  // Per-partition HBM from each partition node's mem_banks (a list + read
-  // per node; 8 of them in CPX), read in parallel.
-  std::vector<uint64_t> part_mem(members.size(), 0);
-  if (partitioned)
-    WorkerPool::instance().parallel_for(members.size(), [&](size_t p) {
-      const KfdNode& n = *members[p];
-      part_mem[p] = n.local_mem_size ? n.local_mem_size : node_memory_bytes(n.dir);
-    });
+  // Per-partition HBM: each partition node's memory banks, read with the
+  // node properties (a partition's share of HBM only changes with a
+  // partition or NPS switch, which rebuilds the KFD topology).
 
   Attributes engines;
   if (partitioned) engines = partition_engine_counts(root, bdf);
@@ -252,7 +229,7 @@ static DevicePtr describe_gpu(const std::string& root, bool in_vm, int index, co
     pi.device_id = info.device_id;
     pi.compute_units = pcus;
     pi.xcds = static_cast<uint32_t>(n.num_xcc);
-    uint64_t mem = part_mem[p];
+    uint64_t mem = n.mem_bytes;
     pi.memory_mib = mem >> 20;
     part_mem_sum += mem;
     pi.compute_partition = info.compute_partition;
@@ -264,7 +241,7 @@ static DevicePtr describe_gpu(const std::string& root, bool in_vm, int index, co
   }
   info.compute_units = cus;
   info.xcds = xcds;
-  if (vram == 0) vram = partitioned ? part_mem_sum : (first.local_mem_size ? first.local_mem_size : node_memory_bytes(first.dir));
+  if (vram == 0) vram = partitioned ? part_mem_sum : first.mem_bytes;
   info.memory_mib = vram >> 20;
 
   bool capable = info.available_compute_partitions.size() > 1;
@@ -305,6 +282,8 @@ std::shared_ptr<const SysfsManager::Topology> SysfsManager::read_topology() cons
       if (!r.ok()) continue;  // EPERM: GPU not allocated to this container
       parse_properties(r.data, nodes[i]);
       usable[i] = nodes[i].gfx_target_version != 0 && nodes[i].simd_count != 0;  // else a CPU node
+      if (usable[i])
+        nodes[i].mem_bytes = nodes[i].local_mem_size ? nodes[i].local_mem_size : kfd_node_memory_bytes(nodes[i].dir);
     }
   };
   size_t chunks = (nodes.size() + kChunk - 1) / kChunk;

@@ -199,7 +199,13 @@ std::vector<PCIDevice> SysfsAmdPCI::Devices() {
   // function or two is read inline.
   constexpr size_t kChunk = 16;
   size_t chunk = kChunk;
-  if (misses.size() > kChunk) {
+  // GFD_PCI_COLD=sysfs: skip the procfs table and read every function's
+  // vendor from sysfs, spread over the pool (A/B measurements).
+  static const bool cold_sysfs = [] {
+    const char* v = std::getenv("GFD_PCI_COLD");
+    return v && std::string(v) == "sysfs";
+  }();
+  if (misses.size() > kChunk && !cold_sysfs) {
     int64_t tp = trace::now_ns();
     auto vendors = proc_pci_vendors(root_);
     trace::record("pci.proc_table", trace::now_ns() - tp);

@@ -77,6 +77,7 @@ struct State {
   long latency_us = 0;
   std::map<std::string, std::unique_ptr<std::mutex>> device_mu;  // by BDF
   std::map<std::string, int> fail;                               // function -> status
+  std::map<std::string, long> calls;                             // function -> device queries made
   bool partition_fn = true;   // partition_bdf=function
   bool socket_per_slot = true;  // sockets=slot
   std::vector<std::vector<uint32_t>> sockets;  // processor indices per socket
@@ -121,6 +122,7 @@ amdsmi_status_t check(amdsmi_processor_handle h, Proc** out, bool cheap = false,
     }
     *out = proc(h);
     if (!*out) return AMDSMI_STATUS_INVAL;
+    s.calls[fn]++;
     auto f = s.fail.find(fn);
     if (f != s.fail.end()) return static_cast<amdsmi_status_t>(f->second);
     latency = s.latency_us;
@@ -154,6 +156,7 @@ int fake_amdsmi_configure(const char* spec) {
   s.stale_after = -1;
   s.latency_us = 0;
   s.fail.clear();
+  s.calls.clear();
   s.queries = 0;
   s.stale = false;
   s.partition_fn = true;
@@ -254,6 +257,14 @@ int fake_amdsmi_configure(const char* spec) {
   return 0;
 }
 int fake_amdsmi_init_calls() { return S().init_calls; }
+// Device queries made through `fn` (e.g. "amdsmi_get_gpu_memory_total") since
+// the last configure.
+long fake_amdsmi_calls(const char* fn) {
+  auto& s = S();
+  std::lock_guard<std::mutex> g(s.mu);
+  auto it = s.calls.find(fn);
+  return it == s.calls.end() ? 0 : it->second;
+}
 int fake_amdsmi_virt_calls() { return S().virt_calls.load(); }
 int fake_amdsmi_shutdown_calls() { return S().shutdown_calls; }
 int fake_amdsmi_initialized() { return S().initialized ? 1 : 0; }

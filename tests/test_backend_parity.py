@@ -12,8 +12,6 @@ with and without the root-only partition resource files.
 
 from __future__ import annotations
 
-from pathlib import Path
-
 import pytest
 
 from conftest import run_daemon
@@ -21,38 +19,6 @@ from gpu_feature_discovery_amd import BUILD_DIR
 from gpu_feature_discovery_amd.utils import golden, synth
 
 FAKE = BUILD_DIR / "libfake_amdsmi.so"
-
-
-def _fake_spec(root: Path, spec: synth.NodeSpec) -> str:
-    """amd-smi's view of the synthetic node: one line per readable GPU."""
-    lines = [f"partition_bdf={spec.partition_layout}", "sockets=slot"]
-    kfd = root / "sys/class/kfd/kfd/topology/nodes"
-    node = spec.cpu_sockets
-    gpu_bdfs = sorted(p.name for p in (root / "sys/bus/pci/devices").iterdir()
-                      if (p / "current_compute_partition").exists())
-    # make_node assigns buses in GPU order; recover each GPU's address from
-    # its first partition node's location_id.
-    for g in spec.gpus:
-        parts = synth.PARTITIONS_PER_MODE[g.compute_partition]
-        first = None
-        for p in range(parts):
-            props = kfd / str(node + p) / "properties"
-            if props.is_file():
-                first = first or props
-        if g.hidden or first is None:
-            node += parts
-            continue
-        loc = int(next(ln.split()[1] for ln in first.read_text().splitlines() if ln.startswith("location_id")))
-        bdf = f"0000:{loc >> 8:02x}:00.0"
-        assert bdf in gpu_bdfs
-        fields = [f"bdf={bdf}", f"mode={g.compute_partition}", f"nps={g.memory_partition}", f"parts={parts}",
-                  f"name={g.product_name}", f"cus={g.cus // parts}", f"xcds={g.xcds // parts}",
-                  f"vram_mib={(g.vram_bytes // parts) >> 20}", f"kfd_base={node}"]
-        if g.visible_partitions is not None:
-            fields.append("visible=" + ",".join(map(str, g.visible_partitions)))
-        lines.append(";".join(fields))
-        node += parts
-    return "\n".join(lines)
 
 
 CASES = {
@@ -77,7 +43,7 @@ def test_amdsmi_and_sysfs_backends_label_identically(binary, tmp_path, case, lay
     outs = {}
     for backend in ("sysfs", "amdsmi"):
         out = tmp_path / f"gfd-{backend}"
-        env = {"GFD_AMDSMI_LIBRARY": str(FAKE), "GFD_FAKE_AMDSMI_SPEC": _fake_spec(root, spec).replace("\n", "|")}
+        env = {"GFD_AMDSMI_LIBRARY": str(FAKE), "GFD_FAKE_AMDSMI_SPEC": synth.fake_amdsmi_spec(root, spec).replace("\n", "|")}
         run_daemon(binary, "--oneshot", "--no-timestamp", f"--backend={backend}", f"--sysfs-root={root}",
                    f"--machine-type-file={root}/sys/class/dmi/id/product_name", f"--mig-strategy={c['strategy']}",
                    f"--output-file={out}", env=env, check=True)
@@ -100,7 +66,7 @@ def test_backends_agree_on_one_visible_partition(binary, tmp_path, layout):
     outs = {}
     for backend in ("sysfs", "amdsmi"):
         out = tmp_path / f"gfd-{backend}"
-        env = {"GFD_AMDSMI_LIBRARY": str(FAKE), "GFD_FAKE_AMDSMI_SPEC": _fake_spec(root, spec).replace("\n", "|")}
+        env = {"GFD_AMDSMI_LIBRARY": str(FAKE), "GFD_FAKE_AMDSMI_SPEC": synth.fake_amdsmi_spec(root, spec).replace("\n", "|")}
         run_daemon(binary, "--oneshot", "--no-timestamp", f"--backend={backend}", f"--sysfs-root={root}",
                    f"--machine-type-file={root}/sys/class/dmi/id/product_name", "--mig-strategy=single",
                    f"--output-file={out}", env=env, check=True)

@@ -30,6 +30,7 @@ struct Fake {
   int (*init_calls)() = nullptr;
   int (*shutdown_calls)() = nullptr;
   int (*virt_calls)() = nullptr;
+  long (*calls)(const char*) = nullptr;
   bool ok = false;
 
   Fake() {
@@ -43,7 +44,8 @@ struct Fake {
     init_calls = reinterpret_cast<int (*)()>(dlsym(h, "fake_amdsmi_init_calls"));
     shutdown_calls = reinterpret_cast<int (*)()>(dlsym(h, "fake_amdsmi_shutdown_calls"));
     virt_calls = reinterpret_cast<int (*)()>(dlsym(h, "fake_amdsmi_virt_calls"));
-    ok = configure && init_calls && shutdown_calls && virt_calls;
+    calls = reinterpret_cast<long (*)(const char*)>(dlsym(h, "fake_amdsmi_calls"));
+    ok = configure && init_calls && shutdown_calls && virt_calls && calls;
   }
 };
 
@@ -502,6 +504,46 @@ TEST(AmdSmiFake_OnePartitionVisibleReadsParentAttributes) {
   m.Shutdown();
   EXPECT_EQ(l["amd.com/gpu.count"], std::string("1"));
   EXPECT_EQ(l["amd.com/gpu.product"], std::string("AMD-Instinct-MI355-OAM-PARTITION-cpx.1xcd.36gb"));
+  fs::remove_all(root);
+}
+
+TEST(AmdSmiFake_PartitionedGpuValuesFromAttributesAndSessionCache) {
+  REQUIRE_FAKE();
+  // A CPX GPU whose parent function publishes its modes and whose 8 KFD
+  // partition nodes (2..9) publish XCD/SDMA counts and memory: after the
+  // first cycle no partition is queried through amd-smi any more (the
+  // partition modes come from two parent attribute reads per cycle).
+  std::string root = temp_root();
+  set_generation(root, "1");
+  std::string pci = root + "/sys/bus/pci/devices/0000:23:00.0";
+  fs::mkdir_all(pci);
+  lm::write_file_atomically(pci + "/device", "0x75a3\n", 0644);
+  lm::write_file_atomically(pci + "/current_compute_partition", "CPX\n", 0644);
+  lm::write_file_atomically(pci + "/current_memory_partition", "NPS1\n", 0644);
+  for (int n = 2; n < 10; ++n) {
+    std::string node = root + "/sys/class/kfd/kfd/topology/nodes/" + std::to_string(n);
+    fs::mkdir_all(node + "/mem_banks/0");
+    lm::write_file_atomically(node + "/properties", "simd_count 128\nnum_sdma_engines 1\nnum_xcc 1\n", 0644);
+    lm::write_file_atomically(node + "/mem_banks/0/properties", "heap_type 1\nsize_in_bytes 38652608512\n", 0644);
+  }
+  fake().configure("bdf=0000:23:00.0;mode=CPX;parts=8;cus=32;xcds=1;vram_mib=36000;kfd_base=2\n");
+  AmdSmiManager m(opts(root, true));
+  for (int c = 0; c < 3; ++c) {
+    m.Init();
+    auto devs = m.GetDevices();
+    EXPECT_EQ(devs.size(), static_cast<size_t>(1));
+    auto parts = devs[0]->GetPartitions();
+    EXPECT_EQ(parts.size(), static_cast<size_t>(8));
+    EXPECT_EQ(parts[7]->Info().partition_id, 7);
+    EXPECT_EQ(parts[0]->GetTotalMemoryMiB(), static_cast<uint64_t>(36862));  // the KFD node's share, not the library's
+    EXPECT_EQ(parts[0]->GetAttributes().at("engines.dma"), std::string("1"));
+    EXPECT_EQ(devs[0]->Info().compute_partition, std::string("CPX"));
+    m.Shutdown();
+  }
+  EXPECT_EQ(fake().calls("amdsmi_get_gpu_kfd_info"), 8L);  // first cycle only
+  EXPECT_EQ(fake().calls("amdsmi_get_gpu_memory_total"), 0L);
+  EXPECT_EQ(fake().calls("amdsmi_get_gpu_compute_partition"), 0L);
+  EXPECT_EQ(fake().calls("amdsmi_get_gpu_memory_partition"), 0L);
   fs::remove_all(root);
 }
 

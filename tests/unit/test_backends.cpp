@@ -84,7 +84,7 @@ struct Tree {
 TEST(Sysfs_TopologyKeptPerKfdGeneration) {
   Tree t;
   std::string nodes = t.root + "/sys/class/kfd/kfd/topology/nodes";
-  SysfsManager m(SysfsOptions{t.root, DeviceFilter()});
+  SysfsManager m(SysfsOptions{t.root, DeviceFilter(), {}});
   auto cycle = [&] {
     m.Init();
     auto d = m.GetDevices();
@@ -114,7 +114,7 @@ TEST(Sysfs_TopologyKeptPerKfdGeneration) {
 
 TEST(Sysfs_EnumeratesSpxAndCpxGpus) {
   Tree t;
-  SysfsManager m(SysfsOptions{t.root, DeviceFilter()});
+  SysfsManager m(SysfsOptions{t.root, DeviceFilter(), {}});
   m.Init();
   auto devs = m.GetDevices();
   EXPECT_EQ(devs.size(), static_cast<size_t>(2));
@@ -151,12 +151,12 @@ TEST(Sysfs_EnumeratesSpxAndCpxGpus) {
 
 TEST(Sysfs_VisibleDeviceFilter) {
   Tree t;
-  SysfsManager m(SysfsOptions{t.root, DeviceFilter::parse("1")});
+  SysfsManager m(SysfsOptions{t.root, DeviceFilter::parse("1"), {}});
   m.Init();
   auto devs = m.GetDevices();
   EXPECT_EQ(devs.size(), static_cast<size_t>(1));
   EXPECT_EQ(devs[0]->Info().bdf, std::string("0000:d9:00.0"));
-  SysfsManager m2(SysfsOptions{t.root, DeviceFilter::parse("0000:23:00.0")});
+  SysfsManager m2(SysfsOptions{t.root, DeviceFilter::parse("0000:23:00.0"), {}});
   m2.Init();
   EXPECT_EQ(m2.GetDevices()[0]->Info().bdf, std::string("0000:23:00.0"));
 }
@@ -166,14 +166,14 @@ TEST(Sysfs_UnreadableNodesAreSkipped) {
   // Node 1 becomes unreadable like GPUs not allocated to the container.
   ::unlink((t.root + "/sys/class/kfd/kfd/topology/nodes/1/properties").c_str());
   fs::mkdir_all(t.root + "/sys/class/kfd/kfd/topology/nodes/1/properties");  // read fails (EISDIR)
-  SysfsManager m(SysfsOptions{t.root, DeviceFilter()});
+  SysfsManager m(SysfsOptions{t.root, DeviceFilter(), {}});
   m.Init();
   EXPECT_EQ(m.GetDevices().size(), static_cast<size_t>(1));
 }
 
 TEST(Sysfs_SnapshotOncePerWindow) {
   Tree t;
-  SysfsManager m(SysfsOptions{t.root, DeviceFilter()});
+  SysfsManager m(SysfsOptions{t.root, DeviceFilter(), {}});
   m.Init();
   auto a = m.GetDevices();
   auto b = m.GetDevices();
@@ -184,7 +184,7 @@ TEST(Sysfs_SnapshotOncePerWindow) {
 }
 
 TEST(Sysfs_MissingTopologyIsInitError) {
-  SysfsManager m(SysfsOptions{"/nonexistent-gfd", DeviceFilter()});
+  SysfsManager m(SysfsOptions{"/nonexistent-gfd", DeviceFilter(), {}});
   EXPECT_THROW_MSG(m.Init(), "KFD topology not available");
   std::string reason;
   EXPECT_FALSE(has_kfd_topology("/nonexistent-gfd", &reason));

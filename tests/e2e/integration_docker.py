@@ -34,7 +34,10 @@ def main() -> int:
         name = f"gfd-amd-it-{int(time.time())}"
         subprocess.run(["docker", "run", "-d", "--rm", "--name", name, "--privileged",
                         "-v", f"{d}:/etc/kubernetes/node-feature-discovery/features.d",
-                        "-v", "/sys:/sys:ro", "-e", f"GFD_MIG_STRATEGY={a.strategy}", "-e", "GFD_SLEEP_INTERVAL=5s",
+                        "-v", "/sys:/sys:ro",
+                        # The node's ROCm release, as the manifests provide it (the image has none).
+                        "-v", "/opt:/host/opt:ro", "-e", "GFD_HOST_ROOT=/host",
+                        "-e", f"GFD_MIG_STRATEGY={a.strategy}", "-e", "GFD_SLEEP_INTERVAL=5s",
                         a.image], check=True)
         try:
             out = Path(d) / "gfd"

@@ -318,3 +318,30 @@ def test_attribute_descriptors_kept_open_and_stable(native):
     assert any(t.endswith("/current_compute_partition") for t in after), after
     assert any(t.endswith("/mem_info_vram_total") for t in after), after
     assert len(after) == len(before), (before, after)
+
+
+def test_eight_gpu_node_from_live_attributes(binary, tmp_path):
+    """BASELINE config 3 (8xMI355X SPX/NPS1) from a one-GPU box: the host's
+    other seven GPUs' KFD nodes are not readable here, but every GPU's
+    amdgpu PCI attributes are (sysfs is not namespaced).  tools/hybrid_root.py
+    builds a root whose PCI tree is the live one and whose KFD topology
+    repeats the allocated GPU's node at each GPU's address; the labels must
+    describe all of the host's MI355X from their live attributes."""
+    root = tmp_path / "hybrid"
+    cp = subprocess.run([sys.executable, str(REPO / "tools" / "hybrid_root.py"), str(root)], capture_output=True,
+                        text=True, timeout=60)
+    assert cp.returncode == 0, cp.stderr
+    n = int(cp.stdout.strip())
+    assert n >= 1
+    for visible, want in (("", n), (f"0-{min(n, 4) - 1}", min(n, 4))):
+        out = tmp_path / f"gfd-{want}"
+        run_daemon(binary, "--oneshot", "--no-timestamp", "--backend=sysfs", f"--sysfs-root={root}",
+                   f"--machine-type-file={root}/sys/class/dmi/id/product_name", f"--visible-devices={visible}",
+                   f"--output-file={out}", check=True, timeout=60)
+        labels = golden.parse_labels(out.read_text())
+        assert labels["amd.com/gpu.count"] == str(want), labels
+        assert "MI355" in labels["amd.com/gpu.product"]
+        assert labels["amd.com/gpu.memory"] == "294896"
+        assert labels["amd.com/gpu.compute-partition"] == "SPX"
+        assert labels["amd.com/gpu.memory-partition"] == "NPS1"
+        assert labels["amd.com/gpu.xgmi.links"] == "7"  # minimum over the GPUs: every one has its 7 hive links

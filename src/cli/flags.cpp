@@ -168,7 +168,8 @@ std::vector<FlagDef> gfd_flags() {
        "the path to a config file as an alternative to command line options or environment variables"},
       // AMD extensions.
       {"backend", {}, T::String, "auto", {"GFD_BACKEND"},
-       "device backend: auto (amd-smi, else KFD sysfs, else none) | amdsmi | sysfs | null | mock"},
+       "device backend: auto (amd-smi once initialised - in the background, KFD sysfs until then; --oneshot: KFD\n\t\t"
+       "sysfs; without amd-smi: KFD sysfs, else none) | amdsmi | sysfs | null | mock"},
       {"sysfs-root", {}, T::String, "/", {"GFD_SYSFS_ROOT"},
        "root prefix for sysfs/procfs reads (synthetic trees for testing)"},
       {"host-root", {}, T::String, "", {"GFD_HOST_ROOT"},

@@ -525,6 +525,87 @@ std::string format_bdf(const amdsmi_bdf_t& b) {
 
 }  // namespace
 
+// The node's GPU processors grouped into physical GPUs (each group ordered
+// as amd-smi listed it), ordered by parent PCI function; every processor's
+// gpu_bdf set.  `parents` caches the parent function per group for the
+// session (resolve_parent_bdf reads sysfs).
+static std::vector<std::vector<ProcInfo>> collect_physical_gpus(AmdSmiLib& L, const std::string& root,
+                                                                std::map<std::string, std::string>& parents) {
+  uint32_t ns = 0;
+  amdsmi_status_t st = L.get_socket_handles(&ns, nullptr);
+  if (st != AMDSMI_STATUS_SUCCESS) call_failed(L, "amdsmi_get_socket_handles", st);
+  std::vector<amdsmi_socket_handle> sockets(ns);
+  if (ns) {
+    st = L.get_socket_handles(&ns, sockets.data());
+    if (st != AMDSMI_STATUS_SUCCESS) call_failed(L, "amdsmi_get_socket_handles", st);
+    sockets.resize(ns);
+  }
+
+  // Collect GPU processors by PCI slot (domain:bus:device - amd-smi's own
+  // socket id, the same for every partition of a GPU under both KFD
+  // location layouts; resource/physical.h).
+  std::map<std::string, std::vector<ProcInfo>> slots;
+  for (auto s : sockets) {
+    uint32_t np = 0;
+    st = L.get_processor_handles(s, &np, nullptr);
+    if (st != AMDSMI_STATUS_SUCCESS) call_failed(L, "amdsmi_get_processor_handles", st);
+    std::vector<amdsmi_processor_handle> procs(np);
+    if (np) {
+      st = L.get_processor_handles(s, &np, procs.data());
+      if (st != AMDSMI_STATUS_SUCCESS) call_failed(L, "amdsmi_get_processor_handles", st);
+      procs.resize(np);
+    }
+    for (auto h : procs) {
+      processor_type_t t;
+      if (L.get_processor_type(h, &t) != AMDSMI_STATUS_SUCCESS || t != AMDSMI_PROCESSOR_TYPE_AMD_GPU) continue;
+      amdsmi_bdf_t b;
+      std::memset(&b, 0, sizeof(b));
+      st = L.get_gpu_device_bdf(h, &b);
+      if (st != AMDSMI_STATUS_SUCCESS) call_failed(L, "amdsmi_get_gpu_device_bdf", st);
+      ProcInfo p;
+      p.h = h;
+      p.bdf = format_bdf(b);
+      slots[bdf_slot(p.bdf)].push_back(p);
+    }
+  }
+
+  // Split slots into physical GPUs.  One processor: a GPU (the hot path, no
+  // further calls).  Several: the partitions of one GPU when they share the
+  // ASIC serial and the family puts partitions on one slot; otherwise
+  // distinct GPUs that happen to share a slot (e.g. ARI virtual functions).
+  std::vector<std::vector<ProcInfo>> physical;
+  for (auto& [slot, procs] : slots) {
+    if (procs.size() == 1) {
+      physical.push_back(std::move(procs));
+      continue;
+    }
+    std::map<std::string, std::vector<ProcInfo>> by_gpu;
+    for (auto& p : procs) {
+      query_identity(L, p);
+      bool partitions = partition_index_in_function_bits(gfx_target_from_amdsmi(p.gfx));
+      by_gpu[partitions ? "serial:" + p.uuid : "bdf:" + p.bdf].push_back(std::move(p));
+    }
+    for (auto& [key, members] : by_gpu) physical.push_back(std::move(members));
+  }
+  // Parent PCI function of each GPU, resolved once per session.
+  for (auto& procs : physical) {
+    std::vector<std::string> bdfs;
+    for (const auto& p : procs) bdfs.push_back(p.bdf);
+    std::string key = str::join(bdfs, ",");
+    auto it = parents.find(key);
+    if (it == parents.end()) {
+      uint32_t device_id = 0;
+      if (procs.size() > 1) device_id = procs.front().device_id;  // identified above
+      it = parents.emplace(key, resolve_parent_bdf(root, bdfs, device_id)).first;
+    }
+    for (auto& p : procs) p.gpu_bdf = it->second;
+  }
+  std::sort(physical.begin(), physical.end(),
+            [](const std::vector<ProcInfo>& a, const std::vector<ProcInfo>& b) { return a[0].gpu_bdf < b[0].gpu_bdf; });
+
+  return physical;
+}
+
 // ---------------------------------------------------------------------------
 // AmdSmiManager
 
@@ -610,78 +691,7 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
   AmdSmiLib& L = *lib_;
   trace::Span span("amdsmi.snapshot");
   int64_t handles_t0 = trace::now_ns();
-  uint32_t ns = 0;
-  amdsmi_status_t st = L.get_socket_handles(&ns, nullptr);
-  if (st != AMDSMI_STATUS_SUCCESS) call_failed(L, "amdsmi_get_socket_handles", st);
-  std::vector<amdsmi_socket_handle> sockets(ns);
-  if (ns) {
-    st = L.get_socket_handles(&ns, sockets.data());
-    if (st != AMDSMI_STATUS_SUCCESS) call_failed(L, "amdsmi_get_socket_handles", st);
-    sockets.resize(ns);
-  }
-
-  // Collect GPU processors by PCI slot (domain:bus:device - amd-smi's own
-  // socket id, the same for every partition of a GPU under both KFD
-  // location layouts; resource/physical.h).
-  std::map<std::string, std::vector<ProcInfo>> slots;
-  for (auto s : sockets) {
-    uint32_t np = 0;
-    st = L.get_processor_handles(s, &np, nullptr);
-    if (st != AMDSMI_STATUS_SUCCESS) call_failed(L, "amdsmi_get_processor_handles", st);
-    std::vector<amdsmi_processor_handle> procs(np);
-    if (np) {
-      st = L.get_processor_handles(s, &np, procs.data());
-      if (st != AMDSMI_STATUS_SUCCESS) call_failed(L, "amdsmi_get_processor_handles", st);
-      procs.resize(np);
-    }
-    for (auto h : procs) {
-      processor_type_t t;
-      if (L.get_processor_type(h, &t) != AMDSMI_STATUS_SUCCESS || t != AMDSMI_PROCESSOR_TYPE_AMD_GPU) continue;
-      amdsmi_bdf_t b;
-      std::memset(&b, 0, sizeof(b));
-      st = L.get_gpu_device_bdf(h, &b);
-      if (st != AMDSMI_STATUS_SUCCESS) call_failed(L, "amdsmi_get_gpu_device_bdf", st);
-      ProcInfo p;
-      p.h = h;
-      p.bdf = format_bdf(b);
-      slots[bdf_slot(p.bdf)].push_back(p);
-    }
-  }
-
-  // Split slots into physical GPUs.  One processor: a GPU (the hot path, no
-  // further calls).  Several: the partitions of one GPU when they share the
-  // ASIC serial and the family puts partitions on one slot; otherwise
-  // distinct GPUs that happen to share a slot (e.g. ARI virtual functions).
-  std::vector<std::vector<ProcInfo>> physical;
-  for (auto& [slot, procs] : slots) {
-    if (procs.size() == 1) {
-      physical.push_back(std::move(procs));
-      continue;
-    }
-    std::map<std::string, std::vector<ProcInfo>> by_gpu;
-    for (auto& p : procs) {
-      query_identity(L, p);
-      bool partitions = partition_index_in_function_bits(gfx_target_from_amdsmi(p.gfx));
-      by_gpu[partitions ? "serial:" + p.uuid : "bdf:" + p.bdf].push_back(std::move(p));
-    }
-    for (auto& [key, members] : by_gpu) physical.push_back(std::move(members));
-  }
-  // Parent PCI function of each GPU, resolved once per session.
-  for (auto& procs : physical) {
-    std::vector<std::string> bdfs;
-    for (const auto& p : procs) bdfs.push_back(p.bdf);
-    std::string key = str::join(bdfs, ",");
-    auto it = parent_bdf_.find(key);
-    if (it == parent_bdf_.end()) {
-      uint32_t device_id = 0;
-      if (procs.size() > 1) device_id = procs.front().device_id;  // identified above
-      it = parent_bdf_.emplace(key, resolve_parent_bdf(opts_.root, bdfs, device_id)).first;
-    }
-    for (auto& p : procs) p.gpu_bdf = it->second;
-  }
-  std::sort(physical.begin(), physical.end(),
-            [](const std::vector<ProcInfo>& a, const std::vector<ProcInfo>& b) { return a[0].gpu_bdf < b[0].gpu_bdf; });
-
+  std::vector<std::vector<ProcInfo>> physical = collect_physical_gpus(L, opts_.root, parent_bdf_);
   trace::record("amdsmi.handles", trace::now_ns() - handles_t0);
 
   // Apply the visible-device filter on physical GPUs (index = parent BDF order).

@@ -68,11 +68,20 @@ void WarmStartManager::fall_back(const std::string& why) {
 void WarmStartManager::Init() {
   if (state_ == State::cold) {
     // A persistent session stays initialised after Shutdown: the warmer
-    // opens it, and the cycle that switches over finds it ready.
+    // opens it and takes one snapshot - the library's first queries of a
+    // device (~1.2 ms on MI355X: ASIC info, KFD node, virtualization mode)
+    // and the session caches are paid here too - so the cycle that switches
+    // over finds everything ready.
     warmer_ = std::thread([this] {
       int64_t t0 = trace::now_ns();
       try {
         preferred_->Init();
+        try {
+          preferred_->GetDevices();
+        } catch (...) {
+          preferred_->Shutdown();
+          throw;
+        }
         preferred_->Shutdown();
       } catch (const std::exception& e) {
         warm_error_ = e.what();

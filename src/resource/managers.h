@@ -82,7 +82,8 @@ class PreferenceManager : public Manager {
 // ~25 ms (it parses all of /proc/cpuinfo, profiles/amdsmi_init_profile.txt)
 // while the KFD topology answers the same questions with byte-identical
 // labels (tests/test_gpu.py).  So the first cycle is labelled from KFD while
-// the preferred manager initialises on a background thread; the first cycle
+// the preferred manager initialises - and takes one snapshot, paying its
+// first-query costs - on a background thread; the first cycle
 // that finds it ready switches to it for good.  If its initialisation
 // failed - or it fails later - the quick manager keeps serving until the
 // manager is rebuilt (SIGHUP), as with PreferenceManager.  Switching happens

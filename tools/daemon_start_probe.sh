@@ -11,5 +11,5 @@ for i in 1 2 3; do
   sleep 1
   kill -TERM $pid
   wait $pid
-  grep -iE "timing:|Detected|Using|Initializing" "$out/run$i.err" | head -8
+  grep -iE "timing:|Detected|Using|Initializing" "$out/run$i.err" | head -12
 done

@@ -4,6 +4,8 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
+#include <chrono>
 #include <cstdio>
 
 #include "lm/keys.h"
@@ -348,6 +350,30 @@ TEST(WriteToFile_AtomicWithMode0644) {
   lm::remove_output_file(path);
   EXPECT_FALSE(fs::exists(path));
   EXPECT_FALSE(fs::exists(std::string(dir) + "/gfd-tmp"));
+  fs::remove_all(dir);
+}
+
+TEST(WriteToFile_ReplaceKeepsExactContentsAndStaysFast) {
+  // Every cycle after the first replaces the file (rename over it).  On ext4
+  // that used to flush the new file inside rename(2) (~55 ms, auto_da_alloc);
+  // the writer preallocates there.  Contents and size must stay exact when
+  // the label set shrinks, and the median replace must stay far below that.
+  char dir[] = "/tmp/gfd-write-XXXXXX";
+  EXPECT_TRUE(mkdtemp(dir) != nullptr);
+  std::string path = std::string(dir) + "/gfd";
+  lm::write_to_file({{"k", std::string(5000, 'v')}}, path);
+  std::vector<double> us;
+  for (int i = 0; i < 9; ++i) {
+    auto t0 = std::chrono::steady_clock::now();
+    lm::write_to_file({{"k", std::to_string(i)}}, path);
+    us.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+    EXPECT_EQ(fs::read_file(path).data, "k=" + std::to_string(i) + "\n");
+  }
+  struct stat st;
+  EXPECT_TRUE(stat(path.c_str(), &st) == 0);
+  EXPECT_EQ(static_cast<long>(st.st_size), 4L);
+  std::sort(us.begin(), us.end());
+  EXPECT_TRUE(us[us.size() / 2] < 5000.0);
   fs::remove_all(dir);
 }
 

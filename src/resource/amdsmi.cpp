@@ -11,6 +11,7 @@
 
 #include "resource/pci_ids.h"
 #include "resource/physical.h"
+#include "resource/sysfs.h"
 #include "resource/versions.h"
 #include "util/dynlib.h"
 #include "util/error.h"
@@ -54,6 +55,9 @@ class AmdSmiLib {
   // Process-wide init state (amdsmi_init is global).
   std::mutex mu;
   int users = 0;
+  // Set once amd-smi has refused asic_info with NOT_SUPPORTED (see
+  // identity_from_kfd); reset by every amdsmi_init, so a session asks once.
+  std::atomic<bool> asic_info_unsupported{false};
 
 #define GFD_AMDSMI_FN(name, ...) amdsmi_status_t (*name)(__VA_ARGS__) = nullptr
   GFD_AMDSMI_FN(init, uint64_t);
@@ -251,6 +255,22 @@ auto timed(const char* name, F&& f) -> decltype(f()) {
 // observed on the MI355X pool.
 bool is_generic_name(const std::string& s) { return s.empty() || s == "AMD Radeon Graphics" || s == "N/A"; }
 
+constexpr uint32_t kNoNode = 0xFFFFFFFFu;
+
+// A numeric field of a KFD node's properties text ("key value" lines).
+std::optional<uint64_t> kfd_field(const std::string& text, const std::string& key) {
+  for (size_t pos = text.find(key); pos != std::string::npos; pos = text.find(key, pos + 1)) {
+    size_t end = pos + key.size();
+    if ((pos == 0 || text[pos - 1] == '\n') && end < text.size() && text[end] == ' ')
+      return std::strtoull(text.c_str() + end + 1, nullptr, 10);
+  }
+  return std::nullopt;
+}
+
+fs::ReadResult kfd_properties(const std::string& root, uint32_t node_id) {
+  return fs::attrs().read(fs::join(root, "sys/class/kfd/kfd/topology/nodes/" + std::to_string(node_id) + "/properties"));
+}
+
 // XCD and SDMA-engine counts of a KFD node (num_xcc, num_sdma_engines) -
 // ~15 us versus ~140 us for amdsmi_get_gpu_xcd_counter, which decodes the
 // full gpu_metrics table.  Zero / -1 when the node cannot be read.
@@ -260,28 +280,74 @@ struct KfdCounts {
 };
 KfdCounts kfd_counts(const std::string& root, uint32_t node_id) {
   KfdCounts c;
-  auto r = fs::attrs().read(fs::join(root, "sys/class/kfd/kfd/topology/nodes/" + std::to_string(node_id) + "/properties"));
+  auto r = kfd_properties(root, node_id);
   if (!r.ok()) return c;
-  auto field = [&](const char* key, size_t len) -> std::optional<unsigned long> {
-    auto pos = r.data.find(key);
-    if (pos == std::string::npos) return std::nullopt;
-    return strtoul(r.data.c_str() + pos + len, nullptr, 10);
-  };
-  static const char kXcc[] = "\nnum_xcc ";
-  static const char kSdma[] = "\nnum_sdma_engines ";
-  if (auto v = field(kXcc, sizeof(kXcc) - 1)) c.num_xcc = static_cast<uint32_t>(*v);
-  if (auto v = field(kSdma, sizeof(kSdma) - 1)) c.num_sdma = static_cast<int>(*v);
+  if (auto v = kfd_field(r.data, "num_xcc")) c.num_xcc = static_cast<uint32_t>(*v);
+  if (auto v = kfd_field(r.data, "num_sdma_engines")) c.num_sdma = static_cast<int>(*v);
   return c;
 }
 uint32_t kfd_num_xcc(const std::string& root, uint32_t node_id) { return kfd_counts(root, node_id).num_xcc; }
 
+// KFD node and partition id of a processor (amdsmi_get_gpu_kfd_info).
+bool query_kfd(AmdSmiLib& L, ProcInfo& p, uint32_t* node_id) {
+  if (!L.get_gpu_kfd_info) return false;
+  amdsmi_kfd_info_t kfd;
+  std::memset(&kfd, 0, sizeof(kfd));
+  if (AMDSMI_CALL("kfd_info", L.get_gpu_kfd_info(p.h, &kfd)) != AMDSMI_STATUS_SUCCESS) return false;
+  if (kfd.current_partition_id != 0xFFFFFFFFu) p.partition_id = kfd.current_partition_id;
+  *node_id = kfd.node_id;
+  return true;
+}
+
+// KFD's gfx_target_version (major*10000 + minor*100 + stepping, decimal) in
+// amd-smi's spelling (hex digits naming the target: 90500 -> 0x950).
+uint64_t amdsmi_gfx_from_kfd(uint64_t v) {
+  uint64_t major = v / 10000, minor = (v / 100) % 100, step = v % 100;
+  uint64_t maj_hex = 0;
+  for (uint64_t shift = 0; major; major /= 10, shift += 4) maj_hex |= (major % 10) << shift;
+  return (maj_hex << 8) | ((minor & 0xF) << 4) | (step & 0xF);
+}
+
+// The processor's identity from its KFD node - the same facts amd-smi's
+// ASIC info reports (vendor/device ID, CUs, ISA target, serial), for when
+// that call is refused.  amd-smi answers it through libdrm_amdgpu, which it
+// dlopens; without that library (a slim image) asic_info returns
+// NOT_SUPPORTED for every processor (measured on the pool,
+// tests/test_gpu.py::test_amdsmi_without_libdrm_labels_identically).  The
+// name comes from the board's product_name attribute (fix_market_name).
+bool identity_from_kfd(AmdSmiLib& L, const std::string& root, ProcInfo& p) {
+  uint32_t node = kNoNode;
+  if (!query_kfd(L, p, &node) || node == kNoNode) return false;
+  auto r = kfd_properties(root, node);
+  if (!r.ok()) return false;
+  uint64_t gfx = kfd_field(r.data, "gfx_target_version").value_or(0);
+  uint64_t device = kfd_field(r.data, "device_id").value_or(0);
+  if (gfx == 0 || device == 0) return false;
+  uint64_t simds = kfd_field(r.data, "simd_count").value_or(0), per_cu = kfd_field(r.data, "simd_per_cu").value_or(0);
+  p.market_name.clear();
+  p.vendor_id = static_cast<uint32_t>(kfd_field(r.data, "vendor_id").value_or(0));
+  p.device_id = static_cast<uint32_t>(device);
+  p.cus = per_cu ? static_cast<uint32_t>(simds / per_cu) : 0;
+  p.gfx = amdsmi_gfx_from_kfd(gfx);
+  p.uuid = amd_uuid(kfd_field(r.data, "unique_id").value_or(0), p.device_id);
+  return true;
+}
+
 // Identity of a processor from its ASIC info (the library caches it after
-// the first call: ~2 us).
-void query_identity(AmdSmiLib& L, ProcInfo& p) {
+// the first call: ~2 us), or from its KFD node when amd-smi cannot answer.
+void query_identity(AmdSmiLib& L, const std::string& root, ProcInfo& p) {
   if (p.identified) return;
+  amdsmi_status_t st = AMDSMI_STATUS_NOT_SUPPORTED;
   amdsmi_asic_info_t asic;
   std::memset(&asic, 0, sizeof(asic));
-  amdsmi_status_t st = AMDSMI_CALL("asic_info", L.get_gpu_asic_info(p.h, &asic));
+  if (!L.asic_info_unsupported.load(std::memory_order_relaxed))
+    st = AMDSMI_CALL("asic_info", L.get_gpu_asic_info(p.h, &asic));
+  if (st == AMDSMI_STATUS_NOT_SUPPORTED) {
+    if (!identity_from_kfd(L, root, p)) call_failed(L, "amdsmi_get_gpu_asic_info", st);
+    L.asic_info_unsupported.store(true, std::memory_order_relaxed);
+    p.identified = true;
+    return;
+  }
   if (st != AMDSMI_STATUS_SUCCESS) call_failed(L, "amdsmi_get_gpu_asic_info", st);
   p.market_name = str::trim(asic.market_name);
   p.vendor_id = asic.vendor_id;
@@ -314,17 +380,6 @@ void fix_market_name(AmdSmiLib& L, const std::string& root, ProcInfo& p) {
   }
 }
 
-// KFD node and partition id of a processor (amdsmi_get_gpu_kfd_info).
-bool query_kfd(AmdSmiLib& L, ProcInfo& p, uint32_t* node_id) {
-  if (!L.get_gpu_kfd_info) return false;
-  amdsmi_kfd_info_t kfd;
-  std::memset(&kfd, 0, sizeof(kfd));
-  if (AMDSMI_CALL("kfd_info", L.get_gpu_kfd_info(p.h, &kfd)) != AMDSMI_STATUS_SUCCESS) return false;
-  if (kfd.current_partition_id != 0xFFFFFFFFu) p.partition_id = kfd.current_partition_id;
-  *node_id = kfd.node_id;
-  return true;
-}
-
 bool sysfs_values_enabled() {
   static const bool on = [] {
     const char* v = std::getenv("GFD_AMDSMI_SYSFS");
@@ -332,8 +387,6 @@ bool sysfs_values_enabled() {
   }();
   return on;
 }
-
-constexpr uint32_t kNoNode = 0xFFFFFFFFu;
 
 // The only processor at its PCI address and in SPX mode: its per-cycle
 // values are the amdgpu attributes amd-smi reads for the same calls
@@ -353,7 +406,7 @@ bool query_unpartitioned(AmdSmiLib& L, const std::string& root, ProcInfo& p, Amd
   auto vram = vram_s ? str::parse_uint(*vram_s) : std::nullopt;
   if (!vram || *vram == 0) return false;
   if (*node_id == kNoNode && !query_kfd(L, p, node_id)) return false;
-  query_identity(L, p);
+  query_identity(L, root, p);
   p.compute_partition = *cp;
   p.memory_partition = *mp;
   p.vram = *vram;
@@ -398,7 +451,7 @@ bool query_partitioned(AmdSmiLib& L, const std::string& root, std::vector<ProcIn
       f.sdma = c.num_sdma;
       f.mem_bytes = mem;
     }
-    query_identity(L, p);
+    query_identity(L, root, p);
     p.partition_id = f.partition_id;
     p.xcds = f.num_xcc;
     p.sdma = f.sdma;
@@ -413,7 +466,7 @@ bool query_partitioned(AmdSmiLib& L, const std::string& root, std::vector<ProcIn
 
 // Every value through amd-smi (partitioned GPUs, or sysfs values disabled).
 void query_proc(AmdSmiLib& L, const std::string& root, ProcInfo& p) {
-  query_identity(L, p);
+  query_identity(L, root, p);
 
   uint64_t total = 0;
   if (AMDSMI_CALL("memory_total", L.get_gpu_memory_total(p.h, AMDSMI_MEM_TYPE_VRAM, &total)) == AMDSMI_STATUS_SUCCESS)
@@ -479,10 +532,18 @@ void query_gpu_caps(AmdSmiLib& L, const ProcInfo& p, const std::string& root, Gp
     }
   }
   // Pre-filled from the session cache when already known (see snapshot()).
+  // Without an answer from amd-smi (it refuses the query when it could not
+  // load libdrm_amdgpu) the driver's classification from sysfs, as the KFD
+  // backend labels it.
   if (x.virtualization.empty() && L.get_gpu_virtualization_mode) {
     amdsmi_virtualization_mode_t vm = AMDSMI_VIRTUALIZATION_MODE_UNKNOWN;
     if (AMDSMI_CALL("virtualization_mode", L.get_gpu_virtualization_mode(p.h, &vm)) == AMDSMI_STATUS_SUCCESS)
       x.virtualization = virt_name(vm);
+  }
+  if (x.virtualization.empty()) {
+    std::string pci = fs::join(root, "sys/bus/pci/devices/" + p.gpu_bdf);
+    if (fs::exists(pci))
+      x.virtualization = classify_virtualization(pci, p.device_id, running_in_vm(root), fs::exists(pci + "/physfn"));
   }
   // Supported memory partition modes: world-readable in sysfs (~5 us);
   // the amd-smi partition-config call (~25 us) only as a fallback.
@@ -496,9 +557,16 @@ void query_gpu_caps(AmdSmiLib& L, const ProcInfo& p, const std::string& root, Gp
     if (AMDSMI_CALL("memory_partition_config", L.get_gpu_memory_partition_config(p.h, &cfg)) == AMDSMI_STATUS_SUCCESS)
       x.available_memory = nps_list(cfg.partition_caps.nps_cap_mask);
   }
-  // Supported compute partition modes: the profile table needs root; the
-  // same information is world-readable in sysfs, which amd-smi itself reads.
-  if (L.get_gpu_accelerator_partition_profile_config) {
+  // Supported compute partition modes: world-readable in sysfs, the source
+  // amd-smi reads too; the library's profile table (root only: NO_PERM for
+  // a pod, and a partial table when amd-smi runs without libdrm_amdgpu)
+  // only as a fallback.
+  if (auto v = AMDSMI_CALL("available_compute_partition(sysfs)",
+                           fs::attrs().read_trimmed(fs::join(root, "sys/bus/pci/devices/" + p.gpu_bdf + "/available_compute_partition")))) {
+    for (auto& m : str::split(*v, ','))
+      if (!str::trim(m).empty()) x.available_compute.push_back(str::trim(m));
+  }
+  if (x.available_compute.empty() && L.get_gpu_accelerator_partition_profile_config) {
     amdsmi_accelerator_partition_profile_config_t cfg;
     std::memset(&cfg, 0, sizeof(cfg));
     if (AMDSMI_CALL("partition_profile_config", L.get_gpu_accelerator_partition_profile_config(p.h, &cfg)) ==
@@ -506,13 +574,6 @@ void query_gpu_caps(AmdSmiLib& L, const ProcInfo& p, const std::string& root, Gp
       for (uint32_t i = 0; i < cfg.num_profiles && i < AMDSMI_MAX_ACCELERATOR_PROFILE; ++i)
         if (const char* n = accel_name(cfg.profiles[i].profile_type)) x.available_compute.push_back(n);
     }
-  }
-  if (x.available_compute.empty()) {
-    auto v = AMDSMI_CALL("available_compute_partition(sysfs)",
-                         fs::attrs().read_trimmed(fs::join(root, "sys/bus/pci/devices/" + p.gpu_bdf + "/available_compute_partition")));
-    if (v)
-      for (auto& m : str::split(*v, ','))
-        if (!str::trim(m).empty()) x.available_compute.push_back(str::trim(m));
   }
 }
 
@@ -523,6 +584,29 @@ std::string format_bdf(const amdsmi_bdf_t& b) {
 }
 
 
+// The PCI address of a processor, decided once per session.  amd-smi's
+// answer stands when it is a PCI function under <root>/sys, or when nothing
+// better is known; otherwise (amd-smi without libdrm_amdgpu reports garbage
+// such as "5ddf28c0:c2:1a.0" with success) the address KFD reports for the
+// processor's node (domain, location_id) - what amd-smi reports when libdrm
+// works, including a partition's index in the function bits.
+std::string checked_bdf(AmdSmiLib& L, const std::string& root, amdsmi_processor_handle h, const amdsmi_bdf_t& b) {
+  std::string bdf = format_bdf(b);
+  if (fs::exists(fs::join(root, "sys/bus/pci/devices/" + bdf))) return bdf;
+  ProcInfo p;
+  p.h = h;
+  uint32_t node = kNoNode;
+  if (!query_kfd(L, p, &node) || node == kNoNode) return bdf;
+  auto r = kfd_properties(root, node);
+  if (!r.ok()) return bdf;
+  uint64_t location = kfd_field(r.data, "location_id").value_or(0);
+  if (location == 0) return bdf;
+  uint64_t domain = kfd_field(r.data, "domain").value_or(0);
+  return str::format("%04llx:%02x:%02x.%x", static_cast<unsigned long long>(domain),
+                     static_cast<unsigned>((location >> 8) & 0xff), static_cast<unsigned>((location >> 3) & 0x1f),
+                     static_cast<unsigned>(location & 0x7));
+}
+
 }  // namespace
 
 // The node's GPU processors grouped into physical GPUs (each group ordered
@@ -530,7 +614,8 @@ std::string format_bdf(const amdsmi_bdf_t& b) {
 // gpu_bdf set.  `parents` caches the parent function per group for the
 // session (resolve_parent_bdf reads sysfs).
 static std::vector<std::vector<ProcInfo>> collect_physical_gpus(AmdSmiLib& L, const std::string& root,
-                                                                std::map<std::string, std::string>& parents) {
+                                                                std::map<std::string, std::string>& parents,
+                                                                std::map<void*, std::string>& proc_bdfs) {
   uint32_t ns = 0;
   amdsmi_status_t st = L.get_socket_handles(&ns, nullptr);
   if (st != AMDSMI_STATUS_SUCCESS) call_failed(L, "amdsmi_get_socket_handles", st);
@@ -558,13 +643,17 @@ static std::vector<std::vector<ProcInfo>> collect_physical_gpus(AmdSmiLib& L, co
     for (auto h : procs) {
       processor_type_t t;
       if (L.get_processor_type(h, &t) != AMDSMI_STATUS_SUCCESS || t != AMDSMI_PROCESSOR_TYPE_AMD_GPU) continue;
-      amdsmi_bdf_t b;
-      std::memset(&b, 0, sizeof(b));
-      st = L.get_gpu_device_bdf(h, &b);
-      if (st != AMDSMI_STATUS_SUCCESS) call_failed(L, "amdsmi_get_gpu_device_bdf", st);
+      auto known = proc_bdfs.find(h);
+      if (known == proc_bdfs.end()) {
+        amdsmi_bdf_t b;
+        std::memset(&b, 0, sizeof(b));
+        st = L.get_gpu_device_bdf(h, &b);
+        if (st != AMDSMI_STATUS_SUCCESS) call_failed(L, "amdsmi_get_gpu_device_bdf", st);
+        known = proc_bdfs.emplace(h, checked_bdf(L, root, h, b)).first;
+      }
       ProcInfo p;
       p.h = h;
-      p.bdf = format_bdf(b);
+      p.bdf = known->second;
       slots[bdf_slot(p.bdf)].push_back(p);
     }
   }
@@ -581,7 +670,7 @@ static std::vector<std::vector<ProcInfo>> collect_physical_gpus(AmdSmiLib& L, co
     }
     std::map<std::string, std::vector<ProcInfo>> by_gpu;
     for (auto& p : procs) {
-      query_identity(L, p);
+      query_identity(L, root, p);
       bool partitions = partition_index_in_function_bits(gfx_target_from_amdsmi(p.gfx));
       by_gpu[partitions ? "serial:" + p.uuid : "bdf:" + p.bdf].push_back(std::move(p));
     }
@@ -621,11 +710,13 @@ void AmdSmiManager::library_init() {
   amdsmi_status_t st = lib_->init(AMDSMI_INIT_AMD_GPUS);
   if (st != AMDSMI_STATUS_SUCCESS) throw Error("amdsmi_init failed: " + lib_->status_str(st));
   lib_->users++;
+  lib_->asic_info_unsupported = false;
   lib_initialized_ = true;
   virt_mode_.clear();
   kfd_node_.clear();
   partition_facts_.clear();
   parent_bdf_.clear();
+  proc_bdf_.clear();
   ++init_count_;
 }
 
@@ -691,7 +782,7 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
   AmdSmiLib& L = *lib_;
   trace::Span span("amdsmi.snapshot");
   int64_t handles_t0 = trace::now_ns();
-  std::vector<std::vector<ProcInfo>> physical = collect_physical_gpus(L, opts_.root, parent_bdf_);
+  std::vector<std::vector<ProcInfo>> physical = collect_physical_gpus(L, opts_.root, parent_bdf_, proc_bdf_);
   trace::record("amdsmi.handles", trace::now_ns() - handles_t0);
 
   // Apply the visible-device filter on physical GPUs (index = parent BDF order).

@@ -122,6 +122,12 @@ class AmdSmiManager : public Manager {
   // for the lifetime of one session: processor addresses and PCI functions
   // only change with a driver reload or partition switch, which re-initialise.
   std::map<std::string, std::string> parent_bdf_;
+  // PCI address of each processor (by handle) for the lifetime of one
+  // session, checked once against sysfs and the processor's KFD node
+  // (checked_bdf in amdsmi.cpp): amd-smi reads it through libdrm and, when
+  // it could not load libdrm_amdgpu, returns uninitialised bytes with
+  // success (measured on the pool).  Also saves the call on every cycle.
+  std::map<void*, std::string> proc_bdf_;
   // Every GPU took the attribute path in the last snapshot (lane sizing).
   bool all_fast_ = false;
 };

@@ -2,6 +2,7 @@
 
 #include <algorithm>
 
+#include "resource/pci_ids.h"
 #include "util/fs.h"
 #include "util/strings.h"
 
@@ -12,6 +13,13 @@ bool partition_index_in_function_bits(const GfxTarget& t) { return t.major == 9 
 std::string bdf_slot(const std::string& bdf) {
   auto dot = bdf.rfind('.');
   return dot == std::string::npos ? bdf : bdf.substr(0, dot);
+}
+
+std::string classify_virtualization(const std::string& pci_dir, uint32_t device_id, bool in_vm, bool has_physfn) {
+  if (is_mxgpu_vf(device_id) || has_physfn) return "guest";
+  if (auto nv = fs::attrs().read_trimmed(fs::join(pci_dir, "sriov_numvfs")); nv && str::parse_uint(*nv).value_or(0) > 0)
+    return "host";
+  return in_vm ? "passthrough" : "baremetal";
 }
 
 std::string resolve_parent_bdf(const std::string& root, std::vector<std::string> member_bdfs, uint32_t device_id) {

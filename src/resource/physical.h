@@ -46,6 +46,13 @@ std::string bdf_slot(const std::string& bdf);
 // member address is returned.
 std::string resolve_parent_bdf(const std::string& root, std::vector<std::string> member_bdfs, uint32_t device_id);
 
+// amdgpu's own virtualization classification (amdgpu_detect_virtualization)
+// from what a container can see, for the PCI function at `pci_dir`: an
+// SR-IOV virtual function (MxGPU VF device ID, or a `physfn` link) runs as a
+// guest; a physical function with VFs enabled is the host; a whole GPU in a
+// VM (`in_vm`: running_in_vm) is passthrough; otherwise bare metal.
+std::string classify_virtualization(const std::string& pci_dir, uint32_t device_id, bool in_vm, bool has_physfn);
+
 // Device-local memory (bytes) of a KFD topology node: the sum of its
 // frame-buffer memory banks (mem_banks/N/properties, heap types 1 and 2).
 // For a partition node that is the partition's share of HBM

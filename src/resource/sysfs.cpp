@@ -103,21 +103,6 @@ std::string bdf_of(const KfdNode& n) {
   unsigned fn = static_cast<unsigned>(n.location_id & 0x7);
   return str::format("%04x:%02x:%02x.%x", static_cast<unsigned>(n.domain), bus, dev, fn);
 }
-
-
-// Fallback names when the board FRU does not expose product_name.
-
-// amdgpu's own classification (amdgpu_detect_virtualization), from what a
-// container can see: an SR-IOV virtual function runs as a guest; a physical
-// function with VFs enabled is the host; a whole GPU inside a VM is
-// passthrough; otherwise bare metal.
-std::string virtualization_mode(const std::string& pci, uint32_t device_id, bool in_vm, bool has_physfn) {
-  if (is_mxgpu_vf(device_id) || has_physfn) return "guest";
-  if (auto nv = fs::attrs().read_trimmed(fs::join(pci, "sriov_numvfs")); nv && str::parse_uint(*nv).value_or(0) > 0)
-    return "host";
-  return in_vm ? "passthrough" : "baremetal";
-}
-
 }  // namespace
 
 bool running_in_vm(const std::string& root) {
@@ -201,7 +186,7 @@ static DevicePtr describe_gpu(const std::string& root, bool in_vm, int index, co
   info.available_compute_partitions = split_list(fs::attrs().read_trimmed(fs::join(pci, "available_compute_partition")).value_or(""));
   info.available_memory_partitions = split_list(fs::attrs().read_trimmed(fs::join(pci, "available_memory_partition")).value_or(""));
   if (auto x = fs::attrs().read_trimmed(fs::join(pci, "xgmi_num_links"))) info.xgmi_links = sum_links(*x);
-  info.virtualization = virtualization_mode(pci, info.device_id, in_vm, has_physfn);
+  info.virtualization = classify_virtualization(pci, info.device_id, in_vm, has_physfn);
 
   bool partitioned = members.size() > 1 || (!info.compute_partition.empty() && info.compute_partition != "SPX");
   uint64_t vram = 0;

@@ -19,6 +19,11 @@
 //   sockets=slot              one socket per PCI slot, i.e. per physical GPU
 //                             (what amd-smi does; the default) - or `one`: a
 //                             single socket holding every processor
+//   no_libdrm=1               amd-smi as it behaves when it cannot load
+//                             libdrm_amdgpu (measured on MI355X): ASIC info
+//                             and virtualization mode NOT_SUPPORTED, the BDF
+//                             call succeeds with garbage, the partition
+//                             profile table lists SPX only
 //   latency_us=N              every device query except handle-table lookups
 //                             (processor type, BDF, ASIC info) busy-waits N us
 //                             holding that GPU's lock (amd-smi serialises per
@@ -75,6 +80,7 @@ struct State {
   std::atomic<int> virt_calls{0};
   int shutdown_calls = 0;
   long latency_us = 0;
+  bool no_libdrm = false;
   std::map<std::string, std::unique_ptr<std::mutex>> device_mu;  // by BDF
   std::map<std::string, int> fail;                               // function -> status
   std::map<std::string, long> calls;                             // function -> device queries made
@@ -155,6 +161,7 @@ int fake_amdsmi_configure(const char* spec) {
   s.init_status = 0;
   s.stale_after = -1;
   s.latency_us = 0;
+  s.no_libdrm = false;
   s.fail.clear();
   s.calls.clear();
   s.queries = 0;
@@ -186,6 +193,14 @@ int fake_amdsmi_configure(const char* spec) {
     }
     if (line.rfind("sockets=", 0) == 0) {
       s.socket_per_slot = line.substr(8) == "slot";
+      continue;
+    }
+    if (line.rfind("no_libdrm=", 0) == 0) {
+      s.no_libdrm = line.substr(10) == "1";
+      if (s.no_libdrm) {
+        s.fail["amdsmi_get_gpu_asic_info"] = AMDSMI_STATUS_NOT_SUPPORTED;
+        s.fail["amdsmi_get_gpu_virtualization_mode"] = AMDSMI_STATUS_NOT_SUPPORTED;
+      }
       continue;
     }
     if (line.rfind("latency_us=", 0) == 0) {
@@ -294,6 +309,7 @@ amdsmi_status_t amdsmi_status_code_to_string(amdsmi_status_t status, const char*
   switch (status) {
     case AMDSMI_STATUS_NOT_INIT: *str = "AMDSMI_STATUS_NOT_INIT: Processor not initialized"; break;
     case AMDSMI_STATUS_DRIVER_NOT_LOADED: *str = "AMDSMI_STATUS_DRIVER_NOT_LOADED: Processor driver not loaded."; break;
+    case AMDSMI_STATUS_NOT_SUPPORTED: *str = "AMDSMI_STATUS_NOT_SUPPORTED: Command not supported."; break;
     default: *str = "AMDSMI_STATUS_FAKE";
   }
   return AMDSMI_STATUS_SUCCESS;
@@ -334,6 +350,12 @@ amdsmi_status_t amdsmi_get_gpu_device_bdf(amdsmi_processor_handle h, amdsmi_bdf_
   Proc* p;
   if (auto st = check(h, &p, true)) return st;
   std::memset(b, 0, sizeof(*b));
+  if (S().no_libdrm) {  // uninitialised bytes, as measured: "5ddf28c0:c2:1a.0"
+    b->domain_number = 0x5ddf28c0;
+    b->bus_number = 0xc2;
+    b->device_number = 0x1a;
+    return AMDSMI_STATUS_SUCCESS;
+  }
   b->domain_number = p->domain;
   b->bus_number = p->bus;
   b->device_number = p->dev;
@@ -417,6 +439,11 @@ amdsmi_status_t amdsmi_get_gpu_accelerator_partition_profile_config(amdsmi_proce
   Proc* p;
   if (auto st = check(h, &p)) return st;
   std::memset(c, 0, sizeof(*c));
+  if (S().no_libdrm) {
+    c->num_profiles = 1;
+    c->profiles[0].profile_type = AMDSMI_ACCELERATOR_PARTITION_SPX;
+    return AMDSMI_STATUS_SUCCESS;
+  }
   c->num_profiles = 4;
   c->profiles[0].profile_type = AMDSMI_ACCELERATOR_PARTITION_SPX;
   c->profiles[1].profile_type = AMDSMI_ACCELERATOR_PARTITION_DPX;

@@ -73,3 +73,34 @@ def test_backends_agree_on_one_visible_partition(binary, tmp_path, layout):
         outs[backend] = out.read_text()
     assert outs["amdsmi"] == outs["sysfs"]
     assert golden.parse_labels(outs["sysfs"])["amd.com/gpu.count"] == "1"
+
+
+@pytest.mark.skipif(not FAKE.exists(), reason="libfake_amdsmi.so not built")
+@pytest.mark.parametrize("layout", ["function", "shared"])
+@pytest.mark.parametrize("case", ["spx", "cpx-single", "dpx-nps2-mixed"])
+def test_amdsmi_without_libdrm_labels_identically(binary, tmp_path, case, layout):
+    """amd-smi without libdrm_amdgpu (a slim image), as measured on the pool
+    with the library hidden (tests/test_gpu.py::
+    test_amdsmi_without_libdrm_labels_identically): asic_info and the
+    virtualization query return NOT_SUPPORTED, the BDF query returns garbage
+    with success, the partition profile table lists SPX only.  The backend
+    takes each processor's address and identity from its KFD node, the
+    virtualization mode and partition modes from the driver's sysfs state;
+    the feature file must equal the KFD-sysfs backend's."""
+    c = CASES[case]
+    spec = synth.NodeSpec(gpus=[synth.GpuSpec(compute_partition=c["mode"], memory_partition=c["nps"])
+                                for _ in range(c["n"])], partition_layout=layout, seed=23)
+    root = synth.make_node(tmp_path / "root", spec)
+    fake_spec = synth.fake_amdsmi_spec(root, spec).replace("\n", "|") + "|no_libdrm=1"
+    outs = {}
+    for backend in ("sysfs", "amdsmi"):
+        out = tmp_path / f"gfd-{backend}"
+        run_daemon(binary, "--oneshot", "--no-timestamp", f"--backend={backend}", f"--sysfs-root={root}",
+                   f"--machine-type-file={root}/sys/class/dmi/id/product_name", f"--mig-strategy={c['strategy']}",
+                   f"--output-file={out}", env={"GFD_AMDSMI_LIBRARY": str(FAKE), "GFD_FAKE_AMDSMI_SPEC": fake_spec},
+                   check=True)
+        outs[backend] = out.read_text()
+    assert outs["amdsmi"] == outs["sysfs"]
+    labels = golden.parse_labels(outs["amdsmi"])
+    assert "MI355" in labels["amd.com/gpu.product"]
+    assert labels["amd.com/gpu.virtualization-mode"] == "baremetal"

@@ -233,6 +233,34 @@ def test_product_name_survives_torch_libdrm(tmp_path):
     assert "MI355" in cp.stdout.strip().splitlines()[-1]
 
 
+def test_amdsmi_without_libdrm_labels_identically(binary, tmp_path):
+    """amd-smi dlopens libdrm_amdgpu for the marketing-name table.  A slim
+    runtime image may lack it: emulated here with a copy of libamd_smi whose
+    libdrm_amdgpu soname is altered (same length) so the dlopen fails.  The
+    library must still initialise and the feature file must not change."""
+    import glob
+
+    libs = sorted(glob.glob("/opt/rocm/lib/libamd_smi.so.*.*"))
+    if not libs:
+        pytest.skip("no versioned libamd_smi under /opt/rocm/lib")
+    blob = open(libs[-1], "rb").read()
+    name = b"libdrm_amdgpu.so.1\x00"
+    assert name in blob
+    patched = tmp_path / "libamd_smi.so"
+    patched.write_bytes(blob.replace(name, b"libdrm_amdgpX.so.1\x00"))
+    files = {}
+    for lib in (libs[-1], str(patched)):
+        out = tmp_path / "gfd"
+        cp = run_daemon(binary, "--oneshot", "--no-timestamp", "--backend=amdsmi", f"--output-file={out}",
+                        env={"GFD_AMDSMI_LIBRARY": lib}, check=True, timeout=120)
+        assert "Using amd-smi manager" in cp.stderr, cp.stderr[-2000:]
+        files[lib] = out.read_text()
+    with_drm, without = golden.parse_labels(files[libs[-1]]), golden.parse_labels(files[str(patched)])
+    assert without == with_drm, {k: (with_drm.get(k), without.get(k)) for k in set(with_drm) | set(without)
+                                 if with_drm.get(k) != without.get(k)}
+    assert "MI355" in without["amd.com/gpu.product"]
+
+
 def test_bench_contract_on_gpu(tmp_path):
     cp = subprocess.run([sys.executable, str(REPO / "bench.py"), "--steps", "20", "--warmup", "2", "--no-extras"],
                         capture_output=True, text=True, timeout=600, cwd=str(REPO))

@@ -540,7 +540,9 @@ TEST(AmdSmiFake_PartitionedGpuValuesFromAttributesAndSessionCache) {
     EXPECT_EQ(devs[0]->Info().compute_partition, std::string("CPX"));
     m.Shutdown();
   }
-  EXPECT_EQ(fake().calls("amdsmi_get_gpu_kfd_info"), 8L);  // first cycle only
+  // First cycle only: 8 for the partition facts, and 7 checking the addresses
+  // of partitions 1-7, which are no PCI functions of this root (00.1-00.7).
+  EXPECT_EQ(fake().calls("amdsmi_get_gpu_kfd_info"), 15L);
   EXPECT_EQ(fake().calls("amdsmi_get_gpu_memory_total"), 0L);
   EXPECT_EQ(fake().calls("amdsmi_get_gpu_compute_partition"), 0L);
   EXPECT_EQ(fake().calls("amdsmi_get_gpu_memory_partition"), 0L);
@@ -593,6 +595,9 @@ const std::string kOneGpu = "bdf=0000:d9:00.0;mode=SPX;parts=1;cus=256;xcds=8;vr
 TEST(AmdSmiFault_AsicInfoFailureIsAnError) {
   REQUIRE_FAKE();
   EXPECT_THROW_MSG(devices_with("fail=amdsmi_get_gpu_asic_info:7\n" + kOneGpu), "amdsmi_get_gpu_asic_info");
+  // NOT_SUPPORTED (no libdrm_amdgpu) falls back to the KFD node; without a
+  // readable node there is no identity either, and the call's error stands.
+  EXPECT_THROW_MSG(devices_with("fail=amdsmi_get_gpu_asic_info:2\n" + kOneGpu), "AMDSMI_STATUS_NOT_SUPPORTED");
 }
 
 TEST(AmdSmiFault_ProcessorHandlesFailureIsAnError) {

@@ -373,3 +373,20 @@ def test_eight_gpu_node_from_live_attributes(binary, tmp_path):
         assert labels["amd.com/gpu.compute-partition"] == "SPX"
         assert labels["amd.com/gpu.memory-partition"] == "NPS1"
         assert labels["amd.com/gpu.xgmi.links"] == "7"  # minimum over the GPUs: every one has its 7 hive links
+
+
+@pytest.mark.parametrize("var", ["ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES",
+                                 "GPU_DEVICE_ORDINAL"])
+def test_runtime_visibility_masks_do_not_hide_gpus(binary, tmp_path, var):
+    """A node labeler describes the node, not the GPUs a runtime mask leaves
+    to one process: a pod that inherits a device plugin's or user's
+    visibility variable (pointing at a GPU that does not exist) still labels
+    every GPU, through amd-smi and KFD alike (profiles/env_probe.txt)."""
+    files = {}
+    for backend in ("amdsmi", "sysfs"):
+        out = tmp_path / f"gfd-{backend}"
+        run_daemon(binary, "--oneshot", "--no-timestamp", f"--backend={backend}", f"--output-file={out}",
+                   env={var: "63"}, check=True, timeout=120)
+        files[backend] = out.read_text()
+    assert files["amdsmi"] == files["sysfs"]
+    assert int(golden.parse_labels(files["amdsmi"])["amd.com/gpu.count"]) >= 1

@@ -125,7 +125,9 @@ class SysfsAmdPCI : public AmdPCI {
     std::string physfn;
     int sriov_numvfs = -1;  // last NumVFs read; -1 = re-read (listing changed)
   };
-  static Identity read_identity(const std::string& addr, const std::string& path, uint64_t ino);
+  // `device_id`: the function's device ID when procfs' device table already
+  // placed it as an AMD function (vendor and device are not re-read), else 0.
+  static Identity read_identity(const std::string& addr, const std::string& path, uint64_t ino, uint32_t device_id = 0);
   std::string root_;
   fs::DirListing listing_;
   bool scanned_ = false;

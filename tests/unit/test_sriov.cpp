@@ -329,17 +329,31 @@ TEST(Sriov_ColdScanTakesVendorsFromProcTable) {
     unsigned d = 0, b = 0, s = 0, f = 0;
     if (std::sscanf(name.c_str(), "%x:%x:%x.%x", &d, &b, &s, &f) != 4) throw std::runtime_error(name);
     std::string vendor = str::trim(fs::read_file(dev + name + "/vendor").data);
-    table += str::format("%04x\t%s75a3\t0\t0\n", (b << 8) | (s << 3) | f, vendor.substr(2).c_str());
+    std::string device = str::trim(fs::read_file(dev + name + "/device").data);
+    if (device.empty()) device = "0x0000";
+    table += str::format("%04x\t%s%s\t0\t0\n", (b << 8) | (s << 3) | f, vendor.substr(2).c_str(), device.substr(2).c_str());
   }
   put_file(root + "/proc/bus/pci/devices", table);
   // A non-AMD function the table places is never read from sysfs ...
   fs::remove_all(dev + "0000:00:05.0/vendor");
   fs::mkdir_all(dev + "0000:00:05.0/vendor");  // unreadable attribute
+  // ... and an AMD function it places has its vendor and device ID from it.
+  std::string amd_fn;
+  for (const auto& [name, ino] : fs::list_dir_ino(dev))
+    if (name != "0000:00:07.0" && str::trim(fs::read_file(dev + name + "/vendor").data) == "0x1002" &&
+        str::trim(fs::read_file(dev + name + "/device").data) == "0x75a3")
+      amd_fn = name;
+  EXPECT_FALSE(amd_fn.empty());
+  fs::remove_all(dev + amd_fn + "/vendor");
+  fs::remove_all(dev + amd_fn + "/device");
   SysfsAmdPCI pci(root);
   auto devs = pci.Devices();
   EXPECT_EQ(devs.size(), static_cast<size_t>(7));  // AMD functions still fully read
   int vfs = 0;
-  for (const auto& d : devs) vfs += !d.physfn.empty();
+  for (const auto& d : devs) {
+    vfs += !d.physfn.empty();
+    if (d.address == amd_fn) EXPECT_EQ(d.device, std::string("0x75a3"));
+  }
   EXPECT_EQ(vfs, 2);
   // ... one the table does not list is.
   fs::remove_all(dev + "0000:00:07.0/vendor");

@@ -85,6 +85,9 @@ def _check_labels(labels: dict, n_gpus: int, hardware: bool) -> list[str]:
               "amd.com/gpu.partition.capable"):
         if k not in labels:
             problems.append(f"missing {k}")
+    from gpu_feature_discovery_amd.utils.golden import k8s_label_problems
+
+    problems += k8s_label_problems(labels)  # what NFD / the API server would reject
     if hardware and labels.get("amd.com/gpu.compute-units") != "256":
         problems.append(f"amd.com/gpu.compute-units={labels.get('amd.com/gpu.compute-units')!r} (want 256)")
     return problems

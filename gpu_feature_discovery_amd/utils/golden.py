@@ -67,3 +67,28 @@ def check_byte_golden(output: str, golden: str | Path, update: bool = False) -> 
         import difflib
         diff = "".join(difflib.unified_diff(expected.splitlines(True), output.splitlines(True), str(path), "output"))
         raise AssertionError(f"output differs from {path}:\n{diff}")
+
+
+# Kubernetes label syntax (apimachinery validation.IsQualifiedName /
+# IsValidLabelValue), which NFD applies before publishing a feature label:
+# an optional DNS-subdomain prefix (<= 253 chars) and '/', a name of <= 63
+# chars, and a value of <= 63 chars; name and non-empty value start and end
+# alphanumeric with [-_.A-Za-z0-9] in between.
+_NAME = re.compile(r"[A-Za-z0-9]([-A-Za-z0-9_.]*[A-Za-z0-9])?")
+_DNS1123_SUBDOMAIN = re.compile(r"[a-z0-9]([-a-z0-9]*[a-z0-9])?(\.[a-z0-9]([-a-z0-9]*[a-z0-9])?)*")
+
+
+def k8s_label_problems(labels: dict[str, str]) -> list[str]:
+    """Labels NFD / the API server would reject, with the reason."""
+    problems = []
+    for key, value in labels.items():
+        prefix, _, name = key.rpartition("/")
+        if "/" in prefix:
+            problems.append(f"{key}: more than one '/'")
+        if prefix and (len(prefix) > 253 or not _DNS1123_SUBDOMAIN.fullmatch(prefix)):
+            problems.append(f"{key}: prefix is not a DNS-1123 subdomain")
+        if len(name) > 63 or not _NAME.fullmatch(name):
+            problems.append(f"{key}: invalid name")
+        if value and (len(value) > 63 or not _NAME.fullmatch(value)):
+            problems.append(f"{key}={value}: invalid value")
+    return problems

@@ -364,3 +364,19 @@ def run_daemon_checked(binary, tmp_path, root, *args, out):
     return run_daemon(binary, "--oneshot", "--no-timestamp", "--backend=sysfs", f"--sysfs-root={root}",
                       f"--machine-type-file={root}/sys/class/dmi/id/product_name", f"--output-file={out}", *args,
                       check=True)
+
+
+@pytest.mark.parametrize("golden_file", sorted(p.name for p in (TESTS / "golden").glob("*.txt")))
+def test_goldens_are_valid_kubernetes_labels(golden_file):
+    """Every label of every byte golden passes the syntax checks NFD and the
+    API server apply (a rejected label is silently missing from the Node)."""
+    labels = golden.parse_labels((TESTS / "golden" / golden_file).read_text())
+    assert labels and golden.k8s_label_problems(labels) == []
+
+
+def test_label_syntax_check_rejects_bad_labels():
+    bad = {"amd.com/gpu.product": "-x", "amd.com/" + "n" * 64: "1", "AMD.com/x": "1", "a/b/c": "1",
+           "amd.com/ok": "v" * 64}
+    flagged = {p.split(":")[0].split("=")[0] for p in golden.k8s_label_problems(bad)}
+    assert flagged == set(bad)
+    assert golden.k8s_label_problems({"amd.com/partition-cpx.1xcd.36gb.count": "16", "amd.com/x": ""}) == []

@@ -88,6 +88,7 @@ def test_daemon_amdsmi_oneshot_matches_regex_golden(binary, tmp_path):
     text = out.read_text()
     golden.check_regex_golden(text, TESTS / "expected-output.txt", select=lambda ln: "sriov" not in ln)
     labels = golden.parse_labels(text)
+    assert golden.k8s_label_problems(labels) == []
     assert labels["amd.com/gpu.arch"] == "gfx950"
     assert labels["amd.com/gpu.family"] == "cdna4"
     assert labels["amd.com/gpu.compute-units"] == "256"

@@ -96,8 +96,29 @@ class AmdSmiLib {
     candidates.push_back("/opt/rocm/lib/libamd_smi.so");
     candidates.push_back("libamd_smi.so.26");
     candidates.push_back("libamd_smi.so");
-    if (!lib_.open(candidates)) {
-      *err = lib_.last_error();
+    // The structs this file passes to the library are laid out by the
+    // amdsmi.h it was compiled against; a library of another major version
+    // (an unversioned libamd_smi.so from a different ROCm) may lay them out
+    // differently, so it is skipped in favour of the next candidate.
+    std::string mismatch;
+    bool opened = false;
+    for (const auto& c : candidates) {
+      if (!lib_.open({c})) continue;
+      amdsmi_status_t (*lib_version)(amdsmi_version_t*) = nullptr;
+      amdsmi_version_t v{};
+      if (lib_.bind("amdsmi_get_lib_version", lib_version) && lib_version(&v) == AMDSMI_STATUS_SUCCESS &&
+          v.major != AMDSMI_LIB_VERSION_MAJOR) {
+        mismatch = c + " is amd-smi " + std::to_string(v.major) + "." + std::to_string(v.minor) +
+                   ", this build needs major version " + std::to_string(AMDSMI_LIB_VERSION_MAJOR);
+        log::printf("Skipping %s", mismatch.c_str());
+        lib_.close();
+        continue;
+      }
+      opened = true;
+      break;
+    }
+    if (!opened) {
+      *err = mismatch.empty() ? lib_.last_error() : mismatch;
       return false;
     }
     bool ok = true;

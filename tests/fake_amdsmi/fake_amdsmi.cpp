@@ -19,6 +19,7 @@
 //   sockets=slot              one socket per PCI slot, i.e. per physical GPU
 //                             (what amd-smi does; the default) - or `one`: a
 //                             single socket holding every processor
+//   lib_major=N               amdsmi_get_lib_version reports major N (26)
 //   no_libdrm=1               amd-smi as it behaves when it cannot load
 //                             libdrm_amdgpu (measured on MI355X): ASIC info
 //                             and virtualization mode NOT_SUPPORTED, the BDF
@@ -81,6 +82,7 @@ struct State {
   int shutdown_calls = 0;
   long latency_us = 0;
   bool no_libdrm = false;
+  uint32_t lib_major = 26;
   std::map<std::string, std::unique_ptr<std::mutex>> device_mu;  // by BDF
   std::map<std::string, int> fail;                               // function -> status
   std::map<std::string, long> calls;                             // function -> device queries made
@@ -162,6 +164,7 @@ int fake_amdsmi_configure(const char* spec) {
   s.stale_after = -1;
   s.latency_us = 0;
   s.no_libdrm = false;
+  s.lib_major = 26;
   s.fail.clear();
   s.calls.clear();
   s.queries = 0;
@@ -193,6 +196,10 @@ int fake_amdsmi_configure(const char* spec) {
     }
     if (line.rfind("sockets=", 0) == 0) {
       s.socket_per_slot = line.substr(8) == "slot";
+      continue;
+    }
+    if (line.rfind("lib_major=", 0) == 0) {
+      s.lib_major = static_cast<uint32_t>(std::atoi(line.c_str() + 10));
       continue;
     }
     if (line.rfind("no_libdrm=", 0) == 0) {
@@ -497,7 +504,7 @@ amdsmi_status_t amdsmi_get_gpu_driver_info(amdsmi_processor_handle h, amdsmi_dri
 
 amdsmi_status_t amdsmi_get_lib_version(amdsmi_version_t* v) {
   std::memset(v, 0, sizeof(*v));
-  v->major = 26;
+  v->major = S().lib_major;
   return AMDSMI_STATUS_SUCCESS;
 }
 

@@ -341,3 +341,22 @@ def test_auto_backend_without_kfd_topology_still_fails_on_init_error(binary, tmp
                     env=_fake_amdsmi_env("init_status=34"))
     assert cp.returncode == 1
     assert "amdsmi_init failed" in cp.stderr
+
+
+def test_amdsmi_of_another_major_version_is_not_used(binary, tmp_path, mi355x_node):
+    """The backend passes amd-smi structs laid out by the amdsmi.h it was
+    built against; a library reporting another major version is refused
+    (with the reason) instead of being fed mismatched structs, and the auto
+    backend labels from KFD."""
+    root = mi355x_node(n_gpus=2)
+    spec = "lib_major=25|bdf=0000:d9:00.0;mode=SPX;parts=1"
+    cp = run_daemon(binary, "--oneshot", "--backend=amdsmi", f"--sysfs-root={root}", "--output-file=",
+                    env=_fake_amdsmi_env(spec))
+    # Refused; the next candidate (a system libamd_smi.so.26, if installed)
+    # is tried instead - here it finds no driver - or loading fails.
+    assert "Skipping " in cp.stderr and "is amd-smi 25.0, this build needs major version 26" in cp.stderr
+    assert cp.returncode == 1 and "amd.com/gpu.count" not in cp.stdout
+    labels, err = _loop_until(binary, tmp_path / "gfd", "--backend=auto", f"--sysfs-root={root}",
+                              env=_fake_amdsmi_env(spec), until="Sleeping for")
+    assert labels["amd.com/gpu.count"] == "2"  # the tree's GPUs, through KFD
+    assert "this build needs major version 26" in err

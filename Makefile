@@ -5,7 +5,7 @@ BUILD_DIR ?= build
 JOBS ?= $(shell nproc 2>/dev/null || echo 8)
 PYTHON ?= python3
 
-.PHONY: all build cmds test test-unit test-gpu coverage asan tsan bench fmt assert-fmt lint check-yamls image clean
+.PHONY: all build cmds test test-unit test-gpu coverage asan tsan fuzz bench fmt assert-fmt lint check-yamls image clean
 
 all: build
 
@@ -30,14 +30,29 @@ test-gpu: build
 # Sanitizer builds of the host code on the mock/synthetic backends (the
 # reference runs `go test` without -race).
 asan:
-	cmake -S . -B build-asan -G Ninja -DCMAKE_BUILD_TYPE=Debug -DGFD_SANITIZE=address,undefined -DGFD_BUILD_PYTHON=OFF
+	cmake -S . -B build-asan -G Ninja -DCMAKE_BUILD_TYPE=Debug -DGFD_SANITIZE=address,undefined,float-cast-overflow -DGFD_BUILD_PYTHON=OFF
 	cmake --build build-asan -j $(JOBS)
 	ASAN_OPTIONS=detect_leaks=1 UBSAN_OPTIONS=halt_on_error=1 GFD_AMDSMI_LIBRARY=build-asan/libfake_amdsmi.so ./build-asan/gfd_unit_tests
+	for t in config pci values; do ASAN_OPTIONS=detect_leaks=1 UBSAN_OPTIONS=halt_on_error=1 \
+	  ./build-asan/fuzz_replay_$$t tests/fuzz/corpus/$$t || exit 1; done
 
 tsan:
 	cmake -S . -B build-tsan -G Ninja -DCMAKE_BUILD_TYPE=Debug -DGFD_SANITIZE=thread -DGFD_BUILD_PYTHON=OFF
 	cmake --build build-tsan -j $(JOBS)
 	TSAN_OPTIONS=halt_on_error=1 GFD_AMDSMI_LIBRARY=build-tsan/libfake_amdsmi.so ./build-tsan/gfd_unit_tests
+
+# libFuzzer + ASan/UBSan over the config reader, the PCI capability walkers
+# and the value parsers (tests/fuzz/); FUZZ_SECONDS per target, new inputs
+# kept in build-fuzz/corpus-<target>, seeds and regressions in tests/fuzz/corpus.
+FUZZ_SECONDS ?= 60
+FUZZ_CXX ?= $(shell command -v clang++ || echo /opt/rocm/lib/llvm/bin/clang++)
+fuzz:
+	cmake -S . -B build-fuzz -G Ninja -DCMAKE_BUILD_TYPE=Debug -DCMAKE_CXX_COMPILER=$(FUZZ_CXX) \
+	  -DGFD_SANITIZE=address,undefined -DGFD_FUZZ=ON -DGFD_BUILD_PYTHON=OFF -DGFD_BUILD_TESTS=OFF
+	cmake --build build-fuzz -j $(JOBS)
+	for t in config pci values; do mkdir -p build-fuzz/corpus-$$t && \
+	  UBSAN_OPTIONS=halt_on_error=1 ./build-fuzz/fuzz_$$t -max_total_time=$(FUZZ_SECONDS) -timeout=10 \
+	    -rss_limit_mb=2048 build-fuzz/corpus-$$t tests/fuzz/corpus/$$t || exit 1; done
 
 coverage:
 	cmake -S . -B build-cov -G Ninja -DCMAKE_BUILD_TYPE=Debug -DGFD_BUILD_PYTHON=OFF \

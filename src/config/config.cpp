@@ -1,5 +1,8 @@
 #include "config/config.h"
 
+#include <cmath>
+#include <limits>
+
 #include "util/error.h"
 #include "util/fs.h"
 #include "util/log.h"
@@ -70,10 +73,27 @@ std::optional<bool> opt_bool(const Node* n, const std::string& path) {
   return n->as_bool();
 }
 
+// An integral number inside [lo, hi] (checked before any conversion: a
+// float outside the target range has no defined conversion).
+std::optional<int64_t> integral_in(const Node& n, double lo, double hi) {
+  if (n.kind() == Node::Kind::Int) {
+    if (static_cast<double>(n.as_int()) < lo || static_cast<double>(n.as_int()) > hi) return std::nullopt;
+    return n.as_int();
+  }
+  if (n.kind() == Node::Kind::Float) {
+    double f = n.as_float();
+    if (!(f >= lo && f <= hi) || f != std::trunc(f)) return std::nullopt;
+    return static_cast<int64_t>(f);
+  }
+  return std::nullopt;
+}
+
+// Go's int is 64 bits; the fields read as int here (replicas) are counts,
+// so a value beyond 32 bits is rejected with Go's type error rather than
+// truncated.
 int to_int(const Node& n, const std::string& path) {
-  if (n.kind() == Node::Kind::Int) return static_cast<int>(n.as_int());
-  if (n.kind() == Node::Kind::Float && n.as_float() == static_cast<double>(static_cast<int64_t>(n.as_float())))
-    return static_cast<int>(n.as_float());
+  if (auto v = integral_in(n, std::numeric_limits<int>::min(), std::numeric_limits<int>::max()))
+    return static_cast<int>(*v);
   type_error(n, path, "int");
 }
 
@@ -82,7 +102,12 @@ int to_int(const Node& n, const std::string& path) {
 std::optional<Nanos> opt_duration(const Node* n, const std::string& /*path*/) {
   if (!n || n->is_null()) return std::nullopt;
   if (n->kind() == Node::Kind::Int) return static_cast<Nanos>(n->as_int());
-  if (n->kind() == Node::Kind::Float) return static_cast<Nanos>(n->as_float());
+  if (n->kind() == Node::Kind::Float) {
+    // time.Duration(float64) truncates; outside int64 there is no duration.
+    double f = n->as_float();
+    if (!(f > -9.2233720368547758e18 && f < 9.2233720368547758e18)) throw Error("invalid duration");
+    return static_cast<Nanos>(f);
+  }
   if (n->kind() == Node::Kind::String) return parse_duration(n->text());
   throw Error("invalid duration");
 }

@@ -95,6 +95,20 @@ TEST(Config_TimeSlicingValidation) {
                    "unsupported type for device");
 }
 
+TEST(Config_OutOfRangeNumbersAreTypeErrors) {
+  // Found by tests/fuzz/fuzz_config.cpp: a float beyond the integer range
+  // was converted with undefined behaviour, a large int silently truncated.
+  auto replicas = [](const std::string& v) {
+    return parse_config_text("sharing:\n  timeSlicing:\n    resources:\n    - name: gpu\n      replicas: " + v + "\n");
+  };
+  EXPECT_THROW_MSG(replicas("1e93"), "of type int");
+  EXPECT_THROW_MSG(replicas("4294967298"), "of type int");
+  EXPECT_THROW_MSG(replicas("2.5"), "of type int");
+  EXPECT_EQ(replicas("4.0").sharing.time_slicing.resources[0].replicas, 4);
+  EXPECT_THROW_MSG(parse_config_text("flags:\n  gfd:\n    sleepInterval: 1e300\n"), "invalid duration");
+  EXPECT_EQ(*parse_config_text("flags:\n  gfd:\n    sleepInterval: 1.5e9\n").flags.gfd.sleep_interval, 1500000000LL);
+}
+
 TEST(Config_PartitionDeviceRefs) {
   auto devices = [](const std::string& items) {
     return parse_config_text("sharing:\n  timeSlicing:\n    resources:\n    - name: gpu\n      replicas: 2\n"

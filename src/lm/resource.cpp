@@ -150,12 +150,18 @@ Labels new_gpu_labels(resource::Manager& manager, const config::Config& config) 
 
   Labels out;
   // Partitioned GPUs first, without sharing; full GPUs override them.
-  for (const auto& [name, d] : partitioned) {
-    Labels l = GFD_WRAP("failed to construct labeler", NewGPUResourceLabelsWithoutSharing(*d, counts[name]));
+  // (Plain pair iteration: GFD_WRAP's lambda cannot capture structured
+  // bindings before C++20.)
+  for (const auto& entry : partitioned) {
+    const Device& d = *entry.second;
+    int count = counts[entry.first];
+    Labels l = GFD_WRAP("failed to construct labeler", NewGPUResourceLabelsWithoutSharing(d, count));
     for (auto& kv : l) out[kv.first] = kv.second;
   }
-  for (const auto& [name, d] : full) {
-    Labels l = GFD_WRAP("failed to construct labeler", NewGPUResourceLabels(&config, *d, counts[name]));
+  for (const auto& entry : full) {
+    const Device& d = *entry.second;
+    int count = counts[entry.first];
+    Labels l = GFD_WRAP("failed to construct labeler", NewGPUResourceLabels(&config, d, count));
     for (auto& kv : l) out[kv.first] = kv.second;
   }
   return out;
@@ -164,7 +170,8 @@ Labels new_gpu_labels(resource::Manager& manager, const config::Config& config) 
 Labels new_partition_device_labels(const std::map<std::string, PartitionResource>& resources,
                                    const config::Config& config) {
   Labels out;
-  for (const auto& [profile, r] : resources) {
+  for (const auto& entry : resources) {
+    const PartitionResource& r = entry.second;
     Labels l = GFD_WRAP("failed to construct labeler", NewPartitionResourceLabels(r.name, &config, *r.device, r.count));
     for (auto& kv : l) out[kv.first] = kv.second;
   }

@@ -53,9 +53,9 @@ LabelerPtr version_labeler(DriverFn&& get_driver, RuntimeFn&& get_runtime) {
     throw Error("error getting driver version: Version \"" + driver + "\" does not match format \"X.Y[.Z]\"");
   std::optional<resource::RuntimeVersion> rt = GFD_WRAP("error getting ROCm runtime version", get_runtime());
   Labels l{
-      {keys::kDriverMajor, parts[0]},
-      {keys::kDriverMinor, parts[1]},
-      {keys::kDriverRev, parts.size() > 2 ? parts[2] : ""},
+      {keys::kDriverMajor, sanitize_label_value(parts[0])},
+      {keys::kDriverMinor, sanitize_label_value(parts[1])},
+      {keys::kDriverRev, parts.size() > 2 ? sanitize_label_value(parts[2]) : ""},
   };
   if (rt) {
     l[keys::kRuntimeMajor] = std::to_string(rt->major);

@@ -27,8 +27,14 @@ class ResourceLabeler {
       : resource_name_(std::move(resource_name)), config_(config) {}
 
   std::string key(const std::string& suffix) const { return resource_name_ + "." + suffix; }
-  Labels single(const std::string& suffix, const std::string& value) const { return Labels{{key(suffix), value}}; }
-  void update(Labels& l, const std::string& suffix, const std::string& value) const { l[key(suffix)] = value; }
+  // Values are passed through sanitize_label_value: whatever a driver
+  // reports, the file never holds a value NFD would reject.
+  Labels single(const std::string& suffix, const std::string& value) const {
+    return Labels{{key(suffix), sanitize_label_value(value)}};
+  }
+  void update(Labels& l, const std::string& suffix, const std::string& value) const {
+    l[key(suffix)] = sanitize_label_value(value);
+  }
 
   // product: non-empty parts joined by '-', spaces replaced, "-SHARED" if
   // replicated (>1) and not renamed (resource.go:159-176).

@@ -420,16 +420,16 @@ bool query_unpartitioned(AmdSmiLib& L, const std::string& root, ProcInfo& p, Amd
   uint32_t* node_id = &kfd->node_id;
   std::string pci = fs::join(root, "sys/bus/pci/devices/" + p.gpu_bdf);
   auto cp = AMDSMI_CALL("compute_partition(sysfs)", fs::attrs().read_trimmed(pci + "/current_compute_partition"));
-  if (!cp || *cp != "SPX") return false;
+  if (!cp || partition_mode(*cp) != "SPX") return false;
   auto mp = AMDSMI_CALL("memory_partition(sysfs)", fs::attrs().read_trimmed(pci + "/current_memory_partition"));
-  if (!mp || mp->empty()) return false;
+  if (!mp || partition_mode(*mp).empty()) return false;
   auto vram_s = AMDSMI_CALL("memory_total(sysfs)", fs::attrs().read_trimmed(pci + "/mem_info_vram_total"));
   auto vram = vram_s ? str::parse_uint(*vram_s) : std::nullopt;
   if (!vram || *vram == 0) return false;
   if (*node_id == kNoNode && !query_kfd(L, p, node_id)) return false;
   query_identity(L, root, p);
-  p.compute_partition = *cp;
-  p.memory_partition = *mp;
+  p.compute_partition = "SPX";
+  p.memory_partition = partition_mode(*mp);
   p.vram = *vram;
   if (kfd->num_xcc == 0 && *node_id != kNoNode) kfd->num_xcc = AMDSMI_CALL("kfd_num_xcc(sysfs)", kfd_num_xcc(root, *node_id));
   p.xcds = kfd->num_xcc;
@@ -452,10 +452,12 @@ bool query_unpartitioned(AmdSmiLib& L, const std::string& root, ProcInfo& p, Amd
 bool query_partitioned(AmdSmiLib& L, const std::string& root, std::vector<ProcInfo>& procs,
                        std::vector<AmdSmiManager::PartitionFacts>& facts) {
   std::string pci = fs::join(root, "sys/bus/pci/devices/" + procs.front().gpu_bdf);
-  auto cp = AMDSMI_CALL("compute_partition(sysfs)", fs::attrs().read_trimmed(pci + "/current_compute_partition"));
-  if (!cp || cp->empty() || *cp == "SPX") return false;
-  auto mp = AMDSMI_CALL("memory_partition(sysfs)", fs::attrs().read_trimmed(pci + "/current_memory_partition"));
-  if (!mp || mp->empty()) return false;
+  auto cp_raw = AMDSMI_CALL("compute_partition(sysfs)", fs::attrs().read_trimmed(pci + "/current_compute_partition"));
+  std::string cp = cp_raw ? partition_mode(*cp_raw) : "";
+  if (cp.empty() || cp == "SPX") return false;
+  auto mp_raw = AMDSMI_CALL("memory_partition(sysfs)", fs::attrs().read_trimmed(pci + "/current_memory_partition"));
+  std::string mp = mp_raw ? partition_mode(*mp_raw) : "";
+  if (mp.empty()) return false;
   for (size_t i = 0; i < procs.size(); ++i) {
     ProcInfo& p = procs[i];
     AmdSmiManager::PartitionFacts& f = facts[i];
@@ -477,8 +479,8 @@ bool query_partitioned(AmdSmiLib& L, const std::string& root, std::vector<ProcIn
     p.xcds = f.num_xcc;
     p.sdma = f.sdma;
     p.vram = f.mem_bytes;
-    p.compute_partition = *cp;
-    p.memory_partition = *mp;
+    p.compute_partition = cp;
+    p.memory_partition = mp;
   }
   fix_market_name(L, root, procs.front());
   for (auto& p : procs) p.market_name = procs.front().market_name;
@@ -504,12 +506,12 @@ void query_proc(AmdSmiLib& L, const std::string& root, ProcInfo& p) {
   if (L.get_gpu_compute_partition) {
     std::memset(buf, 0, sizeof(buf));
     if (AMDSMI_CALL("compute_partition", L.get_gpu_compute_partition(p.h, buf, sizeof(buf))) == AMDSMI_STATUS_SUCCESS)
-      p.compute_partition = str::trim(buf);
+      p.compute_partition = partition_mode(buf);
   }
   if (L.get_gpu_memory_partition) {
     std::memset(buf, 0, sizeof(buf));
     if (AMDSMI_CALL("memory_partition", L.get_gpu_memory_partition(p.h, buf, sizeof(buf))) == AMDSMI_STATUS_SUCCESS)
-      p.memory_partition = str::trim(buf);
+      p.memory_partition = partition_mode(buf);
   }
   if (p.xcds == 0 && L.get_gpu_xcd_counter) {
     uint16_t x = 0;
@@ -570,8 +572,7 @@ void query_gpu_caps(AmdSmiLib& L, const ProcInfo& p, const std::string& root, Gp
   // the amd-smi partition-config call (~25 us) only as a fallback.
   if (auto v = AMDSMI_CALL("available_memory_partition(sysfs)",
                            fs::attrs().read_trimmed(fs::join(root, "sys/bus/pci/devices/" + p.gpu_bdf + "/available_memory_partition")))) {
-    for (auto& m : str::split(*v, ','))
-      if (!str::trim(m).empty()) x.available_memory.push_back(str::trim(m));
+    x.available_memory = partition_mode_list(*v);
   } else if (L.get_gpu_memory_partition_config) {
     amdsmi_memory_partition_config_t cfg;
     std::memset(&cfg, 0, sizeof(cfg));
@@ -584,8 +585,7 @@ void query_gpu_caps(AmdSmiLib& L, const ProcInfo& p, const std::string& root, Gp
   // only as a fallback.
   if (auto v = AMDSMI_CALL("available_compute_partition(sysfs)",
                            fs::attrs().read_trimmed(fs::join(root, "sys/bus/pci/devices/" + p.gpu_bdf + "/available_compute_partition")))) {
-    for (auto& m : str::split(*v, ','))
-      if (!str::trim(m).empty()) x.available_compute.push_back(str::trim(m));
+    x.available_compute = partition_mode_list(*v);
   }
   if (x.available_compute.empty() && L.get_gpu_accelerator_partition_profile_config) {
     amdsmi_accelerator_partition_profile_config_t cfg;

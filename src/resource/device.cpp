@@ -41,6 +41,7 @@ std::optional<GfxTarget> parse_gfx_target(const std::string& in) {
 
 GfxTarget gfx_target_from_kfd(uint64_t v) {
   GfxTarget t;
+  if (v >= 1000000) return t;  // major > 99: not a target KFD reports (unknown)
   t.major = static_cast<int>(v / 10000);
   t.minor = static_cast<int>((v / 100) % 100);
   t.stepping = static_cast<int>(v % 100);
@@ -51,7 +52,7 @@ GfxTarget gfx_target_from_amdsmi(uint64_t v) {
   // amd-smi reports the target as an integer whose hex digits spell the
   // name, e.g. 0x950 for gfx950, 0x90a for gfx90a, 0x1100 for gfx1100.
   GfxTarget t;
-  if (v == 0 || v == UINT64_MAX) return t;
+  if (v == 0 || v > 0xFFFF) return t;  // at most two major digits (gfx12xx); else unknown
   t.stepping = static_cast<int>(v & 0xF);
   t.minor = static_cast<int>((v >> 4) & 0xF);
   uint64_t maj_hex = v >> 8;
@@ -86,6 +87,21 @@ std::string arch_family(const GfxTarget& t) {
     default:
       return "undefined";
   }
+}
+
+std::string partition_mode(const std::string& raw) {
+  std::string t = str::trim(raw);
+  if (t.empty() || t.size() > 16) return "";
+  for (char c : t)
+    if (!((c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z') || (c >= '0' && c <= '9'))) return "";
+  return str::to_upper(t);
+}
+
+std::vector<std::string> partition_mode_list(const std::string& raw) {
+  std::vector<std::string> out;
+  for (const auto& p : str::split(raw, ','))
+    if (auto m = partition_mode(p); !m.empty()) out.push_back(m);
+  return out;
 }
 
 std::string partition_profile_name(const std::string& compute_partition, uint32_t xcds, uint64_t memory_mib) {

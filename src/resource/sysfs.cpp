@@ -73,15 +73,6 @@ void parse_properties(const std::string& text, KfdNode& n) {
   }
 }
 
-std::vector<std::string> split_list(const std::string& s) {
-  std::vector<std::string> out;
-  for (auto& p : str::split(s, ',')) {
-    std::string t = str::trim(p);
-    if (!t.empty()) out.push_back(t);
-  }
-  return out;
-}
-
 // "01 01 01 01 01 01 00 01" -> 7 (links to each hive peer; self is 00).
 int sum_links(const std::string& s) {
   int total = 0;
@@ -181,10 +172,12 @@ static DevicePtr describe_gpu(const std::string& root, bool in_vm, int index, co
   info.gfx = gfx_target_from_kfd(first.gfx_target_version);
   auto product = fs::attrs().read_trimmed(fs::join(pci, "product_name"));
   info.name = product && !product->empty() ? *product : device_name(static_cast<uint32_t>(first.device_id));
-  info.compute_partition = fs::attrs().read_trimmed(fs::join(pci, "current_compute_partition")).value_or("");
-  info.memory_partition = fs::attrs().read_trimmed(fs::join(pci, "current_memory_partition")).value_or("");
-  info.available_compute_partitions = split_list(fs::attrs().read_trimmed(fs::join(pci, "available_compute_partition")).value_or(""));
-  info.available_memory_partitions = split_list(fs::attrs().read_trimmed(fs::join(pci, "available_memory_partition")).value_or(""));
+  info.compute_partition = partition_mode(fs::attrs().read_trimmed(fs::join(pci, "current_compute_partition")).value_or(""));
+  info.memory_partition = partition_mode(fs::attrs().read_trimmed(fs::join(pci, "current_memory_partition")).value_or(""));
+  info.available_compute_partitions =
+      partition_mode_list(fs::attrs().read_trimmed(fs::join(pci, "available_compute_partition")).value_or(""));
+  info.available_memory_partitions =
+      partition_mode_list(fs::attrs().read_trimmed(fs::join(pci, "available_memory_partition")).value_or(""));
   if (auto x = fs::attrs().read_trimmed(fs::join(pci, "xgmi_num_links"))) info.xgmi_links = sum_links(*x);
   info.virtualization = classify_virtualization(pci, info.device_id, in_vm, has_physfn);
 

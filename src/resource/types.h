@@ -60,6 +60,13 @@ std::string arch_family(const GfxTarget& t);
 // CPX/NPS1 (288 GB / 8).  GB is memory rounded to the nearest GiB.  The name
 // is a valid DNS-1123 label sequence so it can be embedded in resource names.
 std::string partition_profile_name(const std::string& compute_partition, uint32_t xcds, uint64_t memory_mib);
+// A compute / memory partition mode as the driver spells it (SPX, CPX,
+// NPS1, ...): trimmed and upper-cased, or "" when the text is not a short
+// alphanumeric token (an unreadable or malformed attribute must not end up
+// in a label name or value - found by tests/fuzz/fuzz_sysfs.cpp).
+std::string partition_mode(const std::string& raw);
+// "SPX, DPX, QPX, CPX" -> {"SPX", "DPX", "QPX", "CPX"}; malformed entries dropped.
+std::vector<std::string> partition_mode_list(const std::string& raw);
 
 // Ordered so label generation is deterministic.
 using Attributes = std::map<std::string, std::string>;

@@ -214,6 +214,20 @@ TEST(GfxTarget_Parsing) {
   EXPECT_EQ(gfx_target_from_amdsmi(0x942).name(), std::string("gfx942"));
   EXPECT_EQ(gfx_target_from_amdsmi(0x1100).name(), std::string("gfx1100"));
   EXPECT_FALSE(gfx_target_from_amdsmi(0).valid());
+  // Out-of-range values are unknown targets, not overflowed majors
+  // (tests/fuzz/corpus/sysfs/regress-huge-gfx-target).
+  EXPECT_FALSE(gfx_target_from_kfd(18446744073709551615ULL).valid());
+  EXPECT_FALSE(gfx_target_from_amdsmi(0xFFFFFFFFFFFFFFFFULL).valid());
+}
+
+TEST(PartitionMode_OnlyShortAlphanumericTokens) {
+  EXPECT_EQ(partition_mode(" cpx\n"), std::string("CPX"));
+  EXPECT_EQ(partition_mode("NPS4"), std::string("NPS4"));
+  EXPECT_EQ(partition_mode("SPX, DPX"), std::string(""));  // a list where one mode belongs
+  EXPECT_EQ(partition_mode(""), std::string(""));
+  EXPECT_EQ(partition_mode(std::string(17, 'A')), std::string(""));
+  EXPECT_EQ(partition_mode_list("SPX, DPX, QPX, CPX\n"), (std::vector<std::string>{"SPX", "DPX", "QPX", "CPX"}));
+  EXPECT_EQ(partition_mode_list("NPS1, N/A, , NPS2"), (std::vector<std::string>{"NPS1", "NPS2"}));
 }
 
 TEST(PartitionProfileName) {

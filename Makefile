@@ -33,7 +33,7 @@ asan:
 	cmake -S . -B build-asan -G Ninja -DCMAKE_BUILD_TYPE=Debug -DGFD_SANITIZE=address,undefined,float-cast-overflow -DGFD_BUILD_PYTHON=OFF
 	cmake --build build-asan -j $(JOBS)
 	ASAN_OPTIONS=detect_leaks=1 UBSAN_OPTIONS=halt_on_error=1 GFD_AMDSMI_LIBRARY=build-asan/libfake_amdsmi.so ./build-asan/gfd_unit_tests
-	for t in config pci values flags sysfs; do ASAN_OPTIONS=detect_leaks=1 UBSAN_OPTIONS=halt_on_error=1 \
+	for t in config pci values flags sysfs amdsmi; do ASAN_OPTIONS=detect_leaks=1 UBSAN_OPTIONS=halt_on_error=1 \
 	  ./build-asan/fuzz_replay_$$t tests/fuzz/corpus/$$t || exit 1; done
 
 tsan:
@@ -50,7 +50,7 @@ fuzz:
 	cmake -S . -B build-fuzz -G Ninja -DCMAKE_BUILD_TYPE=Debug -DCMAKE_CXX_COMPILER=$(FUZZ_CXX) \
 	  -DGFD_SANITIZE=address,undefined -DGFD_FUZZ=ON -DGFD_BUILD_PYTHON=OFF -DGFD_BUILD_TESTS=OFF
 	cmake --build build-fuzz -j $(JOBS)
-	for t in config pci values flags sysfs; do mkdir -p build-fuzz/corpus-$$t && \
+	for t in config pci values flags sysfs amdsmi; do mkdir -p build-fuzz/corpus-$$t && \
 	  UBSAN_OPTIONS=halt_on_error=1 ./build-fuzz/fuzz_$$t -max_total_time=$(FUZZ_SECONDS) -timeout=10 \
 	    -rss_limit_mb=2048 build-fuzz/corpus-$$t tests/fuzz/corpus/$$t || exit 1; done
 

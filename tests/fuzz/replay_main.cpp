@@ -14,6 +14,7 @@
 #include <vector>
 
 extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size);
+extern "C" __attribute__((weak)) int LLVMFuzzerInitialize(int* argc, char*** argv);
 
 namespace {
 void collect(const std::string& path, std::vector<std::string>& out) {
@@ -32,6 +33,7 @@ void collect(const std::string& path, std::vector<std::string>& out) {
 }  // namespace
 
 int main(int argc, char** argv) {
+  if (LLVMFuzzerInitialize) LLVMFuzzerInitialize(&argc, &argv);
   std::vector<std::string> files;
   for (int i = 1; i < argc; ++i) collect(argv[i], files);
   for (const auto& f : files) {

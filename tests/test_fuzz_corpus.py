@@ -15,7 +15,7 @@ from conftest import REPO
 CORPUS = REPO / "tests" / "fuzz" / "corpus"
 
 
-@pytest.mark.parametrize("target", ["config", "pci", "values", "flags", "sysfs"])
+@pytest.mark.parametrize("target", ["config", "pci", "values", "flags", "sysfs", "amdsmi"])
 def test_fuzz_corpus_replays_cleanly(target):
     build = os.environ.get("GFD_BUILD_DIR", str(REPO / "build"))
     exe = os.path.join(build, f"fuzz_replay_{target}")

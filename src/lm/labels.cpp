@@ -219,6 +219,13 @@ void remove_output_file(const std::string& path) {
 
 std::string sanitize_label_value(const std::string& v) {
   auto alnum = [](char c) { return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9'); };
+  // Fast path (every label of a healthy node): already a valid value.
+  if (v.empty()) return v;
+  if (v.size() <= 63 && alnum(v.front()) && alnum(v.back())) {
+    bool ok = true;
+    for (char c : v) ok &= alnum(c) || c == '.' || c == '_' || c == '-';
+    if (ok) return v;
+  }
   std::string out;
   out.reserve(v.size());
   for (char c : v) {

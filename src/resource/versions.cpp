@@ -3,6 +3,8 @@
 #include <sys/utsname.h>
 
 #include <cstdlib>
+#include <map>
+#include <mutex>
 #include <tuple>
 
 #include "util/error.h"
@@ -30,8 +32,31 @@ std::optional<std::string> extract_version(const std::string& s) {
   return std::nullopt;
 }
 
+namespace {
+// amdgpu built into the kernel (the MI355X pool): /sys/module/amdgpu exists
+// but has no `initstate` (only loadable modules have one) and no `version`.
+// Whether the kernel's amdgpu is built in or loadable is fixed until the
+// next boot (a DKMS module cannot replace a built-in driver, and a kernel
+// with a loadable amdgpu never grows a built-in one), so it is decided once
+// the module directory exists; a built-in driver then skips the failing
+// `version` lookup - a path walk every cycle.
+bool builtin_amdgpu(const std::string& root) {
+  static std::mutex mu;
+  static std::map<std::string, bool> known;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = known.find(root);
+  if (it != known.end()) return it->second;
+  std::string dir = fs::join(root, "sys/module/amdgpu");
+  if (!fs::is_dir(dir)) return false;  // not loaded (yet): ask again next time
+  bool builtin = !fs::exists(dir + "/initstate") && !fs::exists(dir + "/version");
+  known.emplace(root, builtin);
+  return builtin;
+}
+}  // namespace
+
 std::string host_driver_version(const std::string& root) {
-  if (auto v = fs::attrs().read_trimmed(fs::join(root, "sys/module/amdgpu/version")); v && !v->empty()) return *v;
+  if (!builtin_amdgpu(root))
+    if (auto v = fs::attrs().read_trimmed(fs::join(root, "sys/module/amdgpu/version")); v && !v->empty()) return *v;
   if (root != "/" && !root.empty()) {
     // Synthetic trees carry the kernel banner under proc/.
     if (auto v = fs::read_trimmed(fs::join(root, "proc/sys/kernel/osrelease")); v && !v->empty()) return *v;

@@ -13,6 +13,7 @@
 #include "lm/node.h"
 #include "lm/resource.h"
 #include "resource/managers.h"
+#include "resource/versions.h"
 #include "test.h"
 #include "util/fs.h"
 
@@ -256,6 +257,30 @@ TEST(VersionLabeler_RuntimeErrorPropagates) {
   resource::MockManager m({resource::new_full_gpu()});
   m.runtime_error = "no rocm";
   EXPECT_THROW_MSG(lm::NewVersionLabeler(m), "error getting ROCm runtime version: no rocm");
+}
+
+TEST(DriverVersion_BuiltinAndLoadableAmdgpu) {
+  char d[] = "/tmp/gfd-drv-XXXXXX";
+  if (!mkdtemp(d)) throw std::runtime_error("mkdtemp");
+  std::string root = d;
+  fs::mkdir_all(root + "/proc/sys/kernel");
+  lm::write_file_atomically(root + "/proc/sys/kernel/osrelease", "6.18.54-ant.1\n", 0644);
+  // Not loaded: the kernel release; asked again every time.
+  EXPECT_EQ(resource::driver_version(root), std::string("6.18.54"));
+  // Built in (parameters only): the kernel release, decided for good.
+  fs::mkdir_all(root + "/sys/module/amdgpu/parameters");
+  EXPECT_EQ(resource::driver_version(root), std::string("6.18.54"));
+  lm::write_file_atomically(root + "/sys/module/amdgpu/version", "6.12.12\n", 0644);  // cannot happen without a reboot
+  EXPECT_EQ(resource::driver_version(root), std::string("6.18.54"));
+  // A loadable (DKMS) module: its version, re-read every time.
+  std::string dkms = root + "/dkms";
+  fs::mkdir_all(dkms + "/sys/module/amdgpu");
+  lm::write_file_atomically(dkms + "/sys/module/amdgpu/initstate", "live\n", 0644);
+  lm::write_file_atomically(dkms + "/sys/module/amdgpu/version", "6.12.12\n", 0644);
+  EXPECT_EQ(resource::driver_version(dkms), std::string("6.12.12"));
+  lm::write_file_atomically(dkms + "/sys/module/amdgpu/version", "6.14.3\n", 0644);
+  EXPECT_EQ(resource::driver_version(dkms), std::string("6.14.3"));
+  fs::remove_all(root);
 }
 
 // Facts read on the daemon's worker (file-backed managers) give the same

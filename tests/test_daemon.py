@@ -360,3 +360,39 @@ def test_amdsmi_of_another_major_version_is_not_used(binary, tmp_path, mi355x_no
                               env=_fake_amdsmi_env(spec), until="Sleeping for")
     assert labels["amd.com/gpu.count"] == "2"  # the tree's GPUs, through KFD
     assert "this build needs major version 26" in err
+
+
+def test_concurrent_reader_never_sees_a_partial_file(binary, tmp_path, mi355x_node):
+    """What the atomic write is for (labels.go:68-114): NFD's worker reads
+    every file in features.d whenever it likes.  With the daemon rewriting
+    the file every millisecond, a reader that lists the directory and reads
+    each regular file (as NFD's local source does) must only ever see the
+    complete label set: never a missing, empty or truncated `gfd`, and never
+    a temporary file outside `gfd-tmp/`."""
+    root = mi355x_node(n_gpus=8)
+    features = tmp_path / "features.d"
+    features.mkdir()
+    out = features / "gfd"
+    p = _start(binary, ["--sleep-interval=1ms", "--backend=sysfs", f"--sysfs-root={root}", f"--output-file={out}",
+                        f"--machine-type-file={root}/sys/class/dmi/id/product_name"])
+    try:
+        assert _wait_for(out.exists)
+        expected = golden.parse_labels(out.read_text())
+        assert len(expected) > 10
+        reads, bad = 0, []
+        end = time.monotonic() + 3
+        while time.monotonic() < end:
+            names = sorted(os.listdir(features))
+            if names != ["gfd", "gfd-tmp"]:
+                bad.append(f"directory listing {names}")
+            text = out.read_text()  # open by path, like NFD
+            reads += 1
+            if not text.endswith("\n") or golden.parse_labels(text) != expected:
+                bad.append(f"partial read: {text[-80:]!r}")
+            if len(bad) > 5:
+                break
+        assert not bad, bad
+        assert reads > 200
+    finally:
+        p.send_signal(signal.SIGTERM)
+        p.communicate(timeout=30)

@@ -9,11 +9,11 @@
 #include <map>
 #include <mutex>
 
+#include "resource/amdsmi_lib.h"
 #include "resource/pci_ids.h"
 #include "resource/physical.h"
 #include "resource/sysfs.h"
 #include "resource/versions.h"
-#include "util/dynlib.h"
 #include "util/error.h"
 #include "util/fs.h"
 #include "util/log.h"
@@ -22,156 +22,6 @@
 #include "util/trace.h"
 
 namespace gfd::resource {
-
-// ---------------------------------------------------------------------------
-// Library binding: dlopen once, bind every entry point once.
-
-class AmdSmiLib {
- public:
-  static AmdSmiLib* get(std::string* err) {
-    static std::once_flag once;
-    static AmdSmiLib* inst = nullptr;
-    static std::string load_error;
-    std::call_once(once, [] {
-      auto* l = new AmdSmiLib();
-      if (l->load(&load_error)) {
-        inst = l;
-      } else {
-        delete l;
-      }
-    });
-    if (!inst && err) *err = load_error;
-    return inst;
-  }
-
-  std::string status_str(amdsmi_status_t st) const {
-    const char* s = nullptr;
-    if (status_code_to_string && status_code_to_string(st, &s) == AMDSMI_STATUS_SUCCESS && s) return s;
-    return "amdsmi status " + std::to_string(static_cast<int>(st));
-  }
-
-  const std::string& path() const { return lib_.path(); }
-
-  // Process-wide init state (amdsmi_init is global).
-  std::mutex mu;
-  int users = 0;
-  // Set once amd-smi has refused asic_info with NOT_SUPPORTED (see
-  // identity_from_kfd); reset by every amdsmi_init, so a session asks once.
-  std::atomic<bool> asic_info_unsupported{false};
-
-#define GFD_AMDSMI_FN(name, ...) amdsmi_status_t (*name)(__VA_ARGS__) = nullptr
-  GFD_AMDSMI_FN(init, uint64_t);
-  GFD_AMDSMI_FN(shut_down, void);
-  GFD_AMDSMI_FN(get_socket_handles, uint32_t*, amdsmi_socket_handle*);
-  GFD_AMDSMI_FN(get_processor_handles, amdsmi_socket_handle, uint32_t*, amdsmi_processor_handle*);
-  GFD_AMDSMI_FN(get_processor_type, amdsmi_processor_handle, processor_type_t*);
-  GFD_AMDSMI_FN(get_gpu_asic_info, amdsmi_processor_handle, amdsmi_asic_info_t*);
-  GFD_AMDSMI_FN(get_gpu_device_bdf, amdsmi_processor_handle, amdsmi_bdf_t*);
-  GFD_AMDSMI_FN(get_gpu_device_uuid, amdsmi_processor_handle, unsigned int*, char*);
-  GFD_AMDSMI_FN(get_gpu_kfd_info, amdsmi_processor_handle, amdsmi_kfd_info_t*);
-  GFD_AMDSMI_FN(get_gpu_memory_total, amdsmi_processor_handle, amdsmi_memory_type_t, uint64_t*);
-  GFD_AMDSMI_FN(get_gpu_compute_partition, amdsmi_processor_handle, char*, uint32_t);
-  GFD_AMDSMI_FN(get_gpu_memory_partition, amdsmi_processor_handle, char*, uint32_t);
-  GFD_AMDSMI_FN(get_gpu_memory_partition_config, amdsmi_processor_handle, amdsmi_memory_partition_config_t*);
-  GFD_AMDSMI_FN(get_gpu_accelerator_partition_profile_config, amdsmi_processor_handle,
-                amdsmi_accelerator_partition_profile_config_t*);
-  GFD_AMDSMI_FN(get_gpu_xgmi_link_status, amdsmi_processor_handle, amdsmi_xgmi_link_status_t*);
-  GFD_AMDSMI_FN(get_gpu_virtualization_mode, amdsmi_processor_handle, amdsmi_virtualization_mode_t*);
-  GFD_AMDSMI_FN(get_gpu_xcd_counter, amdsmi_processor_handle, uint16_t*);
-  GFD_AMDSMI_FN(get_gpu_driver_info, amdsmi_processor_handle, amdsmi_driver_info_t*);
-  GFD_AMDSMI_FN(get_gpu_board_info, amdsmi_processor_handle, amdsmi_board_info_t*);
-  GFD_AMDSMI_FN(get_lib_version, amdsmi_version_t*);
-#undef GFD_AMDSMI_FN
-  amdsmi_status_t (*status_code_to_string)(amdsmi_status_t, const char**) = nullptr;
-
- private:
-  bool load(std::string* err) {
-    std::vector<std::string> candidates;
-    if (const char* p = std::getenv("GFD_AMDSMI_LIBRARY"); p && *p) candidates.push_back(p);
-    if (const char* rp = std::getenv("ROCM_PATH"); rp && *rp) {
-      candidates.push_back(fs::join(rp, "lib/libamd_smi.so.26"));
-      candidates.push_back(fs::join(rp, "lib/libamd_smi.so"));
-    }
-    candidates.push_back("/opt/rocm/lib/libamd_smi.so.26");
-    candidates.push_back("/opt/rocm/lib/libamd_smi.so");
-    candidates.push_back("libamd_smi.so.26");
-    candidates.push_back("libamd_smi.so");
-    // The structs this file passes to the library are laid out by the
-    // amdsmi.h it was compiled against; a library of another major version
-    // (an unversioned libamd_smi.so from a different ROCm) may lay them out
-    // differently, so it is skipped in favour of the next candidate.
-    std::string mismatch;
-    bool opened = false;
-    for (const auto& c : candidates) {
-      if (!lib_.open({c})) continue;
-      amdsmi_status_t (*lib_version)(amdsmi_version_t*) = nullptr;
-      amdsmi_version_t v{};
-      if (lib_.bind("amdsmi_get_lib_version", lib_version) && lib_version(&v) == AMDSMI_STATUS_SUCCESS &&
-          v.major != AMDSMI_LIB_VERSION_MAJOR) {
-        mismatch = c + " is amd-smi " + std::to_string(v.major) + "." + std::to_string(v.minor) +
-                   ", this build needs major version " + std::to_string(AMDSMI_LIB_VERSION_MAJOR);
-        log::printf("Skipping %s", mismatch.c_str());
-        lib_.close();
-        continue;
-      }
-      opened = true;
-      break;
-    }
-    if (!opened) {
-      *err = mismatch.empty() ? lib_.last_error() : mismatch;
-      return false;
-    }
-    bool ok = true;
-    auto need = [&](const char* sym, auto& fn) {
-      if (!lib_.bind(sym, fn)) {
-        ok = false;
-        *err = std::string("symbol ") + sym + " not found in " + lib_.path();
-      }
-    };
-    need("amdsmi_init", init);
-    need("amdsmi_shut_down", shut_down);
-    need("amdsmi_get_socket_handles", get_socket_handles);
-    need("amdsmi_get_processor_handles", get_processor_handles);
-    need("amdsmi_get_processor_type", get_processor_type);
-    need("amdsmi_get_gpu_asic_info", get_gpu_asic_info);
-    need("amdsmi_get_gpu_device_bdf", get_gpu_device_bdf);
-    need("amdsmi_get_gpu_memory_total", get_gpu_memory_total);
-    need("amdsmi_get_gpu_driver_info", get_gpu_driver_info);
-    // Optional: newer partition / topology queries degrade gracefully.
-    lib_.bind("amdsmi_get_gpu_device_uuid", get_gpu_device_uuid);
-    lib_.bind("amdsmi_get_gpu_kfd_info", get_gpu_kfd_info);
-    lib_.bind("amdsmi_get_gpu_compute_partition", get_gpu_compute_partition);
-    lib_.bind("amdsmi_get_gpu_memory_partition", get_gpu_memory_partition);
-    lib_.bind("amdsmi_get_gpu_memory_partition_config", get_gpu_memory_partition_config);
-    lib_.bind("amdsmi_get_gpu_accelerator_partition_profile_config", get_gpu_accelerator_partition_profile_config);
-    lib_.bind("amdsmi_get_gpu_xgmi_link_status", get_gpu_xgmi_link_status);
-    lib_.bind("amdsmi_get_gpu_virtualization_mode", get_gpu_virtualization_mode);
-    lib_.bind("amdsmi_get_gpu_xcd_counter", get_gpu_xcd_counter);
-    lib_.bind("amdsmi_get_gpu_board_info", get_gpu_board_info);
-    lib_.bind("amdsmi_get_lib_version", get_lib_version);
-    lib_.bind("amdsmi_status_code_to_string", status_code_to_string);
-    return ok;
-  }
-
-  DynLib lib_;
-};
-
-bool has_amdsmi(std::string* reason) {
-  std::string err;
-  AmdSmiLib* l = AmdSmiLib::get(&err);
-  if (!l) {
-    if (reason) *reason = "could not load libamd_smi: " + err;
-    return false;
-  }
-  if (reason) {
-    *reason = "found " + l->path();
-    amdsmi_version_t v{};
-    if (l->get_lib_version && l->get_lib_version(&v) == AMDSMI_STATUS_SUCCESS)
-      *reason += " (amd-smi library " + std::to_string(v.major) + "." + std::to_string(v.minor) + "." +
-                 std::to_string(v.release) + ")";
-  }
-  return true;
-}
 
 // ---------------------------------------------------------------------------
 // Snapshot helpers

@@ -2,6 +2,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdlib>
 
 namespace gfd {
@@ -12,7 +13,23 @@ WorkerPool& WorkerPool::instance() {
   return *pool;
 }
 
-WorkerPool::WorkerPool(size_t max_workers) : max_workers_(max_workers ? max_workers : 1) {}
+namespace {
+// GFD_POOL_SPIN_US overrides the bound of the adaptive idle spin (0
+// disables it; A/B measurements).
+int64_t max_spin_ns_from_env() {
+  const char* v = std::getenv("GFD_POOL_SPIN_US");
+  if (!v || !*v) return 200000;
+  return static_cast<int64_t>(std::strtoul(v, nullptr, 10)) * 1000;
+}
+
+int64_t mono_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+}  // namespace
+
+WorkerPool::WorkerPool(size_t max_workers)
+    : max_workers_(max_workers ? max_workers : 1), max_spin_ns_(max_spin_ns_from_env()) {}
 
 WorkerPool::~WorkerPool() {
   {
@@ -49,9 +66,9 @@ void WorkerPool::wake_one() {
   if (idle_.empty()) return;
   Worker* w = idle_.back();
   idle_.pop_back();
-  w->woken = true;
+  w->woken.store(true, std::memory_order_release);
   ++waking_;
-  w->cv.notify_one();
+  w->cv.notify_one();  // no system call when the worker is still spinning
 }
 
 void WorkerPool::loop(Worker* w) {
@@ -59,10 +76,26 @@ void WorkerPool::loop(Worker* w) {
   --spawning_;
   for (;;) {
     while (queue_.empty() && !stop_) {
-      w->woken = false;
+      w->woken.store(false, std::memory_order_relaxed);
       idle_.push_back(w);
-      w->cv.wait(lk, [&] { return w->woken || stop_; });
-      if (w->woken) {
+      // Adaptive spin (the heuristic of adaptive mutexes): when this
+      // worker's last wait for work was short - cycles back to back, as in
+      // a daemon with a short --sleep-interval or the benchmark - stay
+      // runnable for up to twice that long, polling the wake-up flag, before
+      // blocking; a blocked worker costs a futex wake-up plus the
+      // scheduler's latency on top of its task (profiles/pool_spin_ab.txt).
+      // A deployed daemon sleeps 60 s between cycles: its workers' waits
+      // are long, so they block at once and the spin costs nothing.
+      int64_t t0 = mono_ns();
+      if (max_spin_ns_ > 0 && w->last_gap_ns >= 0 && w->last_gap_ns <= max_spin_ns_) {
+        lk.unlock();
+        int64_t until = t0 + std::min(max_spin_ns_, 2 * w->last_gap_ns + 5000);
+        while (!w->woken.load(std::memory_order_acquire) && mono_ns() < until) __builtin_ia32_pause();
+        lk.lock();
+      }
+      w->cv.wait(lk, [&] { return w->woken.load(std::memory_order_relaxed) || stop_; });
+      w->last_gap_ns = mono_ns() - t0;
+      if (w->woken.load(std::memory_order_relaxed)) {
         --waking_;
       } else {
         idle_.erase(std::find(idle_.begin(), idle_.end(), w));  // stopping
@@ -201,9 +234,15 @@ void WorkerPool::parallel_for(size_t n, const std::function<void(size_t)>& fn, s
     for (size_t l = 1; l < lanes; ++l) wake_one();
   }
   body();
-  std::unique_lock<std::mutex> lk(sh->mu);
-  sh->cv.wait(lk, [&] { return sh->done == sh->n; });
-  if (sh->error) std::rethrow_exception(sh->error);
+  std::exception_ptr error;
+  {
+    std::unique_lock<std::mutex> lk(sh->mu);
+    sh->cv.wait(lk, [&] { return sh->done == sh->n; });
+    // Taken out, so that a helper lane dropping the last reference to `sh`
+    // later never destroys the exception this thread is handling.
+    error = std::move(sh->error);
+  }
+  if (error) std::rethrow_exception(error);
 }
 
 size_t gpu_lanes(size_t n_gpus, bool light) {

@@ -78,7 +78,9 @@ class WorkerPool {
  private:
   struct Worker {
     std::condition_variable cv;
-    bool woken = false;
+    // Set (under mu_) by wake_one; read without the lock while spinning.
+    std::atomic<bool> woken{false};
+    int64_t last_gap_ns = -1;  // how long the worker last waited for work (-1: never)
   };
   void ensure_workers(size_t n);
   void wake_one();
@@ -93,6 +95,8 @@ class WorkerPool {
   size_t waking_ = 0;          // woken, not yet running
   size_t spawning_ = 0;        // threads created but not yet parked
   bool stop_ = false;
+  // Upper bound of the adaptive idle spin (see loop()); 0 disables it.
+  int64_t max_spin_ns_;
 };
 
 // Lanes for per-GPU work in one cycle.  light: a few attribute preads per

@@ -159,14 +159,13 @@ def _daemon_loop(binary: str, args: list[str], cycles: int, interval: str = "2ms
 
 
 def _cold_process(binary: str, args: list[str], runs: int) -> dict:
-    """Oneshot Job mode: fork+exec the daemon binary per label file (the
-    whole process: start, backend selection, one cycle, exit)."""
-    ms = []
-    for _ in range(runs):
-        t0 = time.perf_counter_ns()
-        subprocess.run([binary, "--oneshot", *args], check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
-                       timeout=60)
-        ms.append((time.perf_counter_ns() - t0) / 1e6)
+    """Oneshot Job mode: spawn the daemon binary per label file (the whole
+    process: start, backend selection, one cycle, exit), timed from spawn to
+    exit with a blocking waitpid (utils/proc.py: subprocess.run's polling
+    wait quantised round 1's numbers to 3.5 / 7.5 / 31.5 / 63.5 ms)."""
+    from gpu_feature_discovery_amd.utils.proc import spawn_wait_ms
+
+    ms = [spawn_wait_ms([binary, "--oneshot", *args], timeout=60) for _ in range(runs)]
     return {"p50_ms": round(_percentile(ms, 0.5), 3), "p90_ms": round(_percentile(ms, 0.9), 3), "runs": runs,
             "args": " ".join(a for a in args if not a.startswith(("--output-file", "--sysfs-root", "--machine")))}
 

@@ -12,13 +12,10 @@ bin=./build/gpu-feature-discovery
   python3 - "$bin" "$out" <<'PY'
 import statistics, subprocess, sys, time
 binary, out = sys.argv[1], sys.argv[2]
+sys.path.insert(0, ".")
+from gpu_feature_discovery_amd.utils.proc import spawn_wait_ms  # blocking waitpid, no polling quantisation
 def wall(cmd, n=30, env=None):
-    xs = []
-    for _ in range(n):
-        t0 = time.perf_counter_ns()
-        subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, check=True, timeout=60, env=env)
-        xs.append((time.perf_counter_ns() - t0) / 1e6)
-    xs.sort()
+    xs = sorted(spawn_wait_ms(cmd, timeout=60, env=env) for _ in range(n))
     return f"p50 {statistics.median(xs):8.3f} ms  p90 {xs[int(0.9 * (len(xs) - 1))]:8.3f} ms"
 o = ["--oneshot", f"--output-file={out}/gfd"]
 print("## process wall time (30 runs each)")

@@ -1,5 +1,9 @@
 #include "resource/sysfs.h"
 
+#if defined(__x86_64__)
+#include <cpuid.h>
+#endif
+
 #include <algorithm>
 #include <cerrno>
 #include <map>
@@ -97,15 +101,32 @@ std::string bdf_of(const KfdNode& n) {
 }  // namespace
 
 bool running_in_vm(const std::string& root) {
-  // The first processor's "flags" line is enough (reading all of
-  // /proc/cpuinfo on a 256-thread host is ~400 KB).
-  auto r = fs::read_file(fs::join(root, "proc/cpuinfo"), 16384);
-  if (!r.ok()) return false;
-  auto flags = r.data.find("\nflags");
-  if (flags == std::string::npos) return false;
-  auto eol = r.data.find('\n', flags + 1);
-  std::string line = r.data.substr(flags, eol == std::string::npos ? std::string::npos : eol - flags);
-  return (line + " ").find(" hypervisor ") != std::string::npos;
+#if defined(__x86_64__)
+  // The kernel's "hypervisor" flag is CPUID leaf 1, ECX bit 31: asking the
+  // CPU costs 0.08 us on the pool versus 15-90 us for the kernel to format
+  // the start of /proc/cpuinfo (profiles/cpuinfo_probe.txt).
+  if (root.empty() || root == "/") {
+    unsigned a = 0, b = 0, c = 0, d = 0;
+    if (__get_cpuid(1, &a, &b, &c, &d)) return (c >> 31) & 1u;
+  }
+#endif
+  // The first processor's "flags" line (synthetic trees, other
+  // architectures): read the start of the file, more only if that line is
+  // not complete yet (all of /proc/cpuinfo on a 256-thread host is ~400 KB).
+  for (size_t max : {size_t{4096}, size_t{16384}}) {
+    auto r = fs::read_file(fs::join(root, "proc/cpuinfo"), max);
+    if (!r.ok()) return false;
+    auto flags = r.data.find("\nflags");
+    if (flags == std::string::npos) {
+      if (r.data.size() < max) return false;
+      continue;
+    }
+    auto eol = r.data.find('\n', flags + 1);
+    if (eol == std::string::npos && r.data.size() >= max) continue;
+    std::string line = r.data.substr(flags, eol == std::string::npos ? std::string::npos : eol - flags);
+    return (line + " ").find(" hypervisor ") != std::string::npos;
+  }
+  return false;
 }
 
 bool has_kfd_topology(const std::string& root, std::string* reason) {

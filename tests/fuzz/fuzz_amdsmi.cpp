@@ -4,8 +4,11 @@
 // xGMI table, product name, KFD node properties, memory banks).  As for
 // fuzz_sysfs.cpp: labels or gfd::Error, no crash, only valid label values.
 //
-// The fake reports one MI355X at 0000:75:00.0 whose KFD node is 1 (SPX) or,
-// for inputs of odd length, a CPX GPU whose 8 partitions are nodes 1..8.
+// The first three NUL-separated fields script what the fake library itself
+// answers - the market name, the compute-partition string, and
+// "cus,xcds,vram_mib,links,virt,parts" - so amd-smi's own values are
+// arbitrary too; the fake reports that GPU at 0000:75:00.0 with KFD nodes
+// from 1.  The remaining fields are the sysfs files.
 #include <dlfcn.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -14,6 +17,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <optional>
 #include <string>
 
 #include "cli/daemon.h"
@@ -73,21 +77,49 @@ extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
     g_configure = reinterpret_cast<int (*)(const char*)>(dlsym(h, "fake_amdsmi_configure"));
     if (!g_configure) std::abort();
   }
-  bool cpx = size % 2 == 1;
-  g_configure(cpx ? "bdf=0000:75:00.0;mode=CPX;parts=8;cus=32;xcds=1;vram_mib=36862;kfd_base=1\n"
-                  : "bdf=0000:75:00.0;mode=SPX;parts=1;cus=256;xcds=8;vram_mib=294896;kfd_base=1\n");
   std::string in(reinterpret_cast<const char*>(data), size);
+  auto next_field = [&](size_t& pos) -> std::optional<std::string> {
+    if (pos > in.size()) return std::nullopt;
+    size_t end = in.find('\0', pos);
+    if (end == std::string::npos) end = in.size();
+    std::string f = in.substr(pos, end - pos);
+    pos = end + 1;
+    return f;
+  };
+  auto clean = [](std::string v) {  // the fake's spec separators
+    for (char& c : v)
+      if (c == ';' || c == '|' || c == '\n' || c == '=') c = '_';
+    return v.substr(0, 64);
+  };
   size_t pos = 0;
+  std::string name = clean(next_field(pos).value_or("AMD Instinct MI355 OAM"));
+  std::string mode = clean(next_field(pos).value_or("SPX"));
+  unsigned long nums[6] = {256, 8, 294896, 7, 1, 1};  // cus, xcds, vram_mib, links, virt, parts
+  {
+    std::string f = next_field(pos).value_or("");
+    size_t i = 0;
+    for (const char* p = f.c_str(); *p && i < 6; ++i) {
+      char* end = nullptr;
+      nums[i] = std::strtoul(p, &end, 10);
+      if (end == p) break;
+      p = *end == ',' ? end + 1 : end;
+    }
+  }
+  unsigned long parts = nums[5] % 9;  // 0..8 partitions
+  char spec[512];
+  std::snprintf(spec, sizeof(spec),
+                "bdf=0000:75:00.0;mode=%s;parts=%lu;name=%s;cus=%lu;xcds=%lu;vram_mib=%lu;links=%lu;virt=%lu;kfd_base=1\n",
+                mode.c_str(), parts, name.c_str(), nums[0] % 100000, nums[1] % 1000, nums[2] % (1ul << 40),
+                nums[3] % 64, nums[4] % 8);
+  g_configure(spec);
   for (const char* f : kFiles) {
     std::string path = g_root + "/" + f;
-    if (pos > in.size()) {
+    auto v = next_field(pos);
+    if (!v) {
       ::unlink(path.c_str());
       continue;
     }
-    size_t end = in.find('\0', pos);
-    if (end == std::string::npos) end = in.size();
-    gfd::lm::write_file_atomically(path, in.substr(pos, end - pos), 0644);
-    pos = end + 1;
+    gfd::lm::write_file_atomically(path, *v, 0644);
   }
   static const char* const kStrategies[] = {"none", "single", "mixed"};
   gfd::config::Config c;

@@ -64,8 +64,11 @@ void WorkerPool::wake_one() {
   // the per-cycle PCI scan took 180 us instead of 86 us once 8 workers
   // existed and took turns).
   if (idle_.empty()) return;
-  Worker* w = idle_.back();
-  idle_.pop_back();
+  // The spinning worker first (it needs no system call to start), else the
+  // most recently parked one.
+  auto it = std::find_if(idle_.rbegin(), idle_.rend(), [](const Worker* x) { return x->spinning; });
+  Worker* w = it != idle_.rend() ? *it : idle_.back();
+  idle_.erase(it != idle_.rend() ? std::next(it).base() : idle_.end() - 1);
   w->woken.store(true, std::memory_order_release);
   ++waking_;
   w->cv.notify_one();  // no system call when the worker is still spinning
@@ -86,12 +89,19 @@ void WorkerPool::loop(Worker* w) {
       // scheduler's latency on top of its task (profiles/pool_spin_ab.txt).
       // A deployed daemon sleeps 60 s between cycles: its workers' waits
       // are long, so they block at once and the spin costs nothing.
+      // One spinner at a time: several spinning lanes (a multi-GPU cycle)
+      // slowed the cycle's own thread more than their wake-ups cost
+      // (profiles/pool_spin_ab.txt, 8-GPU rows).
       int64_t t0 = mono_ns();
-      if (max_spin_ns_ > 0 && w->last_gap_ns >= 0 && w->last_gap_ns <= max_spin_ns_) {
+      if (max_spin_ns_ > 0 && !spinner_ && w->last_gap_ns >= 0 && w->last_gap_ns <= max_spin_ns_) {
+        spinner_ = true;
+        w->spinning = true;
         lk.unlock();
         int64_t until = t0 + std::min(max_spin_ns_, 2 * w->last_gap_ns + 5000);
         while (!w->woken.load(std::memory_order_acquire) && mono_ns() < until) __builtin_ia32_pause();
         lk.lock();
+        w->spinning = false;
+        spinner_ = false;
       }
       w->cv.wait(lk, [&] { return w->woken.load(std::memory_order_relaxed) || stop_; });
       w->last_gap_ns = mono_ns() - t0;

@@ -81,6 +81,7 @@ class WorkerPool {
     // Set (under mu_) by wake_one; read without the lock while spinning.
     std::atomic<bool> woken{false};
     int64_t last_gap_ns = -1;  // how long the worker last waited for work (-1: never)
+    bool spinning = false;     // in its adaptive spin (guarded by mu_)
   };
   void ensure_workers(size_t n);
   void wake_one();
@@ -97,6 +98,7 @@ class WorkerPool {
   bool stop_ = false;
   // Upper bound of the adaptive idle spin (see loop()); 0 disables it.
   int64_t max_spin_ns_;
+  bool spinner_ = false;  // a worker is spinning (at most one does; guarded by mu_)
 };
 
 // Lanes for per-GPU work in one cycle.  light: a few attribute preads per

@@ -7,11 +7,15 @@ mkdir -p $out
 root=$(mktemp -d /tmp/gfd-hybrid-XXXXXX)
 n=$(python3 tools/hybrid_root.py $root) || exit 1
 echo "GPUs in the hybrid root: $n"
-for g in 1 2 4 8; do
-  [ $g -le $n ] || break
-  timeout -k 10 300 python bench.py --gpus $g --steps 2000 --warmup 200 --backend sysfs --sysfs-root $root --no-extras \
-    > $out/sysfs_$g.json 2> $out/sysfs_$g.err || { echo "bench $g failed"; cat $out/sysfs_$g.err | tail -5; exit 1; }
-  python3 -c "
+# GFD_POOL_SPIN_US: the pool's adaptive idle spin off (0) and on (default).
+for spin in 0 200; do
+  for g in 1 2 4 8; do
+    [ $g -le $n ] || break
+    GFD_POOL_SPIN_US=$spin timeout -k 10 300 python bench.py --gpus $g --steps 2000 --warmup 200 --backend sysfs \
+      --sysfs-root $root --no-extras > $out/sysfs_$g.json 2> $out/sysfs_$g.err ||
+      { echo "bench $g failed"; tail -5 $out/sysfs_$g.err; exit 1; }
+    python3 -c "
 import json; r=json.load(open('$out/sysfs_$g.json'))
-print('%d GPU(s): p50 %.4f ms p90 %.4f ms labels_ok=%s count=%s | %s' % ($g, r['value'], r['p90_ms'], r['labels_ok'], r['n_gpus'], ' '.join('%s=%.4f' % kv for kv in r['extras']['phases_ms'].items())))"
+print('spin %sus %d GPU(s): p50 %.4f ms p90 %.4f ms labels_ok=%s count=%s | %s' % ('$spin', $g, r['value'], r['p90_ms'], r['labels_ok'], r['n_gpus'], ' '.join('%s=%.4f' % kv for kv in r['phases_p50_ms'].items())))"
+  done
 done | tee $out/curve.txt

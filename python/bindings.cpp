@@ -26,6 +26,7 @@
 #include "sriov/sriov.h"
 #include "util/duration.h"
 #include "util/error.h"
+#include "util/affinity.h"
 #include "util/log.h"
 
 namespace py = pybind11;
@@ -103,6 +104,10 @@ py::dict device_to_dict(const resource::Device& d) {
 class Session {
  public:
   Session(const std::vector<std::string>& args, const std::map<std::string, std::string>& env, bool use_env) {
+    // The daemon's start-up CPU policy (gfd_main), once per process, before
+    // the first session starts any pool worker (util/affinity.h).
+    static const std::string pinned = affinity::pin_to_current_l3();
+    (void)pinned;
     auto ctx = cli::Context::parse(cli::gfd_flags(), args, use_env ? &env : nullptr);
     config_ = cli::load_config(ctx);
     config::disable_resource_renaming(config_);

@@ -11,6 +11,7 @@
 #include "info/version.h"
 #include "lm/node.h"
 #include "resource/factory.h"
+#include "util/affinity.h"
 #include "util/error.h"
 #include "util/log.h"
 #include "util/pool.h"
@@ -333,6 +334,8 @@ int gfd_main(int argc, char** argv) {
     return 0;
   }
   g_timeline.main_ns = trace::now_ns();
+  // Before any thread exists: workers inherit the mask (util/affinity.h).
+  if (std::string pinned = affinity::pin_to_current_l3(); !pinned.empty()) log::printf("CPU affinity: %s", pinned.c_str());
   int rc = 0;
   {
     log::printf("Starting OS watcher.");

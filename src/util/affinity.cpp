@@ -1,0 +1,56 @@
+#include "util/affinity.h"
+
+#include <sched.h>
+
+#include <cstdlib>
+#include <vector>
+
+#include "util/fs.h"
+#include "util/strings.h"
+
+namespace gfd::affinity {
+
+std::vector<int> parse_cpu_list(const std::string& s) {
+  std::vector<int> out;
+  for (const auto& part : str::split(str::trim(s), ',')) {
+    if (part.empty()) continue;
+    auto range = str::split_n(part, '-', 2);
+    auto lo = str::parse_uint(range[0]);
+    auto hi = range.size() == 2 ? str::parse_uint(range[1]) : lo;
+    if (!lo || !hi || *hi < *lo || *hi >= CPU_SETSIZE) return {};
+    for (uint64_t c = *lo; c <= *hi; ++c) out.push_back(static_cast<int>(c));
+  }
+  return out;
+}
+
+std::string pin_to_current_l3(const std::string& sys_root) {
+  if (const char* v = std::getenv("GFD_CPU_AFFINITY"); v && std::string(v) == "none") return "";
+  int cpu = sched_getcpu();
+  if (cpu < 0) return "";
+  // The L3 is the cache index whose level is 3 (index3 on x86, but look).
+  std::string base = fs::join(sys_root, "sys/devices/system/cpu/cpu" + std::to_string(cpu) + "/cache");
+  std::string list;
+  for (const auto& idx : fs::list_dir(base)) {
+    if (idx.rfind("index", 0) != 0) continue;
+    if (fs::read_trimmed(fs::join(base, idx + "/level")).value_or("") == "3") {
+      list = fs::read_trimmed(fs::join(base, idx + "/shared_cpu_list")).value_or("");
+      break;
+    }
+  }
+  std::vector<int> l3 = parse_cpu_list(list);
+  if (l3.empty()) return "";
+  cpu_set_t allowed;
+  CPU_ZERO(&allowed);
+  if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return "";
+  cpu_set_t pin;
+  CPU_ZERO(&pin);
+  for (int c : l3)
+    if (CPU_ISSET(c, &allowed)) CPU_SET(c, &pin);
+  int n_pin = CPU_COUNT(&pin), n_allowed = CPU_COUNT(&allowed);
+  if (n_pin == 0 || n_pin == n_allowed) return "";
+  if (sched_setaffinity(0, sizeof(pin), &pin) != 0) return "";
+  return "threads kept on the " + std::to_string(n_pin) + " CPUs sharing cpu" + std::to_string(cpu) +
+         "'s L3 cache (" + list + ") of " + std::to_string(n_allowed) + " allowed";
+}
+
+}  // namespace gfd::affinity

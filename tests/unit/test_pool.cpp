@@ -2,10 +2,21 @@
 #include <atomic>
 #include <stdexcept>
 
+#include <sched.h>
+
+#include <string>
+#include <vector>
+
+#include "lm/labels.h"
 #include "test.h"
+#include "util/affinity.h"
+#include "util/fs.h"
 #include "util/pool.h"
 
 using gfd::WorkerPool;
+namespace affinity = gfd::affinity;
+namespace fs = gfd::fs;
+namespace lm = gfd::lm;
 
 TEST(Pool_ParallelForVisitsEveryIndexOnce) {
   WorkerPool pool(4);
@@ -127,4 +138,41 @@ TEST(Pool_GpuLanesPolicy) {
   EXPECT_EQ(gfd::gpu_lanes(8, true), static_cast<size_t>(4));
   EXPECT_EQ(gfd::gpu_lanes(16, true), static_cast<size_t>(4));
   EXPECT_EQ(gfd::gpu_lanes(8, false), static_cast<size_t>(8));
+}
+
+// ---- L3-domain pinning (util/affinity.h) ----
+
+TEST(Affinity_ParseCpuList) {
+  EXPECT_TRUE(affinity::parse_cpu_list("0-3,128-129\n") == (std::vector<int>{0, 1, 2, 3, 128, 129}));
+  EXPECT_TRUE(affinity::parse_cpu_list("5") == (std::vector<int>{5}));
+  EXPECT_TRUE(affinity::parse_cpu_list("3-1").empty());
+  EXPECT_TRUE(affinity::parse_cpu_list("x").empty());
+}
+
+TEST(Affinity_PinsToTheCurrentL3DomainWithinTheAllowedSet) {
+  cpu_set_t before;
+  CPU_ZERO(&before);
+  EXPECT_TRUE(sched_getaffinity(0, sizeof(before), &before) == 0);
+  if (CPU_COUNT(&before) < 2) return;  // nothing to narrow
+  // A synthetic topology in which every CPU has an L3 of its own.
+  char d[] = "/tmp/gfd-aff-XXXXXX";
+  EXPECT_TRUE(mkdtemp(d) != nullptr);
+  std::string root = d;
+  for (int c = 0; c < CPU_SETSIZE; ++c) {
+    if (!CPU_ISSET(c, &before)) continue;
+    std::string idx = root + "/sys/devices/system/cpu/cpu" + std::to_string(c) + "/cache/index3";
+    fs::mkdir_all(idx);
+    lm::write_file_atomically(idx + "/level", "3\n", 0644);
+    lm::write_file_atomically(idx + "/shared_cpu_list", std::to_string(c) + "\n", 0644);
+  }
+  std::string what = affinity::pin_to_current_l3(root);
+  cpu_set_t after;
+  CPU_ZERO(&after);
+  EXPECT_TRUE(sched_getaffinity(0, sizeof(after), &after) == 0);
+  EXPECT_EQ(CPU_COUNT(&after), 1);
+  EXPECT_TRUE(what.find("threads kept on the 1 CPUs") != std::string::npos);
+  // Already within one domain: nothing changes.
+  EXPECT_EQ(affinity::pin_to_current_l3(root), std::string(""));
+  EXPECT_TRUE(sched_setaffinity(0, sizeof(before), &before) == 0);
+  fs::remove_all(root);
 }

@@ -300,13 +300,8 @@ void start(const Context& ctx, SignalWatcher& sigs) {
 
     bool restart;
     {
-      // The SR-IOV scanner first, and its cold first scan (every PCI
-      // function's identity) started on a worker now: it overlaps backend
-      // selection and enumeration instead of starting with the first cycle
-      // - most of a Job process's run (profiles/oneshot_breakdown_r2.txt).
-      auto sriov = sriov::new_sriov_lib(c.sysfs_root());
-      WorkerPool::instance().submit([sriov] { sriov->Prefetch(); });
       resource::ManagerPtr manager = resource::new_manager(c);
+      auto sriov = sriov::new_sriov_lib(c.sysfs_root());
       if (!g_timeline.manager_ns) g_timeline.manager_ns = trace::now_ns();
 
       log::printf("Start running");

@@ -61,23 +61,10 @@ std::optional<Info> Lib::Classify(const PCIDevice& d) {
   return std::nullopt;
 }
 
-std::vector<PCIDevice> Lib::scan() {
-  std::lock_guard<std::mutex> g(mu_);
-  return pci_->Devices();
-}
-
-void Lib::Prefetch() {
-  try {
-    scan();
-  } catch (const std::exception&) {
-    // The cycle's own scan reports it.
-  }
-}
-
 std::vector<Function> Lib::Devices() {
   std::vector<PCIDevice> devices;
   try {
-    devices = scan();
+    devices = pci_->Devices();
   } catch (const std::exception& e) {
     throw Error(std::string("error getting AMD specific PCI devices: ") + e.what());
   }

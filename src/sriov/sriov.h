@@ -23,8 +23,6 @@
 #pragma once
 
 #include <memory>
-#include <mutex>
-#include <optional>
 #include <string>
 #include <vector>
 
@@ -71,10 +69,6 @@ class Interface {
  public:
   virtual ~Interface() = default;
   virtual std::vector<Function> Devices() = 0;
-  // Warm whatever the first Devices() would have to read cold (a process's
-  // first PCI scan reads every function's identity: ~1.3 ms on the pool);
-  // safe to run on another thread while Devices() is called.
-  virtual void Prefetch() {}
   // Version of the SR-IOV host driver (GIM) loaded on this node; nullopt
   // when it is not (bare metal, amdgpu-only hosts, guests).
   virtual std::optional<std::string> HostDriverVersion() { return std::nullopt; }
@@ -84,17 +78,14 @@ class Lib : public Interface {
  public:
   explicit Lib(std::shared_ptr<AmdPCI> pci, std::string root = "") : pci_(std::move(pci)), root_(std::move(root)) {}
   std::vector<Function> Devices() override;
-  void Prefetch() override;
   // <root>/sys/module/gim/version (no root: not looked up).
   std::optional<std::string> HostDriverVersion() override;
   // Classifies one PCI function; nullopt if it is not SR-IOV relevant.
   static std::optional<Info> Classify(const PCIDevice& d);
 
  private:
-  std::vector<PCIDevice> scan();
   std::shared_ptr<AmdPCI> pci_;
   std::string root_;
-  std::mutex mu_;  // one scan at a time (the PCI scanner keeps state between scans)
 };
 
 std::shared_ptr<Interface> new_sriov_lib(const std::string& root);

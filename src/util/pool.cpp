@@ -22,6 +22,14 @@ int64_t max_spin_ns_from_env() {
   return static_cast<int64_t>(std::strtoul(v, nullptr, 10)) * 1000;
 }
 
+inline void cpu_relax() {
+#if defined(__x86_64__) || defined(__i386__)
+  __builtin_ia32_pause();
+#elif defined(__aarch64__)
+  asm volatile("yield");
+#endif
+}
+
 int64_t mono_ns() {
   return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
       .count();
@@ -91,14 +99,14 @@ void WorkerPool::loop(Worker* w) {
       // are long, so they block at once and the spin costs nothing.
       // One spinner at a time: several spinning lanes (a multi-GPU cycle)
       // slowed the cycle's own thread more than their wake-ups cost
-      // (profiles/pool_spin_ab.txt, 8-GPU rows).
+      // (profiles/hybrid_8gpu_scaling.txt, "every worker spinning").
       int64_t t0 = mono_ns();
       if (max_spin_ns_ > 0 && !spinner_ && w->last_gap_ns >= 0 && w->last_gap_ns <= max_spin_ns_) {
         spinner_ = true;
         w->spinning = true;
         lk.unlock();
         int64_t until = t0 + std::min(max_spin_ns_, 2 * w->last_gap_ns + 5000);
-        while (!w->woken.load(std::memory_order_acquire) && mono_ns() < until) __builtin_ia32_pause();
+        while (!w->woken.load(std::memory_order_acquire) && mono_ns() < until) cpu_relax();
         lk.lock();
         w->spinning = false;
         spinner_ = false;

@@ -249,6 +249,9 @@ void fix_market_name(AmdSmiLib& L, const std::string& root, ProcInfo& p) {
         !is_generic_name(str::trim(b.product_name)))
       p.market_name = str::trim(b.product_name);
   }
+  // Nothing better known (no libdrm, no FRU): the model of the device ID,
+  // the KFD backend's fallback too.
+  if (p.market_name.empty() && p.device_id) p.market_name = device_name(p.device_id);
 }
 
 bool sysfs_values_enabled() {

@@ -104,3 +104,26 @@ def test_amdsmi_without_libdrm_labels_identically(binary, tmp_path, case, layout
     labels = golden.parse_labels(outs["amdsmi"])
     assert "MI355" in labels["amd.com/gpu.product"]
     assert labels["amd.com/gpu.virtualization-mode"] == "baremetal"
+
+
+@pytest.mark.skipif(not FAKE.exists(), reason="libfake_amdsmi.so not built")
+def test_without_libdrm_or_fru_name_both_backends_use_the_device_model(binary, tmp_path):
+    """No marketing name from amd-smi (no libdrm) and no board FRU
+    product_name attribute: both backends fall back to the model of the PCI
+    device ID, so the product label stays the same."""
+    spec = synth.NodeSpec(gpus=[synth.GpuSpec() for _ in range(2)], seed=24)
+    root = synth.make_node(tmp_path / "root", spec)
+    for f in root.glob("sys/bus/pci/devices/*/product_name"):
+        f.unlink()
+    # No FRU: the board-info call has nothing to report either.
+    fake_spec = (synth.fake_amdsmi_spec(root, spec).replace("\n", "|") +
+                 "|no_libdrm=1|fail=amdsmi_get_gpu_board_info:2")
+    outs = {}
+    for backend in ("sysfs", "amdsmi"):
+        out = tmp_path / f"gfd-{backend}"
+        run_daemon(binary, "--oneshot", "--no-timestamp", f"--backend={backend}", f"--sysfs-root={root}",
+                   f"--machine-type-file={root}/sys/class/dmi/id/product_name", f"--output-file={out}",
+                   env={"GFD_AMDSMI_LIBRARY": str(FAKE), "GFD_FAKE_AMDSMI_SPEC": fake_spec}, check=True)
+        outs[backend] = out.read_text()
+    assert outs["amdsmi"] == outs["sysfs"]
+    assert "MI3" in golden.parse_labels(outs["amdsmi"])["amd.com/gpu.product"]

@@ -387,3 +387,25 @@ def test_runtime_visibility_masks_do_not_hide_gpus(binary, tmp_path, var):
         files[backend] = out.read_text()
     assert files["amdsmi"] == files["sysfs"]
     assert int(golden.parse_labels(files["amdsmi"])["amd.com/gpu.count"]) >= 1
+
+
+def test_daemon_pins_itself_to_one_l3_domain(binary, tmp_path):
+    """On the pool's 2-socket hosts the daemon keeps its threads on the CPUs
+    sharing one L3 cache (util/affinity.h), within the allowed set; with
+    GFD_CPU_AFFINITY=none it does not.  (The daemon is started with every
+    CPU of the box allowed: this test process may itself be pinned by an
+    earlier in-process session.)"""
+    def run(env):
+        def widen():
+            os.sched_setaffinity(0, range(os.cpu_count()))  # the kernel keeps the cgroup's share
+
+        e = {k: v for k, v in os.environ.items() if not k.startswith("GFD_")}
+        e.update(env)
+        return subprocess.run([binary, "--oneshot", "--backend=null", "--output-file="], capture_output=True,
+                              text=True, timeout=60, env=e, preexec_fn=widen, check=True)
+
+    on = run({})
+    lines = [ln for ln in on.stderr.splitlines() if "CPU affinity:" in ln]
+    assert len(lines) == 1, on.stderr[-2000:]
+    assert "sharing cpu" in lines[0] and "L3 cache" in lines[0], lines[0]
+    assert "CPU affinity:" not in run({"GFD_CPU_AFFINITY": "none"}).stderr

@@ -66,6 +66,7 @@ extern "C" int LLVMFuzzerInitialize(int*, char***) {
   for (int n = 1; n <= 8; ++n) gfd::fs::mkdir_all(g_root + "/sys/class/kfd/kfd/topology/nodes/" + std::to_string(n) + "/mem_banks/0");
   gfd::fs::mkdir_all(g_root + "/sys/bus/pci/devices/0000:75:00.0/compute_partition_config/dec");
   gfd::fs::mkdir_all(g_root + "/sys/module/amdgpu");
+  std::atexit([] { gfd::fs::remove_all(g_root); });
   return 0;
 }
 

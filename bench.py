@@ -17,7 +17,10 @@ device value - memory, partition modes, xGMI links, partition
 capabilities, versions, machine type - is read from the driver each step.
 
 The label set of every step is checked for correctness (count == N GPUs,
-gfx950/cdna4 arch, MI355 product, HBM size) before timing is reported.
+gfx950/cdna4 arch, MI355 product, HBM size, valid Kubernetes label syntax)
+before timing is reported.  Like the daemon at start-up, the in-process
+session keeps its threads on the CPUs that share one L3 cache
+(src/util/affinity.h; GFD_CPU_AFFINITY=none to compare).
 
 N>1: launched by the driver as one process per GPU under torch.distributed
 (gloo, 127.0.0.1); rank 0 labels the node restricted to GPUs 0..N-1 (the

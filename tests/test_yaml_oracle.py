@@ -104,7 +104,23 @@ def _check(native, doc, flow, width):
     ("a: &x\n- 1\n- 2\nb: *x\n", {"a": [1, 2], "b": [1, 2]}),
     ("a: !!str 1\nb: !!str 0x10\nd: !!float 3\ne: !!str\nf: !!int '3'\nt: !!str 1.50\n",
      {"a": "1", "b": "0x10", "d": 3.0, "e": "", "f": 3, "t": "1.50"}),
+    # Every double-quoted escape YAML 1.1 defines, 8/16/32-bit code points.
+    ('a: "\\0\\a\\b\\t\\n\\v\\f\\r\\e\\ \\"\\/\\\\\\N\\_\\x41\\u00e9\\U0001F600"\n',
+     {"a": "\0\a\b\t\n\v\f\r\x1b \"/\\\x85\xa0A\u00e9\U0001F600"}),
+    # Tags on other scalars, a BOM, octal and binary ints (YAML 1.1), document end.
+    ("a: !!bool yes\nb: !!null ''\nc: !!float 1\n", {"a": True, "b": None, "c": 1.0}),
+    ("\ufeffa: 1\n", {"a": 1}),
 ])
 def test_pinned_cases(native, text, expected):
     assert native.parse_yaml(text) == expected
     assert yaml.safe_load(text) == expected
+
+
+def test_integer_prefixes_follow_go_yaml_not_pyyaml(native):
+    """Where the reference's parser and PyYAML disagree, go-yaml v2 wins:
+    it resolves plain integers with Go's strconv.ParseInt(s, 0, 64), which
+    (Go >= 1.13; the reference builds with 1.18, versions.mk) reads 0o17 as
+    octal - PyYAML keeps it a string."""
+    text = "a: 0o17\nb: 017\nc: 0b101\nd: 0x1F\n"
+    assert native.parse_yaml(text) == {"a": 15, "b": 15, "c": 5, "d": 31}
+    assert yaml.safe_load(text)["a"] == "0o17"  # the oracle's YAML 1.1 reading differs

@@ -222,7 +222,7 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
     log::printf("Writing labels to output file");
     trace::Span span("write");
     try {
-      lm::write_to_file(r.labels, config.output_file());
+      lm::write_to_file(r.labels, config.output_file(), !config.oneshot());
     } catch (const std::exception& e) {
       throw Error("error writing file '" + config.output_file() + "': " + e.what());
     }

@@ -5,6 +5,8 @@
 #include <sys/vfs.h>
 #include <unistd.h>
 
+#include <mutex>
+#include <optional>
 #include <string>
 
 #include <cerrno>
@@ -14,6 +16,7 @@
 
 #include "util/error.h"
 #include "util/fs.h"
+#include "util/pool.h"
 
 namespace gfd::lm {
 
@@ -150,13 +153,81 @@ std::string render(const Labels& labels) {
   return out;
 }
 
-void write_file_atomically(const std::string& path, const std::string& contents, unsigned perm) {
-  std::string abs = fs::absolute(path);
-  std::string tmp_dir = fs::join(fs::dirname(abs), "gfd-tmp");
+namespace {
+
+// The next cycle's temporary file, created on a worker right after a
+// cycle's rename (write_to_file with prepare_next): the daemon's next write
+// is then write + close + rename, without the ~7 us create - a third of the
+// write on the MI355X hosts (profiles/write_probe.txt) - on its critical
+// path.  The creation overlaps the daemon's sleep (or, back to back, the
+// next cycle's enumeration).  One slot per process, tagged with its
+// directory; a write elsewhere discards it.
+struct PreparedTemp {
+  std::mutex mu;
+  std::optional<WorkerPool::Task> task;  // creating the file
+  std::string dir, name;
+  int fd = -1;
+};
+
+PreparedTemp& prepared() {
+  static auto* p = new PreparedTemp;  // never destroyed: a worker may still use it at exit
+  return *p;
+}
+
+// Waits for (or drops) the creation in flight and returns the prepared file
+// if it is in `tmp_dir`; any other prepared file is removed.
+int take_prepared(const std::string& tmp_dir, std::string* name, bool run_pending) {
+  PreparedTemp& p = prepared();
+  std::optional<WorkerPool::Task> task;
+  {
+    std::lock_guard<std::mutex> lk(p.mu);
+    task.swap(p.task);
+  }
+  if (task) {
+    if (run_pending)
+      task->run_or_wait();
+    else
+      task->cancel_or_wait();
+  }
+  std::lock_guard<std::mutex> lk(p.mu);
+  if (p.fd < 0) return -1;
+  int fd = p.fd;
+  p.fd = -1;
+  if (p.dir != tmp_dir) {
+    ::close(fd);
+    ::unlink(p.name.c_str());
+    return -1;
+  }
+  *name = std::move(p.name);
+  return fd;
+}
+
+void prepare_next(const std::string& tmp_dir, unsigned perm) {
+  PreparedTemp& p = prepared();
+  std::lock_guard<std::mutex> lk(p.mu);
+  if (p.task || p.fd >= 0) return;
+  p.task = WorkerPool::instance().submit([tmp_dir, perm] {
+    std::string name;
+    int fd = create_temp(tmp_dir, perm, &name);  // no mkdir: a missing directory is the next write's business
+    if (fd < 0) return;
+    PreparedTemp& q = prepared();
+    std::lock_guard<std::mutex> lk2(q.mu);
+    q.dir = tmp_dir;
+    q.name = std::move(name);
+    q.fd = fd;
+  });
+}
+
+// One attempt: false (nothing thrown, nothing left behind) when a prepared
+// file vanished before its rename - the caller retries with a fresh one.
+bool write_atomically_once(const std::string& path, const std::string& tmp_dir, const std::string& contents,
+                           unsigned perm, bool use_prepared) {
+  std::string tmpl;
+  int fd = use_prepared ? take_prepared(tmp_dir, &tmpl, true) : -1;
+  bool prepared_fd = fd >= 0;
   // The temporary directory normally exists from the previous cycle: try the
   // create first and make the directory only when it is missing.
-  std::string tmpl;
-  int fd = create_temp(tmp_dir, perm, &tmpl);
+  if (fd < 0) fd = create_temp(tmp_dir, perm, &tmpl);
   if (fd < 0 && errno == ENOENT) {
     try {
       fs::mkdir_all(tmp_dir);
@@ -191,12 +262,36 @@ void write_file_atomically(const std::string& path, const std::string& contents,
   if (::rename(tmpl.c_str(), path.c_str()) != 0) {
     int e = errno;
     ::unlink(tmpl.c_str());
+    // A prepared file removed behind our back (gfd-tmp/ deleted between
+    // cycles): not an error of this cycle.
+    if (prepared_fd && e == ENOENT) return false;
     fs::remove_all(tmp_dir);
     throw Error("error moving temporary file to '" + path + "': " + fs::errno_str(e));
   }
+  return true;
 }
 
-void write_to_file(const Labels& labels, const std::string& path) {
+}  // namespace
+
+void write_file_atomically(const std::string& path, const std::string& contents, unsigned perm, bool prepare) {
+  std::string abs = fs::absolute(path);
+  std::string tmp_dir = fs::join(fs::dirname(abs), "gfd-tmp");
+  if (!write_atomically_once(path, tmp_dir, contents, perm, true))
+    write_atomically_once(path, tmp_dir, contents, perm, false);
+  // GFD_WRITE_PREPARE=never: every write creates its own file (A/B).
+  static const bool never = [] {
+    const char* v = std::getenv("GFD_WRITE_PREPARE");
+    return v && std::string(v) == "never";
+  }();
+  if (prepare && !never) prepare_next(tmp_dir, perm);
+}
+
+void discard_prepared_temp() {
+  std::string unused;
+  take_prepared("", &unused, false);
+}
+
+void write_to_file(const Labels& labels, const std::string& path, bool prepare_next) {
   std::string out = render(labels);
   if (path.empty()) {
     if (fwrite(out.data(), 1, out.size(), stdout) != out.size() || fflush(stdout) != 0)
@@ -204,13 +299,14 @@ void write_to_file(const Labels& labels, const std::string& path) {
     return;
   }
   try {
-    write_file_atomically(path, out, 0644);
+    write_file_atomically(path, out, 0644, prepare_next);
   } catch (const std::exception& e) {
     throw Error("error atomically writing file '" + path + "': " + e.what());
   }
 }
 
 void remove_output_file(const std::string& path) {
+  discard_prepared_temp();
   std::string abs = fs::absolute(path);
   std::string tmp_dir = fs::join(fs::dirname(abs), "gfd-tmp");
   if (int e = fs::remove_all(tmp_dir)) throw Error("failed to remove temporary output directory: " + fs::errno_str(e));

@@ -47,9 +47,15 @@ std::string render(const Labels& labels);
 
 // Write labels to `path` atomically (temp file in <dir>/gfd-tmp, rename,
 // chmod 0644).  An empty path writes to stdout.  Throws gfd::Error.
-void write_to_file(const Labels& labels, const std::string& path);
+// prepare_next (a daemon that will write again): afterwards a worker
+// creates the next write's temporary file, so the next write does not pay
+// the create; the empty file waits in <dir>/gfd-tmp until then.
+void write_to_file(const Labels& labels, const std::string& path, bool prepare_next = false);
 // Atomic write of arbitrary contents (labels.go:68-114).
-void write_file_atomically(const std::string& path, const std::string& contents, unsigned perm);
+void write_file_atomically(const std::string& path, const std::string& contents, unsigned perm,
+                           bool prepare_next = false);
+// Closes and removes a prepared temporary file (waiting for its creation).
+void discard_prepared_temp();
 // Removes <dir>/gfd-tmp and the output file (main.go:212-232).
 void remove_output_file(const std::string& path);
 

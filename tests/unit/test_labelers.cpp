@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <thread>
 
 #include "lm/keys.h"
 #include "lm/labels.h"
@@ -429,6 +430,94 @@ TEST(WriteToFile_RecoversFromABlockedTemporaryDirectory) {
   EXPECT_FALSE(fs::exists(std::string(dir) + "/gfd-tmp"));
   lm::write_to_file({{"k", "v"}}, path);
   EXPECT_EQ(fs::read_file(path).data, std::string("k=v\n"));
+  fs::remove_all(dir);
+}
+
+namespace {
+// The prepared temporary file(s) in <dir>/gfd-tmp once the worker made one.
+std::vector<std::string> wait_prepared(const std::string& dir) {
+  for (int i = 0; i < 2000; ++i) {
+    auto names = fs::list_dir(dir + "/gfd-tmp");
+    if (!names.empty()) return names;
+    std::this_thread::sleep_for(std::chrono::milliseconds(1));
+  }
+  return {};
+}
+}  // namespace
+
+TEST(WriteToFile_PreparesTheNextTemporaryFile) {
+  char dir[] = "/tmp/gfd-write-XXXXXX";
+  EXPECT_TRUE(mkdtemp(dir) != nullptr);
+  std::string path = std::string(dir) + "/gfd";
+  lm::write_to_file({{"k", "1"}}, path, true);
+  auto first = wait_prepared(dir);
+  EXPECT_EQ(first.size(), static_cast<size_t>(1));
+  // The next write consumes it (and prepares another).
+  lm::write_to_file({{"k", "2"}}, path, true);
+  EXPECT_EQ(fs::read_file(path).data, std::string("k=2\n"));
+  auto second = wait_prepared(dir);
+  EXPECT_EQ(second.size(), static_cast<size_t>(1));
+  EXPECT_TRUE(!first.empty() && !second.empty() && first[0] != second[0]);
+  struct stat st;
+  EXPECT_TRUE(stat(path.c_str(), &st) == 0);
+  EXPECT_EQ(static_cast<int>(st.st_mode & 0777), 0644);
+  // Exit: nothing left behind.
+  lm::remove_output_file(path);
+  EXPECT_FALSE(fs::exists(std::string(dir) + "/gfd-tmp"));
+  EXPECT_FALSE(fs::exists(path));
+  fs::remove_all(dir);
+}
+
+TEST(WriteToFile_PreparedFileRemovedBetweenCycles) {
+  // gfd-tmp/ deleted by someone else between two cycles: the write that
+  // finds its prepared file gone writes through a fresh one.
+  char dir[] = "/tmp/gfd-write-XXXXXX";
+  EXPECT_TRUE(mkdtemp(dir) != nullptr);
+  std::string path = std::string(dir) + "/gfd";
+  lm::write_to_file({{"k", "1"}}, path, true);
+  EXPECT_EQ(wait_prepared(dir).size(), static_cast<size_t>(1));
+  fs::remove_all(std::string(dir) + "/gfd-tmp");
+  lm::write_to_file({{"k", "2"}}, path, false);
+  EXPECT_EQ(fs::read_file(path).data, std::string("k=2\n"));
+  EXPECT_EQ(fs::list_dir(std::string(dir) + "/gfd-tmp").size(), static_cast<size_t>(0));
+  fs::remove_all(dir);
+}
+
+TEST(WriteToFile_PreparedFileOfAnotherDirectoryIsDiscarded) {
+  char a[] = "/tmp/gfd-write-XXXXXX", b[] = "/tmp/gfd-write-XXXXXX";
+  EXPECT_TRUE(mkdtemp(a) != nullptr && mkdtemp(b) != nullptr);
+  lm::write_to_file({{"k", "a"}}, std::string(a) + "/gfd", true);
+  EXPECT_EQ(wait_prepared(a).size(), static_cast<size_t>(1));
+  lm::write_to_file({{"k", "b"}}, std::string(b) + "/gfd", false);
+  EXPECT_EQ(fs::read_file(std::string(b) + "/gfd").data, std::string("k=b\n"));
+  EXPECT_EQ(fs::list_dir(std::string(a) + "/gfd-tmp").size(), static_cast<size_t>(0));
+  EXPECT_EQ(fs::list_dir(std::string(b) + "/gfd-tmp").size(), static_cast<size_t>(0));
+  // discard_prepared_temp: the same for a session that ends.
+  lm::write_to_file({{"k", "b2"}}, std::string(b) + "/gfd", true);
+  EXPECT_EQ(wait_prepared(b).size(), static_cast<size_t>(1));
+  lm::discard_prepared_temp();
+  EXPECT_EQ(fs::list_dir(std::string(b) + "/gfd-tmp").size(), static_cast<size_t>(0));
+  fs::remove_all(a);
+  fs::remove_all(b);
+}
+
+TEST(ReadFile_LongFileInFullOrCut) {
+  // Files longer than a page (the procfs PCI table): contents and the
+  // max_bytes cut must be exact.
+  char dir[] = "/tmp/gfd-read-XXXXXX";
+  EXPECT_TRUE(mkdtemp(dir) != nullptr);
+  std::string p = std::string(dir) + "/big";
+  std::string data;
+  for (int i = 0; i < 20000; ++i) data += std::to_string(i) + "\n";
+  {
+    int fd = ::open(p.c_str(), O_CREAT | O_WRONLY, 0644);
+    EXPECT_TRUE(fd >= 0 && ::write(fd, data.data(), data.size()) == static_cast<ssize_t>(data.size()));
+    ::close(fd);
+  }
+  EXPECT_TRUE(fs::read_file(p, 4u << 20).data == data);
+  EXPECT_TRUE(fs::read_file(p, 100000).data == data.substr(0, 100000));
+  EXPECT_TRUE(fs::read_file(p, 4096).data == data.substr(0, 4096));
+  EXPECT_TRUE(fs::read_file(p, 5000).data == data.substr(0, 5000));
   fs::remove_all(dir);
 }
 

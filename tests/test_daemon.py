@@ -93,6 +93,41 @@ def test_loop_rewrites_file_with_constant_timestamp(binary, tmp_path):
     assert not (tmp_path / "gfd-tmp").exists()
 
 
+@pytest.mark.parametrize("prepare", ["default", "never"])
+def test_loop_keeps_one_prepared_temporary_file(binary, tmp_path, prepare):
+    """Loop mode: between cycles gfd-tmp/ holds the next cycle's (empty, 0644)
+    temporary file, which that cycle renames into place; with
+    GFD_WRITE_PREPARE=never it stays empty, as in the reference.  Either way
+    exit removes everything."""
+    out = tmp_path / "gfd"
+    env = {"GFD_WRITE_PREPARE": "never"} if prepare == "never" else None
+    p = _start(binary, ["--sleep-interval=200ms", *_base(tmp_path, out)], env=env)
+    tmp = tmp_path / "gfd-tmp"
+    try:
+        assert _wait_for(out.exists), "first write"
+        if prepare == "default":
+            assert _wait_for(lambda: len(list(tmp.iterdir())) == 1), list(tmp.iterdir())
+            (first,) = tmp.iterdir()
+            st = first.stat()
+            assert st.st_size == 0 and oct(st.st_mode & 0o777) == "0o644"
+            ino = first.stat().st_ino
+            m0 = out.stat().st_mtime_ns
+            assert _wait_for(lambda: out.stat().st_mtime_ns > m0, timeout=5), "file not rewritten"
+            assert out.stat().st_ino == ino  # the prepared file became the feature file
+            assert not first.exists()
+            assert _wait_for(lambda: len(list(tmp.iterdir())) == 1)
+        else:
+            m0 = out.stat().st_mtime_ns
+            assert _wait_for(lambda: out.stat().st_mtime_ns > m0, timeout=5), "file not rewritten"
+            assert list(tmp.iterdir()) == []
+        assert golden.parse_labels(out.read_text())["amd.com/gpu.product"] == "MOCKMODEL"
+    finally:
+        p.send_signal(signal.SIGTERM)
+        p.communicate(timeout=10)
+    assert p.returncode == 0
+    assert not out.exists() and not tmp.exists()
+
+
 @pytest.mark.parametrize("sig,name", [(signal.SIGINT, "interrupt"), (signal.SIGQUIT, "quit")])
 def test_other_signals_exit_cleanly(binary, tmp_path, sig, name):
     out = tmp_path / "gfd"

@@ -9,6 +9,17 @@
 
 namespace gfd::resource {
 
+namespace {
+// amdsmi_get_lib_version's struct, with room to spare: the library being
+// probed may be of another major version, whose struct is laid out
+// differently (older ones started with a `year` field).
+union VersionBuf {
+  amdsmi_version_t v;
+  unsigned char slack[128];
+  VersionBuf() : slack{} {}
+};
+}  // namespace
+
 bool AmdSmiLib::load(std::string* err) {
   const std::string versioned = "libamd_smi.so." + std::to_string(AMDSMI_LIB_VERSION_MAJOR);
   std::vector<std::string> candidates;
@@ -30,8 +41,9 @@ bool AmdSmiLib::load(std::string* err) {
   for (const auto& c : candidates) {
     if (!lib_.open({c})) continue;
     amdsmi_status_t (*lib_version)(amdsmi_version_t*) = nullptr;
-    amdsmi_version_t v{};
-    if (lib_.bind("amdsmi_get_lib_version", lib_version) && lib_version(&v) == AMDSMI_STATUS_SUCCESS &&
+    VersionBuf buf;
+    const amdsmi_version_t& v = buf.v;
+    if (lib_.bind("amdsmi_get_lib_version", lib_version) && lib_version(&buf.v) == AMDSMI_STATUS_SUCCESS &&
         v.major != AMDSMI_LIB_VERSION_MAJOR) {
       mismatch = c + " is amd-smi " + std::to_string(v.major) + "." + std::to_string(v.minor) +
                  ", this build needs major version " + std::to_string(AMDSMI_LIB_VERSION_MAJOR);
@@ -87,8 +99,9 @@ bool has_amdsmi(std::string* reason) {
   }
   if (reason) {
     *reason = "found " + l->path();
-    amdsmi_version_t v{};
-    if (l->get_lib_version && l->get_lib_version(&v) == AMDSMI_STATUS_SUCCESS)
+    VersionBuf buf;
+    const amdsmi_version_t& v = buf.v;
+    if (l->get_lib_version && l->get_lib_version(&buf.v) == AMDSMI_STATUS_SUCCESS)
       *reason += " (amd-smi library " + std::to_string(v.major) + "." + std::to_string(v.minor) + "." +
                  std::to_string(v.release) + ")";
   }

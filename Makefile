@@ -61,8 +61,9 @@ coverage:
 	find build-cov -name '*.gcda' -delete
 	./build-cov/gfd_unit_tests > /dev/null
 	GFD_AMDSMI_LIBRARY=build-cov/libfake_amdsmi.so ./build-cov/gfd_unit_tests > /dev/null
-	# The daemon binary under the Python end-to-end tests adds its own counts.
-	GFD_BINARY=$(CURDIR)/build-cov/gpu-feature-discovery $(PYTHON) -m pytest tests -q -m "not gpu" -p no:cacheprovider
+	# The daemon binary under the Python end-to-end tests and the fuzz-corpus
+	# replays add their own counts.
+	GFD_BINARY=$(CURDIR)/build-cov/gpu-feature-discovery GFD_BUILD_DIR=$(CURDIR)/build-cov $(PYTHON) -m pytest tests -q -m "not gpu" -p no:cacheprovider
 	@for f in src/*/*.cpp; do gcov -n -o build-cov/CMakeFiles/gfdcore.dir/$$f.o $$f 2>/dev/null | \
 	  grep -A1 "^File '.*$$f'" | tail -1 | sed "s|Lines executed:|$$f |"; done | \
 	  awk '{split($$2, p, "%"); n = $$4; hit += p[1] * n / 100; tot += n; print} \

@@ -97,3 +97,56 @@ TEST(Yaml_UnicodeEscapes) {
   Node n = parse("a: \"\\u00b5s \\U0001F600\"\n");
   EXPECT_EQ(n.get("a")->text(), std::string("\xC2\xB5s \xF0\x9F\x98\x80"));
 }
+
+TEST(Yaml_DoubleQuotedEscapesAndFolding) {
+  // Every escape YAML 1.1 defines (values pinned against PyYAML).
+  Node n = parse("a: \"\\0\\a\\b\\t\\n\\v\\f\\r\\e\\ \\\"\\/\\\\\\N\\_\\x41\"\n");
+  EXPECT_EQ(n.get("a")->text(), std::string("\0\a\b\t\n\v\f\r\x1b \"/\\\xC2\x85\xC2\xA0" "A", 18));
+  // A UTF-16 surrogate pair is one code point.
+  EXPECT_EQ(parse("a: \"\\ud83d\\ude00\"\n").get("a")->text(), std::string("\xF0\x9F\x98\x80"));
+  // An escaped line break joins the lines; an unescaped one folds to a space,
+  // an empty line to a newline - in double, single and plain scalars alike.
+  EXPECT_EQ(parse("a: \"x\\\n   y\"\n").get("a")->text(), std::string("xy"));
+  EXPECT_EQ(parse("a: \"one\n  two\n\n  three\"\n").get("a")->text(), std::string("one two\nthree"));
+  EXPECT_EQ(parse("a: 'one\n  two'\n").get("a")->text(), std::string("one two"));
+  EXPECT_EQ(parse("a: plain\n  continued\n  more\n").get("a")->text(), std::string("plain continued more"));
+  EXPECT_THROW_MSG(parse("a: \"\\q\"\n"), "unknown escape character 'q'");
+}
+
+TEST(Yaml_Tags) {
+  Node n = parse("a: !!str 1\nb: !!str true\nc: !!str ~\nd: !!float 2\ne: !!null ''\nf: !!str 1.5\ng: !!int '7'\n"
+                 "h: !!bool 'yes'\n");
+  EXPECT_EQ(to_json(n), std::string("{\"a\":\"1\",\"b\":\"true\",\"c\":\"~\",\"d\":2,\"e\":null,\"f\":\"1.5\",\"g\":7,"
+                                    "\"h\":true}"));
+  EXPECT_TRUE(n.get("d")->kind() == Node::Kind::Float);
+  EXPECT_THROW_MSG(parse("a: !!str {k: v}\n"), "!!str");
+}
+
+TEST(Yaml_FlowCollectionsWithAnchorsTagsAndMerges) {
+  Node n = parse("a: [&x 1, *x, !!str 2, !!float 3, a: 1]\nb: {<<: {m: 1}, k: *x}\nc: {<<: [{p: 1}, {q: 2}]}\n");
+  EXPECT_EQ(to_json(n), std::string("{\"a\":[1,1,\"2\",3,{\"a\":1}],\"b\":{\"k\":1,\"m\":1},\"c\":{\"p\":1,\"q\":2}}"));
+  EXPECT_THROW_MSG(parse("a: [1 2] x\n"), "flow");
+  EXPECT_THROW_MSG(parse("a: {k: v\n"), "flow");
+}
+
+TEST(Yaml_BlockScalarIndicators) {
+  Node n = parse("keep: |+\n  x\n\nnext: >-\n  a\n\n  b\nind: |2\n    deep\n");
+  EXPECT_EQ(n.get("keep")->text(), std::string("x\n\n"));
+  EXPECT_EQ(n.get("next")->text(), std::string("a\nb"));
+  EXPECT_EQ(n.get("ind")->text(), std::string("  deep\n"));
+  EXPECT_THROW_MSG(parse("a: |x\n  y\n"), "invalid block scalar header");
+}
+
+TEST(Yaml_ByteOrderMarkEndMarkerEmptyCollections) {
+  EXPECT_EQ(to_json(parse("\xEF\xBB\xBF" "a: 1\n")), std::string("{\"a\":1}"));
+  EXPECT_EQ(to_json(parse("a: 1\n...\n")), std::string("{\"a\":1}"));
+  EXPECT_EQ(to_json(parse("a: []\nb: {}\n")), std::string("{\"a\":[],\"b\":{}}"));
+  EXPECT_EQ(to_json(parse("- a\n- - b\n  - c\n-\n  d: 1\n")), std::string("[\"a\",[\"b\",\"c\"],{\"d\":1}]"));
+}
+
+TEST(Yaml_IntegerPrefixesAndJsonEscapes) {
+  // go-yaml v2 resolves plain integers with Go's strconv.ParseInt(s, 0, 64):
+  // 0o17 is octal there (PyYAML keeps it a string; tests/test_yaml_oracle.py).
+  EXPECT_EQ(to_json(parse("a: 0o17\nb: 0b101\nc: 017\n")), std::string("{\"a\":15,\"b\":5,\"c\":15}"));
+  EXPECT_EQ(to_json(parse("a: \"q\\\"b\\\\c\\nd\\re\"\n")), std::string("{\"a\":\"q\\\"b\\\\c\\nd\\re\"}"));
+}

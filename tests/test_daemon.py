@@ -371,6 +371,34 @@ def test_auto_backend_oneshot_reads_kfd_without_loading_amdsmi(binary, tmp_path,
     assert "amd-smi platform" not in cp.stderr
 
 
+def test_auto_backend_per_cycle_session_prefers_amdsmi_then_kfd(binary, tmp_path, mi355x_node):
+    """--amdsmi-session=per-cycle: no background start (every cycle pays
+    amdsmi_init anyway); amd-smi first, the KFD topology if its init fails."""
+    root = mi355x_node(n_gpus=2)
+    spec = "bdf=0000:d9:00.0;mode=SPX;parts=1;cus=256;xcds=8;vram_mib=294896;links=7;virt=1"
+    args = ("--backend=auto", "--amdsmi-session=per-cycle", f"--sysfs-root={root}")
+    labels, err = _loop_until(binary, tmp_path / "a", *args, env=_fake_amdsmi_env(spec),
+                              until="Using amd-smi manager, KFD sysfs manager if amd-smi fails to initialize")
+    assert labels["amd.com/gpu.count"] == "1"  # the fake's GPU
+    labels, err = _loop_until(binary, tmp_path / "b", *args, env=_fake_amdsmi_env("init_status=34"),
+                              until="Using amd-smi manager, KFD sysfs manager if amd-smi fails to initialize")
+    assert labels["amd.com/gpu.count"] == "2"  # the tree's GPUs
+    assert "amdsmi_init failed" in err or "failed to initialize" in err
+
+
+def test_auto_backend_without_kfd_topology_uses_amdsmi(binary, tmp_path, mi355x_node):
+    root = mi355x_node(n_gpus=2)
+    kfd = Path(root) / "sys/class/kfd"
+    import shutil
+
+    shutil.rmtree(kfd)
+    spec = "bdf=0000:d9:00.0;mode=SPX;parts=1;cus=256;xcds=8;vram_mib=294896;links=7;virt=1"
+    labels, err = _loop_until(binary, tmp_path / "gfd", "--backend=auto", f"--sysfs-root={root}",
+                              env=_fake_amdsmi_env(spec), until="Using amd-smi manager")
+    assert "Detected non-KFD platform" in err
+    assert labels["amd.com/gpu.count"] == "1"
+
+
 def test_auto_backend_without_kfd_topology_still_fails_on_init_error(binary, tmp_path):
     cp = run_daemon(binary, "--oneshot", "--backend=auto", f"--sysfs-root={tmp_path}", "--output-file=",
                     env=_fake_amdsmi_env("init_status=34"))

@@ -67,7 +67,10 @@ const std::string& root() {
     gfd::fs::mkdir_all(s + "/proc/bus/pci");
     gfd::lm::write_file_atomically(s + "/sys/class/kfd/kfd/topology/nodes/0/properties", "cpu_cores_count 64\n", 0644);
     gfd::lm::write_file_atomically(s + "/sys/bus/pci/devices/0000:75:00.0/vendor", "0x1002\n", 0644);
-    std::atexit([] { gfd::fs::remove_all(root()); });
+    // Not root(): by exit time the static it returns may already be
+    // destroyed (its destructor was registered after this handler).
+    static const std::string* const tree = new std::string(s);
+    std::atexit([] { gfd::fs::remove_all(*tree); });
     return s;
   }();
   return r;

@@ -17,6 +17,7 @@
 #include "util/error.h"
 #include "util/fs.h"
 #include "util/pool.h"
+#include "util/trace.h"
 
 namespace gfd::lm {
 
@@ -223,6 +224,7 @@ void prepare_next(const std::string& tmp_dir, unsigned perm) {
 bool write_atomically_once(const std::string& path, const std::string& tmp_dir, const std::string& contents,
                            unsigned perm, bool use_prepared) {
   std::string tmpl;
+  int64_t t0 = trace::now_ns();
   int fd = use_prepared ? take_prepared(tmp_dir, &tmpl, true) : -1;
   bool prepared_fd = fd >= 0;
   // The temporary directory normally exists from the previous cycle: try the
@@ -247,6 +249,8 @@ bool write_atomically_once(const std::string& path, const std::string& tmp_dir, 
     fs::remove_all(tmp_dir);
     throw Error(msg);
   };
+  int64_t t1 = trace::now_ns();
+  trace::record(prepared_fd ? "write.take" : "write.create", t1 - t0);
   // Best effort: a file system without fallocate(2) just takes the write.
   if (!contents.empty() && wants_prealloc(fd)) (void)::fallocate(fd, 0, 0, static_cast<off_t>(contents.size()));
   if (!write_all(fd, contents)) fail("error writing temporary file '" + tmpl + "': " + fs::errno_str(errno));
@@ -259,6 +263,8 @@ bool write_atomically_once(const std::string& path, const std::string& tmp_dir, 
     fs::remove_all(tmp_dir);
     throw Error("error writing temporary file '" + tmpl + "': " + fs::errno_str(e));
   }
+  int64_t t2 = trace::now_ns();
+  trace::record("write.data", t2 - t1);
   if (::rename(tmpl.c_str(), path.c_str()) != 0) {
     int e = errno;
     ::unlink(tmpl.c_str());
@@ -268,6 +274,7 @@ bool write_atomically_once(const std::string& path, const std::string& tmp_dir, 
     fs::remove_all(tmp_dir);
     throw Error("error moving temporary file to '" + path + "': " + fs::errno_str(e));
   }
+  trace::record("write.rename", trace::now_ns() - t2);
   return true;
 }
 

@@ -161,13 +161,16 @@ namespace {
 // is then write + close + rename, without the ~7 us create - a third of the
 // write on the MI355X hosts (profiles/write_probe.txt) - on its critical
 // path.  The creation overlaps the daemon's sleep (or, back to back, the
-// next cycle's enumeration).  One slot per process, tagged with its
-// directory; a write elsewhere discards it.
+// next cycle's enumeration).  Where the write preallocates (wants_prealloc),
+// the worker also allocates the blocks for the previous file's size beyond
+// EOF (FALLOC_FL_KEEP_SIZE), so the write does not pay that either.  One
+// slot per process, tagged with its directory; a write elsewhere discards it.
 struct PreparedTemp {
   std::mutex mu;
   std::optional<WorkerPool::Task> task;  // creating the file
   std::string dir, name;
   int fd = -1;
+  size_t allocated = 0;  // bytes of blocks preallocated
 };
 
 PreparedTemp& prepared() {
@@ -177,7 +180,7 @@ PreparedTemp& prepared() {
 
 // Waits for (or drops) the creation in flight and returns the prepared file
 // if it is in `tmp_dir`; any other prepared file is removed.
-int take_prepared(const std::string& tmp_dir, std::string* name, bool run_pending) {
+int take_prepared(const std::string& tmp_dir, std::string* name, bool run_pending, size_t* allocated = nullptr) {
   PreparedTemp& p = prepared();
   std::optional<WorkerPool::Task> task;
   {
@@ -200,22 +203,28 @@ int take_prepared(const std::string& tmp_dir, std::string* name, bool run_pendin
     return -1;
   }
   *name = std::move(p.name);
+  if (allocated) *allocated = p.allocated;
   return fd;
 }
 
-void prepare_next(const std::string& tmp_dir, unsigned perm) {
+void prepare_next(const std::string& tmp_dir, unsigned perm, size_t size_hint) {
   PreparedTemp& p = prepared();
   std::lock_guard<std::mutex> lk(p.mu);
   if (p.task || p.fd >= 0) return;
-  p.task = WorkerPool::instance().submit([tmp_dir, perm] {
+  p.task = WorkerPool::instance().submit([tmp_dir, perm, size_hint] {
     std::string name;
     int fd = create_temp(tmp_dir, perm, &name);  // no mkdir: a missing directory is the next write's business
     if (fd < 0) return;
+    size_t allocated = 0;
+    if (size_hint > 0 && wants_prealloc(fd) &&
+        ::fallocate(fd, FALLOC_FL_KEEP_SIZE, 0, static_cast<off_t>(size_hint)) == 0)
+      allocated = size_hint;
     PreparedTemp& q = prepared();
     std::lock_guard<std::mutex> lk2(q.mu);
     q.dir = tmp_dir;
     q.name = std::move(name);
     q.fd = fd;
+    q.allocated = allocated;
   });
 }
 
@@ -224,8 +233,9 @@ void prepare_next(const std::string& tmp_dir, unsigned perm) {
 bool write_atomically_once(const std::string& path, const std::string& tmp_dir, const std::string& contents,
                            unsigned perm, bool use_prepared) {
   std::string tmpl;
+  size_t allocated = 0;
   int64_t t0 = trace::now_ns();
-  int fd = use_prepared ? take_prepared(tmp_dir, &tmpl, true) : -1;
+  int fd = use_prepared ? take_prepared(tmp_dir, &tmpl, true, &allocated) : -1;
   bool prepared_fd = fd >= 0;
   // The temporary directory normally exists from the previous cycle: try the
   // create first and make the directory only when it is missing.
@@ -252,7 +262,8 @@ bool write_atomically_once(const std::string& path, const std::string& tmp_dir, 
   int64_t t1 = trace::now_ns();
   trace::record(prepared_fd ? "write.take" : "write.create", t1 - t0);
   // Best effort: a file system without fallocate(2) just takes the write.
-  if (!contents.empty() && wants_prealloc(fd)) (void)::fallocate(fd, 0, 0, static_cast<off_t>(contents.size()));
+  if (contents.size() > allocated && wants_prealloc(fd))
+    (void)::fallocate(fd, 0, 0, static_cast<off_t>(contents.size()));
   if (!write_all(fd, contents)) fail("error writing temporary file '" + tmpl + "': " + fs::errno_str(errno));
   // Created with `perm` already; chmod only what the umask took away.
   if ((perm & process_umask()) != 0 && ::fchmod(fd, perm) != 0)
@@ -290,7 +301,7 @@ void write_file_atomically(const std::string& path, const std::string& contents,
     const char* v = std::getenv("GFD_WRITE_PREPARE");
     return v && std::string(v) == "never";
   }();
-  if (prepare && !never) prepare_next(tmp_dir, perm);
+  if (prepare && !never) prepare_next(tmp_dir, perm, contents.size());
 }
 
 void discard_prepared_temp() {

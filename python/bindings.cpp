@@ -115,9 +115,9 @@ class Session {
     sriov_ = sriov::new_sriov_lib(config_.sysfs_root());
     timestamp_ = lm::NewTimestampLabeler(config_);
   }
-  // A loop-mode session's writes leave the next cycle's temporary file
-  // prepared (lm::write_to_file); do not leave it behind.
-  ~Session() { lm::discard_prepared_temp(); }
+  // A loop-mode session's cycles leave the next cycle's temporary file
+  // prepared (lm::temp_preparer); do not leave it behind.
+  ~Session() { lm::discard_prepared_temps(); }
   Session(const Session&) = delete;
   Session& operator=(const Session&) = delete;
 

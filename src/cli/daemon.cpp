@@ -165,13 +165,23 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
     std::string m = v ? v : "";
     return m == "split" ? Tasks::split : m == "inline" ? Tasks::inline_ : Tasks::sequence;
   }();
+  // Loop mode: the same worker then creates the temporary file of a later
+  // cycle's write (lm::temp_preparer) - never waited for, so it runs after
+  // the two even if this thread took them over.
+  std::function<void()> prepare_temp;
+  if (write && !config.oneshot()) prepare_temp = lm::temp_preparer(config.output_file());
   WorkerPool::Task facts_task, sriov_task;
   bool facts_done = false;
   if (mode == Tasks::split) {
     facts_task = WorkerPool::instance().submit(read_facts);
     sriov_task = WorkerPool::instance().submit(scan_sriov);
+    if (prepare_temp) WorkerPool::instance().submit(std::move(prepare_temp));
+    prepare_temp = nullptr;
   } else if (mode == Tasks::sequence) {
-    auto seq = WorkerPool::instance().submit_sequence({read_facts, scan_sriov});
+    std::vector<std::function<void()>> fns{read_facts, scan_sriov};
+    if (prepare_temp) fns.push_back(std::move(prepare_temp));
+    prepare_temp = nullptr;
+    auto seq = WorkerPool::instance().submit_sequence(std::move(fns));
     facts_task = seq[0];
     sriov_task = seq[1];
   }
@@ -222,11 +232,12 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
     log::printf("Writing labels to output file");
     trace::Span span("write");
     try {
-      lm::write_to_file(r.labels, config.output_file(), !config.oneshot());
+      lm::write_to_file(r.labels, config.output_file());
     } catch (const std::exception& e) {
       throw Error("error writing file '" + config.output_file() + "': " + e.what());
     }
   }
+  if (prepare_temp) prepare_temp();  // GFD_CYCLE_TASKS=inline: on this thread, after the write
   r.total_ns = trace::now_ns() - t0;
   r.phases = trace::phases();
   return r;

@@ -5,6 +5,9 @@
 #include <sys/vfs.h>
 #include <unistd.h>
 
+#include <condition_variable>
+#include <deque>
+#include <functional>
 #include <mutex>
 #include <optional>
 #include <string>
@@ -156,77 +159,75 @@ std::string render(const Labels& labels) {
 
 namespace {
 
-// The next cycle's temporary file, created on a worker right after a
-// cycle's rename (write_to_file with prepare_next): the daemon's next write
-// is then write + close + rename, without the ~7 us create - a third of the
-// write on the MI355X hosts (profiles/write_probe.txt) - on its critical
-// path.  The creation overlaps the daemon's sleep (or, back to back, the
-// next cycle's enumeration).  Where the write preallocates (wants_prealloc),
-// the worker also allocates the blocks for the previous file's size beyond
-// EOF (FALLOC_FL_KEEP_SIZE), so the write does not pay that either.  One
-// slot per process, tagged with its directory; a write elsewhere discards it.
-struct PreparedTemp {
-  std::mutex mu;
-  std::optional<WorkerPool::Task> task;  // creating the file
+// Temporary files created ahead of the writes that use them (loop mode):
+// the daemon's cycle hands temp_preparer()'s job to the worker that already
+// runs its node facts and SR-IOV scan, after those, so the next cycle's file
+// is created - and, where the write preallocates (wants_prealloc), its blocks
+// allocated beyond EOF for the last size (FALLOC_FL_KEEP_SIZE) - while this
+// cycle enumerates and writes.  A write then is write + close + rename; the
+// ~7 us create plus allocation (more on some hosts' overlayfs) are off its
+// critical path (profiles/write_prepare_ab.txt).  At most kMaxPrepared files
+// are ready or being made; a write takes the oldest in its directory and
+// creates its own when none is ready, never waiting for a worker.
+constexpr size_t kMaxPrepared = 2;
+
+struct Prepared {
   std::string dir, name;
   int fd = -1;
   size_t allocated = 0;  // bytes of blocks preallocated
 };
 
-PreparedTemp& prepared() {
-  static auto* p = new PreparedTemp;  // never destroyed: a worker may still use it at exit
+struct PreparedTemps {
+  std::mutex mu;
+  std::condition_variable cv;  // in_flight dropped
+  std::deque<Prepared> ready;
+  size_t in_flight = 0;  // preparer jobs handed out and not yet finished or dropped
+  size_t last_size = 0;  // of the last write: the next file's preallocation
+};
+
+PreparedTemps& prepared() {
+  static auto* p = new PreparedTemps;  // never destroyed: a worker may still use it at exit
   return *p;
 }
 
-// Waits for (or drops) the creation in flight and returns the prepared file
-// if it is in `tmp_dir`; any other prepared file is removed.
-int take_prepared(const std::string& tmp_dir, std::string* name, bool run_pending, size_t* allocated = nullptr) {
-  PreparedTemp& p = prepared();
-  std::optional<WorkerPool::Task> task;
-  {
-    std::lock_guard<std::mutex> lk(p.mu);
-    task.swap(p.task);
-  }
-  if (task) {
-    if (run_pending)
-      task->run_or_wait();
-    else
-      task->cancel_or_wait();
-  }
-  std::lock_guard<std::mutex> lk(p.mu);
-  if (p.fd < 0) return -1;
-  int fd = p.fd;
-  p.fd = -1;
-  if (p.dir != tmp_dir) {
-    ::close(fd);
-    ::unlink(p.name.c_str());
-    return -1;
-  }
-  *name = std::move(p.name);
-  if (allocated) *allocated = p.allocated;
-  return fd;
+void drop(Prepared& f) {
+  ::close(f.fd);
+  ::unlink(f.name.c_str());
 }
 
-void prepare_next(const std::string& tmp_dir, unsigned perm, size_t size_hint) {
-  PreparedTemp& p = prepared();
+// The oldest prepared file in `tmp_dir` (fd, name and preallocation), or -1;
+// prepared files of other directories are removed.
+int take_prepared(const std::string& tmp_dir, std::string* name, size_t* allocated) {
+  PreparedTemps& p = prepared();
   std::lock_guard<std::mutex> lk(p.mu);
-  if (p.task || p.fd >= 0) return;
-  p.task = WorkerPool::instance().submit([tmp_dir, perm, size_hint] {
-    std::string name;
-    int fd = create_temp(tmp_dir, perm, &name);  // no mkdir: a missing directory is the next write's business
-    if (fd < 0) return;
-    size_t allocated = 0;
-    if (size_hint > 0 && wants_prealloc(fd) &&
-        ::fallocate(fd, FALLOC_FL_KEEP_SIZE, 0, static_cast<off_t>(size_hint)) == 0)
-      allocated = size_hint;
-    PreparedTemp& q = prepared();
-    std::lock_guard<std::mutex> lk2(q.mu);
-    q.dir = tmp_dir;
-    q.name = std::move(name);
-    q.fd = fd;
-    q.allocated = allocated;
-  });
+  while (!p.ready.empty()) {
+    Prepared f = std::move(p.ready.front());
+    p.ready.pop_front();
+    if (f.dir != tmp_dir) {
+      drop(f);
+      continue;
+    }
+    *name = std::move(f.name);
+    *allocated = f.allocated;
+    return f.fd;
+  }
+  return -1;
 }
+
+// Counts a handed-out preparer job until it has run (finish) or was
+// dropped unrun (the job, and with it this ticket, destroyed).
+struct InFlight {
+  bool finished = false;
+  void finish() {
+    PreparedTemps& p = prepared();
+    std::lock_guard<std::mutex> lk(p.mu);
+    if (finished) return;
+    finished = true;
+    --p.in_flight;
+    p.cv.notify_all();
+  }
+  ~InFlight() { finish(); }
+};
 
 // One attempt: false (nothing thrown, nothing left behind) when a prepared
 // file vanished before its rename - the caller retries with a fresh one.
@@ -235,7 +236,7 @@ bool write_atomically_once(const std::string& path, const std::string& tmp_dir, 
   std::string tmpl;
   size_t allocated = 0;
   int64_t t0 = trace::now_ns();
-  int fd = use_prepared ? take_prepared(tmp_dir, &tmpl, true, &allocated) : -1;
+  int fd = use_prepared ? take_prepared(tmp_dir, &tmpl, &allocated) : -1;
   bool prepared_fd = fd >= 0;
   // The temporary directory normally exists from the previous cycle: try the
   // create first and make the directory only when it is missing.
@@ -291,25 +292,63 @@ bool write_atomically_once(const std::string& path, const std::string& tmp_dir, 
 
 }  // namespace
 
-void write_file_atomically(const std::string& path, const std::string& contents, unsigned perm, bool prepare) {
+void write_file_atomically(const std::string& path, const std::string& contents, unsigned perm) {
   std::string abs = fs::absolute(path);
   std::string tmp_dir = fs::join(fs::dirname(abs), "gfd-tmp");
   if (!write_atomically_once(path, tmp_dir, contents, perm, true))
     write_atomically_once(path, tmp_dir, contents, perm, false);
+  PreparedTemps& p = prepared();
+  std::lock_guard<std::mutex> lk(p.mu);
+  p.last_size = contents.size();
+}
+
+std::function<void()> temp_preparer(const std::string& path) {
   // GFD_WRITE_PREPARE=never: every write creates its own file (A/B).
   static const bool never = [] {
     const char* v = std::getenv("GFD_WRITE_PREPARE");
     return v && std::string(v) == "never";
   }();
-  if (prepare && !never) prepare_next(tmp_dir, perm, contents.size());
+  if (never || path.empty()) return {};
+  std::string tmp_dir = fs::join(fs::dirname(fs::absolute(path)), "gfd-tmp");
+  PreparedTemps& p = prepared();
+  size_t hint;
+  {
+    std::lock_guard<std::mutex> lk(p.mu);
+    size_t have = p.in_flight;
+    for (const auto& f : p.ready) have += f.dir == tmp_dir;
+    if (have >= kMaxPrepared) return {};
+    ++p.in_flight;
+    hint = p.last_size;
+  }
+  auto ticket = std::make_shared<InFlight>();
+  return [tmp_dir, hint, ticket] {
+    Prepared f;
+    f.dir = tmp_dir;
+    // No mkdir: a missing directory is the next write's business.
+    f.fd = create_temp(tmp_dir, 0644, &f.name);
+    if (f.fd >= 0) {
+      if (hint > 0 && wants_prealloc(f.fd) &&
+          ::fallocate(f.fd, FALLOC_FL_KEEP_SIZE, 0, static_cast<off_t>(hint)) == 0)
+        f.allocated = hint;
+      PreparedTemps& q = prepared();
+      std::lock_guard<std::mutex> lk(q.mu);
+      q.ready.push_back(std::move(f));
+    }
+    ticket->finish();
+  };
 }
 
-void discard_prepared_temp() {
-  std::string unused;
-  take_prepared("", &unused, false);
+void discard_prepared_temps() {
+  PreparedTemps& p = prepared();
+  std::unique_lock<std::mutex> lk(p.mu);
+  // A job handed out runs soon (or is dropped): its file must not outlive
+  // this call.
+  p.cv.wait(lk, [&] { return p.in_flight == 0; });
+  for (auto& f : p.ready) drop(f);
+  p.ready.clear();
 }
 
-void write_to_file(const Labels& labels, const std::string& path, bool prepare_next) {
+void write_to_file(const Labels& labels, const std::string& path) {
   std::string out = render(labels);
   if (path.empty()) {
     if (fwrite(out.data(), 1, out.size(), stdout) != out.size() || fflush(stdout) != 0)
@@ -317,14 +356,14 @@ void write_to_file(const Labels& labels, const std::string& path, bool prepare_n
     return;
   }
   try {
-    write_file_atomically(path, out, 0644, prepare_next);
+    write_file_atomically(path, out, 0644);
   } catch (const std::exception& e) {
     throw Error("error atomically writing file '" + path + "': " + e.what());
   }
 }
 
 void remove_output_file(const std::string& path) {
-  discard_prepared_temp();
+  discard_prepared_temps();
   std::string abs = fs::absolute(path);
   std::string tmp_dir = fs::join(fs::dirname(abs), "gfd-tmp");
   if (int e = fs::remove_all(tmp_dir)) throw Error("failed to remove temporary output directory: " + fs::errno_str(e));

@@ -13,6 +13,7 @@
 //     spaces, so a DMI string like "Server (X)" would be rejected by NFD.
 #pragma once
 
+#include <functional>
 #include <map>
 #include <memory>
 #include <string>
@@ -46,16 +47,19 @@ LabelerPtr merge(std::vector<LabelerPtr> labelers);
 std::string render(const Labels& labels);
 
 // Write labels to `path` atomically (temp file in <dir>/gfd-tmp, rename,
-// chmod 0644).  An empty path writes to stdout.  Throws gfd::Error.
-// prepare_next (a daemon that will write again): afterwards a worker
-// creates the next write's temporary file, so the next write does not pay
-// the create; the empty file waits in <dir>/gfd-tmp until then.
-void write_to_file(const Labels& labels, const std::string& path, bool prepare_next = false);
+// chmod 0644).  An empty path writes to stdout.  Throws gfd::Error.  A
+// temporary file prepared by temp_preparer()'s job is used if one is ready.
+void write_to_file(const Labels& labels, const std::string& path);
 // Atomic write of arbitrary contents (labels.go:68-114).
-void write_file_atomically(const std::string& path, const std::string& contents, unsigned perm,
-                           bool prepare_next = false);
-// Closes and removes a prepared temporary file (waiting for its creation).
-void discard_prepared_temp();
+void write_file_atomically(const std::string& path, const std::string& contents, unsigned perm);
+// Loop mode: a job that creates the temporary file of a later write to
+// `path` (blocks preallocated for the last written size where the write
+// preallocates), for a worker to run while a cycle enumerates; empty when
+// enough files are prepared or GFD_WRITE_PREPARE=never.  The empty files
+// wait in <dir>/gfd-tmp until used.
+std::function<void()> temp_preparer(const std::string& path);
+// Waits for handed-out jobs, then closes and removes every prepared file.
+void discard_prepared_temps();
 // Removes <dir>/gfd-tmp and the output file (main.go:212-232).
 void remove_output_file(const std::string& path);
 

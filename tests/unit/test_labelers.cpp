@@ -434,36 +434,38 @@ TEST(WriteToFile_RecoversFromABlockedTemporaryDirectory) {
 }
 
 namespace {
-// The prepared temporary file(s) in <dir>/gfd-tmp once the worker made one.
-std::vector<std::string> wait_prepared(const std::string& dir) {
-  for (int i = 0; i < 2000; ++i) {
-    auto names = fs::list_dir(dir + "/gfd-tmp");
-    if (!names.empty()) return names;
-    std::this_thread::sleep_for(std::chrono::milliseconds(1));
-  }
-  return {};
+// What the daemon's cycle does: run the preparer job (here inline), write.
+void prepare_then_write(const Labels& l, const std::string& path) {
+  if (auto job = lm::temp_preparer(path)) job();
+  lm::write_to_file(l, path);
 }
 }  // namespace
 
-TEST(WriteToFile_PreparesTheNextTemporaryFile) {
+TEST(WriteToFile_UsesPreparedTemporaryFiles) {
   char dir[] = "/tmp/gfd-write-XXXXXX";
   EXPECT_TRUE(mkdtemp(dir) != nullptr);
-  std::string path = std::string(dir) + "/gfd";
-  lm::write_to_file({{"k", "1"}}, path, true);
-  auto first = wait_prepared(dir);
-  EXPECT_EQ(first.size(), static_cast<size_t>(1));
-  // The next write consumes it (and prepares another).
-  lm::write_to_file({{"k", "2"}}, path, true);
-  EXPECT_EQ(fs::read_file(path).data, std::string("k=2\n"));
-  auto second = wait_prepared(dir);
-  EXPECT_EQ(second.size(), static_cast<size_t>(1));
-  EXPECT_TRUE(!first.empty() && !second.empty() && first[0] != second[0]);
+  std::string path = std::string(dir) + "/gfd", tmp = std::string(dir) + "/gfd-tmp";
+  lm::write_to_file({{"k", "0"}}, path);  // creates gfd-tmp/
+  // At most two are prepared ahead.
+  for (int i = 0; i < 3; ++i)
+    if (auto job = lm::temp_preparer(path)) job();
+  auto ready = fs::list_dir(tmp);
+  EXPECT_EQ(ready.size(), static_cast<size_t>(2));
   struct stat st;
+  EXPECT_TRUE(stat((tmp + "/" + ready[0]).c_str(), &st) == 0);
+  EXPECT_EQ(static_cast<long>(st.st_size), 0L);
+  EXPECT_EQ(static_cast<int>(st.st_mode & 0777), 0644);
+  // A write takes one of them: its inode becomes the feature file.
+  lm::write_to_file({{"k", "1"}}, path);
+  EXPECT_EQ(fs::read_file(path).data, std::string("k=1\n"));
+  auto left = fs::list_dir(tmp);
+  EXPECT_EQ(left.size(), static_cast<size_t>(1));
+  EXPECT_TRUE(left.size() == 1 && (left[0] == ready[0] || left[0] == ready[1]));
   EXPECT_TRUE(stat(path.c_str(), &st) == 0);
   EXPECT_EQ(static_cast<int>(st.st_mode & 0777), 0644);
   // Exit: nothing left behind.
   lm::remove_output_file(path);
-  EXPECT_FALSE(fs::exists(std::string(dir) + "/gfd-tmp"));
+  EXPECT_FALSE(fs::exists(tmp));
   EXPECT_FALSE(fs::exists(path));
   fs::remove_all(dir);
 }
@@ -476,11 +478,12 @@ TEST(WriteToFile_PreparedReplaceKeepsExactContentsAndStaysFast) {
   char dir[] = "/tmp/gfd-write-XXXXXX";
   EXPECT_TRUE(mkdtemp(dir) != nullptr);
   std::string path = std::string(dir) + "/gfd";
-  lm::write_to_file({{"k", std::string(5000, 'v')}}, path, true);
+  prepare_then_write({{"k", std::string(5000, 'v')}}, path);
   std::vector<double> us;
   for (int i = 0; i < 9; ++i) {
+    if (auto job = lm::temp_preparer(path)) job();
     auto t0 = std::chrono::steady_clock::now();
-    lm::write_to_file({{"k", std::to_string(i)}}, path, true);
+    lm::write_to_file({{"k", std::to_string(i)}}, path);
     us.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
     EXPECT_EQ(fs::read_file(path).data, "k=" + std::to_string(i) + "\n");
   }
@@ -499,10 +502,11 @@ TEST(WriteToFile_PreparedFileRemovedBetweenCycles) {
   char dir[] = "/tmp/gfd-write-XXXXXX";
   EXPECT_TRUE(mkdtemp(dir) != nullptr);
   std::string path = std::string(dir) + "/gfd";
-  lm::write_to_file({{"k", "1"}}, path, true);
-  EXPECT_EQ(wait_prepared(dir).size(), static_cast<size_t>(1));
+  prepare_then_write({{"k", "1"}}, path);
+  if (auto job = lm::temp_preparer(path)) job();
+  EXPECT_EQ(fs::list_dir(std::string(dir) + "/gfd-tmp").size(), static_cast<size_t>(1));
   fs::remove_all(std::string(dir) + "/gfd-tmp");
-  lm::write_to_file({{"k", "2"}}, path, false);
+  lm::write_to_file({{"k", "2"}}, path);
   EXPECT_EQ(fs::read_file(path).data, std::string("k=2\n"));
   EXPECT_EQ(fs::list_dir(std::string(dir) + "/gfd-tmp").size(), static_cast<size_t>(0));
   fs::remove_all(dir);
@@ -511,17 +515,29 @@ TEST(WriteToFile_PreparedFileRemovedBetweenCycles) {
 TEST(WriteToFile_PreparedFileOfAnotherDirectoryIsDiscarded) {
   char a[] = "/tmp/gfd-write-XXXXXX", b[] = "/tmp/gfd-write-XXXXXX";
   EXPECT_TRUE(mkdtemp(a) != nullptr && mkdtemp(b) != nullptr);
-  lm::write_to_file({{"k", "a"}}, std::string(a) + "/gfd", true);
-  EXPECT_EQ(wait_prepared(a).size(), static_cast<size_t>(1));
-  lm::write_to_file({{"k", "b"}}, std::string(b) + "/gfd", false);
-  EXPECT_EQ(fs::read_file(std::string(b) + "/gfd").data, std::string("k=b\n"));
+  std::string pa = std::string(a) + "/gfd", pb = std::string(b) + "/gfd";
+  lm::write_to_file({{"k", "a"}}, pa);
+  if (auto job = lm::temp_preparer(pa)) job();
+  EXPECT_EQ(fs::list_dir(std::string(a) + "/gfd-tmp").size(), static_cast<size_t>(1));
+  lm::write_to_file({{"k", "b"}}, pb);
+  EXPECT_EQ(fs::read_file(pb).data, std::string("k=b\n"));
   EXPECT_EQ(fs::list_dir(std::string(a) + "/gfd-tmp").size(), static_cast<size_t>(0));
   EXPECT_EQ(fs::list_dir(std::string(b) + "/gfd-tmp").size(), static_cast<size_t>(0));
-  // discard_prepared_temp: the same for a session that ends.
-  lm::write_to_file({{"k", "b2"}}, std::string(b) + "/gfd", true);
-  EXPECT_EQ(wait_prepared(b).size(), static_cast<size_t>(1));
-  lm::discard_prepared_temp();
+  // discard_prepared_temps: the same for a session that ends - including a
+  // job handed out but not run yet, which it waits for.
+  if (auto job = lm::temp_preparer(pb)) job();
+  auto pending = lm::temp_preparer(pb);
+  EXPECT_TRUE(static_cast<bool>(pending));
+  std::thread t([job = std::move(pending)] {
+    std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    job();
+  });
+  lm::discard_prepared_temps();
+  t.join();
   EXPECT_EQ(fs::list_dir(std::string(b) + "/gfd-tmp").size(), static_cast<size_t>(0));
+  // A job dropped unrun does not hold discard up.
+  { auto dropped = lm::temp_preparer(pb); }
+  lm::discard_prepared_temps();
   fs::remove_all(a);
   fs::remove_all(b);
 }

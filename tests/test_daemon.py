@@ -95,7 +95,7 @@ def test_loop_rewrites_file_with_constant_timestamp(binary, tmp_path):
 
 @pytest.mark.parametrize("prepare", ["default", "never"])
 def test_loop_keeps_one_prepared_temporary_file(binary, tmp_path, prepare):
-    """Loop mode: between cycles gfd-tmp/ holds the next cycle's (empty, 0644)
+    """Loop mode: between cycles gfd-tmp/ holds a later cycle's (empty, 0644)
     temporary file, which that cycle renames into place; with
     GFD_WRITE_PREPARE=never it stays empty, as in the reference.  Either way
     exit removes everything."""

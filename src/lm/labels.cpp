@@ -183,6 +183,7 @@ struct PreparedTemps {
   std::deque<Prepared> ready;
   size_t in_flight = 0;  // preparer jobs handed out and not yet finished or dropped
   size_t last_size = 0;  // of the last write: the next file's preallocation
+  size_t serial = 0;     // preparer jobs handed out so far (picks the subdirectory)
 };
 
 PreparedTemps& prepared() {
@@ -311,7 +312,7 @@ std::function<void()> temp_preparer(const std::string& path) {
   if (never || path.empty()) return {};
   std::string tmp_dir = fs::join(fs::dirname(fs::absolute(path)), "gfd-tmp");
   PreparedTemps& p = prepared();
-  size_t hint;
+  size_t hint, serial;
   {
     std::lock_guard<std::mutex> lk(p.mu);
     size_t have = p.in_flight;
@@ -319,13 +320,20 @@ std::function<void()> temp_preparer(const std::string& path) {
     if (have >= kMaxPrepared) return {};
     ++p.in_flight;
     hint = p.last_size;
+    serial = p.serial++;
   }
   auto ticket = std::make_shared<InFlight>();
-  return [tmp_dir, hint, ticket] {
+  return [tmp_dir, hint, serial, ticket] {
     Prepared f;
     f.dir = tmp_dir;
-    // No mkdir: a missing directory is the next write's business.
-    f.fd = create_temp(tmp_dir, 0644, &f.name);
+    // In one of two subdirectories, alternately: the file the write renames
+    // out of gfd-tmp/<x>/ was made a cycle earlier in the other one, so this
+    // create (tens of us on some overlayfs hosts) does not hold the directory
+    // lock that rename needs (profiles/write_prepare_ab.txt).  gfd-tmp/
+    // itself is not re-created: a missing one is the next write's business.
+    std::string sub = tmp_dir + (serial % 2 ? "/b" : "/a");
+    f.fd = create_temp(sub, 0644, &f.name);
+    if (f.fd < 0 && errno == ENOENT && ::mkdir(sub.c_str(), 0755) == 0) f.fd = create_temp(sub, 0644, &f.name);
     if (f.fd >= 0) {
       if (hint > 0 && wants_prealloc(f.fd) &&
           ::fallocate(f.fd, FALLOC_FL_KEEP_SIZE, 0, static_cast<off_t>(hint)) == 0)

@@ -93,12 +93,16 @@ def test_loop_rewrites_file_with_constant_timestamp(binary, tmp_path):
     assert not (tmp_path / "gfd-tmp").exists()
 
 
+def _prepared(tmp: Path) -> list[Path]:
+    return sorted(f for sub in ("a", "b") if (tmp / sub).is_dir() for f in (tmp / sub).iterdir())
+
+
 @pytest.mark.parametrize("prepare", ["default", "never"])
-def test_loop_keeps_one_prepared_temporary_file(binary, tmp_path, prepare):
-    """Loop mode: between cycles gfd-tmp/ holds a later cycle's (empty, 0644)
-    temporary file, which that cycle renames into place; with
-    GFD_WRITE_PREPARE=never it stays empty, as in the reference.  Either way
-    exit removes everything."""
+def test_loop_keeps_prepared_temporary_files(binary, tmp_path, prepare):
+    """Loop mode: between cycles gfd-tmp/{a,b}/ hold one or two (empty, 0644)
+    temporary files made for later cycles, which those cycles rename into
+    place; with GFD_WRITE_PREPARE=never gfd-tmp/ stays empty, as in the
+    reference.  Either way exit removes everything."""
     out = tmp_path / "gfd"
     env = {"GFD_WRITE_PREPARE": "never"} if prepare == "never" else None
     p = _start(binary, ["--sleep-interval=200ms", *_base(tmp_path, out)], env=env)
@@ -106,16 +110,16 @@ def test_loop_keeps_one_prepared_temporary_file(binary, tmp_path, prepare):
     try:
         assert _wait_for(out.exists), "first write"
         if prepare == "default":
-            assert _wait_for(lambda: len(list(tmp.iterdir())) == 1), list(tmp.iterdir())
-            (first,) = tmp.iterdir()
-            st = first.stat()
-            assert st.st_size == 0 and oct(st.st_mode & 0o777) == "0o644"
-            ino = first.stat().st_ino
+            assert _wait_for(lambda: 1 <= len(_prepared(tmp)) <= 2), _prepared(tmp)
+            ready = _prepared(tmp)
+            for f in ready:
+                st = f.stat()
+                assert st.st_size == 0 and oct(st.st_mode & 0o777) == "0o644"
+            inos = {f.stat().st_ino for f in ready}
             m0 = out.stat().st_mtime_ns
             assert _wait_for(lambda: out.stat().st_mtime_ns > m0, timeout=5), "file not rewritten"
-            assert out.stat().st_ino == ino  # the prepared file became the feature file
-            assert not first.exists()
-            assert _wait_for(lambda: len(list(tmp.iterdir())) == 1)
+            assert out.stat().st_ino in inos  # a prepared file became the feature file
+            assert _wait_for(lambda: 1 <= len(_prepared(tmp)) <= 2)
         else:
             m0 = out.stat().st_mtime_ns
             assert _wait_for(lambda: out.stat().st_mtime_ns > m0, timeout=5), "file not rewritten"

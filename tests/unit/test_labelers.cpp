@@ -439,6 +439,13 @@ void prepare_then_write(const Labels& l, const std::string& path) {
   if (auto job = lm::temp_preparer(path)) job();
   lm::write_to_file(l, path);
 }
+// Prepared files: gfd-tmp/{a,b}/gfd-XXXXXX.
+std::vector<std::string> prepared_files(const std::string& dir) {
+  std::vector<std::string> out;
+  for (const char* sub : {"/gfd-tmp/a", "/gfd-tmp/b"})
+    for (const auto& n : fs::list_dir(dir + sub)) out.push_back(dir + sub + "/" + n);
+  return out;
+}
 }  // namespace
 
 TEST(WriteToFile_UsesPreparedTemporaryFiles) {
@@ -449,16 +456,19 @@ TEST(WriteToFile_UsesPreparedTemporaryFiles) {
   // At most two are prepared ahead.
   for (int i = 0; i < 3; ++i)
     if (auto job = lm::temp_preparer(path)) job();
-  auto ready = fs::list_dir(tmp);
+  auto ready = prepared_files(dir);
   EXPECT_EQ(ready.size(), static_cast<size_t>(2));
+  // One in each subdirectory (a write renames out of one while the next is
+  // made in the other).
+  EXPECT_EQ(fs::list_dir(tmp + "/a").size(), static_cast<size_t>(1));
   struct stat st;
-  EXPECT_TRUE(stat((tmp + "/" + ready[0]).c_str(), &st) == 0);
+  EXPECT_TRUE(stat(ready[0].c_str(), &st) == 0);
   EXPECT_EQ(static_cast<long>(st.st_size), 0L);
   EXPECT_EQ(static_cast<int>(st.st_mode & 0777), 0644);
   // A write takes one of them: its inode becomes the feature file.
   lm::write_to_file({{"k", "1"}}, path);
   EXPECT_EQ(fs::read_file(path).data, std::string("k=1\n"));
-  auto left = fs::list_dir(tmp);
+  auto left = prepared_files(dir);
   EXPECT_EQ(left.size(), static_cast<size_t>(1));
   EXPECT_TRUE(left.size() == 1 && (left[0] == ready[0] || left[0] == ready[1]));
   EXPECT_TRUE(stat(path.c_str(), &st) == 0);
@@ -504,11 +514,15 @@ TEST(WriteToFile_PreparedFileRemovedBetweenCycles) {
   std::string path = std::string(dir) + "/gfd";
   prepare_then_write({{"k", "1"}}, path);
   if (auto job = lm::temp_preparer(path)) job();
-  EXPECT_EQ(fs::list_dir(std::string(dir) + "/gfd-tmp").size(), static_cast<size_t>(1));
+  EXPECT_EQ(prepared_files(dir).size(), static_cast<size_t>(1));
   fs::remove_all(std::string(dir) + "/gfd-tmp");
   lm::write_to_file({{"k", "2"}}, path);
   EXPECT_EQ(fs::read_file(path).data, std::string("k=2\n"));
-  EXPECT_EQ(fs::list_dir(std::string(dir) + "/gfd-tmp").size(), static_cast<size_t>(0));
+  EXPECT_EQ(prepared_files(dir).size(), static_cast<size_t>(0));
+  // The preparer does not re-create a removed gfd-tmp/ on its own.
+  fs::remove_all(std::string(dir) + "/gfd-tmp");
+  if (auto job = lm::temp_preparer(path)) job();
+  EXPECT_FALSE(fs::exists(std::string(dir) + "/gfd-tmp"));
   fs::remove_all(dir);
 }
 
@@ -518,11 +532,11 @@ TEST(WriteToFile_PreparedFileOfAnotherDirectoryIsDiscarded) {
   std::string pa = std::string(a) + "/gfd", pb = std::string(b) + "/gfd";
   lm::write_to_file({{"k", "a"}}, pa);
   if (auto job = lm::temp_preparer(pa)) job();
-  EXPECT_EQ(fs::list_dir(std::string(a) + "/gfd-tmp").size(), static_cast<size_t>(1));
+  EXPECT_EQ(prepared_files(a).size(), static_cast<size_t>(1));
   lm::write_to_file({{"k", "b"}}, pb);
   EXPECT_EQ(fs::read_file(pb).data, std::string("k=b\n"));
-  EXPECT_EQ(fs::list_dir(std::string(a) + "/gfd-tmp").size(), static_cast<size_t>(0));
-  EXPECT_EQ(fs::list_dir(std::string(b) + "/gfd-tmp").size(), static_cast<size_t>(0));
+  EXPECT_EQ(prepared_files(a).size(), static_cast<size_t>(0));
+  EXPECT_EQ(prepared_files(b).size(), static_cast<size_t>(0));
   // discard_prepared_temps: the same for a session that ends - including a
   // job handed out but not run yet, which it waits for.
   if (auto job = lm::temp_preparer(pb)) job();
@@ -534,7 +548,7 @@ TEST(WriteToFile_PreparedFileOfAnotherDirectoryIsDiscarded) {
   });
   lm::discard_prepared_temps();
   t.join();
-  EXPECT_EQ(fs::list_dir(std::string(b) + "/gfd-tmp").size(), static_cast<size_t>(0));
+  EXPECT_EQ(prepared_files(b).size(), static_cast<size_t>(0));
   // A job dropped unrun does not hold discard up.
   { auto dropped = lm::temp_preparer(pb); }
   lm::discard_prepared_temps();

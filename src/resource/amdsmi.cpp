@@ -730,26 +730,20 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
   // same lane.  (Two passes - all attribute attempts, then the library
   // fallbacks - left the second pass's helper lanes queued behind the first
   // pass's, so its items ran mostly serially on the caller: 8 GPUs 0.94 ms
-  // instead of 0.22 ms over the latency-modelled fake.)  Lanes: two GPUs per
-  // lane while every GPU took the attribute path last cycle - on one thread
-  // a cycle after the daemon's sleep runs on a cold, down-clocked core
-  // (8 GPUs' reads: 170 us serial vs 36 us on four lanes), while back to back
-  // the pool only adds fan-out (26 us serial, 32 us on four lanes) -
-  // profiles/multi_gpu_read_probe.txt; one GPU per lane otherwise.
+  // instead of 0.22 ms over the latency-modelled fake.)  Lanes: one GPU per
+  // lane (gpu_lanes: a cycle after the daemon's sleep runs on cold,
+  // down-clocked cores - 8 GPUs' reads 170 us on one thread vs 36 us on four
+  // lanes, profiles/multi_gpu_read_probe.txt - and with the pinned pool one
+  // GPU per lane is also fastest back to back).
   int64_t t_gpus = trace::now_ns();
-  std::vector<char> fast_ok(gpus.size(), 0);
-  size_t lanes = opts_.threads > 0 ? static_cast<size_t>(opts_.threads) : gpu_lanes(gpus.size(), all_fast_);
+  size_t lanes = opts_.threads > 0 ? static_cast<size_t>(opts_.threads) : gpu_lanes(gpus.size());
   WorkerPool::instance().parallel_for(
       gpus.size(),
       [&](size_t i) {
-        if (sysfs_values && work(gpus[i], true)) {
-          fast_ok[i] = 1;
-          return;
-        }
+        if (sysfs_values && work(gpus[i], true)) return;
         work(gpus[i], false);
       },
       lanes);
-  all_fast_ = std::all_of(fast_ok.begin(), fast_ok.end(), [](char c) { return c != 0; });
   trace::record("amdsmi.gpus", trace::now_ns() - t_gpus);
   // Per-GPU phase times: the slowest GPU (items may have run on pool
   // threads, whose trace records are their own).

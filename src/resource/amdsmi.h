@@ -128,8 +128,6 @@ class AmdSmiManager : public Manager {
   // it could not load libdrm_amdgpu, returns uninitialised bytes with
   // success (measured on the pool).  Also saves the call on every cycle.
   std::map<void*, std::string> proc_bdf_;
-  // Every GPU took the attribute path in the last snapshot (lane sizing).
-  bool all_fast_ = false;
 };
 
 }  // namespace gfd::resource

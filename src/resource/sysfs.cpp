@@ -344,9 +344,7 @@ std::vector<DevicePtr> SysfsManager::enumerate() {
   // Unpartitioned GPUs: ~10 attribute preads each, two GPUs per lane (see
   // AmdSmiManager::snapshot); partitioned ones also list and read each
   // partition node's memory banks, one GPU per lane.
-  bool any_partitioned = false;
-  for (const auto& v : visible) any_partitioned |= v.second->members.size() > 1;
-  size_t lanes = gpu_lanes(visible.size(), !any_partitioned);
+  size_t lanes = gpu_lanes(visible.size());
   WorkerPool::instance().parallel_for(
       visible.size(),
       [&](size_t i) {

@@ -263,13 +263,13 @@ void WorkerPool::parallel_for(size_t n, const std::function<void(size_t)>& fn, s
   if (error) std::rethrow_exception(error);
 }
 
-size_t gpu_lanes(size_t n_gpus, bool light) {
+size_t gpu_lanes(size_t n_gpus) {
   static const size_t forced = [] {
     const char* v = std::getenv("GFD_GPU_LANES");
     return v && *v ? static_cast<size_t>(std::strtoul(v, nullptr, 10)) : size_t{0};
   }();
   if (forced) return forced;
-  return light ? std::min<size_t>(4, (n_gpus + 1) / 2) : 8;
+  return std::max<size_t>(1, std::min<size_t>(8, n_gpus));
 }
 
 }  // namespace gfd

@@ -101,12 +101,14 @@ class WorkerPool {
   bool spinner_ = false;  // a worker is spinning (at most one does; guarded by mu_)
 };
 
-// Lanes for per-GPU work in one cycle.  light: a few attribute preads per
-// GPU (two GPUs per lane, at most four: a cycle after the daemon's sleep runs
-// on cold cores, where one thread is 4-5x slower than four, while back to
-// back the fan-out costs a little - profiles/multi_gpu_read_probe.txt);
-// otherwise (tens of library calls per GPU) one GPU per lane.
-// GFD_GPU_LANES=N overrides both (measurements).
-size_t gpu_lanes(size_t n_gpus, bool light);
+// Lanes for per-GPU work in one cycle: one GPU per lane, at most 8 (the
+// pool's size).  With the daemon pinned to one L3 domain and a spinning
+// worker, spreading even the light SPX path (a few attribute preads per
+// GPU) over one lane per GPU measured fastest back to back at 2, 4 and 8
+// GPUs (0.032 / 0.034 / 0.041 ms vs 0.034 / 0.040 / 0.043 with two GPUs per
+// lane) and the same after a 1 s sleep (profiles/hybrid_8gpu_scaling.txt);
+// round 1's two-per-lane rule came from an unpinned pool.  GFD_GPU_LANES=N
+// overrides it (measurements).
+size_t gpu_lanes(size_t n_gpus);
 
 }  // namespace gfd

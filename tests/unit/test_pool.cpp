@@ -132,12 +132,11 @@ TEST(Pool_GpuLanesPolicy) {
   // Light per-GPU work: two GPUs per lane, at most four lanes; heavy work
   // (library calls): one GPU per lane, the pool's width.
   if (std::getenv("GFD_GPU_LANES")) return;  // overridden for a measurement
-  EXPECT_EQ(gfd::gpu_lanes(1, true), static_cast<size_t>(1));
-  EXPECT_EQ(gfd::gpu_lanes(2, true), static_cast<size_t>(1));
-  EXPECT_EQ(gfd::gpu_lanes(3, true), static_cast<size_t>(2));
-  EXPECT_EQ(gfd::gpu_lanes(8, true), static_cast<size_t>(4));
-  EXPECT_EQ(gfd::gpu_lanes(16, true), static_cast<size_t>(4));
-  EXPECT_EQ(gfd::gpu_lanes(8, false), static_cast<size_t>(8));
+  EXPECT_EQ(gfd::gpu_lanes(0), static_cast<size_t>(1));
+  EXPECT_EQ(gfd::gpu_lanes(1), static_cast<size_t>(1));
+  EXPECT_EQ(gfd::gpu_lanes(2), static_cast<size_t>(2));
+  EXPECT_EQ(gfd::gpu_lanes(8), static_cast<size_t>(8));
+  EXPECT_EQ(gfd::gpu_lanes(16), static_cast<size_t>(8));
 }
 
 // ---- L3-domain pinning (util/affinity.h) ----

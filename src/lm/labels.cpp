@@ -5,6 +5,7 @@
 #include <sys/vfs.h>
 #include <unistd.h>
 
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <functional>
@@ -350,8 +351,9 @@ void discard_prepared_temps() {
   PreparedTemps& p = prepared();
   std::unique_lock<std::mutex> lk(p.mu);
   // A job handed out runs soon (or is dropped): its file must not outlive
-  // this call.
-  p.cv.wait(lk, [&] { return p.in_flight == 0; });
+  // this call.  Bounded all the same - exit must not hang on a worker stuck
+  // in the file system; its file would then stay behind in gfd-tmp/.
+  p.cv.wait_for(lk, std::chrono::seconds(5), [&] { return p.in_flight == 0; });
   for (auto& f : p.ready) drop(f);
   p.ready.clear();
 }

@@ -297,7 +297,8 @@ bool write_atomically_once(const std::string& path, const std::string& tmp_dir, 
 void write_file_atomically(const std::string& path, const std::string& contents, unsigned perm) {
   std::string abs = fs::absolute(path);
   std::string tmp_dir = fs::join(fs::dirname(abs), "gfd-tmp");
-  if (!write_atomically_once(path, tmp_dir, contents, perm, true))
+  // Prepared files are created 0644 - the feature file's mode.
+  if (!write_atomically_once(path, tmp_dir, contents, perm, perm == 0644))
     write_atomically_once(path, tmp_dir, contents, perm, false);
   PreparedTemps& p = prepared();
   std::lock_guard<std::mutex> lk(p.mu);

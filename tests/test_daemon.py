@@ -170,6 +170,31 @@ def test_sighup_reloads_config(binary, tmp_path):
     assert err.count("Loading configuration.") == 2
 
 
+def test_sighup_to_a_new_output_file_leaves_nothing_in_the_old_directory(binary, tmp_path):
+    """A reload that moves the feature file: the old file and its gfd-tmp/
+    (with any prepared temporary files) go, the new directory gets both."""
+    old_dir, new_dir = tmp_path / "old", tmp_path / "new"
+    old_dir.mkdir()
+    new_dir.mkdir()
+    cfg = tmp_path / "config.yaml"
+    cfg.write_text(f"version: v1\nflags:\n  gfd:\n    outputFile: {old_dir / 'gfd'}\n")
+    base = [a for a in _base(tmp_path, old_dir / "gfd") if not a.startswith("--output-file")]
+    p = _start(binary, ["--sleep-interval=50ms", f"--config-file={cfg}", *base])
+    try:
+        assert _wait_for(lambda: (old_dir / "gfd").exists() and (old_dir / "gfd-tmp").exists())
+        cfg.write_text(f"version: v1\nflags:\n  gfd:\n    outputFile: {new_dir / 'gfd'}\n")
+        p.send_signal(signal.SIGHUP)
+        assert _wait_for(lambda: (new_dir / "gfd").exists(), timeout=10)
+        assert _wait_for(lambda: not (old_dir / "gfd").exists() and not (old_dir / "gfd-tmp").exists(), timeout=5), \
+            list(old_dir.rglob("*"))
+        assert golden.parse_labels((new_dir / "gfd").read_text())["amd.com/gpu.product"] == "MOCKMODEL"
+    finally:
+        p.send_signal(signal.SIGTERM)
+        _, err = p.communicate(timeout=10)
+    assert p.returncode == 0, err
+    assert list(old_dir.iterdir()) == [] and list(new_dir.iterdir()) == []
+
+
 @pytest.mark.parametrize(
     "error_on_init,fail_on_init,strategy,expect_error",
     [

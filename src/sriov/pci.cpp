@@ -4,6 +4,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <string_view>
 #include <unordered_map>
 #include <unordered_set>
 
@@ -86,13 +87,22 @@ namespace {
 // function - 367 files on an 8-GPU MI355X host.  The table has no PCI
 // domain, so a bus/devfn listed twice is dropped (those functions are read
 // from sysfs).  Empty when the table cannot be read.
-std::unordered_map<uint32_t, uint32_t> proc_pci_vendors(const std::string& root) {
-  std::unordered_map<uint32_t, uint32_t> out;
+struct ProcFunction {
+  uint32_t id = 0;    // vendor << 16 | device
+  bool port = false;  // bound to pcieport: a PCIe port (bridge), never a GPU
+};
+
+std::unordered_map<uint32_t, ProcFunction> proc_pci_functions(const std::string& root) {
+  std::unordered_map<uint32_t, ProcFunction> out;
   auto r = fs::read_file(fs::join(root, "proc/bus/pci/devices"), 4u << 20);
   if (!r.ok()) return out;
   std::unordered_set<uint32_t> dup;
   const char* p = r.data.c_str();
   const char* end = p + r.data.size();
+  // The kernel's line (drivers/pci/proc.c, show_device): bus/devfn,
+  // vendor/device, irq, 7 resource starts, 7 sizes, then the bound driver's
+  // name (empty if none) - 18 tab-separated fields.
+  constexpr int kDriverField = 17;
   while (p < end) {
     const char* eol = static_cast<const char*>(std::memchr(p, '\n', static_cast<size_t>(end - p)));
     if (!eol) eol = end;
@@ -102,8 +112,18 @@ std::unordered_map<uint32_t, uint32_t> proc_pci_vendors(const std::string& root)
       char* q2 = nullptr;
       unsigned long id = std::strtoul(q + 1, &q2, 16);
       if (q2 && q2 > q + 1 && q2 <= eol) {
+        ProcFunction f;
+        f.id = static_cast<uint32_t>(id);
+        int tabs = 0;
+        const char* last = p;
+        for (const char* c = p; c < eol; ++c)
+          if (*c == '\t') {
+            ++tabs;
+            last = c + 1;
+          }
+        f.port = tabs == kDriverField && std::string_view(last, static_cast<size_t>(eol - last)) == "pcieport";
         auto key = static_cast<uint32_t>(bbdf & 0xffff);
-        if (!out.emplace(key, static_cast<uint32_t>(id)).second) dup.insert(key);
+        if (!out.emplace(key, f).second) dup.insert(key);
       }
     }
     p = eol + 1;
@@ -212,22 +232,24 @@ std::vector<PCIDevice> SysfsAmdPCI::Devices() {
   }();
   if (misses.size() > kChunk && !cold_sysfs) {
     int64_t tp = trace::now_ns();
-    auto vendors = proc_pci_vendors(root_);
+    auto table = proc_pci_functions(root_);
     trace::record("pci.proc_table", trace::now_ns() - tp);
-    if (!vendors.empty()) {
+    if (!table.empty()) {
       uint32_t amd = static_cast<uint32_t>(std::strtoul(kAmdVendorId, nullptr, 16));
       std::vector<size_t> amd_or_unknown;
       for (size_t m : misses) {
         auto key = bus_devfn(next[m].first);
-        auto v = key ? vendors.find(*key) : vendors.end();
-        if (v == vendors.end()) {
+        auto v = key ? table.find(*key) : table.end();
+        if (v == table.end()) {
           amd_or_unknown.push_back(m);
           known_device.push_back(0);
-        } else if ((v->second >> 16) == amd && (v->second & 0xffff) != 0) {
+        } else if ((v->second.id >> 16) == amd && (v->second.id & 0xffff) != 0 && !v->second.port) {
           amd_or_unknown.push_back(m);
-          known_device.push_back(v->second & 0xffff);
+          known_device.push_back(v->second.id & 0xffff);
         }
-        // else: another vendor's function - identity stays "not relevant"
+        // else: another vendor's function, or an AMD PCIe port (the switch
+        // ports next to every MI355X: half the host's AMD functions) -
+        // identity stays "not relevant"
       }
       misses.swap(amd_or_unknown);
       // A few functions per lane (~2-4 reads each now that vendor and device

@@ -369,6 +369,55 @@ TEST(Sriov_ColdScanTakesVendorsFromProcTable) {
   fs::remove_all(root);
 }
 
+TEST(Sriov_ColdScanSkipsFunctionsBoundToPcieport) {
+  // The kernel's full table line: 18 tab-separated fields, the last the
+  // bound driver.  An AMD function bound to pcieport (the PCIe switch ports
+  // next to each MI355X) is a bridge: its identity is never read.
+  std::string root = pci_host(20, 0);
+  std::string dev = root + "/sys/bus/pci/devices/";
+  auto line = [](const std::string& name, const std::string& vendev, const std::string& driver) {
+    unsigned d = 0, b = 0, s = 0, f = 0;
+    if (std::sscanf(name.c_str(), "%x:%x:%x.%x", &d, &b, &s, &f) != 4) throw std::runtime_error(name);
+    std::string l = str::format("%04x\t%s\t0", (b << 8) | (s << 3) | f, vendev.c_str());
+    for (int i = 0; i < 14; ++i) l += "\t0000000000000000";
+    return l + "\t" + driver + "\n";
+  };
+  std::string table, port, gpu;
+  for (const auto& [name, ino] : fs::list_dir_ino(dev)) {
+    std::string vendor = str::trim(fs::read_file(dev + name + "/vendor").data);
+    std::string device = str::trim(fs::read_file(dev + name + "/device").data);
+    if (device.empty()) device = "0x0000";
+    std::string vd = vendor.substr(2) + device.substr(2);
+    bool amd = vendor == "0x1002";
+    if (amd && gpu.empty()) gpu = name;
+    std::string driver = amd ? "amdgpu" : "";
+    table += line(name, vd, driver);
+  }
+  // An extra AMD function bound to pcieport whose attributes cannot be read.
+  port = "0000:7f:00.0";
+  fs::mkdir_all(dev + port + "/class");  // unreadable as a file
+  put_file(dev + port + "/vendor", "0x1002\n");
+  table += line(port, "10021501", "pcieport");
+  put_file(root + "/proc/bus/pci/devices", table);
+  SysfsAmdPCI pci(root);
+  auto devs = pci.Devices();
+  EXPECT_FALSE(gpu.empty());
+  bool has_gpu = false, has_port = false;
+  for (const auto& d : devs) {
+    has_gpu |= d.address == gpu;
+    has_port |= d.address == port;
+  }
+  EXPECT_TRUE(has_gpu);
+  EXPECT_FALSE(has_port);
+  // The same function with the short (driverless) line format is read - and
+  // its unreadable class is an error.
+  table.resize(table.size() - line(port, "10021501", "pcieport").size());
+  put_file(root + "/proc/bus/pci/devices", table + str::format("%04x\t10021501\t0\t0\n", 0x7f << 8));
+  SysfsAmdPCI cold(root);
+  EXPECT_THROW_MSG(cold.Devices(), "unable to read PCI device class for 0000:7f:00.0");
+  fs::remove_all(root);
+}
+
 TEST(Fs_AttrReaderKeepsOnlySysfsDescriptors) {
   char d[] = "/tmp/gfd-attr-XXXXXX";
   if (!mkdtemp(d)) throw std::runtime_error("mkdtemp");

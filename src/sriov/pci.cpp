@@ -233,6 +233,11 @@ std::vector<PCIDevice> SysfsAmdPCI::Devices() {
   if (misses.size() > kChunk && !cold_sysfs) {
     int64_t tp = trace::now_ns();
     auto table = proc_pci_functions(root_);
+    // GFD_PCI_PORTS=read: read AMD PCIe ports too (A/B measurements).
+    static const bool skip_ports = [] {
+      const char* v = std::getenv("GFD_PCI_PORTS");
+      return !(v && std::string(v) == "read");
+    }();
     trace::record("pci.proc_table", trace::now_ns() - tp);
     if (!table.empty()) {
       uint32_t amd = static_cast<uint32_t>(std::strtoul(kAmdVendorId, nullptr, 16));
@@ -243,7 +248,7 @@ std::vector<PCIDevice> SysfsAmdPCI::Devices() {
         if (v == table.end()) {
           amd_or_unknown.push_back(m);
           known_device.push_back(0);
-        } else if ((v->second.id >> 16) == amd && (v->second.id & 0xffff) != 0 && !v->second.port) {
+        } else if ((v->second.id >> 16) == amd && (v->second.id & 0xffff) != 0 && !(v->second.port && skip_ports)) {
           amd_or_unknown.push_back(m);
           known_device.push_back(v->second.id & 0xffff);
         }

@@ -30,16 +30,28 @@ def _rss_kib(pid: int) -> int:
     return 0
 
 
-def _fds(pid: int) -> int:
+def _fds(pid: int) -> tuple[int, int]:
     # Minimum over a short window: a cycle in flight holds transient
     # descriptors (the temp output file, an amd-smi device node), a leak
     # raises the floor.  The window must catch the daemon between cycles at
-    # least once (see the per-cycle interval below).
-    n = []
+    # least once (see the per-cycle interval below).  Prepared temporary
+    # files (gfd-tmp/a|b/gfd-*, up to two kept open between cycles by design,
+    # src/lm/labels.cpp PreparedTemps) are counted apart: how many are ready
+    # at a sample depends on timing, not on leaks - that made the floor
+    # 15 or 16 from run to run.  Returns (floor without them, most of them).
+    n, prepared = [], []
     for _ in range(40):
-        n.append(len(os.listdir(f"/proc/{pid}/fd")))
+        targets = []
+        for fd in os.listdir(f"/proc/{pid}/fd"):
+            try:
+                targets.append(os.readlink(f"/proc/{pid}/fd/{fd}"))
+            except OSError:  # closed between listdir and readlink
+                pass
+        k = sum(1 for t in targets if "/gfd-tmp/" in t)
+        n.append(len(targets) - k)
+        prepared.append(k)
         time.sleep(0.01)
-    return min(n)
+    return min(n), max(prepared)
 
 
 def soak(binary: str, args: list[str], seconds: float, hup_at: float | None = None, interval: str = "1ms") -> dict:
@@ -65,7 +77,7 @@ def soak(binary: str, args: list[str], seconds: float, hup_at: float | None = No
         while cycles[0] < 200 and time.monotonic() < deadline and p.poll() is None:
             time.sleep(0.05)
         assert p.poll() is None, "".join(tail)
-        rss0, fd0, c0 = _rss_kib(p.pid), _fds(p.pid), cycles[0]
+        rss0, (fd0, prep0), c0 = _rss_kib(p.pid), _fds(p.pid), cycles[0]
         t0 = time.monotonic()
         hupped = False
         while time.monotonic() - t0 < seconds and p.poll() is None:
@@ -74,7 +86,7 @@ def soak(binary: str, args: list[str], seconds: float, hup_at: float | None = No
                 hupped = True
             time.sleep(0.05)
         assert p.poll() is None, "".join(tail)
-        rss1, fd1, c1 = _rss_kib(p.pid), _fds(p.pid), cycles[0]
+        rss1, (fd1, prep1), c1 = _rss_kib(p.pid), _fds(p.pid), cycles[0]
     finally:
         p.send_signal(signal.SIGTERM)
         try:
@@ -83,7 +95,7 @@ def soak(binary: str, args: list[str], seconds: float, hup_at: float | None = No
             p.kill()
             rc = p.wait()
         t.join(timeout=10)
-    return {"rc": rc, "rss0": rss0, "rss1": rss1, "fd0": fd0, "fd1": fd1, "cycles": c1 - c0, "reloads": reloads[0],
+    return {"rc": rc, "rss0": rss0, "rss1": rss1, "fd0": fd0, "fd1": fd1, "prepared": max(prep0, prep1), "cycles": c1 - c0, "reloads": reloads[0],
             "tail": "".join(tail)}
 
 
@@ -91,6 +103,7 @@ def _assert_steady(r: dict, min_cycles: int):
     assert r["rc"] == 0, r["tail"]
     assert r["cycles"] >= min_cycles, r
     assert r["fd1"] <= r["fd0"], f"file descriptors grew {r['fd0']} -> {r['fd1']}"
+    assert r["prepared"] <= 2, f"{r['prepared']} prepared temporary files open (at most two by design)"
     # Allocator noise only: a leak of even 100 bytes/cycle over thousands of
     # cycles would exceed this.
     assert r["rss1"] - r["rss0"] <= 1024, f"RSS grew {r['rss0']} -> {r['rss1']} KiB over {r['cycles']} cycles"
@@ -122,4 +135,4 @@ def test_soak_amdsmi_backend_no_growth(binary, tmp_path, session):
     _assert_steady(r, min_cycles=int(seconds * (15 if per_cycle else 200)))
     assert r["reloads"] == 1, r["tail"]
     print(f"soak[{session}]: {r['cycles']} cycles in {seconds:.0f}s, RSS {r['rss0']} -> {r['rss1']} KiB, "
-          f"fds {r['fd0']} -> {r['fd1']}")
+          f"fds {r['fd0']} -> {r['fd1']} (+ up to {r['prepared']} prepared temporary files)")

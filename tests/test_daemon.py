@@ -100,26 +100,39 @@ def _prepared(tmp: Path) -> list[Path]:
 @pytest.mark.parametrize("prepare", ["default", "never"])
 def test_loop_keeps_prepared_temporary_files(binary, tmp_path, prepare):
     """Loop mode: between cycles gfd-tmp/{a,b}/ hold one or two (empty, 0644)
-    temporary files made for later cycles, which those cycles rename into
-    place; with GFD_WRITE_PREPARE=never gfd-tmp/ stays empty, as in the
-    reference.  Either way exit removes everything."""
+    temporary files made for later cycles, which those cycles swap into
+    place, and at most one old feature file swapped out (RENAME_EXCHANGE)
+    that the next cycle's worker unlinks; with GFD_WRITE_PREPARE=never
+    gfd-tmp/ stays empty, as in the reference.  Either way exit removes
+    everything."""
     out = tmp_path / "gfd"
     env = {"GFD_WRITE_PREPARE": "never"} if prepare == "never" else None
     p = _start(binary, ["--sleep-interval=200ms", *_base(tmp_path, out)], env=env)
     tmp = tmp_path / "gfd-tmp"
+
+    def split():  # (prepared, retired) - retired ones hold labels
+        ready, old = [], []
+        for f in _prepared(tmp):
+            try:
+                st = f.stat()
+            except FileNotFoundError:  # unlinked by the worker meanwhile
+                continue
+            (old if st.st_size else ready).append((f, st))
+        return ready, old
+
     try:
         assert _wait_for(out.exists), "first write"
         if prepare == "default":
-            assert _wait_for(lambda: 1 <= len(_prepared(tmp)) <= 2), _prepared(tmp)
-            ready = _prepared(tmp)
-            for f in ready:
-                st = f.stat()
-                assert st.st_size == 0 and oct(st.st_mode & 0o777) == "0o644"
-            inos = {f.stat().st_ino for f in ready}
+            assert _wait_for(lambda: 1 <= len(split()[0]) <= 2), _prepared(tmp)
+            ready, old = split()
+            assert len(old) <= 1, old
+            for f, st in ready:
+                assert oct(st.st_mode & 0o777) == "0o644"
+            inos = {st.st_ino for _, st in ready}
             m0 = out.stat().st_mtime_ns
             assert _wait_for(lambda: out.stat().st_mtime_ns > m0, timeout=5), "file not rewritten"
             assert out.stat().st_ino in inos  # a prepared file became the feature file
-            assert _wait_for(lambda: 1 <= len(_prepared(tmp)) <= 2)
+            assert _wait_for(lambda: 1 <= len(split()[0]) <= 2 and len(split()[1]) <= 1)
         else:
             m0 = out.stat().st_mtime_ns
             assert _wait_for(lambda: out.stat().st_mtime_ns > m0, timeout=5), "file not rewritten"

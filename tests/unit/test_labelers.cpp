@@ -465,18 +465,66 @@ TEST(WriteToFile_UsesPreparedTemporaryFiles) {
   EXPECT_TRUE(stat(ready[0].c_str(), &st) == 0);
   EXPECT_EQ(static_cast<long>(st.st_size), 0L);
   EXPECT_EQ(static_cast<int>(st.st_mode & 0777), 0644);
-  // A write takes one of them: its inode becomes the feature file.
+  // A write takes one of them: its inode becomes the feature file, and the
+  // old feature file takes its name (RENAME_EXCHANGE) until the next
+  // preparer job unlinks it.
   lm::write_to_file({{"k", "1"}}, path);
   EXPECT_EQ(fs::read_file(path).data, std::string("k=1\n"));
   auto left = prepared_files(dir);
-  EXPECT_EQ(left.size(), static_cast<size_t>(1));
-  EXPECT_TRUE(left.size() == 1 && (left[0] == ready[0] || left[0] == ready[1]));
+  EXPECT_EQ(left.size(), static_cast<size_t>(2));
+  std::string retired = fs::read_file(ready[0]).data == "k=0\n" ? ready[0] : ready[1];
+  EXPECT_EQ(fs::read_file(retired).data, std::string("k=0\n"));
   EXPECT_TRUE(stat(path.c_str(), &st) == 0);
   EXPECT_EQ(static_cast<int>(st.st_mode & 0777), 0644);
+  if (auto job = lm::temp_preparer(path)) job();
+  EXPECT_FALSE(fs::exists(retired));
+  EXPECT_EQ(prepared_files(dir).size(), static_cast<size_t>(2));
+  EXPECT_EQ(fs::read_file(path).data, std::string("k=1\n"));
   // Exit: nothing left behind.
   lm::remove_output_file(path);
   EXPECT_FALSE(fs::exists(tmp));
   EXPECT_FALSE(fs::exists(path));
+  fs::remove_all(dir);
+}
+
+TEST(WriteToFile_ExchangeNeverSwapsADirectoryIntoTheTemporaryDirectory) {
+  // Loop mode replaces the feature file with RENAME_EXCHANGE; a directory
+  // where the feature file belongs must fail the write as rename(2) does
+  // (EISDIR), stay where it is, and not be removed with gfd-tmp/ at exit.
+  char dir[] = "/tmp/gfd-write-XXXXXX";
+  EXPECT_TRUE(mkdtemp(dir) != nullptr);
+  std::string path = std::string(dir) + "/gfd";
+  prepare_then_write({{"k", "1"}}, path);
+  EXPECT_TRUE(::unlink(path.c_str()) == 0);
+  EXPECT_TRUE(::mkdir(path.c_str(), 0755) == 0);
+  EXPECT_TRUE(::close(::open((path + "/keep").c_str(), O_CREAT | O_WRONLY, 0644)) == 0);
+  if (auto job = lm::temp_preparer(path)) job();
+  EXPECT_THROW_MSG(lm::write_to_file({{"k", "2"}}, path), "error moving temporary file");
+  EXPECT_TRUE(fs::exists(path + "/keep"));
+  lm::discard_prepared_temps();
+  fs::remove_all(std::string(dir) + "/gfd-tmp");
+  EXPECT_TRUE(fs::exists(path + "/keep"));
+  fs::remove_all(dir);
+}
+
+TEST(WriteToFile_ExchangeKeepsReadersOfTheOldFile) {
+  // A reader that opened the feature file before a write keeps reading the
+  // old contents, whole, after the exchange and after the worker unlinks it.
+  char dir[] = "/tmp/gfd-write-XXXXXX";
+  EXPECT_TRUE(mkdtemp(dir) != nullptr);
+  std::string path = std::string(dir) + "/gfd";
+  prepare_then_write({{"k", "old"}}, path);
+  int rfd = ::open(path.c_str(), O_RDONLY);
+  EXPECT_TRUE(rfd >= 0);
+  prepare_then_write({{"k", "new"}}, path);
+  if (auto job = lm::temp_preparer(path)) job();
+  char buf[16] = {};
+  EXPECT_EQ(::pread(rfd, buf, sizeof(buf) - 1, 0), static_cast<ssize_t>(6));
+  EXPECT_EQ(std::string(buf), std::string("k=old\n"));
+  ::close(rfd);
+  EXPECT_EQ(fs::read_file(path).data, std::string("k=new\n"));
+  lm::remove_output_file(path);
+  EXPECT_FALSE(fs::exists(std::string(dir) + "/gfd-tmp"));
   fs::remove_all(dir);
 }
 

@@ -97,16 +97,17 @@ def _prepared(tmp: Path) -> list[Path]:
     return sorted(f for sub in ("a", "b") if (tmp / sub).is_dir() for f in (tmp / sub).iterdir())
 
 
-@pytest.mark.parametrize("prepare", ["default", "never"])
+@pytest.mark.parametrize("prepare", ["default", "never", "no-exchange"])
 def test_loop_keeps_prepared_temporary_files(binary, tmp_path, prepare):
     """Loop mode: between cycles gfd-tmp/{a,b}/ hold one or two (empty, 0644)
     temporary files made for later cycles, which those cycles swap into
     place, and at most one old feature file swapped out (RENAME_EXCHANGE)
     that the next cycle's worker unlinks; with GFD_WRITE_PREPARE=never
     gfd-tmp/ stays empty, as in the reference.  Either way exit removes
-    everything."""
+    everything.  GFD_WRITE_EXCHANGE=never renames prepared files over the
+    feature file: no old one is left for the worker."""
     out = tmp_path / "gfd"
-    env = {"GFD_WRITE_PREPARE": "never"} if prepare == "never" else None
+    env = {"never": {"GFD_WRITE_PREPARE": "never"}, "no-exchange": {"GFD_WRITE_EXCHANGE": "never"}}.get(prepare)
     p = _start(binary, ["--sleep-interval=200ms", *_base(tmp_path, out)], env=env)
     tmp = tmp_path / "gfd-tmp"
 
@@ -122,10 +123,10 @@ def test_loop_keeps_prepared_temporary_files(binary, tmp_path, prepare):
 
     try:
         assert _wait_for(out.exists), "first write"
-        if prepare == "default":
+        if prepare != "never":
             assert _wait_for(lambda: 1 <= len(split()[0]) <= 2), _prepared(tmp)
             ready, old = split()
-            assert len(old) <= 1, old
+            assert len(old) <= (1 if prepare == "default" else 0), old
             for f, st in ready:
                 assert oct(st.st_mode & 0o777) == "0o644"
             inos = {st.st_ino for _, st in ready}
@@ -133,6 +134,8 @@ def test_loop_keeps_prepared_temporary_files(binary, tmp_path, prepare):
             assert _wait_for(lambda: out.stat().st_mtime_ns > m0, timeout=5), "file not rewritten"
             assert out.stat().st_ino in inos  # a prepared file became the feature file
             assert _wait_for(lambda: 1 <= len(split()[0]) <= 2 and len(split()[1]) <= 1)
+            if prepare == "no-exchange":
+                assert split()[1] == []
         else:
             m0 = out.stat().st_mtime_ns
             assert _wait_for(lambda: out.stat().st_mtime_ns > m0, timeout=5), "file not rewritten"

@@ -144,10 +144,10 @@ std::optional<uint32_t> bus_devfn(const std::string& addr) {
 }  // namespace
 
 SysfsAmdPCI::Identity SysfsAmdPCI::read_identity(const std::string& addr, const std::string& p, uint64_t ino,
-                                                 uint32_t device_id) {
+                                                 uint32_t device_id, bool amd) {
   Identity id;
   id.ino = ino;
-  if (device_id == 0) {
+  if (device_id == 0 && !amd) {
     auto vendor = fs::read_file(fs::join(p, "vendor"), 64);
     if (!vendor.ok()) throw Error("unable to read PCI device vendor id for " + addr + ": " + fs::errno_str(vendor.err));
     if (str::trim(vendor.data) != kAmdVendorId) return id;
@@ -230,8 +230,56 @@ std::vector<PCIDevice> SysfsAmdPCI::Devices() {
     const char* v = std::getenv("GFD_PCI_COLD");
     return v && std::string(v) == "sysfs";
   }();
+  // Functions bound to amdgpu (AMD's: its ID table names vendor 0x1002 only)
+  // in a cold scan: their identity reads start on the pool at once and run
+  // while this thread reads the procfs table (0.5-0.65 ms on a 367-function
+  // host: the kernel restarts its device walk for every page it hands out),
+  // which then only has to name the other AMD functions (none on the pool's
+  // hosts once the PCIe ports are skipped).
+  std::vector<size_t> early;
+  WorkerPool::Task early_task;
+  struct EarlyGuard {  // the task reads `next`: it must be done before it goes
+    WorkerPool::Task* t;
+    bool armed = false;
+    ~EarlyGuard() {
+      if (armed) t->cancel_or_wait();
+    }
+  } early_guard{&early_task};
+  // GFD_PCI_AMDGPU=table: amdgpu's functions wait for the table too (A/B).
+  static const bool early_reads = [] {
+    const char* v = std::getenv("GFD_PCI_AMDGPU");
+    return !(v && std::string(v) == "table");
+  }();
   if (misses.size() > kChunk && !cold_sysfs) {
     int64_t tp = trace::now_ns();
+    std::vector<char> miss(next.size(), 0);
+    for (size_t m : misses) miss[m] = 1;
+    for (const auto& name : early_reads ? fs::list_dir(fs::join(root_, "sys/bus/pci/drivers/amdgpu"))
+                                        : std::vector<std::string>{}) {
+      if (!bus_devfn(name)) continue;  // bind, unbind, module, ...
+      auto it = std::lower_bound(next.begin(), next.end(), name,
+                                 [](const std::pair<std::string, Identity>& e, const std::string& n) { return e.first < n; });
+      size_t i = static_cast<size_t>(it - next.begin());
+      if (it != next.end() && it->first == name && miss[i]) {
+        early.push_back(i);
+        miss[i] = 0;
+      }
+    }
+    if (!early.empty()) {
+      misses.erase(std::remove_if(misses.begin(), misses.end(), [&](size_t m) { return !miss[m]; }), misses.end());
+      early_task = WorkerPool::instance().submit([&] {
+        constexpr size_t kEarlyChunk = 2;
+        WorkerPool::instance().parallel_for((early.size() + kEarlyChunk - 1) / kEarlyChunk, [&](size_t c) {
+          for (size_t k = c * kEarlyChunk; k < std::min(early.size(), (c + 1) * kEarlyChunk); ++k) {
+            auto& [addr, id] = next[early[k]];
+            id = read_identity(addr, fs::join(dir, addr), id.ino, 0, true);
+          }
+        });
+      });
+      early_guard.armed = true;
+    }
+    trace::record("pci.amdgpu", trace::now_ns() - tp);
+    tp = trace::now_ns();
     auto table = proc_pci_functions(root_);
     // GFD_PCI_PORTS=read: read AMD PCIe ports too (A/B measurements).
     static const bool skip_ports = [] {
@@ -276,6 +324,10 @@ std::vector<PCIDevice> SysfsAmdPCI::Devices() {
       WorkerPool::instance().parallel_for(chunks, read_chunk);
     else if (chunks == 1)
       read_chunk(0);
+    if (early_guard.armed) {
+      early_guard.armed = false;
+      early_task.run_or_wait();
+    }
   } catch (...) {
     listing_.reset();  // the next scan must see this listing as changed again
     throw;

@@ -127,7 +127,10 @@ class SysfsAmdPCI : public AmdPCI {
   };
   // `device_id`: the function's device ID when procfs' device table already
   // placed it as an AMD function (vendor and device are not re-read), else 0.
-  static Identity read_identity(const std::string& addr, const std::string& path, uint64_t ino, uint32_t device_id = 0);
+  // device_id: from the procfs table (0 = read it); amd: the vendor is known
+  // to be AMD (bound to amdgpu) - no vendor read.
+  static Identity read_identity(const std::string& addr, const std::string& path, uint64_t ino, uint32_t device_id = 0,
+                                bool amd = false);
   std::string root_;
   fs::DirListing listing_;
   bool scanned_ = false;

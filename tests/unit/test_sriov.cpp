@@ -9,6 +9,7 @@
 #include "util/fs.h"
 #include "util/strings.h"
 
+#include <algorithm>
 #include <sys/wait.h>
 #include <unistd.h>
 
@@ -366,6 +367,56 @@ TEST(Sriov_ColdScanTakesVendorsFromProcTable) {
   put_file(dev + "0000:00:07.0/vendor", "0x1022\n");
   SysfsAmdPCI ambiguous(root);
   EXPECT_THROW_MSG(ambiguous.Devices(), "unable to read PCI device vendor id for 0000:00:05.0");
+  fs::remove_all(root);
+}
+
+TEST(Sriov_ColdScanReadsAmdgpuFunctionsAlongsideTheTable) {
+  // Functions listed in sys/bus/pci/drivers/amdgpu are read on the pool
+  // while the procfs table is read, without a vendor read (amdgpu binds AMD
+  // functions only); the result is the same scan.
+  std::string root = pci_host(200, 2);
+  std::string dev = root + "/sys/bus/pci/devices/";
+  std::string table;
+  for (const auto& [name, ino] : fs::list_dir_ino(dev)) {
+    unsigned d = 0, b = 0, s = 0, f = 0;
+    if (std::sscanf(name.c_str(), "%x:%x:%x.%x", &d, &b, &s, &f) != 4) throw std::runtime_error(name);
+    std::string vendor = str::trim(fs::read_file(dev + name + "/vendor").data);
+    std::string device = str::trim(fs::read_file(dev + name + "/device").data);
+    if (device.empty()) device = "0x0000";
+    table += str::format("%04x\t%s%s\t0\t0\n", (b << 8) | (s << 3) | f, vendor.substr(2).c_str(), device.substr(2).c_str());
+  }
+  put_file(root + "/proc/bus/pci/devices", table);
+  auto summary = [](const std::vector<PCIDevice>& devs) {
+    std::string out;
+    for (const auto& d : devs)
+      out += d.address + " " + d.device + " " + d.class_code + " " + std::to_string(d.sriov_totalvfs) + " " +
+             std::to_string(d.sriov_numvfs) + " " + d.physfn + "\n";
+    return out;
+  };
+  std::string want = summary(SysfsAmdPCI(root).Devices());
+  EXPECT_EQ(std::count(want.begin(), want.end(), '\n'), 7L);
+  // amdgpu's driver directory: the 5 PFs, its control files, and a function
+  // that is not on the bus listing (ignored).
+  std::string drv = root + "/sys/bus/pci/drivers/amdgpu/";
+  for (int g = 0; g < 4; ++g) fs::mkdir_all(drv + str::format("0000:%02x:00.0", 0x11 + 0x10 * g));
+  fs::mkdir_all(drv + "0000:c1:00.0");
+  fs::mkdir_all(drv + "0000:ee:00.0");
+  for (const char* f : {"bind", "unbind", "uevent", "new_id"}) put_file(drv + f, "");
+  fs::mkdir_all(drv + "module");
+  // Their vendor attribute is not needed any more.
+  fs::remove_all(dev + "0000:11:00.0/vendor");
+  fs::mkdir_all(dev + "0000:11:00.0/vendor");  // unreadable as a file
+  EXPECT_EQ(summary(SysfsAmdPCI(root).Devices()), want);
+  // Without the procfs table the rest are read from sysfs, the amdgpu ones once.
+  fs::remove_all(root + "/proc");
+  EXPECT_EQ(summary(SysfsAmdPCI(root).Devices()), want);
+  // An amdgpu function whose class cannot be read fails the scan, from the
+  // pool task, with the same error as the serial path.
+  fs::remove_all(dev + "0000:21:00.0/class");
+  fs::mkdir_all(dev + "0000:21:00.0/class");
+  put_file(root + "/proc/bus/pci/devices", table);
+  SysfsAmdPCI bad(root);
+  EXPECT_THROW_MSG(bad.Devices(), "unable to read PCI device class for 0000:21:00.0");
   fs::remove_all(root);
 }
 

@@ -132,13 +132,27 @@ std::unordered_map<uint32_t, ProcFunction> proc_pci_functions(const std::string&
   return out;
 }
 
-// "DDDD:BB:DD.F" -> bus << 8 | dev << 3 | fn.
+// "DDDD:BB:DD.F" (sysfs' PCI device names; the domain may be longer) ->
+// bus << 8 | dev << 3 | fn.  Hand-parsed: sscanf cost ~0.2 us per name,
+// 70 us for the ~350 names a cold scan looks up.
 std::optional<uint32_t> bus_devfn(const std::string& addr) {
-  unsigned dom = 0, bus = 0, dev = 0, fn = 0;
-  char tail = 0;
-  if (std::sscanf(addr.c_str(), "%x:%x:%x.%x%c", &dom, &bus, &dev, &fn, &tail) != 4) return std::nullopt;
-  if (bus > 0xff || dev > 0x1f || fn > 7) return std::nullopt;
-  return static_cast<uint32_t>((bus << 8) | (dev << 3) | fn);
+  auto hex = [](char c) -> int {
+    if (c >= '0' && c <= '9') return c - '0';
+    if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+    if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+    return -1;
+  };
+  // The fixed-width tail ":BB:DD.F" after a domain of 4+ hex digits.
+  size_t n = addr.size();
+  if (n < 12) return std::nullopt;
+  const char* t = addr.c_str() + n - 8;
+  for (size_t i = 0; i + 8 < n; ++i)
+    if (hex(addr[i]) < 0) return std::nullopt;
+  int b1 = hex(t[1]), b0 = hex(t[2]), d1 = hex(t[4]), d0 = hex(t[5]), f = hex(t[7]);
+  if (t[0] != ':' || t[3] != ':' || t[6] != '.' || b1 < 0 || b0 < 0 || d1 < 0 || d0 < 0 || f < 0) return std::nullopt;
+  unsigned bus = static_cast<unsigned>(b1 << 4 | b0), dev = static_cast<unsigned>(d1 << 4 | d0);
+  if (dev > 0x1f || f > 7) return std::nullopt;
+  return static_cast<uint32_t>((bus << 8) | (dev << 3) | static_cast<unsigned>(f));
 }
 
 }  // namespace

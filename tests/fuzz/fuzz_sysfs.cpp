@@ -67,6 +67,19 @@ const std::string& root() {
     gfd::fs::mkdir_all(s + "/proc/bus/pci");
     gfd::lm::write_file_atomically(s + "/sys/class/kfd/kfd/topology/nodes/0/properties", "cpu_cores_count 64\n", 0644);
     gfd::lm::write_file_atomically(s + "/sys/bus/pci/devices/0000:75:00.0/vendor", "0x1002\n", 0644);
+    // Enough other functions for the cold scan's procfs-table path (more
+    // than 16 unread functions), and amdgpu's driver directory naming the
+    // GPU (its identity read on the pool while the table is read).
+    for (int i = 0; i < 24; ++i) {
+      char name[32];
+      std::snprintf(name, sizeof(name), "0000:%02x:%02x.0", i / 8, i % 8);
+      std::string dev = s + "/sys/bus/pci/devices/" + name;
+      gfd::fs::mkdir_all(dev);
+      gfd::lm::write_file_atomically(dev + "/vendor", i % 5 ? "0x1022\n" : "0x1002\n", 0644);
+      gfd::lm::write_file_atomically(dev + "/class", i % 3 ? "0x060400\n" : "0x120000\n", 0644);
+    }
+    gfd::fs::mkdir_all(s + "/sys/bus/pci/drivers/amdgpu/0000:75:00.0");
+    gfd::lm::write_file_atomically(s + "/sys/bus/pci/drivers/amdgpu/bind", "", 0644);
     // Not root(): by exit time the static it returns may already be
     // destroyed (its destructor was registered after this handler).
     static const std::string* const tree = new std::string(s);

@@ -87,6 +87,10 @@ def soak(binary: str, args: list[str], seconds: float, hup_at: float | None = No
             time.sleep(0.05)
         assert p.poll() is None, "".join(tail)
         rss1, (fd1, prep1), c1 = _rss_kib(p.pid), _fds(p.pid), cycles[0]
+        # Files in gfd-tmp/: prepared ones and old feature files swapped out
+        # by exchanges, which the next cycle's worker unlinks.
+        out = next((a.split("=", 1)[1] for a in args if a.startswith("--output-file=")), "")
+        tmp_files = sum(len(fs) for _, _, fs in os.walk(os.path.join(os.path.dirname(out), "gfd-tmp"))) if out else 0
     finally:
         p.send_signal(signal.SIGTERM)
         try:
@@ -95,7 +99,7 @@ def soak(binary: str, args: list[str], seconds: float, hup_at: float | None = No
             p.kill()
             rc = p.wait()
         t.join(timeout=10)
-    return {"rc": rc, "rss0": rss0, "rss1": rss1, "fd0": fd0, "fd1": fd1, "prepared": max(prep0, prep1), "cycles": c1 - c0, "reloads": reloads[0],
+    return {"rc": rc, "rss0": rss0, "rss1": rss1, "fd0": fd0, "fd1": fd1, "prepared": max(prep0, prep1), "tmp_files": tmp_files, "cycles": c1 - c0, "reloads": reloads[0],
             "tail": "".join(tail)}
 
 
@@ -104,6 +108,9 @@ def _assert_steady(r: dict, min_cycles: int):
     assert r["cycles"] >= min_cycles, r
     assert r["fd1"] <= r["fd0"], f"file descriptors grew {r['fd0']} -> {r['fd1']}"
     assert r["prepared"] <= 2, f"{r['prepared']} prepared temporary files open (at most two by design)"
+    # Two prepared + the swapped-out files no worker job has reached yet (one
+    # between cycles; two if a cycle's write beats the previous cycle's job).
+    assert r["tmp_files"] <= 4, f"{r['tmp_files']} files in gfd-tmp/: old feature files are not being unlinked"
     # Allocator noise only: a leak of even 100 bytes/cycle over thousands of
     # cycles would exceed this.
     assert r["rss1"] - r["rss0"] <= 1024, f"RSS grew {r['rss0']} -> {r['rss1']} KiB over {r['cycles']} cycles"

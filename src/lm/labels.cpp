@@ -173,6 +173,16 @@ namespace {
 // creates its own when none is ready, never waiting for a worker.
 constexpr size_t kMaxPrepared = 2;
 
+// GFD_WRITE_PREPARE_MAX=N (1-8): another bound (A/B measurements).
+size_t max_prepared() {
+  static const size_t n = [] {
+    const char* v = std::getenv("GFD_WRITE_PREPARE_MAX");
+    long x = v ? std::strtol(v, nullptr, 10) : 0;
+    return x >= 1 && x <= 8 ? static_cast<size_t>(x) : kMaxPrepared;
+  }();
+  return n;
+}
+
 struct Prepared {
   std::string dir, name;
   int fd = -1;
@@ -379,7 +389,7 @@ std::function<void()> temp_preparer(const std::string& path) {
     std::lock_guard<std::mutex> lk(p.mu);
     size_t have = p.in_flight;
     for (const auto& f : p.ready) have += f.dir == tmp_dir;
-    ticket->creates = have < kMaxPrepared;
+    ticket->creates = have < max_prepared();
     if (!ticket->creates && p.retired.empty()) {
       ticket->finished = true;  // never handed out
       return {};

@@ -507,6 +507,25 @@ TEST(WriteToFile_ExchangeNeverSwapsADirectoryIntoTheTemporaryDirectory) {
   fs::remove_all(dir);
 }
 
+TEST(WriteToFile_ExchangeWithTheFeatureFileRemovedBetweenCycles) {
+  // Someone deleted the feature file since the last cycle: the exchange has
+  // nothing to swap with (ENOENT) and the prepared file is renamed into place.
+  char dir[] = "/tmp/gfd-write-XXXXXX";
+  EXPECT_TRUE(mkdtemp(dir) != nullptr);
+  std::string path = std::string(dir) + "/gfd";
+  prepare_then_write({{"k", "1"}}, path);
+  prepare_then_write({{"k", "2"}}, path);
+  EXPECT_TRUE(::unlink(path.c_str()) == 0);
+  prepare_then_write({{"k", "3"}}, path);
+  EXPECT_EQ(fs::read_file(path).data, std::string("k=3\n"));
+  prepare_then_write({{"k", "4"}}, path);
+  EXPECT_EQ(fs::read_file(path).data, std::string("k=4\n"));
+  lm::remove_output_file(path);
+  EXPECT_FALSE(fs::exists(std::string(dir) + "/gfd-tmp"));
+  EXPECT_FALSE(fs::exists(path));
+  fs::remove_all(dir);
+}
+
 TEST(WriteToFile_ExchangeKeepsReadersOfTheOldFile) {
   // A reader that opened the feature file before a write keeps reading the
   // old contents, whole, after the exchange and after the worker unlinks it.

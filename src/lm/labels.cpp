@@ -171,7 +171,14 @@ namespace {
 // critical path (profiles/write_prepare_ab.txt).  At most kMaxPrepared files
 // are ready or being made; a write takes the oldest in its directory and
 // creates its own when none is ready, never waiting for a worker.
-constexpr size_t kMaxPrepared = 2;
+//
+// Four, not two: back to back, a worker's create (and the unlink of the file
+// the last exchange swapped out) can take longer than a whole cycle, and
+// with two ready some writes still made their own file - bench p90
+// 0.024-0.036 -> 0.021-0.024 ms with four, p50 and cold cycles unchanged
+// (profiles/write_prepare_ab.txt, last section).  An empty file and a
+// descriptor each.
+constexpr size_t kMaxPrepared = 4;
 
 // GFD_WRITE_PREPARE_MAX=N (1-8): another bound (A/B measurements).
 size_t max_prepared() {

@@ -211,7 +211,7 @@ struct PreparedTemps {
   size_t in_flight = 0;  // files being made by preparer jobs handed out and not yet finished or dropped
   size_t jobs = 0;       // preparer jobs handed out and not yet finished or dropped
   size_t last_size = 0;  // of the last write: the next file's preallocation
-  size_t serial = 0;     // preparer jobs handed out so far (picks the subdirectory)
+  size_t serial = 0;     // files handed out to be made so far (picks the subdirectory)
 };
 
 PreparedTemps& prepared() {
@@ -404,7 +404,7 @@ std::function<void()> temp_preparer(const std::string& path) {
     p.in_flight += ticket->creates;
     ++p.jobs;
     hint = p.last_size;
-    serial = p.serial++;
+    serial = ticket->creates ? p.serial++ : 0;
   }
   return [tmp_dir, hint, serial, ticket] {
     // Old feature files the last writes swapped out (replace_file): unlinked
@@ -424,12 +424,16 @@ std::function<void()> temp_preparer(const std::string& path) {
     }
     Prepared f;
     f.dir = tmp_dir;
-    // In one of two subdirectories, alternately: the file the write renames
-    // out of gfd-tmp/<x>/ was made a cycle earlier in the other one, so this
-    // create (tens of us on some overlayfs hosts) does not hold the directory
-    // lock that rename needs (profiles/write_prepare_ab.txt).  gfd-tmp/
-    // itself is not re-created: a missing one is the next write's business.
-    std::string sub = tmp_dir + (serial % 2 ? "/b" : "/a");
+    // Round-robin over one subdirectory more than files can be ready or
+    // being made (gfd-tmp/a, b, ...): writes take files in the order they
+    // were made, so the file a write swaps out of gfd-tmp/<x>/ - and the old
+    // feature file left there, which a later job unlinks - never shares <x>
+    // with a create or unlink in flight, and those (tens of us on some
+    // overlayfs hosts) never hold the directory lock the exchange needs.
+    // With two subdirectories and four files they did: exchange 4 -> 54 us
+    // on a slow-create box (profiles/write_prepare_ab.txt).  gfd-tmp/ itself
+    // is not re-created: a missing one is the next write's business.
+    std::string sub = tmp_dir + "/" + static_cast<char>('a' + serial % (max_prepared() + 1));
     f.fd = create_temp(sub, 0644, &f.name);
     if (f.fd < 0 && errno == ENOENT && ::mkdir(sub.c_str(), 0755) == 0) f.fd = create_temp(sub, 0644, &f.name);
     if (f.fd >= 0) {

@@ -35,7 +35,7 @@ def _fds(pid: int) -> tuple[int, int]:
     # descriptors (the temp output file, an amd-smi device node), a leak
     # raises the floor.  The window must catch the daemon between cycles at
     # least once (see the per-cycle interval below).  Prepared temporary
-    # files (gfd-tmp/a|b/gfd-*, up to four kept open between cycles by design,
+    # files (gfd-tmp/<a-e>/gfd-*, up to four kept open between cycles by design,
     # src/lm/labels.cpp PreparedTemps) are counted apart: how many are ready
     # at a sample depends on timing, not on leaks - that made the floor
     # 15 or 16 from run to run.  Returns (floor without them, most of them).

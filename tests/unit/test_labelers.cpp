@@ -439,11 +439,12 @@ void prepare_then_write(const Labels& l, const std::string& path) {
   if (auto job = lm::temp_preparer(path)) job();
   lm::write_to_file(l, path);
 }
-// Prepared files: gfd-tmp/{a,b}/gfd-XXXXXX.
+// Prepared files: gfd-tmp/<a-e>/gfd-XXXXXX.
 std::vector<std::string> prepared_files(const std::string& dir) {
   std::vector<std::string> out;
-  for (const char* sub : {"/gfd-tmp/a", "/gfd-tmp/b"})
-    for (const auto& n : fs::list_dir(dir + sub)) out.push_back(dir + sub + "/" + n);
+  for (const auto& sub : fs::list_dir(dir + "/gfd-tmp"))
+    for (const auto& n : fs::list_dir(dir + "/gfd-tmp/" + sub)) out.push_back(dir + "/gfd-tmp/" + sub + "/" + n);
+  std::sort(out.begin(), out.end());
   return out;
 }
 }  // namespace
@@ -458,9 +459,10 @@ TEST(WriteToFile_UsesPreparedTemporaryFiles) {
     if (auto job = lm::temp_preparer(path)) job();
   auto ready = prepared_files(dir);
   EXPECT_EQ(ready.size(), static_cast<size_t>(4));
-  // Alternately in the two subdirectories (a write renames out of one while
-  // the next is made in the other).
-  EXPECT_EQ(fs::list_dir(tmp + "/a").size(), static_cast<size_t>(2));
+  // Round-robin over five subdirectories (a write swaps out of one while
+  // the next files are made in others).
+  for (const char* sub : {"/a", "/b", "/c", "/d"}) EXPECT_EQ(fs::list_dir(tmp + sub).size(), static_cast<size_t>(1));
+  EXPECT_FALSE(fs::exists(tmp + "/e"));
   struct stat st;
   EXPECT_TRUE(stat(ready[0].c_str(), &st) == 0);
   EXPECT_EQ(static_cast<long>(st.st_size), 0L);

@@ -283,8 +283,6 @@ def main() -> int:
                 # sleeps 60 s), each starting on cold, down-clocked cores.
                 if a.cold_cycles > 1:
                     cold = _daemon_loop(binary, loop_args, a.cold_cycles, interval="1s")
-                    extras["cold_cycle_inline_tasks"] = _daemon_loop(binary, loop_args, a.cold_cycles, interval="1s",
-                                                                    env={"GFD_CYCLE_TASKS": "inline"})
                 if backend == "amdsmi":
                     extras["amdsmi_per_cycle_session"] = _time_variant(
                         _session_args("amdsmi", n, out, None, ["--amdsmi-session=per-cycle"]), max(10, a.steps // 10), 2)

@@ -26,7 +26,6 @@
 #include "sriov/sriov.h"
 #include "util/duration.h"
 #include "util/error.h"
-#include "util/affinity.h"
 #include "util/log.h"
 
 namespace py = pybind11;
@@ -103,20 +102,21 @@ py::dict device_to_dict(const resource::Device& d) {
 // exactly as `start` does, then any number of labeling cycles.
 class Session {
  public:
-  Session(const std::vector<std::string>& args, const std::map<std::string, std::string>& env, bool use_env) {
-    // The daemon's start-up CPU policy (gfd_main), once per process, before
-    // the first session starts any pool worker (util/affinity.h).
-    static const std::string pinned = affinity::pin_to_current_l3();
-    (void)pinned;
+  // A library leaves the host process's CPU placement alone: the daemon's
+  // opt-in --cpu-affinity is applied by gfd_main only, never here.
+  Session(const std::vector<std::string>& args, const std::map<std::string, std::string>& env, bool use_env,
+          bool amdsmi_library_only) {
     auto ctx = cli::Context::parse(cli::gfd_flags(), args, use_env ? &env : nullptr);
     config_ = cli::load_config(ctx);
     config::disable_resource_renaming(config_);
+    config_.amdsmi_library_only = amdsmi_library_only;
     manager_ = resource::new_manager(config_);
     sriov_ = sriov::new_sriov_lib(config_.sysfs_root());
     timestamp_ = lm::NewTimestampLabeler(config_);
   }
   // A loop-mode session's cycles leave the next cycle's temporary file
-  // prepared (lm::temp_preparer); do not leave it behind.
+  // prepared and the old feature file to unlink (lm::temp_preparer); do not
+  // leave them behind.
   ~Session() { lm::discard_prepared_temps(); }
   Session(const Session&) = delete;
   Session& operator=(const Session&) = delete;
@@ -216,11 +216,14 @@ PYBIND11_MODULE(_gfd, m) {
   m.def("sanitize_label_value", &lm::sanitize_label_value);
 
   py::class_<Session>(m, "Session")
-      .def(py::init([](const std::vector<std::string>& args, py::object env) {
-             if (env.is_none()) return std::make_unique<Session>(args, std::map<std::string, std::string>{}, false);
-             return std::make_unique<Session>(args, env.cast<std::map<std::string, std::string>>(), true);
+      .def(py::init([](const std::vector<std::string>& args, py::object env, bool amdsmi_library_only) {
+             if (env.is_none())
+               return std::make_unique<Session>(args, std::map<std::string, std::string>{}, false, amdsmi_library_only);
+             return std::make_unique<Session>(args, env.cast<std::map<std::string, std::string>>(), true,
+                                              amdsmi_library_only);
            }),
-           py::arg("args") = std::vector<std::string>{}, py::arg("env") = py::none())
+           py::arg("args") = std::vector<std::string>{}, py::arg("env") = py::none(),
+           py::arg("amdsmi_library_only") = false)
       .def("cycle", &Session::cycle, py::arg("write") = true)
       .def("bench", &Session::bench, py::arg("steps"), py::arg("warmup") = 0, py::arg("write") = true)
       .def("bench_phases", &Session::bench_phases)

@@ -4,7 +4,6 @@
 #include <time.h>
 
 #include <cerrno>
-#include <cstdlib>
 #include <functional>
 #include <cstdio>
 
@@ -156,42 +155,17 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
     sriov_ns = trace::now_ns() - s0;
   };
   // Both on one worker, in that order: two workers measured slower (each
-  // task 1.5-4x longer on the second, colder core).  GFD_CYCLE_TASKS=split
-  // submits them separately, =inline runs both on this thread (facts when
-  // the labeler needs them, the scan after it) - for A/B measurements.
-  enum class Tasks { sequence, split, inline_ };
-  static const Tasks mode = [] {
-    const char* v = std::getenv("GFD_CYCLE_TASKS");
-    std::string m = v ? v : "";
-    return m == "split" ? Tasks::split : m == "inline" ? Tasks::inline_ : Tasks::sequence;
-  }();
-  // Loop mode: the same worker then creates the temporary file of a later
-  // cycle's write (lm::temp_preparer) - never waited for, so it runs after
-  // the two even if this thread took them over.
-  std::function<void()> prepare_temp;
-  if (write && !config.oneshot()) prepare_temp = lm::temp_preparer(config.output_file());
-  WorkerPool::Task facts_task, sriov_task;
-  bool facts_done = false;
-  if (mode == Tasks::split) {
-    facts_task = WorkerPool::instance().submit(read_facts);
-    sriov_task = WorkerPool::instance().submit(scan_sriov);
-    if (prepare_temp) WorkerPool::instance().submit(std::move(prepare_temp));
-    prepare_temp = nullptr;
-  } else if (mode == Tasks::sequence) {
-    std::vector<std::function<void()>> fns{read_facts, scan_sriov};
-    if (prepare_temp) fns.push_back(std::move(prepare_temp));
-    prepare_temp = nullptr;
-    auto seq = WorkerPool::instance().submit_sequence(std::move(fns));
-    facts_task = seq[0];
-    sriov_task = seq[1];
-  }
+  // task 1.5-4x longer on the second, colder core; profiles/ab_cycle_tasks.txt).
+  // Loop mode: the same worker then unlinks the old feature file and creates
+  // the temporary file of a later cycle's write (lm::temp_preparer) - never
+  // waited for, so it runs after the two even if this thread took them over.
+  std::vector<std::function<void()>> fns{read_facts, scan_sriov};
+  if (write && !config.oneshot())
+    if (auto prepare = lm::temp_preparer(config.output_file())) fns.push_back(std::move(prepare));
+  auto seq = WorkerPool::instance().submit_sequence(std::move(fns));
+  WorkerPool::Task facts_task = seq[0], sriov_task = seq[1];
   auto join_facts = [&]() -> const lm::NodeFacts& {
-    if (mode != Tasks::inline_) {
-      facts_task.run_or_wait();
-    } else if (!facts_done) {
-      read_facts();
-      facts_done = true;
-    }
+    facts_task.run_or_wait();
     return facts;
   };
   lm::LabelerPtr device;
@@ -199,18 +173,12 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
     device = GFD_WRAP("error creating device labeler", lm::NewDeviceLabeler(manager, config, join_facts));
   } catch (...) {
     // Neither task may outlive this frame (they write its locals).
-    if (mode != Tasks::inline_) {
-      facts_task.cancel_or_wait();
-      sriov_task.cancel_or_wait();
-    }
+    facts_task.cancel_or_wait();
+    sriov_task.cancel_or_wait();
     throw;
   }
-  if (mode != Tasks::inline_) {
-    facts_task.cancel_or_wait();  // no devices: the labeler never needed them
-    sriov_task.run_or_wait();
-  } else {
-    scan_sriov();
-  }
+  facts_task.cancel_or_wait();  // no devices: the labeler never needed them
+  sriov_task.run_or_wait();
   trace::record("facts(overlapped)", facts_ns);
   trace::record("sriov(overlapped)", sriov_ns);
   if (sriov_error) {
@@ -237,7 +205,6 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
       throw Error("error writing file '" + config.output_file() + "': " + e.what());
     }
   }
-  if (prepare_temp) prepare_temp();  // GFD_CYCLE_TASKS=inline: on this thread, after the write
   r.total_ns = trace::now_ns() - t0;
   r.phases = trace::phases();
   return r;
@@ -296,6 +263,7 @@ struct ProcessTimeline {
 }  // namespace
 
 void start(const Context& ctx, SignalWatcher& sigs) {
+  bool swept = false;
   for (;;) {
     log::printf("Loading configuration.");
     config::Config c;
@@ -306,6 +274,18 @@ void start(const Context& ctx, SignalWatcher& sigs) {
     }
     config::disable_resource_renaming(c);
     log::printf("\nRunning with config:\n%s", config::to_json(c).c_str());
+    // A process killed without its exit cleanup (OOM, SIGKILL, node crash)
+    // left its temporary files in <dir>/gfd-tmp: remove them before the
+    // first write.  Loop mode only - a oneshot Job leaves the directory to
+    // the DaemonSet that may share it.
+    if (!swept && !c.oneshot() && !c.output_file().empty()) {
+      swept = true;
+      try {
+        lm::sweep_temp_dir(c.output_file());
+      } catch (const std::exception& e) {
+        log::printf("Warning: %s", e.what());
+      }
+    }
     g_timeline.enabled = c.trace_timing();
     if (!g_timeline.configured_ns) g_timeline.configured_ns = trace::now_ns();
 
@@ -345,8 +325,15 @@ int gfd_main(int argc, char** argv) {
     return 0;
   }
   g_timeline.main_ns = trace::now_ns();
-  // Before any thread exists: workers inherit the mask (util/affinity.h).
-  if (std::string pinned = affinity::pin_to_current_l3(); !pinned.empty()) log::printf("CPU affinity: %s", pinned.c_str());
+  // Opt-in (--cpu-affinity=l3), before any thread exists: workers inherit
+  // the mask (util/affinity.h).
+  std::string placement = ctx.String("cpu-affinity");
+  if (placement == "l3") {
+    if (std::string pinned = affinity::pin_to_current_l3(); !pinned.empty()) log::printf("CPU affinity: %s", pinned.c_str());
+  } else if (placement != "none") {
+    log::printf("Error: unknown --cpu-affinity '%s' (expected none or l3)", placement.c_str());
+    return 1;
+  }
   int rc = 0;
   {
     log::printf("Starting OS watcher.");

@@ -116,6 +116,10 @@ struct Config {
   Flags flags;
   Resources resources;
   Sharing sharing;
+  // Test hook, not a flag or config key (the Python bindings set it): the
+  // amd-smi backend answers every query through the library instead of the
+  // amdgpu attributes it reads directly for unpartitioned GPUs.
+  bool amdsmi_library_only = false;
 
   // Convenience accessors; defaults apply if a field was never populated.
   std::string mig_strategy() const { return flags.mig_strategy.value_or(kMigStrategyNone); }

@@ -720,7 +720,13 @@ class Parser {
           continue;
         }
         if (sq) {
-          if (c == '\'') sq = false;  // '' re-opens on the next character
+          // '' is an escaped quote: the scalar stays open ("'''['" is "'[").
+          if (c == '\'') {
+            if (i + 1 < t.size() && t[i + 1] == '\'')
+              ++i;
+            else
+              sq = false;
+          }
           continue;
         }
         if (c == ' ' || c == '\t' || c == '\n') continue;

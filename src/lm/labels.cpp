@@ -7,11 +7,10 @@
 
 #include <chrono>
 #include <condition_variable>
-#include <deque>
 #include <functional>
 #include <mutex>
-#include <optional>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include <cerrno>
@@ -21,7 +20,6 @@
 
 #include "util/error.h"
 #include "util/fs.h"
-#include "util/pool.h"
 #include "util/trace.h"
 
 namespace gfd::lm {
@@ -124,15 +122,7 @@ int create_temp(const std::string& dir, unsigned perm, std::string* name) {
 // rename is a plain directory update (0.03 ms).  Overlayfs is included
 // because its upper layer is commonly ext4 (the call passes through).
 // Elsewhere (tmpfs, xfs, ...) the extra allocation would be pure cost.
-// GFD_WRITE_PREALLOC=always|never overrides the file-system check (A/B).
 bool wants_prealloc(int fd) {
-  static const int forced = [] {
-    const char* v = std::getenv("GFD_WRITE_PREALLOC");
-    if (!v) return -1;
-    std::string s(v);
-    return s == "always" ? 1 : s == "never" ? 0 : -1;
-  }();
-  if (forced >= 0) return forced == 1;
   struct statfs sf;
   if (::fstatfs(fd, &sf) != 0) return false;
   constexpr unsigned long kExt4 = 0xEF53, kOverlay = 0x794c7630;
@@ -161,151 +151,88 @@ std::string render(const Labels& labels) {
 
 namespace {
 
-// Temporary files created ahead of the writes that use them (loop mode):
-// the daemon's cycle hands temp_preparer()'s job to the worker that already
-// runs its node facts and SR-IOV scan, after those, so the next cycle's file
-// is created - and, where the write preallocates (wants_prealloc), its blocks
-// allocated beyond EOF for the last size (FALLOC_FL_KEEP_SIZE) - while this
-// cycle enumerates and writes.  A write then is write + close + rename; the
-// ~7 us create plus allocation (more on some hosts' overlayfs) are off its
-// critical path (profiles/write_prepare_ab.txt).  At most kMaxPrepared files
-// are ready or being made; a write takes the oldest in its directory and
-// creates its own when none is ready, never waiting for a worker.
+// Loop-mode state of the writer, kept between cycles: at most one temporary
+// file made ahead of the write that will use it, and at most one old feature
+// file waiting to be unlinked.  Both live in <dir>/gfd-tmp/, which the daemon
+// empties at start-up (sweep_temp_dir) and removes at exit, so a crash leaves
+// at most these two files behind until the next start.
 //
-// Four, not two: back to back, a worker's create (and the unlink of the file
-// the last exchange swapped out) can take longer than a whole cycle, and
-// with two ready some writes still made their own file - bench p90
-// 0.024-0.036 -> 0.021-0.024 ms with four, p50 and cold cycles unchanged
-// (profiles/write_prepare_ab.txt, last section).  An empty file and a
-// descriptor each.
-constexpr size_t kMaxPrepared = 4;
-
-// GFD_WRITE_PREPARE_MAX=N (1-8): another bound (A/B measurements).
-size_t max_prepared() {
-  static const size_t n = [] {
-    const char* v = std::getenv("GFD_WRITE_PREPARE_MAX");
-    long x = v ? std::strtol(v, nullptr, 10) : 0;
-    return x >= 1 && x <= 8 ? static_cast<size_t>(x) : kMaxPrepared;
-  }();
-  return n;
-}
-
-struct Prepared {
-  std::string dir, name;
-  int fd = -1;
-  size_t allocated = 0;  // bytes of blocks preallocated
-};
-
-// Old feature files swapped out of place by a write's RENAME_EXCHANGE, now
-// under a temporary name in gfd-tmp/<x>/, waiting for a worker to unlink them.
-struct Retired {
-  std::string dir, name;
-};
-
-struct PreparedTemps {
+// Why each exists, measured with the daemon's cycles 1 s apart (the deployed
+// cadence is 60 s, so every cycle starts cold):
+//   * The prepared file: a cold create on the box's overlayfs costs 0.1-0.2
+//     ms, more than the rest of the write.  The cycle's worker makes the next
+//     file after its node-facts and SR-IOV tasks, off the critical path:
+//     write p50 0.055-0.090 ms vs 0.147-0.282 ms creating in the write
+//     (profiles/writer_ab_r3.txt).
+//   * The exchange: a rename over the old feature file frees its inode
+//     inside rename(2); on ext4 (the usual file system of NFD's features.d
+//     hostPath) that is most of a cold replace, 0.34-0.58 ms vs 0.03 ms for
+//     renameat2(RENAME_EXCHANGE), which leaves the old file under the
+//     temporary name for the next worker job to unlink
+//     (profiles/rename_exchange_ab.txt).  Readers see the old file or the
+//     new one under `path`, never neither, exactly as with a rename.
+struct WriterState {
   std::mutex mu;
-  std::condition_variable cv;  // in_flight or jobs dropped
-  std::deque<Prepared> ready;
-  std::vector<Retired> retired;
-  std::string no_exchange_dir;  // temporary directory whose file system refused RENAME_EXCHANGE
-  size_t in_flight = 0;  // files being made by preparer jobs handed out and not yet finished or dropped
-  size_t jobs = 0;       // preparer jobs handed out and not yet finished or dropped
-  size_t last_size = 0;  // of the last write: the next file's preallocation
-  size_t serial = 0;     // files handed out to be made so far (picks the subdirectory)
+  std::condition_variable cv;  // job finished
+  std::string dir;             // gfd-tmp/ of the prepared file
+  std::string name;            // the prepared file ("" = none)
+  int fd = -1;
+  size_t allocated = 0;        // bytes preallocated beyond EOF
+  std::string retired;         // old feature file to unlink ("" = none)
+  std::string no_exchange_dir; // whose file system refused RENAME_EXCHANGE
+  bool job = false;            // a preparer job is handed out, not yet finished or dropped
+  size_t last_size = 0;        // of the last write: the next file's preallocation
 };
 
-PreparedTemps& prepared() {
-  static auto* p = new PreparedTemps;  // never destroyed: a worker may still use it at exit
-  return *p;
+WriterState& writer() {
+  static auto* w = new WriterState;  // never destroyed: a worker may still use it at exit
+  return *w;
 }
 
-void drop(Prepared& f) {
-  ::close(f.fd);
-  ::unlink(f.name.c_str());
-}
-
-// The oldest prepared file in `tmp_dir` (fd, name and preallocation), or -1;
-// prepared files of other directories are removed.
+// Takes the prepared file if it is in `tmp_dir` (fd, name, preallocation),
+// else -1; a prepared file elsewhere is removed.
 int take_prepared(const std::string& tmp_dir, std::string* name, size_t* allocated) {
-  PreparedTemps& p = prepared();
-  std::lock_guard<std::mutex> lk(p.mu);
-  while (!p.ready.empty()) {
-    Prepared f = std::move(p.ready.front());
-    p.ready.pop_front();
-    if (f.dir != tmp_dir) {
-      drop(f);
-      continue;
-    }
-    *name = std::move(f.name);
-    *allocated = f.allocated;
-    return f.fd;
+  WriterState& w = writer();
+  std::lock_guard<std::mutex> lk(w.mu);
+  if (w.fd < 0) return -1;
+  int fd = std::exchange(w.fd, -1);
+  std::string n = std::move(w.name);
+  w.name.clear();
+  if (w.dir != tmp_dir) {
+    ::close(fd);
+    ::unlink(n.c_str());
+    return -1;
   }
-  return -1;
+  *name = std::move(n);
+  *allocated = w.allocated;
+  return fd;
 }
 
-// Counts a handed-out preparer job (and the file it makes, if it makes one)
-// until it has run (finish) or was dropped unrun (the job, and with it this
-// ticket, destroyed).
-struct InFlight {
-  bool creates = false;
-  bool finished = false;
-  void finish() {
-    PreparedTemps& p = prepared();
-    std::lock_guard<std::mutex> lk(p.mu);
-    if (finished) return;
-    finished = true;
-    p.in_flight -= creates;
-    --p.jobs;
-    p.cv.notify_all();
-  }
-  ~InFlight() { finish(); }
-};
-
-// Replace `path` with the finished temporary file `tmpl`.
-//
-// In loop mode (a prepared file, so a preparer job comes every cycle) the two
-// names are swapped with renameat2(RENAME_EXCHANGE) and the old feature file,
-// now under the temporary name, is left for the next preparer job to unlink.
-// A rename over the old file drops its inode inside the call - on ext4 (the
-// usual file system of NFD's features.d hostPath) that eviction is most of a
-// cold replace: 0.46 ms vs 0.05 ms for the exchange, cycles 1 s apart
-// (profiles/rename_exchange_ab.txt).  Readers see the same thing either way:
-// the old file or the new one under `path`, never neither.  No feature file
-// yet (first write), a file system without the exchange, or something other
-// than a file at `path` (a directory must fail like rename(2) would, not be
-// swapped into gfd-tmp/): a plain rename.  GFD_WRITE_EXCHANGE=never: always a
-// plain rename (A/B).  Returns 0 or an errno.
+// Replaces `path` by the finished temporary file `tmpl`.  `exchange` (loop
+// mode): swap the two names when `path` is a regular file and no old file
+// still waits to be unlinked; the old file is then left under `tmpl` for the
+// next preparer job.  Anything else - no feature file yet, a directory or
+// other non-file at `path` (which must fail like rename(2) would), a file
+// system without the exchange - is a plain rename.  Returns 0 or an errno.
 int replace_file(const std::string& tmpl, const std::string& path, const std::string& tmp_dir, bool exchange) {
-  static const bool never = [] {
-    const char* v = std::getenv("GFD_WRITE_EXCHANGE");
-    return v && std::string(v) == "never";
-  }();
-  PreparedTemps& p = prepared();
-  if (exchange && !never) {
-    {
-      std::lock_guard<std::mutex> lk(p.mu);
-      exchange = p.no_exchange_dir != tmp_dir;
+  WriterState& w = writer();
+  if (exchange) {
+    std::lock_guard<std::mutex> lk(w.mu);
+    exchange = w.retired.empty() && w.no_exchange_dir != tmp_dir;
+  }
+  struct stat st;
+  if (exchange && ::lstat(path.c_str(), &st) == 0 && S_ISREG(st.st_mode)) {
+    if (::renameat2(AT_FDCWD, tmpl.c_str(), AT_FDCWD, path.c_str(), RENAME_EXCHANGE) == 0) {
+      std::lock_guard<std::mutex> lk(w.mu);
+      w.retired = tmpl;
+      return 0;
     }
-    if (exchange && ::renameat2(AT_FDCWD, tmpl.c_str(), AT_FDCWD, path.c_str(), RENAME_EXCHANGE) == 0) {
-      struct stat st;
-      if (::lstat(tmpl.c_str(), &st) == 0 && !S_ISDIR(st.st_mode)) {
-        std::lock_guard<std::mutex> lk(p.mu);
-        p.retired.push_back({tmp_dir, tmpl});
-        return 0;
-      }
-      // Swapped a directory out of `path`: put it back, rename decides.
-      if (::renameat2(AT_FDCWD, tmpl.c_str(), AT_FDCWD, path.c_str(), RENAME_EXCHANGE) != 0) return errno;
-    } else if (exchange && (errno == EINVAL || errno == ENOSYS || errno == EOPNOTSUPP)) {
-      std::lock_guard<std::mutex> lk(p.mu);
-      p.no_exchange_dir = tmp_dir;
+    if (errno == EINVAL || errno == ENOSYS || errno == EOPNOTSUPP) {
+      std::lock_guard<std::mutex> lk(w.mu);
+      w.no_exchange_dir = tmp_dir;
     }
   }
   return ::rename(tmpl.c_str(), path.c_str()) == 0 ? 0 : errno;
-}
-
-void unlink_retired(std::vector<Retired>& files) {
-  for (const auto& f : files) ::unlink(f.name.c_str());
-  files.clear();
 }
 
 // One attempt: false (nothing thrown, nothing left behind) when a prepared
@@ -328,6 +255,8 @@ bool write_atomically_once(const std::string& path, const std::string& tmp_dir, 
     }
     fd = create_temp(tmp_dir, perm, &tmpl);
   }
+  // Failures remove gfd-tmp/ like the reference (labels.go:81-85): a
+  // prepared file lost with it is a vanished prepared file (retried).
   if (fd < 0) {
     int e = errno;
     fs::remove_all(tmp_dir);
@@ -368,101 +297,89 @@ bool write_atomically_once(const std::string& path, const std::string& tmp_dir, 
   return true;
 }
 
+std::string temp_dir_of(const std::string& path) { return fs::join(fs::dirname(fs::absolute(path)), "gfd-tmp"); }
+
 }  // namespace
 
 void write_file_atomically(const std::string& path, const std::string& contents, unsigned perm) {
-  std::string abs = fs::absolute(path);
-  std::string tmp_dir = fs::join(fs::dirname(abs), "gfd-tmp");
+  std::string tmp_dir = temp_dir_of(path);
   // Prepared files are created 0644 - the feature file's mode.
   if (!write_atomically_once(path, tmp_dir, contents, perm, perm == 0644))
     write_atomically_once(path, tmp_dir, contents, perm, false);
-  PreparedTemps& p = prepared();
-  std::lock_guard<std::mutex> lk(p.mu);
-  p.last_size = contents.size();
+  WriterState& w = writer();
+  std::lock_guard<std::mutex> lk(w.mu);
+  w.last_size = contents.size();
 }
 
 std::function<void()> temp_preparer(const std::string& path) {
-  // GFD_WRITE_PREPARE=never: every write creates its own file (A/B).
-  static const bool never = [] {
-    const char* v = std::getenv("GFD_WRITE_PREPARE");
-    return v && std::string(v) == "never";
-  }();
-  if (never || path.empty()) return {};
-  std::string tmp_dir = fs::join(fs::dirname(fs::absolute(path)), "gfd-tmp");
-  PreparedTemps& p = prepared();
-  size_t hint, serial;
-  auto ticket = std::make_shared<InFlight>();
+  if (path.empty()) return {};
+  std::string tmp_dir = temp_dir_of(path);
+  WriterState& w = writer();
+  size_t hint;
   {
-    std::lock_guard<std::mutex> lk(p.mu);
-    size_t have = p.in_flight;
-    for (const auto& f : p.ready) have += f.dir == tmp_dir;
-    ticket->creates = have < max_prepared();
-    if (!ticket->creates && p.retired.empty()) {
-      ticket->finished = true;  // never handed out
-      return {};
-    }
-    p.in_flight += ticket->creates;
-    ++p.jobs;
-    hint = p.last_size;
-    serial = ticket->creates ? p.serial++ : 0;
+    std::lock_guard<std::mutex> lk(w.mu);
+    if (w.job || (w.fd >= 0 && w.dir == tmp_dir && w.retired.empty())) return {};
+    w.job = true;
+    hint = w.last_size;
   }
-  return [tmp_dir, hint, serial, ticket] {
-    // Old feature files the last writes swapped out (replace_file): unlinked
-    // here, off the write's path.  After this job's create, which the next
-    // write may need sooner.
-    std::vector<Retired> old;
-    auto take_retired = [&] {
-      PreparedTemps& q = prepared();
+  // Clears `job` when the job has run or was dropped unrun.
+  std::shared_ptr<void> ticket(nullptr, [](void*) {
+    WriterState& q = writer();
+    std::lock_guard<std::mutex> lk(q.mu);
+    q.job = false;
+    q.cv.notify_all();
+  });
+  return [tmp_dir, hint, ticket] {
+    WriterState& q = writer();
+    std::string old;
+    bool make;
+    {
       std::lock_guard<std::mutex> lk(q.mu);
       old.swap(q.retired);
-    };
-    if (!ticket->creates) {
-      take_retired();
-      unlink_retired(old);
-      ticket->finish();
-      return;
+      make = q.fd < 0;
     }
-    Prepared f;
-    f.dir = tmp_dir;
-    // Round-robin over one subdirectory more than files can be ready or
-    // being made (gfd-tmp/a, b, ...): writes take files in the order they
-    // were made, so the file a write swaps out of gfd-tmp/<x>/ - and the old
-    // feature file left there, which a later job unlinks - never shares <x>
-    // with a create or unlink in flight, and those (tens of us on some
-    // overlayfs hosts) never hold the directory lock the exchange needs.
-    // With two subdirectories and four files they did: exchange 4 -> 54 us
-    // on a slow-create box (profiles/write_prepare_ab.txt).  gfd-tmp/ itself
-    // is not re-created: a missing one is the next write's business.
-    std::string sub = tmp_dir + "/" + static_cast<char>('a' + serial % (max_prepared() + 1));
-    f.fd = create_temp(sub, 0644, &f.name);
-    if (f.fd < 0 && errno == ENOENT && ::mkdir(sub.c_str(), 0755) == 0) f.fd = create_temp(sub, 0644, &f.name);
-    if (f.fd >= 0) {
-      if (hint > 0 && wants_prealloc(f.fd) &&
-          ::fallocate(f.fd, FALLOC_FL_KEEP_SIZE, 0, static_cast<off_t>(hint)) == 0)
-        f.allocated = hint;
-      PreparedTemps& q = prepared();
-      std::lock_guard<std::mutex> lk(q.mu);
-      q.ready.push_back(std::move(f));
-    }
-    take_retired();
-    unlink_retired(old);
-    ticket->finish();
+    if (!old.empty()) ::unlink(old.c_str());
+    if (!make) return;
+    // gfd-tmp/ itself is not re-created: a missing one is the next write's
+    // business.
+    std::string name;
+    int fd = create_temp(tmp_dir, 0644, &name);
+    if (fd < 0) return;
+    size_t allocated = 0;
+    if (hint > 0 && wants_prealloc(fd) && ::fallocate(fd, FALLOC_FL_KEEP_SIZE, 0, static_cast<off_t>(hint)) == 0)
+      allocated = hint;
+    std::lock_guard<std::mutex> lk(q.mu);
+    q.dir = tmp_dir;
+    q.name = std::move(name);
+    q.fd = fd;
+    q.allocated = allocated;
   };
 }
 
 void discard_prepared_temps() {
-  PreparedTemps& p = prepared();
-  std::unique_lock<std::mutex> lk(p.mu);
+  WriterState& w = writer();
+  std::unique_lock<std::mutex> lk(w.mu);
   // A job handed out runs soon (or is dropped): its file must not outlive
   // this call.  Bounded all the same - exit must not hang on a worker stuck
-  // in the file system; its file would then stay behind in gfd-tmp/.
-  // system_clock: a steady_clock wait is pthread_cond_clockwait, which GCC
-  // 11's ThreadSanitizer does not intercept (it then reports the job's lock
-  // of `mu` as a double lock); a clock step only moves this safety bound.
-  p.cv.wait_until(lk, std::chrono::system_clock::now() + std::chrono::seconds(5), [&] { return p.jobs == 0; });
-  for (auto& f : p.ready) drop(f);
-  p.ready.clear();
-  unlink_retired(p.retired);
+  // in the file system; a file it makes later stays in gfd-tmp/ until the
+  // next start's sweep.  system_clock: a steady_clock wait is
+  // pthread_cond_clockwait, which GCC 11's ThreadSanitizer does not intercept.
+  w.cv.wait_until(lk, std::chrono::system_clock::now() + std::chrono::seconds(1), [&] { return !w.job; });
+  if (w.fd >= 0) {
+    ::close(w.fd);
+    ::unlink(w.name.c_str());
+    w.fd = -1;
+    w.name.clear();
+  }
+  if (!w.retired.empty()) ::unlink(w.retired.c_str());
+  w.retired.clear();
+}
+
+void sweep_temp_dir(const std::string& path) {
+  if (path.empty()) return;
+  std::string tmp_dir = temp_dir_of(path);
+  if (int e = fs::remove_all(tmp_dir))
+    throw Error("failed to remove stale temporary directory '" + tmp_dir + "': " + fs::errno_str(e));
 }
 
 void write_to_file(const Labels& labels, const std::string& path) {
@@ -482,7 +399,7 @@ void write_to_file(const Labels& labels, const std::string& path) {
 void remove_output_file(const std::string& path) {
   discard_prepared_temps();
   std::string abs = fs::absolute(path);
-  std::string tmp_dir = fs::join(fs::dirname(abs), "gfd-tmp");
+  std::string tmp_dir = temp_dir_of(abs);
   if (int e = fs::remove_all(tmp_dir)) throw Error("failed to remove temporary output directory: " + fs::errno_str(e));
   if (::unlink(abs.c_str()) != 0) throw Error("failed to remove output file: " + fs::errno_str(errno));
 }

@@ -47,19 +47,25 @@ LabelerPtr merge(std::vector<LabelerPtr> labelers);
 std::string render(const Labels& labels);
 
 // Write labels to `path` atomically (temp file in <dir>/gfd-tmp, rename,
-// chmod 0644).  An empty path writes to stdout.  Throws gfd::Error.  A
-// temporary file prepared by temp_preparer()'s job is used if one is ready.
+// 0644).  An empty path writes to stdout.  Throws gfd::Error.  A temporary
+// file prepared by temp_preparer()'s job is used if one is ready; the write
+// that uses one (loop mode) swaps it with the old feature file
+// (RENAME_EXCHANGE) and leaves the old file for the next job to unlink.
 void write_to_file(const Labels& labels, const std::string& path);
 // Atomic write of arbitrary contents (labels.go:68-114).
 void write_file_atomically(const std::string& path, const std::string& contents, unsigned perm);
-// Loop mode: a job that creates the temporary file of a later write to
-// `path` (blocks preallocated for the last written size where the write
-// preallocates), for a worker to run while a cycle enumerates; empty when
-// enough files are prepared or GFD_WRITE_PREPARE=never.  The empty files
-// wait in <dir>/gfd-tmp until used.
+// Loop mode: a job for a worker to run while a cycle enumerates - it unlinks
+// the old feature file the last write swapped out and creates the temporary
+// file of the next write to `path` (blocks preallocated for the last written
+// size where the write preallocates).  Empty when there is nothing to do or
+// a job is still out.  At most one file of each kind waits in <dir>/gfd-tmp.
 std::function<void()> temp_preparer(const std::string& path);
-// Waits for handed-out jobs, then closes and removes every prepared file.
+// Waits (bounded) for a handed-out job, then removes the prepared file and
+// the old feature file.
 void discard_prepared_temps();
+// Start-up: removes <dir>/gfd-tmp left by a process that did not exit
+// cleanly (one GFD per node writes there, as the reference assumes).
+void sweep_temp_dir(const std::string& path);
 // Removes <dir>/gfd-tmp and the output file (main.go:212-232).
 void remove_output_file(const std::string& path);
 

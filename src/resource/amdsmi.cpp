@@ -254,14 +254,6 @@ void fix_market_name(AmdSmiLib& L, const std::string& root, ProcInfo& p) {
   if (p.market_name.empty() && p.device_id) p.market_name = device_name(p.device_id);
 }
 
-bool sysfs_values_enabled() {
-  static const bool on = [] {
-    const char* v = std::getenv("GFD_AMDSMI_SYSFS");
-    return !(v && std::string(v) == "0");
-  }();
-  return on;
-}
-
 // The only processor at its PCI address and in SPX mode: its per-cycle
 // values are the amdgpu attributes amd-smi reads for the same calls
 // (mem_info_vram_total for memory_total(VRAM), current_compute_partition /
@@ -689,7 +681,7 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
       }
     }
   }
-  const bool sysfs_values = sysfs_values_enabled();
+  const bool sysfs_values = opts_.sysfs_values;
 
   // One GPU's values and capabilities, always on one thread: amdgpu
   // serialises a device's queries on its own locks (amd-smi adds a

@@ -42,6 +42,7 @@ struct AmdSmiOptions {
   std::string root = "/";       // for the KFD generation check / sysfs hints
   DeviceFilter filter;
   int threads = 0;              // 0 = auto (one per physical GPU, max 8)
+  bool sysfs_values = true;     // false: every value through the library (test hook)
   VersionSources versions;  // its root is `root`
 };
 

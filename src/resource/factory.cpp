@@ -1,14 +1,11 @@
 #include "resource/factory.h"
 
-#include <cstdlib>
-
 #include "resource/amdsmi.h"
 #include "resource/managers.h"
 #include "resource/sysfs.h"
 #include "resource/versions.h"
 #include "util/error.h"
 #include "util/log.h"
-#include "util/strings.h"
 
 namespace gfd::resource {
 
@@ -35,7 +32,7 @@ AmdSmiOptions amdsmi_options(const config::Config& c) {
   o.root = c.sysfs_root();
   o.filter = DeviceFilter::parse(c.visible_devices());
   o.versions = version_sources(c);
-  if (const char* t = std::getenv("GFD_AMDSMI_THREADS"); t && *t) o.threads = static_cast<int>(str::parse_uint(t).value_or(0));
+  o.sysfs_values = !c.amdsmi_library_only;
   return o;
 }
 

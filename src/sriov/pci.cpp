@@ -238,12 +238,6 @@ std::vector<PCIDevice> SysfsAmdPCI::Devices() {
   constexpr size_t kChunk = 16;
   size_t chunk = kChunk;
   std::vector<uint32_t> known_device;  // aligned with misses: device ID from procfs, 0 = unknown
-  // GFD_PCI_COLD=sysfs: skip the procfs table and read every function's
-  // vendor from sysfs, spread over the pool (A/B measurements).
-  static const bool cold_sysfs = [] {
-    const char* v = std::getenv("GFD_PCI_COLD");
-    return v && std::string(v) == "sysfs";
-  }();
   // Functions bound to amdgpu (AMD's: its ID table names vendor 0x1002 only)
   // in a cold scan: their identity reads start on the pool at once and run
   // while this thread reads the procfs table (0.5-0.65 ms on a 367-function
@@ -259,17 +253,11 @@ std::vector<PCIDevice> SysfsAmdPCI::Devices() {
       if (armed) t->cancel_or_wait();
     }
   } early_guard{&early_task};
-  // GFD_PCI_AMDGPU=table: amdgpu's functions wait for the table too (A/B).
-  static const bool early_reads = [] {
-    const char* v = std::getenv("GFD_PCI_AMDGPU");
-    return !(v && std::string(v) == "table");
-  }();
-  if (misses.size() > kChunk && !cold_sysfs) {
+  if (misses.size() > kChunk) {
     int64_t tp = trace::now_ns();
     std::vector<char> miss(next.size(), 0);
     for (size_t m : misses) miss[m] = 1;
-    for (const auto& name : early_reads ? fs::list_dir(fs::join(root_, "sys/bus/pci/drivers/amdgpu"))
-                                        : std::vector<std::string>{}) {
+    for (const auto& name : fs::list_dir(fs::join(root_, "sys/bus/pci/drivers/amdgpu"))) {
       if (!bus_devfn(name)) continue;  // bind, unbind, module, ...
       auto it = std::lower_bound(next.begin(), next.end(), name,
                                  [](const std::pair<std::string, Identity>& e, const std::string& n) { return e.first < n; });
@@ -295,11 +283,6 @@ std::vector<PCIDevice> SysfsAmdPCI::Devices() {
     trace::record("pci.amdgpu", trace::now_ns() - tp);
     tp = trace::now_ns();
     auto table = proc_pci_functions(root_);
-    // GFD_PCI_PORTS=read: read AMD PCIe ports too (A/B measurements).
-    static const bool skip_ports = [] {
-      const char* v = std::getenv("GFD_PCI_PORTS");
-      return !(v && std::string(v) == "read");
-    }();
     trace::record("pci.proc_table", trace::now_ns() - tp);
     if (!table.empty()) {
       uint32_t amd = static_cast<uint32_t>(std::strtoul(kAmdVendorId, nullptr, 16));
@@ -310,7 +293,7 @@ std::vector<PCIDevice> SysfsAmdPCI::Devices() {
         if (v == table.end()) {
           amd_or_unknown.push_back(m);
           known_device.push_back(0);
-        } else if ((v->second.id >> 16) == amd && (v->second.id & 0xffff) != 0 && !(v->second.port && skip_ports)) {
+        } else if ((v->second.id >> 16) == amd && (v->second.id & 0xffff) != 0 && !v->second.port) {
           amd_or_unknown.push_back(m);
           known_device.push_back(v->second.id & 0xffff);
         }

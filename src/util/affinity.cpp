@@ -2,7 +2,6 @@
 
 #include <sched.h>
 
-#include <cstdlib>
 #include <vector>
 
 #include "util/fs.h"
@@ -24,7 +23,6 @@ std::vector<int> parse_cpu_list(const std::string& s) {
 }
 
 std::string pin_to_current_l3(const std::string& sys_root) {
-  if (const char* v = std::getenv("GFD_CPU_AFFINITY"); v && std::string(v) == "none") return "";
   int cpu = sched_getcpu();
   if (cpu < 0) return "";
   // The L3 is the cache index whose level is 3 (index3 on x86, but look).

@@ -2,8 +2,6 @@
 
 #include <algorithm>
 #include <atomic>
-#include <chrono>
-#include <cstdlib>
 
 namespace gfd {
 
@@ -13,31 +11,8 @@ WorkerPool& WorkerPool::instance() {
   return *pool;
 }
 
-namespace {
-// GFD_POOL_SPIN_US overrides the bound of the adaptive idle spin (0
-// disables it; A/B measurements).
-int64_t max_spin_ns_from_env() {
-  const char* v = std::getenv("GFD_POOL_SPIN_US");
-  if (!v || !*v) return 200000;
-  return static_cast<int64_t>(std::strtoul(v, nullptr, 10)) * 1000;
-}
 
-inline void cpu_relax() {
-#if defined(__x86_64__) || defined(__i386__)
-  __builtin_ia32_pause();
-#elif defined(__aarch64__)
-  asm volatile("yield");
-#endif
-}
-
-int64_t mono_ns() {
-  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
-      .count();
-}
-}  // namespace
-
-WorkerPool::WorkerPool(size_t max_workers)
-    : max_workers_(max_workers ? max_workers : 1), max_spin_ns_(max_spin_ns_from_env()) {}
+WorkerPool::WorkerPool(size_t max_workers) : max_workers_(max_workers ? max_workers : 1) {}
 
 WorkerPool::~WorkerPool() {
   {
@@ -72,14 +47,11 @@ void WorkerPool::wake_one() {
   // the per-cycle PCI scan took 180 us instead of 86 us once 8 workers
   // existed and took turns).
   if (idle_.empty()) return;
-  // The spinning worker first (it needs no system call to start), else the
-  // most recently parked one.
-  auto it = std::find_if(idle_.rbegin(), idle_.rend(), [](const Worker* x) { return x->spinning; });
-  Worker* w = it != idle_.rend() ? *it : idle_.back();
-  idle_.erase(it != idle_.rend() ? std::next(it).base() : idle_.end() - 1);
-  w->woken.store(true, std::memory_order_release);
+  Worker* w = idle_.back();
+  idle_.pop_back();
+  w->woken = true;
   ++waking_;
-  w->cv.notify_one();  // no system call when the worker is still spinning
+  w->cv.notify_one();
 }
 
 void WorkerPool::loop(Worker* w) {
@@ -87,33 +59,12 @@ void WorkerPool::loop(Worker* w) {
   --spawning_;
   for (;;) {
     while (queue_.empty() && !stop_) {
-      w->woken.store(false, std::memory_order_relaxed);
+      // Idle workers block at once: the daemon sleeps a minute between
+      // cycles, and a spinning worker would only burn a tenant's core.
+      w->woken = false;
       idle_.push_back(w);
-      // Adaptive spin (the heuristic of adaptive mutexes): when this
-      // worker's last wait for work was short - cycles back to back, as in
-      // a daemon with a short --sleep-interval or the benchmark - stay
-      // runnable for up to twice that long, polling the wake-up flag, before
-      // blocking; a blocked worker costs a futex wake-up plus the
-      // scheduler's latency on top of its task (profiles/pool_spin_ab.txt).
-      // A deployed daemon sleeps 60 s between cycles: its workers' waits
-      // are long, so they block at once and the spin costs nothing.
-      // One spinner at a time: several spinning lanes (a multi-GPU cycle)
-      // slowed the cycle's own thread more than their wake-ups cost
-      // (profiles/hybrid_8gpu_scaling.txt, "every worker spinning").
-      int64_t t0 = mono_ns();
-      if (max_spin_ns_ > 0 && !spinner_ && w->last_gap_ns >= 0 && w->last_gap_ns <= max_spin_ns_) {
-        spinner_ = true;
-        w->spinning = true;
-        lk.unlock();
-        int64_t until = t0 + std::min(max_spin_ns_, 2 * w->last_gap_ns + 5000);
-        while (!w->woken.load(std::memory_order_acquire) && mono_ns() < until) cpu_relax();
-        lk.lock();
-        w->spinning = false;
-        spinner_ = false;
-      }
-      w->cv.wait(lk, [&] { return w->woken.load(std::memory_order_relaxed) || stop_; });
-      w->last_gap_ns = mono_ns() - t0;
-      if (w->woken.load(std::memory_order_relaxed)) {
+      w->cv.wait(lk, [&] { return w->woken || stop_; });
+      if (w->woken) {
         --waking_;
       } else {
         idle_.erase(std::find(idle_.begin(), idle_.end(), w));  // stopping
@@ -263,13 +214,6 @@ void WorkerPool::parallel_for(size_t n, const std::function<void(size_t)>& fn, s
   if (error) std::rethrow_exception(error);
 }
 
-size_t gpu_lanes(size_t n_gpus) {
-  static const size_t forced = [] {
-    const char* v = std::getenv("GFD_GPU_LANES");
-    return v && *v ? static_cast<size_t>(std::strtoul(v, nullptr, 10)) : size_t{0};
-  }();
-  if (forced) return forced;
-  return std::max<size_t>(1, std::min<size_t>(8, n_gpus));
-}
+size_t gpu_lanes(size_t n_gpus) { return std::max<size_t>(1, std::min<size_t>(8, n_gpus)); }
 
 }  // namespace gfd

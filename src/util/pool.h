@@ -78,10 +78,7 @@ class WorkerPool {
  private:
   struct Worker {
     std::condition_variable cv;
-    // Set (under mu_) by wake_one; read without the lock while spinning.
-    std::atomic<bool> woken{false};
-    int64_t last_gap_ns = -1;  // how long the worker last waited for work (-1: never)
-    bool spinning = false;     // in its adaptive spin (guarded by mu_)
+    bool woken = false;  // set by wake_one (guarded by mu_)
   };
   void ensure_workers(size_t n);
   void wake_one();
@@ -96,19 +93,12 @@ class WorkerPool {
   size_t waking_ = 0;          // woken, not yet running
   size_t spawning_ = 0;        // threads created but not yet parked
   bool stop_ = false;
-  // Upper bound of the adaptive idle spin (see loop()); 0 disables it.
-  int64_t max_spin_ns_;
-  bool spinner_ = false;  // a worker is spinning (at most one does; guarded by mu_)
 };
 
 // Lanes for per-GPU work in one cycle: one GPU per lane, at most 8 (the
-// pool's size).  With the daemon pinned to one L3 domain and a spinning
-// worker, spreading even the light SPX path (a few attribute preads per
-// GPU) over one lane per GPU measured fastest back to back at 2, 4 and 8
-// GPUs (0.032 / 0.034 / 0.041 ms vs 0.034 / 0.040 / 0.043 with two GPUs per
-// lane) and the same after a 1 s sleep (profiles/hybrid_8gpu_scaling.txt);
-// round 1's two-per-lane rule came from an unpinned pool.  GFD_GPU_LANES=N
-// overrides it (measurements).
+// pool's size).  Spreading even the light SPX path (a few attribute preads
+// per GPU) over one lane per GPU measured fastest at 2, 4 and 8 GPUs, back
+// to back and after a 1 s sleep (profiles/hybrid_8gpu_scaling.txt).
 size_t gpu_lanes(size_t n_gpus);
 
 }  // namespace gfd

@@ -93,63 +93,123 @@ def test_loop_rewrites_file_with_constant_timestamp(binary, tmp_path):
     assert not (tmp_path / "gfd-tmp").exists()
 
 
-def _prepared(tmp: Path) -> list[Path]:  # gfd-tmp/<a-e>/gfd-XXXXXX
+def _temps(tmp: Path) -> list[tuple[Path, os.stat_result]]:  # gfd-tmp/gfd-XXXXXX
+    out = []
     try:
-        subs = [d for d in tmp.iterdir() if d.is_dir()]
+        names = sorted(tmp.iterdir())
     except FileNotFoundError:
         return []
-    return sorted(f for sub in subs for f in sub.iterdir())
+    for f in names:
+        try:
+            out.append((f, f.stat()))
+        except FileNotFoundError:  # unlinked by the worker meanwhile
+            pass
+    return out
 
 
-@pytest.mark.parametrize("prepare", ["default", "never", "no-exchange"])
-def test_loop_keeps_prepared_temporary_files(binary, tmp_path, prepare):
-    """Loop mode: between cycles gfd-tmp/{a-e}/ hold one to four (empty, 0644)
-    temporary files made for later cycles, which those cycles swap into
-    place, and at most one old feature file swapped out (RENAME_EXCHANGE)
-    that the next cycle's worker unlinks; with GFD_WRITE_PREPARE=never
-    gfd-tmp/ stays empty, as in the reference.  Either way exit removes
-    everything.  GFD_WRITE_EXCHANGE=never renames prepared files over the
-    feature file: no old one is left for the worker."""
+def _split(tmp: Path):
+    """(prepared, retired): prepared files are empty, the old feature file a
+    write swapped out holds labels."""
+    ready, old = [], []
+    for f, st in _temps(tmp):
+        (old if st.st_size else ready).append((f, st))
+    return ready, old
+
+
+def test_loop_keeps_one_prepared_file_and_at_most_one_old_file(binary, tmp_path):
+    """Loop mode: between cycles gfd-tmp/ holds one empty 0644 file made for
+    the next write, which that write swaps into place (RENAME_EXCHANGE), and
+    at most one old feature file swapped out, which the next cycle's worker
+    unlinks.  Exit removes everything (main.go:149-156)."""
     out = tmp_path / "gfd"
-    env = {"never": {"GFD_WRITE_PREPARE": "never"}, "no-exchange": {"GFD_WRITE_EXCHANGE": "never"}}.get(prepare)
-    p = _start(binary, ["--sleep-interval=200ms", *_base(tmp_path, out)], env=env)
     tmp = tmp_path / "gfd-tmp"
-
-    def split():  # (prepared, retired) - retired ones hold labels
-        ready, old = [], []
-        for f in _prepared(tmp):
-            try:
-                st = f.stat()
-            except FileNotFoundError:  # unlinked by the worker meanwhile
-                continue
-            (old if st.st_size else ready).append((f, st))
-        return ready, old
-
+    p = _start(binary, ["--sleep-interval=200ms", *_base(tmp_path, out)])
     try:
         assert _wait_for(out.exists), "first write"
-        if prepare != "never":
-            assert _wait_for(lambda: 1 <= len(split()[0]) <= 4), _prepared(tmp)
-            ready, old = split()
-            assert len(old) <= (1 if prepare == "default" else 0), old
+        assert _wait_for(lambda: len(_split(tmp)[0]) == 1), _temps(tmp)
+        for _ in range(3):
+            ready, old = _split(tmp)
+            assert len(ready) <= 1 and len(old) <= 1, _temps(tmp)
+            assert len(_temps(tmp)) <= 2
             for f, st in ready:
                 assert oct(st.st_mode & 0o777) == "0o644"
             inos = {st.st_ino for _, st in ready}
             m0 = out.stat().st_mtime_ns
             assert _wait_for(lambda: out.stat().st_mtime_ns > m0, timeout=5), "file not rewritten"
-            assert out.stat().st_ino in inos  # a prepared file became the feature file
-            assert _wait_for(lambda: 1 <= len(split()[0]) <= 4 and len(split()[1]) <= 1)
-            if prepare == "no-exchange":
-                assert split()[1] == []
-        else:
-            m0 = out.stat().st_mtime_ns
-            assert _wait_for(lambda: out.stat().st_mtime_ns > m0, timeout=5), "file not rewritten"
-            assert list(tmp.iterdir()) == []
+            if inos:
+                assert out.stat().st_ino in inos  # the prepared file became the feature file
         assert golden.parse_labels(out.read_text())["amd.com/gpu.product"] == "MOCKMODEL"
     finally:
         p.send_signal(signal.SIGTERM)
         p.communicate(timeout=10)
     assert p.returncode == 0
     assert not out.exists() and not tmp.exists()
+
+
+def test_sigkilled_daemons_leave_a_bounded_gfd_tmp(binary, tmp_path):
+    """A daemon killed without its exit cleanup (OOM, SIGKILL) leaves its
+    prepared and old files in gfd-tmp/; the next start sweeps them before its
+    first write, so restarts never accumulate files (the reference leaks one
+    temporary file per crash, labels.go:68-114)."""
+    out = tmp_path / "gfd"
+    tmp = tmp_path / "gfd-tmp"
+    for _ in range(3):
+        p = _start(binary, ["--sleep-interval=50ms", *_base(tmp_path, out)])
+        try:
+            # Several cycles: a prepared file and an old one are waiting.
+            assert _wait_for(lambda: out.exists() and len(_temps(tmp)) >= 1)
+            time.sleep(0.3)
+        finally:
+            p.kill()
+            p.wait(timeout=10)
+        assert 1 <= len(_temps(tmp)) <= 2, _temps(tmp)
+    stale = {f for f, _ in _temps(tmp)}
+    p = _start(binary, ["--sleep-interval=10s", *_base(tmp_path, out)])
+    try:
+        m0 = out.stat().st_mtime_ns
+        assert _wait_for(lambda: out.stat().st_mtime_ns > m0), "first cycle"
+        assert _wait_for(lambda: len(_temps(tmp)) == 1)  # the next write's file
+        left = _temps(tmp)
+        assert len(left) <= 2, left
+        assert not stale & {f for f, _ in left}, left
+    finally:
+        p.send_signal(signal.SIGTERM)
+        p.communicate(timeout=10)
+    assert p.returncode == 0
+    assert not out.exists() and not tmp.exists()
+
+
+def test_oneshot_leaves_gfd_tmp_alone(binary, tmp_path):
+    """Only the loop daemon sweeps gfd-tmp/ at start: a oneshot Job may share
+    the directory with a running DaemonSet."""
+    out = tmp_path / "gfd"
+    tmp = tmp_path / "gfd-tmp"
+    tmp.mkdir()
+    (tmp / "gfd-other").write_text("")
+    run_daemon(binary, "--oneshot", *_base(tmp_path, out), check=True)
+    assert [f.name for f in tmp.iterdir()] == ["gfd-other"]
+
+
+def test_exchange_never_swaps_a_directory_into_gfd_tmp(binary, tmp_path):
+    """Something other than a regular file at the output path (here a
+    directory that appears between cycles) makes the write fail like
+    rename(2) would; the directory is never swapped into gfd-tmp/ and
+    deleted with it."""
+    out = tmp_path / "gfd"
+    p = _start(binary, ["--sleep-interval=100ms", *_base(tmp_path, out)])
+    try:
+        assert _wait_for(lambda: out.exists() and len(_split(tmp_path / "gfd-tmp")[0]) == 1)
+        out.unlink()
+        out.mkdir()
+        (out / "keep").write_text("user data")
+        p.wait(timeout=10)  # the write fails: exit 1
+    finally:
+        if p.poll() is None:
+            p.kill()
+        _, err = p.communicate(timeout=10)
+    assert p.returncode == 1, err
+    assert "error moving temporary file" in err
+    assert (out / "keep").read_text() == "user data"
 
 
 @pytest.mark.parametrize("sig,name", [(signal.SIGINT, "interrupt"), (signal.SIGQUIT, "quit")])
@@ -508,3 +568,13 @@ def test_concurrent_reader_never_sees_a_partial_file(binary, tmp_path, mi355x_no
     finally:
         p.send_signal(signal.SIGTERM)
         p.communicate(timeout=30)
+
+
+def test_cpu_affinity_is_opt_in(binary, tmp_path):
+    """No CPU placement change unless asked (--cpu-affinity=l3); an unknown
+    value is an error."""
+    args = ["--oneshot", *_base(tmp_path, tmp_path / "gfd")]
+    assert "CPU affinity:" not in run_daemon(binary, *args, check=True).stderr
+    run_daemon(binary, "--cpu-affinity=l3", *args, check=True)
+    cp = run_daemon(binary, "--cpu-affinity=numa", *args)
+    assert cp.returncode == 1 and "unknown --cpu-affinity 'numa'" in cp.stderr

@@ -59,18 +59,16 @@ def test_sysfs_backend_agrees_with_amdsmi(amdsmi_devices, sysfs_devices):
         assert {k: a[k] for k in keys} == {k: s[k] for k in keys}
 
 
-def test_amdsmi_sysfs_values_match_library_calls(amdsmi_devices):
+def test_amdsmi_sysfs_values_match_library_calls(native, amdsmi_devices):
     """An unpartitioned GPU's per-cycle values are read from the amdgpu
-    attributes amd-smi itself reads; with that turned off (GFD_AMDSMI_SYSFS=0,
-    read once per process) every value comes from the library calls, and the
-    devices must be identical."""
-    code = ("import sys, json; sys.path.insert(0, %r)\n"
-            "import gpu_feature_discovery_amd as g\n"
-            "print(json.dumps(g.native().Session(['--backend=amdsmi']).devices()))\n" % str(REPO))
-    cp = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
-                        env={**os.environ, "GFD_AMDSMI_SYSFS": "0"})
-    assert cp.returncode == 0, cp.stderr[-2000:]
-    assert json.loads(cp.stdout.strip().splitlines()[-1]) == json.loads(json.dumps(amdsmi_devices))
+    attributes amd-smi itself reads; with that turned off (the bindings'
+    test hook, amdsmi_library_only) every value comes from the library calls,
+    and the devices and the label files must be identical."""
+    lib = native.Session(["--backend=amdsmi"], amdsmi_library_only=True)
+    assert lib.devices() == amdsmi_devices
+    common = ["--backend=amdsmi", "--no-timestamp", "--output-file="]
+    assert (native.Session(common, amdsmi_library_only=True).cycle(False)["labels"]
+            == native.Session(common).cycle(False)["labels"])
 
 
 def test_label_sets_identical_across_backends(native, tmp_path):
@@ -389,12 +387,11 @@ def test_runtime_visibility_masks_do_not_hide_gpus(binary, tmp_path, var):
     assert int(golden.parse_labels(files["amdsmi"])["amd.com/gpu.count"]) >= 1
 
 
-def test_daemon_pins_itself_to_one_l3_domain(binary, tmp_path):
-    """On the pool's 2-socket hosts the daemon keeps its threads on the CPUs
-    sharing one L3 cache (util/affinity.h), within the allowed set; with
-    GFD_CPU_AFFINITY=none it does not.  (The daemon is started with every
-    CPU of the box allowed: this test process may itself be pinned by an
-    earlier in-process session.)"""
+def test_daemon_pins_itself_to_one_l3_domain_only_when_asked(binary, tmp_path):
+    """CPU placement is opt-in: by default the daemon leaves its threads to
+    the scheduler; with --cpu-affinity=l3 (GFD_CPU_AFFINITY=l3) it keeps them
+    on the CPUs sharing one L3 cache (util/affinity.h), within the allowed
+    set.  (Started with every CPU of the box allowed.)"""
     def run(env):
         def widen():
             os.sched_setaffinity(0, range(os.cpu_count()))  # the kernel keeps the cgroup's share
@@ -404,8 +401,8 @@ def test_daemon_pins_itself_to_one_l3_domain(binary, tmp_path):
         return subprocess.run([binary, "--oneshot", "--backend=null", "--output-file="], capture_output=True,
                               text=True, timeout=60, env=e, preexec_fn=widen, check=True)
 
-    on = run({})
+    assert "CPU affinity:" not in run({}).stderr
+    on = run({"GFD_CPU_AFFINITY": "l3"})
     lines = [ln for ln in on.stderr.splitlines() if "CPU affinity:" in ln]
     assert len(lines) == 1, on.stderr[-2000:]
     assert "sharing cpu" in lines[0] and "L3 cache" in lines[0], lines[0]
-    assert "CPU affinity:" not in run({"GFD_CPU_AFFINITY": "none"}).stderr

@@ -28,7 +28,7 @@ if os.environ.get("CI"):
 else:
     yaml = pytest.importorskip("yaml")
     hypothesis = pytest.importorskip("hypothesis")
-from hypothesis import given, settings, strategies as st  # noqa: E402
+from hypothesis import example, given, settings, strategies as st  # noqa: E402
 
 # Plain scalars go-yaml v2 resolves differently from PyYAML.  (U+0085, NEL,
 # is a YAML 1.1 line break that PyYAML does not round-trip; not generated.)
@@ -63,6 +63,10 @@ def test_native_reader_matches_pyyaml(native, doc, flow, width):
 
 
 @settings(max_examples=150, deadline=None)
+# Round-2 regression: PyYAML dumps the string "'[" as '''[' - a '' escape
+# followed by a bracket that is text, not the end of the flow collection.
+@example(shared=["'["], keys=["a", "b"], flow=True)
+@example(shared={"a": "'["}, keys=["a", "b"], flow=True)
 @given(shared=st.one_of(st.lists(_docs, min_size=1, max_size=3), st.dictionaries(_keys, _docs, min_size=1, max_size=3)),
        keys=st.lists(_keys, min_size=2, max_size=4, unique=True), flow=st.booleans())
 def test_anchors_and_aliases_match_pyyaml(native, shared, keys, flow):
@@ -94,6 +98,8 @@ def _check(native, doc, flow, width):
     ('k:\n- "a\\\n  b"\n', {"k": ["ab"]}),         # escaped line break
     ("{'0': [0']}\n", {"0": ["0'"]}),                 # quote inside a plain flow scalar
     ("{0  0: null}\n", {"0  0": None}),               # blanks inside a flow plain scalar
+    ("['''[']\n", ["'["]),                            # '' escape before a bracket
+    ("{a: '''['}\n", {"a": "'["}),
     ('{a: "x\\\n    #"}\n', {"a": "x#"}),           # '#' on a quoted continuation line
     ("a: 1.1125369292536007e-308\n", {"a": 1.1125369292536007e-308}),  # subnormal float
     # Anchors, aliases, merge keys, standard tags.

@@ -439,11 +439,10 @@ void prepare_then_write(const Labels& l, const std::string& path) {
   if (auto job = lm::temp_preparer(path)) job();
   lm::write_to_file(l, path);
 }
-// Prepared files: gfd-tmp/<a-e>/gfd-XXXXXX.
+// Files waiting in gfd-tmp/ (gfd-XXXXXX): prepared or swapped out.
 std::vector<std::string> prepared_files(const std::string& dir) {
   std::vector<std::string> out;
-  for (const auto& sub : fs::list_dir(dir + "/gfd-tmp"))
-    for (const auto& n : fs::list_dir(dir + "/gfd-tmp/" + sub)) out.push_back(dir + "/gfd-tmp/" + sub + "/" + n);
+  for (const auto& n : fs::list_dir(dir + "/gfd-tmp")) out.push_back(dir + "/gfd-tmp/" + n);
   std::sort(out.begin(), out.end());
   return out;
 }
@@ -454,40 +453,71 @@ TEST(WriteToFile_UsesPreparedTemporaryFiles) {
   EXPECT_TRUE(mkdtemp(dir) != nullptr);
   std::string path = std::string(dir) + "/gfd", tmp = std::string(dir) + "/gfd-tmp";
   lm::write_to_file({{"k", "0"}}, path);  // creates gfd-tmp/
-  // At most four are prepared ahead.
-  for (int i = 0; i < 5; ++i)
+  // One file is prepared ahead; further jobs have nothing to do.
+  for (int i = 0; i < 3; ++i)
     if (auto job = lm::temp_preparer(path)) job();
   auto ready = prepared_files(dir);
-  EXPECT_EQ(ready.size(), static_cast<size_t>(4));
-  // Round-robin over five subdirectories (a write swaps out of one while
-  // the next files are made in others).
-  for (const char* sub : {"/a", "/b", "/c", "/d"}) EXPECT_EQ(fs::list_dir(tmp + sub).size(), static_cast<size_t>(1));
-  EXPECT_FALSE(fs::exists(tmp + "/e"));
+  EXPECT_EQ(ready.size(), static_cast<size_t>(1));
+  EXPECT_FALSE(static_cast<bool>(lm::temp_preparer(path)));
   struct stat st;
   EXPECT_TRUE(stat(ready[0].c_str(), &st) == 0);
   EXPECT_EQ(static_cast<long>(st.st_size), 0L);
   EXPECT_EQ(static_cast<int>(st.st_mode & 0777), 0644);
-  // A write takes one of them: its inode becomes the feature file, and the
-  // old feature file takes its name (RENAME_EXCHANGE) until the next
-  // preparer job unlinks it.
+  ino_t ino = st.st_ino;
+  // A write takes it: its inode becomes the feature file, and the old
+  // feature file takes its name (RENAME_EXCHANGE) until the next preparer
+  // job unlinks it and makes the next file.
   lm::write_to_file({{"k", "1"}}, path);
   EXPECT_EQ(fs::read_file(path).data, std::string("k=1\n"));
-  auto left = prepared_files(dir);
-  EXPECT_EQ(left.size(), static_cast<size_t>(4));
-  std::string retired;
-  for (const auto& f : ready)
-    if (fs::read_file(f).data == "k=0\n") retired = f;
-  EXPECT_FALSE(retired.empty());
   EXPECT_TRUE(stat(path.c_str(), &st) == 0);
+  EXPECT_EQ(st.st_ino, ino);
   EXPECT_EQ(static_cast<int>(st.st_mode & 0777), 0644);
-  if (auto job = lm::temp_preparer(path)) job();
-  EXPECT_FALSE(fs::exists(retired));
-  EXPECT_EQ(prepared_files(dir).size(), static_cast<size_t>(4));
-  EXPECT_EQ(fs::read_file(path).data, std::string("k=1\n"));
+  EXPECT_TRUE(prepared_files(dir) == ready);
+  EXPECT_EQ(fs::read_file(ready[0]).data, std::string("k=0\n"));
+  // Without a prepared file the next write renames over the feature file,
+  // and an old file waiting for its unlink is not displaced.
+  lm::write_to_file({{"k", "2"}}, path);
+  EXPECT_EQ(fs::read_file(path).data, std::string("k=2\n"));
+  EXPECT_EQ(fs::read_file(ready[0]).data, std::string("k=0\n"));
+  auto job = lm::temp_preparer(path);
+  EXPECT_TRUE(static_cast<bool>(job));
+  job();
+  EXPECT_FALSE(fs::exists(ready[0]));
+  auto next = prepared_files(dir);
+  EXPECT_EQ(next.size(), static_cast<size_t>(1));
+  EXPECT_EQ(fs::read_file(next[0]).data, std::string());
+  EXPECT_EQ(fs::read_file(path).data, std::string("k=2\n"));
   // Exit: nothing left behind.
   lm::remove_output_file(path);
   EXPECT_FALSE(fs::exists(tmp));
   EXPECT_FALSE(fs::exists(path));
+  fs::remove_all(dir);
+}
+
+TEST(WriteToFile_SteadyLoopKeepsAtMostTwoFilesInTheTemporaryDirectory) {
+  char dir[] = "/tmp/gfd-write-XXXXXX";
+  EXPECT_TRUE(mkdtemp(dir) != nullptr);
+  std::string path = std::string(dir) + "/gfd";
+  for (int i = 0; i < 20; ++i) {
+    prepare_then_write({{"k", std::to_string(i)}}, path);
+    EXPECT_TRUE(prepared_files(dir).size() <= static_cast<size_t>(2));
+    EXPECT_EQ(fs::read_file(path).data, "k=" + std::to_string(i) + "\n");
+  }
+  lm::remove_output_file(path);
+  fs::remove_all(dir);
+}
+
+TEST(SweepTempDir_RemovesWhatACrashLeft) {
+  char dir[] = "/tmp/gfd-write-XXXXXX";
+  EXPECT_TRUE(mkdtemp(dir) != nullptr);
+  std::string path = std::string(dir) + "/gfd", tmp = std::string(dir) + "/gfd-tmp";
+  fs::mkdir_all(tmp + "/a");  // round-2 layout: subdirectories
+  for (const char* n : {"/gfd-abc123", "/a/gfd-def456"})
+    EXPECT_TRUE(::close(::open((tmp + n).c_str(), O_CREAT | O_WRONLY, 0644)) == 0);
+  lm::sweep_temp_dir(path);
+  EXPECT_FALSE(fs::exists(tmp));
+  lm::sweep_temp_dir(path);  // nothing there: fine
+  lm::sweep_temp_dir("");    // stdout mode: nothing to do
   fs::remove_all(dir);
 }
 
@@ -611,6 +641,7 @@ TEST(WriteToFile_PreparedFileOfAnotherDirectoryIsDiscarded) {
   // discard_prepared_temps: the same for a session that ends - including a
   // job handed out but not run yet, which it waits for.
   if (auto job = lm::temp_preparer(pb)) job();
+  lm::write_to_file({{"k", "b2"}}, pb);  // takes the prepared file; the old one waits
   auto pending = lm::temp_preparer(pb);
   EXPECT_TRUE(static_cast<bool>(pending));
   std::thread t([job = std::move(pending)] {
@@ -621,7 +652,11 @@ TEST(WriteToFile_PreparedFileOfAnotherDirectoryIsDiscarded) {
   t.join();
   EXPECT_EQ(prepared_files(b).size(), static_cast<size_t>(0));
   // A job dropped unrun does not hold discard up.
-  { auto dropped = lm::temp_preparer(pb); }
+  lm::write_to_file({{"k", "b3"}}, pb);
+  {
+    auto dropped = lm::temp_preparer(pb);
+    EXPECT_TRUE(static_cast<bool>(dropped));
+  }
   lm::discard_prepared_temps();
   fs::remove_all(a);
   fs::remove_all(b);

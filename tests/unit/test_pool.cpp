@@ -129,9 +129,7 @@ TEST(Pool_CancelOrWaitDropsUnstartedTask) {
 }
 
 TEST(Pool_GpuLanesPolicy) {
-  // Light per-GPU work: two GPUs per lane, at most four lanes; heavy work
-  // (library calls): one GPU per lane, the pool's width.
-  if (std::getenv("GFD_GPU_LANES")) return;  // overridden for a measurement
+  // One GPU per lane, at most the pool's width.
   EXPECT_EQ(gfd::gpu_lanes(0), static_cast<size_t>(1));
   EXPECT_EQ(gfd::gpu_lanes(1), static_cast<size_t>(1));
   EXPECT_EQ(gfd::gpu_lanes(2), static_cast<size_t>(2));

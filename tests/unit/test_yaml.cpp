@@ -129,6 +129,15 @@ TEST(Yaml_FlowCollectionsWithAnchorsTagsAndMerges) {
   EXPECT_THROW_MSG(parse("a: {k: v\n"), "flow");
 }
 
+TEST(Yaml_FlowSingleQuoteEscapeKeepsScalarOpen) {
+  // '' inside a single-quoted flow scalar is an escaped quote, so a bracket
+  // after it is text, not the collection's end (PyYAML dumps '[ as '''[').
+  EXPECT_EQ(to_json(parse("['''[']\n")), std::string("[\"'[\"]"));
+  EXPECT_EQ(to_json(parse("{a: '''['}\n")), std::string("{\"a\":\"'[\"}"));
+  EXPECT_EQ(to_json(parse("a: ['x''}', 'y']\n")), std::string("{\"a\":[\"x'}\",\"y\"]}"));
+  EXPECT_EQ(to_json(parse("a: ['it''s',\n  'b']\n")), std::string("{\"a\":[\"it's\",\"b\"]}"));
+}
+
 TEST(Yaml_BlockScalarIndicators) {
   Node n = parse("keep: |+\n  x\n\nnext: >-\n  a\n\n  b\nind: |2\n    deep\n");
   EXPECT_EQ(n.get("keep")->text(), std::string("x\n\n"));

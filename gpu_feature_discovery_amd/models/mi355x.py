@@ -74,8 +74,11 @@ def partitions(compute_mode: str, memory_mode: str = "NPS1") -> list[Partition]:
 
     Memory is split evenly over the compute partitions (each partition sees
     its share of HBM regardless of NPS mode; NPS decides locality, not
-    capacity), which is what the KFD ``mem_banks`` of each partition node
-    report on the pool.
+    capacity).  That is the model of upstream amdgpu's per-XCP memory
+    (``KFD_XCP_MEMORY_SIZE``, reported in each partition node's KFD
+    ``mem_banks``), not a measurement: the pool runs SPX/NPS1 only and
+    cannot switch modes (profiles/hw_probe.md), so no partitioned MI355X has
+    been observed.
     """
     n = PARTITIONS_PER_MODE[compute_mode]
     if memory_mode not in NPS_COUNT:

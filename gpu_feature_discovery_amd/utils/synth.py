@@ -9,8 +9,10 @@ MI355X pool (verified by tools/hw_probe.sh; see profiles/hw_probe.md):
   (DPX/QPX/CPX: 2/4/8 nodes).  A partition node's ``location_id`` follows
   ``NodeSpec.partition_layout``: ``"function"`` (upstream amdgpu on GC
   9.4.3-class parts ORs the partition index into the PCI function bits, so
-  partition k of ``bb:00.0`` reports ``bb:00.k``) or ``"shared"`` (older
-  kernels: every partition reports the parent's location),
+  partition k of ``bb:00.0`` reports ``bb:00.k``), ``"shared"`` (older
+  kernels: every partition reports the parent's location) or
+  ``"distinct-ids"`` (function addresses, and every partition reports its
+  own ``unique_id`` / ASIC serial - a kernel with per-XCP identities),
 * ``sys/bus/pci/devices/<bdf>/...`` - product name, partition modes, VRAM,
   xGMI link table, SR-IOV attributes, configuration space,
 * ``sys/module/amdgpu/version``, ``sys/class/dmi/id/product_name``.
@@ -73,7 +75,7 @@ class NodeSpec:
     seed: int = 0
     hive_size: int = 8  # GPUs per xGMI hive (MI355X platforms: 8)
     hypervisor: bool = False  # CPU "hypervisor" flag (running inside a VM)
-    partition_layout: str = "function"  # "function" | "shared" (see module docstring)
+    partition_layout: str = "function"  # "function" | "shared" | "distinct-ids" (see module docstring)
     rocm_version_file: bool = True  # write opt/rocm/.info/version
     gim_version: str | None = None  # SR-IOV host driver (GIM) loaded: sys/module/gim/version
 
@@ -170,7 +172,7 @@ def make_node(root: str | os.PathLike, spec: NodeSpec) -> Path:
     _write(root / "sys/module/amdgpu/version", spec.driver_version + "\n")
     if spec.gim_version:
         _write(root / "sys/module/gim/version", spec.gim_version + "\n")
-    if spec.partition_layout not in ("function", "shared"):
+    if spec.partition_layout not in ("function", "shared", "distinct-ids"):
         raise ValueError(f"unknown partition_layout {spec.partition_layout!r}")
     if spec.rocm_version_file:
         _write(root / "opt/rocm/.info/version", spec.rocm_version + "\n")
@@ -202,13 +204,14 @@ def make_node(root: str | os.PathLike, spec: NodeSpec) -> Path:
         for p in range(parts):
             ndir = topo / f"nodes/{node}"
             # kfd_topology.c: location_id = pci_dev_id | xcp node id.
-            node_location = location | p if spec.partition_layout == "function" and parts > 1 else location
+            node_location = location | p if spec.partition_layout != "shared" and parts > 1 else location
+            node_unique = unique ^ (p + 1) if spec.partition_layout == "distinct-ids" and parts > 1 else unique
             if g.hidden or (g.visible_partitions is not None and p not in g.visible_partitions):
                 # Unreadable: the kernel returns EPERM; a directory named
                 # `properties` makes every read fail the same way (EISDIR).
                 (ndir / "properties").mkdir(parents=True, exist_ok=True)
             else:
-                _write(ndir / "properties", _kfd_properties(g, parts, node_location, render, unique, xcc))
+                _write(ndir / "properties", _kfd_properties(g, parts, node_location, render, node_unique, xcc))
                 _write(ndir / "mem_banks/0/properties", f"heap_type 1\nsize_in_bytes {node_mem}\nflags 0\nwidth 8192\n")
                 _write(ndir / "gpu_id", f"{rng.randint(1000, 65535)}\n")
             node += 1
@@ -275,7 +278,10 @@ def fake_amdsmi_spec(root: str | os.PathLike, spec: NodeSpec, latency_us: int = 
     would see the node ``make_node(root, spec)`` built: same PCI addresses,
     partition layout and KFD nodes, one line per readable GPU."""
     root = Path(root)
-    lines = [f"partition_bdf={spec.partition_layout}", "sockets=slot"]
+    bdfs = "shared" if spec.partition_layout == "shared" else "function"
+    lines = [f"partition_bdf={bdfs}", "sockets=slot"]
+    if spec.partition_layout == "distinct-ids":
+        lines.append("partition_serials=distinct")
     if latency_us:
         lines.append(f"latency_us={latency_us}")
     kfd = root / "sys/class/kfd/kfd/topology/nodes"

@@ -525,9 +525,11 @@ static std::vector<std::vector<ProcInfo>> collect_physical_gpus(AmdSmiLib& L, co
   }
 
   // Split slots into physical GPUs.  One processor: a GPU (the hot path, no
-  // further calls).  Several: the partitions of one GPU when they share the
-  // ASIC serial and the family puts partitions on one slot; otherwise
-  // distinct GPUs that happen to share a slot (e.g. ARI virtual functions).
+  // further calls).  Several: the partitions of one GPU when the family puts
+  // partitions on one slot and they share the device ID - not the ASIC
+  // serial, which a kernel reporting one per partition would split a CPX GPU
+  // by (split_by_identity); otherwise distinct GPUs that happen to share a
+  // slot.
   std::vector<std::vector<ProcInfo>> physical;
   for (auto& [slot, procs] : slots) {
     if (procs.size() == 1) {
@@ -538,9 +540,13 @@ static std::vector<std::vector<ProcInfo>> collect_physical_gpus(AmdSmiLib& L, co
     for (auto& p : procs) {
       query_identity(L, root, p);
       bool partitions = partition_index_in_function_bits(gfx_target_from_amdsmi(p.gfx));
-      by_gpu[partitions ? "serial:" + p.uuid : "bdf:" + p.bdf].push_back(std::move(p));
+      by_gpu[partitions ? "device:" + std::to_string(p.device_id) : "bdf:" + p.bdf].push_back(std::move(p));
     }
-    for (auto& [key, members] : by_gpu) physical.push_back(std::move(members));
+    for (auto& [key, members] : by_gpu)
+      for (auto& g : split_by_identity(
+               root, std::move(members), [](const ProcInfo& p) { return p.uuid; },
+               [](const ProcInfo& p) { return p.bdf; }))
+        physical.push_back(std::move(g));
   }
   // Parent PCI function of each GPU, resolved once per session.
   for (auto& procs : physical) {

@@ -1,12 +1,30 @@
 #include "resource/physical.h"
 
 #include <algorithm>
+#include <mutex>
+#include <set>
 
 #include "resource/pci_ids.h"
 #include "util/fs.h"
+#include "util/log.h"
 #include "util/strings.h"
 
 namespace gfd::resource {
+
+bool all_pci_functions(const std::string& root, const std::vector<std::string>& bdfs) {
+  for (const auto& b : bdfs)
+    if (!fs::exists(fs::join(root, "sys/bus/pci/devices/" + b + "/device"))) return false;
+  return true;
+}
+
+void log_identity_mismatch(const std::string& slot, size_t members) {
+  static std::mutex mu;
+  static std::set<std::string> logged;
+  std::lock_guard<std::mutex> lk(mu);
+  if (!logged.insert(slot).second) return;
+  log::printf("Warning: the %zu partitions of the GPU at %s report different serial numbers; counted as one GPU "
+              "(grouped by PCI slot and device ID)", members, slot.c_str());
+}
 
 bool partition_index_in_function_bits(const GfxTarget& t) { return t.major == 9 && t.minor >= 4; }
 

@@ -38,6 +38,45 @@ bool partition_index_in_function_bits(const GfxTarget& t);
 // "dddd:bb:dd.f" -> "dddd:bb:dd" (amd-smi's socket id of the function).
 std::string bdf_slot(const std::string& bdf);
 
+// The members (KFD nodes or amd-smi processors) that one PCI slot and
+// device ID group as one physical GPU, checked against their identities
+// (`id_of`: KFD unique_id / amd-smi ASIC serial; `bdf_of`: the member's
+// address).  Current kernels give every partition the GPU's serial, so a
+// group that agrees is one GPU.  One that disagrees is either a GPU whose
+// kernel reports a serial per partition - kept whole, with a warning (once
+// per slot), rather than counted as 8 GPUs - or distinct GPUs that share a
+// slot (SR-IOV virtual functions behind ARI), told apart by every member
+// being a PCI function of its own under <root>/sys/bus/pci/devices
+// (partition addresses other than the GPU's own are not): split by serial.
+bool all_pci_functions(const std::string& root, const std::vector<std::string>& bdfs);
+void log_identity_mismatch(const std::string& slot, size_t members);
+template <typename T, typename IdOf, typename BdfOf>
+std::vector<std::vector<T>> split_by_identity(const std::string& root, std::vector<T> members, IdOf id_of,
+                                              BdfOf bdf_of) {
+  bool agree = true;
+  for (const auto& m : members) agree = agree && id_of(m) == id_of(members.front());
+  if (agree) return {std::move(members)};
+  std::vector<std::string> bdfs;
+  for (const auto& m : members) bdfs.push_back(bdf_of(m));
+  if (!all_pci_functions(root, bdfs)) {
+    log_identity_mismatch(bdf_slot(bdfs.front()), members.size());
+    return {std::move(members)};
+  }
+  std::vector<std::vector<T>> out;
+  std::vector<decltype(id_of(members.front()))> ids;
+  for (auto& m : members) {
+    auto id = id_of(m);
+    size_t i = 0;
+    while (i < ids.size() && !(ids[i] == id)) ++i;
+    if (i == ids.size()) {
+      ids.push_back(id);
+      out.emplace_back();
+    }
+    out[i].push_back(std::move(m));
+  }
+  return out;
+}
+
 // Parent PCI function of a physical GPU whose members (partitions, or the
 // GPU itself) report `member_bdfs`.  `device_id` 0 accepts any device.
 // Candidates: the member addresses in ascending order, then the slot's

@@ -294,21 +294,30 @@ std::shared_ptr<const SysfsManager::Topology> SysfsManager::read_topology() cons
     if (usable[i]) topo->nodes.push_back(std::move(nodes[i]));
   std::sort(topo->nodes.begin(), topo->nodes.end(), [](const KfdNode& a, const KfdNode& b) { return a.id < b.id; });
 
-  // 2. Group partitions by physical GPU: (domain, location, unique_id), with
+  // 2. Group partitions by physical GPU: (domain, location, device ID), with
   //    the PCI function bits - where partition-capable parts put the
-  //    partition index - masked (resource/physical.h).
+  //    partition index - masked (resource/physical.h).  Not the ASIC serial
+  //    (unique_id): every partition of a GPU reports the GPU's on current
+  //    kernels, but a kernel reporting one per partition must not turn a CPX
+  //    GPU into 8 GPUs (split_by_identity).
   struct Key {
-    uint64_t domain, location, unique_id;
+    uint64_t domain, location, device_id;
     bool operator<(const Key& o) const {
-      return std::tie(domain, location, unique_id) < std::tie(o.domain, o.location, o.unique_id);
+      return std::tie(domain, location, device_id) < std::tie(o.domain, o.location, o.device_id);
     }
   };
   std::map<Key, std::vector<const KfdNode*>> groups;
   for (const auto& n : topo->nodes) {
     bool masked = partition_index_in_function_bits(gfx_target_from_kfd(n.gfx_target_version));
-    groups[Key{n.domain, masked ? (n.location_id & ~uint64_t{7}) : n.location_id, n.unique_id}].push_back(&n);
+    groups[Key{n.domain, masked ? (n.location_id & ~uint64_t{7}) : n.location_id, n.device_id}].push_back(&n);
   }
-  for (auto& [key, members] : groups) {
+  std::vector<std::vector<const KfdNode*>> physical;
+  for (auto& [key, members] : groups)
+    for (auto& g : split_by_identity(
+             opts_.root, std::move(members), [](const KfdNode* n) { return n->unique_id; },
+             [](const KfdNode* n) { return bdf_of(*n); }))
+      physical.push_back(std::move(g));
+  for (auto& members : physical) {
     std::vector<std::string> bdfs;
     for (const auto* n : members) bdfs.push_back(bdf_of(*n));
     Topology::Gpu g;

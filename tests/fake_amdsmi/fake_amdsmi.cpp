@@ -16,6 +16,9 @@
 //                             function p (upstream amdgpu on GC 9.4.3-class
 //                             parts; the default) - or `shared`: every
 //                             partition reports the parent's BDF (older kernels)
+//   partition_serials=distinct  each partition reports its own ASIC serial
+//                             (the GPU's with the partition index appended),
+//                             as a kernel with per-XCP identities would
 //   sockets=slot              one socket per PCI slot, i.e. per physical GPU
 //                             (what amd-smi does; the default) - or `one`: a
 //                             single socket holding every processor
@@ -88,6 +91,7 @@ struct State {
   std::map<std::string, long> calls;                             // function -> device queries made
   bool partition_fn = true;   // partition_bdf=function
   bool socket_per_slot = true;  // sockets=slot
+  bool distinct_serials = false;  // partition_serials=distinct
   std::vector<std::vector<uint32_t>> sockets;  // processor indices per socket
 };
 
@@ -171,6 +175,7 @@ int fake_amdsmi_configure(const char* spec) {
   s.stale = false;
   s.partition_fn = true;
   s.socket_per_slot = true;
+  s.distinct_serials = false;
   s.sockets.clear();
   std::istringstream in(spec);
   std::string line;
@@ -192,6 +197,10 @@ int fake_amdsmi_configure(const char* spec) {
     }
     if (line.rfind("partition_bdf=", 0) == 0) {
       s.partition_fn = line.substr(14) == "function";
+      continue;
+    }
+    if (line.rfind("partition_serials=", 0) == 0) {
+      s.distinct_serials = line.substr(18) == "distinct";
       continue;
     }
     if (line.rfind("sockets=", 0) == 0) {
@@ -254,6 +263,8 @@ int fake_amdsmi_configure(const char* spec) {
       q.gpu = base.bdf;
       q.partition_id = static_cast<uint32_t>(p);
       if (base.kfd_node != 0xFFFFFFFFu) q.kfd_node = base.kfd_node + static_cast<uint32_t>(p);
+      if (parts > 1 && s.distinct_serials)
+        q.serial = (base.serial.empty() ? "3A7C178B7C5E" + base.bdf.substr(5, 2) + "5C" : base.serial) + std::to_string(p);
       if (parts > 1 && s.partition_fn) {
         // kfd_topology.c: location_id = pci_dev_id | xcp node id.
         q.fn = base.fn | static_cast<uint32_t>(p);

@@ -32,7 +32,7 @@ CASES = {
 
 @pytest.mark.skipif(not FAKE.exists(), reason="libfake_amdsmi.so not built")
 @pytest.mark.parametrize("privileged", [False, True], ids=["pod", "privileged"])
-@pytest.mark.parametrize("layout", ["function", "shared"])
+@pytest.mark.parametrize("layout", ["function", "shared", "distinct-ids"])
 @pytest.mark.parametrize("case", list(CASES))
 def test_amdsmi_and_sysfs_backends_label_identically(binary, tmp_path, case, layout, privileged):
     c = CASES[case]
@@ -58,7 +58,7 @@ def test_amdsmi_and_sysfs_backends_label_identically(binary, tmp_path, case, lay
 
 
 @pytest.mark.skipif(not FAKE.exists(), reason="libfake_amdsmi.so not built")
-@pytest.mark.parametrize("layout", ["function", "shared"])
+@pytest.mark.parametrize("layout", ["function", "shared", "distinct-ids"])
 def test_backends_agree_on_one_visible_partition(binary, tmp_path, layout):
     spec = synth.NodeSpec(gpus=[synth.GpuSpec(compute_partition="CPX", visible_partitions=[5])],
                           partition_layout=layout, seed=22)
@@ -76,7 +76,7 @@ def test_backends_agree_on_one_visible_partition(binary, tmp_path, layout):
 
 
 @pytest.mark.skipif(not FAKE.exists(), reason="libfake_amdsmi.so not built")
-@pytest.mark.parametrize("layout", ["function", "shared"])
+@pytest.mark.parametrize("layout", ["function", "shared", "distinct-ids"])
 @pytest.mark.parametrize("case", ["spx", "cpx-single", "dpx-nps2-mixed"])
 def test_amdsmi_without_libdrm_labels_identically(binary, tmp_path, case, layout):
     """amd-smi without libdrm_amdgpu (a slim image), as measured on the pool

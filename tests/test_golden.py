@@ -156,7 +156,7 @@ def test_synthetic_spx_matches_regex_golden(binary, tmp_path):
 # as bb:00.k in its KFD location_id (kfd_topology.c ORs the XCP node id in);
 # older ones give every partition the parent's location.  Both must produce
 # the same labels (resource/physical.h).
-LAYOUTS = ["function", "shared"]
+LAYOUTS = ["function", "shared", "distinct-ids"]
 
 
 @pytest.mark.parametrize("layout", LAYOUTS)

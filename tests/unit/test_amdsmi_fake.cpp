@@ -552,11 +552,16 @@ TEST(AmdSmiFake_PartitionedGpuValuesFromAttributesAndSessionCache) {
 TEST(AmdSmiFake_DistinctGpusOnOneSlotStaySeparate) {
   REQUIRE_FAKE();
   // Two SR-IOV virtual functions a guest sees on one slot (ARI): different
-  // ASIC serials, so two GPUs, not one GPU with two partitions.
+  // ASIC serials and each a PCI function of its own, so two GPUs, not one
+  // GPU with two partitions.
   fake().configure(
       "bdf=0000:05:00.0;mode=SPX;parts=1;serial=0x1111222233334444\n"
       "bdf=0000:05:00.1;mode=SPX;parts=1;serial=0x5555666677778888\n");
   std::string root = temp_root();
+  for (const char* fn : {"0000:05:00.0", "0000:05:00.1"}) {
+    fs::mkdir_all(root + "/sys/bus/pci/devices/" + fn);
+    lm::write_file_atomically(root + "/sys/bus/pci/devices/" + fn + "/device", "0x75a3\n", 0644);
+  }
   AmdSmiManager m(opts(root, false));
   m.Init();
   auto devs = m.GetDevices();
@@ -565,6 +570,25 @@ TEST(AmdSmiFake_DistinctGpusOnOneSlotStaySeparate) {
   EXPECT_FALSE(devs[1]->IsPartitioned());
   EXPECT_EQ(devs[0]->Info().bdf, std::string("0000:05:00.0"));
   EXPECT_EQ(devs[1]->Info().bdf, std::string("0000:05:00.1"));
+  m.Shutdown();
+  fs::remove_all(root);
+}
+
+TEST(AmdSmiFake_PartitionsWithTheirOwnSerialsStayOneGpu) {
+  REQUIRE_FAKE();
+  // A kernel that gives every CPX partition its own ASIC serial: the
+  // partitions (0000:05:00.1-7 are not PCI functions) are still one GPU.
+  fake().configure("partition_serials=distinct\nbdf=0000:05:00.0;mode=CPX;parts=8;cus=32;xcds=1;vram_mib=36862\n");
+  std::string root = temp_root();
+  fs::mkdir_all(root + "/sys/bus/pci/devices/0000:05:00.0");
+  lm::write_file_atomically(root + "/sys/bus/pci/devices/0000:05:00.0/device", "0x75a3\n", 0644);
+  AmdSmiManager m(opts(root, false));
+  m.Init();
+  auto devs = m.GetDevices();
+  EXPECT_EQ(devs.size(), static_cast<size_t>(1));
+  EXPECT_TRUE(devs[0]->IsPartitioned());
+  EXPECT_EQ(devs[0]->GetPartitions().size(), static_cast<size_t>(8));
+  EXPECT_EQ(devs[0]->Info().bdf, std::string("0000:05:00.0"));
   m.Shutdown();
   fs::remove_all(root);
 }

@@ -51,11 +51,32 @@ void PreferenceManager::Init() {
   throw Error("no resource manager could be initialized (" + errors + ")");
 }
 
+struct WarmStartManager::Warmer {
+  std::mutex mu;
+  std::condition_variable cv;
+  bool done = false;
+  std::string error;    // empty: the preferred manager is ready
+  std::string devices;  // its first snapshot (device_summary)
+  int64_t ns = 0;
+};
+
 WarmStartManager::WarmStartManager(ManagerPtr preferred, ManagerPtr quick)
     : preferred_(std::move(preferred)), quick_(std::move(quick)), current_(quick_) {}
 
 WarmStartManager::~WarmStartManager() {
-  if (warmer_.joinable()) warmer_.join();
+  if (!thread_.joinable()) return;
+  std::unique_lock<std::mutex> lk(warmer_->mu);
+  // system_clock: see lm::discard_prepared_temps (TSan and clockwait).
+  if (warmer_->cv.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(teardown_wait_ms),
+                             [&] { return warmer_->done; })) {
+    lk.unlock();
+    thread_.join();
+    return;
+  }
+  lk.unlock();
+  log::printf("Warning: the %s manager is still initializing after %lld ms; not waiting for it",
+              preferred_->Name().c_str(), static_cast<long long>(teardown_wait_ms));
+  thread_.detach();  // it owns what it uses (the manager and its state)
 }
 
 void WarmStartManager::fall_back(const std::string& why) {
@@ -65,6 +86,12 @@ void WarmStartManager::fall_back(const std::string& why) {
   current_ = quick_;
 }
 
+std::vector<DevicePtr> WarmStartManager::GetDevices() {
+  auto devs = current_->GetDevices();
+  if (state_ == State::warming) quick_devices_ = device_summary(devs);
+  return devs;
+}
+
 void WarmStartManager::Init() {
   if (state_ == State::cold) {
     // A persistent session stays initialised after Shutdown: the warmer
@@ -72,35 +99,53 @@ void WarmStartManager::Init() {
     // device (~1.2 ms on MI355X: ASIC info, KFD node, virtualization mode)
     // and the session caches are paid here too - so the cycle that switches
     // over finds everything ready.
-    warmer_ = std::thread([this] {
+    warmer_ = std::make_shared<Warmer>();
+    thread_ = std::thread([w = warmer_, m = preferred_] {
       int64_t t0 = trace::now_ns();
+      std::string error, devices;
       try {
-        preferred_->Init();
+        m->Init();
         try {
-          preferred_->GetDevices();
+          devices = device_summary(m->GetDevices());
         } catch (...) {
-          preferred_->Shutdown();
+          m->Shutdown();
           throw;
         }
-        preferred_->Shutdown();
+        m->Shutdown();
       } catch (const std::exception& e) {
-        warm_error_ = e.what();
+        error = e.what();
       }
-      warm_ns_ = trace::now_ns() - t0;
-      warm_done_.store(true, std::memory_order_release);
+      std::lock_guard<std::mutex> lk(w->mu);
+      w->error = std::move(error);
+      w->devices = std::move(devices);
+      w->ns = trace::now_ns() - t0;
+      w->done = true;
+      w->cv.notify_all();
     });
     state_ = State::warming;
     log::printf("Initializing the %s manager in the background; labeling from the %s manager meanwhile",
                 preferred_->Name().c_str(), quick_->Name().c_str());
-  } else if (state_ == State::warming && warm_done_.load(std::memory_order_acquire)) {
-    warmer_.join();
-    if (!warm_error_.empty()) {
-      fall_back(warm_error_);
-    } else {
-      log::printf("Using the %s manager (initialized in the background in %.1f ms)", preferred_->Name().c_str(),
-                  static_cast<double>(warm_ns_) / 1e6);
-      state_ = State::preferred;
-      current_ = preferred_;
+  } else if (state_ == State::warming) {
+    std::unique_lock<std::mutex> lk(warmer_->mu);
+    if (warmer_->done) {
+      std::string error = warmer_->error, devices = warmer_->devices;
+      int64_t ns = warmer_->ns;
+      lk.unlock();
+      thread_.join();
+      if (!error.empty()) {
+        fall_back(error);
+      } else {
+        log::printf("Using the %s manager (initialized in the background in %.1f ms)", preferred_->Name().c_str(),
+                    static_cast<double>(ns) / 1e6);
+        if (!quick_devices_.empty() && devices != quick_devices_)
+          log::printf("Warning: the %s manager describes the GPUs differently from the %s manager; labels change "
+                      "now:\n%s:\n%s%s:\n%s",
+                      preferred_->Name().c_str(), quick_->Name().c_str(), quick_->Name().c_str(),
+                      quick_devices_.c_str(), preferred_->Name().c_str(), devices.c_str());
+        state_ = State::preferred;
+        current_ = preferred_;
+      }
+      quick_devices_.clear();
     }
   }
   if (state_ == State::preferred) {
@@ -112,6 +157,22 @@ void WarmStartManager::Init() {
     }
   }
   quick_->Init();
+}
+
+std::string device_summary(const std::vector<DevicePtr>& devices) {
+  std::string out;
+  auto line = [&](const Device& d, const std::string& indent) {
+    const auto& i = d.Info();
+    out += indent + i.bdf + " " + d.GetName() + " " + i.gfx.name() + " cu=" + std::to_string(i.compute_units) +
+           " xcd=" + std::to_string(i.xcds) + " mem=" + std::to_string(i.memory_mib) + "MiB " + i.compute_partition + "/" +
+           i.memory_partition + " xgmi=" + std::to_string(i.xgmi_links) + " " + i.virtualization + "\n";
+  };
+  for (const auto& d : devices) {
+    line(*d, "");
+    if (!d->IsPartition())
+      for (const auto& p : d->GetPartitions()) line(*p, "  ");
+  }
+  return out;
 }
 
 ManagerPtr with_config(ManagerPtr m, const config::Config& c) {

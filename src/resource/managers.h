@@ -13,6 +13,8 @@
 
 #include "config/config.h"
 #include <atomic>
+#include <condition_variable>
+#include <mutex>
 #include <thread>
 
 #include "config/yaml.h"
@@ -91,28 +93,37 @@ class PreferenceManager : public Manager {
 class WarmStartManager : public Manager {
  public:
   WarmStartManager(ManagerPtr preferred, ManagerPtr quick);
-  ~WarmStartManager() override;  // waits for a background initialisation
+  // Waits for a background initialisation, at most teardown_wait_ms: a
+  // library wedged in its init must not keep the daemon from exiting on
+  // SIGTERM or reloading on SIGHUP (the warmer is then left to finish alone).
+  ~WarmStartManager() override;
   void Init() override;
   void Shutdown() override { current_->Shutdown(); }
-  std::vector<DevicePtr> GetDevices() override { return current_->GetDevices(); }
+  std::vector<DevicePtr> GetDevices() override;
   std::string GetDriverVersion() override { return current_->GetDriverVersion(); }
   std::optional<RuntimeVersion> GetRuntimeVersion() override { return current_->GetRuntimeVersion(); }
   std::string Name() const override { return current_->Name(); }
   std::optional<VersionSources> VersionFiles() const override { return current_->VersionFiles(); }
   // The preferred manager is the one in use.
   bool warmed() const { return state_ == State::preferred; }
+  int64_t teardown_wait_ms = 5000;
 
  private:
   enum class State { cold, warming, preferred, quick_only };
   void fall_back(const std::string& why);
+  struct Warmer;
 
   ManagerPtr preferred_, quick_, current_;
   State state_ = State::cold;
-  std::thread warmer_;
-  std::atomic<bool> warm_done_{false};
-  std::string warm_error_;  // set by the warmer before warm_done_
-  int64_t warm_ns_ = 0;
+  std::thread thread_;
+  std::shared_ptr<Warmer> warmer_;
+  std::string quick_devices_;  // the quick manager's last devices (device_summary), while warming
 };
+
+// What the labels of `devices` depend on, one line per device (and
+// partition): compared when the daemon switches backends, so a difference
+// between them - and the label change it causes - is logged.
+std::string device_summary(const std::vector<DevicePtr>& devices);
 
 // Wrap `m` in a FallbackManager unless failOnInitError is set.
 ManagerPtr with_config(ManagerPtr m, const config::Config& c);

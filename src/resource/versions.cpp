@@ -117,6 +117,13 @@ std::optional<RuntimeVersion> rocm_version(const VersionSources& s, std::string*
     return v;
   }
   if (!s.host_root.empty()) {
+    // A host root without opt/ is a missing mount (the manifests mount the
+    // host's /opt at <host-root>/opt), not a node without ROCm: labeling on
+    // would silently drop amd.com/rocm.runtime.*, which the reference always
+    // emits.  A mounted /opt that holds no ROCm is a node without it.
+    if (!fs::is_dir(fs::join(s.host_root, "opt")))
+      throw Error("--host-root " + s.host_root + " has no opt/ directory: mount the host's /opt there to read the ROCm "
+                  "runtime version");
     std::string path = fs::resolve_in_root(s.host_root, "opt/rocm/.info/version");
     if (!path.empty())
       if (auto v = from(path)) return v;

@@ -127,3 +127,46 @@ def test_without_libdrm_or_fru_name_both_backends_use_the_device_model(binary, t
         outs[backend] = out.read_text()
     assert outs["amdsmi"] == outs["sysfs"]
     assert "MI3" in golden.parse_labels(outs["amdsmi"])["amd.com/gpu.product"]
+
+
+def _loop_stderr(binary, args, env, until, timeout=20.0):
+    import os
+    import signal
+    import subprocess
+    import time
+
+    p = subprocess.Popen([binary, "--sleep-interval=20ms", *args], stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
+                         text=True, env={**{k: v for k, v in os.environ.items() if not k.startswith("GFD_")}, **env})
+    err, waiting = [], list(until)
+    try:
+        end = time.monotonic() + timeout
+        for line in p.stderr:
+            err.append(line)
+            if waiting and waiting[0] in line:
+                waiting.pop(0)
+            if not waiting or time.monotonic() > end:
+                break
+    finally:
+        p.send_signal(signal.SIGTERM)
+        _, rest = p.communicate(timeout=30)
+        err.append(rest or "")
+    return "".join(err)
+
+
+@pytest.mark.skipif(not FAKE.exists(), reason="libfake_amdsmi.so not built")
+@pytest.mark.parametrize("agree", [True, False])
+def test_warm_start_switch_logs_a_backend_disagreement(binary, tmp_path, agree):
+    """The loop daemon labels its first cycles from KFD while amd-smi starts
+    in the background; at the switch it compares what both report and logs
+    any difference (the labels change at that cycle), silent when they agree."""
+    spec = synth.NodeSpec(gpus=[synth.GpuSpec()], seed=31)
+    root = synth.make_node(tmp_path / "root", spec)
+    fake = synth.fake_amdsmi_spec(root, spec)
+    if not agree:
+        fake = fake.replace("name=AMD Instinct MI355 OAM", "name=AMD Instinct MI355X")
+    env = {"GFD_AMDSMI_LIBRARY": str(FAKE), "GFD_FAKE_AMDSMI_SPEC": fake.replace("\n", "|")}
+    err = _loop_stderr(binary, ["--backend=auto", f"--sysfs-root={root}", f"--output-file={tmp_path / 'gfd'}",
+                                f"--machine-type-file={root}/sys/class/dmi/id/product_name"], env,
+                       until=["initialized in the background in", "Sleeping for"])
+    assert "initialized in the background in" in err, err[-3000:]
+    assert ("describes the GPUs differently" in err) != agree, err[-3000:]

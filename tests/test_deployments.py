@@ -65,6 +65,9 @@ def _check_host_opt(spec, container):
     --host-root=/host points the daemon at - never from the image."""
     vols = {v["name"]: v for v in spec["volumes"]}
     assert vols["host-opt"]["hostPath"]["path"] == "/opt"
+    # Directory, not DirectoryOrCreate: the labeler never writes to the host
+    # (a node without /opt fails to mount, visibly).
+    assert vols["host-opt"]["hostPath"]["type"] == "Directory"
     (m,) = [m for m in container["volumeMounts"] if m["name"] == "host-opt"]
     assert m["mountPath"] == "/host/opt" and m["readOnly"] is True
 

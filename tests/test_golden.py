@@ -347,6 +347,19 @@ def test_driver_only_host_gets_no_runtime_labels(binary, tmp_path):
     assert "no ROCm release found on the node" in cp.stderr
 
 
+def test_host_root_without_opt_mount_fails_loudly(binary, tmp_path):
+    """A manifest that sets GFD_HOST_ROOT but does not mount the host's /opt
+    there: the cycle fails with the reason instead of dropping the
+    amd.com/rocm.runtime.* labels with a warning."""
+    root = synth.make_mi355x_node(tmp_path / "root", n_gpus=1, rocm_version="7.2.0")
+    host = tmp_path / "host"
+    host.mkdir()
+    cp = run_daemon(binary, "--oneshot", "--backend=sysfs", f"--sysfs-root={root}", "--output-file=",
+                    f"--host-root={host}")
+    assert cp.returncode == 1
+    assert "has no opt/ directory" in cp.stderr
+
+
 def test_explicit_rocm_version_file(binary, tmp_path):
     root = synth.make_mi355x_node(tmp_path / "root", n_gpus=1, rocm_version="7.2.0")
     f = tmp_path / "version"

@@ -4,6 +4,10 @@
 // backend here is fully testable on CPU because it only reads files.)
 #include <unistd.h>
 
+#include <chrono>
+#include <condition_variable>
+#include <mutex>
+
 #include "config/config.h"
 #include "lm/labels.h"
 #include "resource/amdsmi.h"
@@ -321,6 +325,19 @@ TEST(RocmVersion_DriverOnlyHostHasNone) {
   fs::remove_all(host);
 }
 
+TEST(RocmVersion_HostRootWithoutOptIsAMissingMount) {
+  // --host-root set but the host's /opt not mounted there: an error (the
+  // cycle fails), not a silent drop of amd.com/rocm.runtime.*.
+  std::string image = mktemp_dir(), host = mktemp_dir();
+  put(image + "/opt/rocm/.info/version", "7.2.0\n");
+  VersionSources s;
+  s.root = image;
+  s.host_root = host;
+  EXPECT_THROW_MSG(rocm_version(s), "has no opt/ directory");
+  fs::remove_all(image);
+  fs::remove_all(host);
+}
+
 TEST(RocmVersion_ExplicitFileMustBeReadable) {
   std::string d = mktemp_dir();
   VersionSources s;
@@ -498,6 +515,51 @@ TEST(WarmStart_DestructorWaitsForTheWarmer) {
     w.Shutdown();
   }  // must not leave a running thread behind (TSan / std::terminate)
   EXPECT_EQ(smi->init_calls, 1);
+}
+
+namespace {
+// A preferred manager whose Init blocks until released: a library wedged in
+// its initialisation.
+struct BlockingManager : MockManager {
+  std::mutex mu;
+  std::condition_variable cv;
+  bool released = false, finished = false;
+  void Init() override {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return released; });
+  }
+  void release() {
+    std::lock_guard<std::mutex> lk(mu);
+    released = true;
+    cv.notify_all();
+  }
+};
+}  // namespace
+
+TEST(WarmStart_DestructorDoesNotWaitForeverForAWedgedInit) {
+  auto smi = std::make_shared<BlockingManager>();
+  auto kfd = std::make_shared<MockManager>(std::vector<DevicePtr>{new_full_gpu()});
+  auto t0 = std::chrono::steady_clock::now();
+  {
+    WarmStartManager w(smi, kfd);
+    w.teardown_wait_ms = 50;
+    w.Init();
+    EXPECT_EQ(w.GetDevices().size(), static_cast<size_t>(1));
+    w.Shutdown();
+  }  // SIGTERM / SIGHUP: the manager goes while the warmer is stuck
+  auto ms = std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
+  EXPECT_TRUE(ms < 2000);
+  smi->release();  // the detached warmer finishes on its own (it owns smi)
+  for (int i = 0; i < 2000 && smi.use_count() > 1; ++i) usleep(1000);
+  EXPECT_EQ(smi.use_count(), 1L);
+}
+
+TEST(DeviceSummary_ShowsWhatTheLabelsDependOn) {
+  auto a = device_summary({new_full_gpu()});
+  EXPECT_EQ(a, device_summary({new_full_gpu()}));
+  EXPECT_TRUE(a != device_summary({new_full_gpu(), new_full_gpu()}));
+  EXPECT_TRUE(a.find("MOCKMODEL") != std::string::npos);
+  EXPECT_TRUE(a.find("mem=300MiB") != std::string::npos);
 }
 
 TEST(AmdSmi_InitFailsCleanlyWithoutDriver) {

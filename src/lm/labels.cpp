@@ -151,11 +151,11 @@ std::string render(const Labels& labels) {
 
 namespace {
 
-// Loop-mode state of the writer, kept between cycles: at most one temporary
-// file made ahead of the write that will use it, and at most one old feature
-// file waiting to be unlinked.  Both live in <dir>/gfd-tmp/, which the daemon
-// empties at start-up (sweep_temp_dir) and removes at exit, so a crash leaves
-// at most these two files behind until the next start.
+// Loop-mode state of the writer, kept between cycles: up to two temporary
+// files made ahead of the writes that will use them, and at most one old
+// feature file waiting to be unlinked.  All live in <dir>/gfd-tmp/, which the
+// daemon empties at start-up (sweep_temp_dir) and removes at exit, so a crash
+// leaves at most these files behind until the next start.
 //
 // Why each exists, measured with the daemon's cycles 1 s apart (the deployed
 // cadence is 60 s, so every cycle starts cold):
@@ -163,7 +163,9 @@ namespace {
 //     ms, more than the rest of the write.  The cycle's worker makes the next
 //     file after its node-facts and SR-IOV tasks, off the critical path:
 //     write p50 0.055-0.090 ms vs 0.147-0.282 ms creating in the write
-//     (profiles/writer_ab_r3.txt).
+//     (profiles/writer_ab_r3.txt).  Two, not one: the job runs while its own
+//     cycle writes, so the file a write uses must come from an earlier
+//     cycle's job - with one, every other write made its own file.
 //   * The exchange: a rename over the old feature file frees its inode
 //     inside rename(2); on ext4 (the usual file system of NFD's features.d
 //     hostPath) that is most of a cold replace, 0.34-0.58 ms vs 0.03 ms for
@@ -171,17 +173,23 @@ namespace {
 //     temporary name for the next worker job to unlink
 //     (profiles/rename_exchange_ab.txt).  Readers see the old file or the
 //     new one under `path`, never neither, exactly as with a rename.
+constexpr size_t kMaxPrepared = 2;
+
+struct Prepared {
+  std::string name;
+  int fd = -1;
+  size_t allocated = 0;  // bytes preallocated beyond EOF
+};
+
 struct WriterState {
   std::mutex mu;
-  std::condition_variable cv;  // job finished
-  std::string dir;             // gfd-tmp/ of the prepared file
-  std::string name;            // the prepared file ("" = none)
-  int fd = -1;
-  size_t allocated = 0;        // bytes preallocated beyond EOF
-  std::string retired;         // old feature file to unlink ("" = none)
-  std::string no_exchange_dir; // whose file system refused RENAME_EXCHANGE
-  bool job = false;            // a preparer job is handed out, not yet finished or dropped
-  size_t last_size = 0;        // of the last write: the next file's preallocation
+  std::condition_variable cv;   // job finished
+  std::string dir;              // gfd-tmp/ of the prepared files
+  std::vector<Prepared> ready;  // oldest first
+  std::string retired;          // old feature file to unlink ("" = none)
+  std::string no_exchange_dir;  // whose file system refused RENAME_EXCHANGE
+  bool job = false;             // a preparer job is handed out, not yet finished or dropped
+  size_t last_size = 0;         // of the last write: the next file's preallocation
 };
 
 WriterState& writer() {
@@ -189,23 +197,26 @@ WriterState& writer() {
   return *w;
 }
 
-// Takes the prepared file if it is in `tmp_dir` (fd, name, preallocation),
-// else -1; a prepared file elsewhere is removed.
+void drop_ready(WriterState& w) {  // caller holds mu
+  for (auto& f : w.ready) {
+    ::close(f.fd);
+    ::unlink(f.name.c_str());
+  }
+  w.ready.clear();
+}
+
+// Takes the oldest prepared file if it is in `tmp_dir` (fd, name,
+// preallocation), else -1; prepared files elsewhere are removed.
 int take_prepared(const std::string& tmp_dir, std::string* name, size_t* allocated) {
   WriterState& w = writer();
   std::lock_guard<std::mutex> lk(w.mu);
-  if (w.fd < 0) return -1;
-  int fd = std::exchange(w.fd, -1);
-  std::string n = std::move(w.name);
-  w.name.clear();
-  if (w.dir != tmp_dir) {
-    ::close(fd);
-    ::unlink(n.c_str());
-    return -1;
-  }
-  *name = std::move(n);
-  *allocated = w.allocated;
-  return fd;
+  if (w.dir != tmp_dir) drop_ready(w);
+  if (w.ready.empty()) return -1;
+  Prepared f = std::move(w.ready.front());
+  w.ready.erase(w.ready.begin());
+  *name = std::move(f.name);
+  *allocated = f.allocated;
+  return f.fd;
 }
 
 // Replaces `path` by the finished temporary file `tmpl`.  `exchange` (loop
@@ -318,7 +329,8 @@ std::function<void()> temp_preparer(const std::string& path) {
   size_t hint;
   {
     std::lock_guard<std::mutex> lk(w.mu);
-    if (w.job || (w.fd >= 0 && w.dir == tmp_dir && w.retired.empty())) return {};
+    size_t have = w.dir == tmp_dir ? w.ready.size() : 0;
+    if (w.job || (have >= kMaxPrepared && w.retired.empty())) return {};
     w.job = true;
     hint = w.last_size;
   }
@@ -336,23 +348,21 @@ std::function<void()> temp_preparer(const std::string& path) {
     {
       std::lock_guard<std::mutex> lk(q.mu);
       old.swap(q.retired);
-      make = q.fd < 0;
+      make = q.dir != tmp_dir || q.ready.size() < kMaxPrepared;
     }
     if (!old.empty()) ::unlink(old.c_str());
     if (!make) return;
     // gfd-tmp/ itself is not re-created: a missing one is the next write's
     // business.
-    std::string name;
-    int fd = create_temp(tmp_dir, 0644, &name);
-    if (fd < 0) return;
-    size_t allocated = 0;
-    if (hint > 0 && wants_prealloc(fd) && ::fallocate(fd, FALLOC_FL_KEEP_SIZE, 0, static_cast<off_t>(hint)) == 0)
-      allocated = hint;
+    Prepared f;
+    f.fd = create_temp(tmp_dir, 0644, &f.name);
+    if (f.fd < 0) return;
+    if (hint > 0 && wants_prealloc(f.fd) && ::fallocate(f.fd, FALLOC_FL_KEEP_SIZE, 0, static_cast<off_t>(hint)) == 0)
+      f.allocated = hint;
     std::lock_guard<std::mutex> lk(q.mu);
+    if (q.dir != tmp_dir) drop_ready(q);
     q.dir = tmp_dir;
-    q.name = std::move(name);
-    q.fd = fd;
-    q.allocated = allocated;
+    q.ready.push_back(std::move(f));
   };
 }
 
@@ -365,12 +375,7 @@ void discard_prepared_temps() {
   // next start's sweep.  system_clock: a steady_clock wait is
   // pthread_cond_clockwait, which GCC 11's ThreadSanitizer does not intercept.
   w.cv.wait_until(lk, std::chrono::system_clock::now() + std::chrono::seconds(1), [&] { return !w.job; });
-  if (w.fd >= 0) {
-    ::close(w.fd);
-    ::unlink(w.name.c_str());
-    w.fd = -1;
-    w.name.clear();
-  }
+  drop_ready(w);
   if (!w.retired.empty()) ::unlink(w.retired.c_str());
   w.retired.clear();
 }

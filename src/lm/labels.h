@@ -58,9 +58,10 @@ void write_file_atomically(const std::string& path, const std::string& contents,
 // the old feature file the last write swapped out and creates the temporary
 // file of the next write to `path` (blocks preallocated for the last written
 // size where the write preallocates).  Empty when there is nothing to do or
-// a job is still out.  At most one file of each kind waits in <dir>/gfd-tmp.
+// a job is still out.  At most two prepared files and one old feature file
+// wait in <dir>/gfd-tmp.
 std::function<void()> temp_preparer(const std::string& path);
-// Waits (bounded) for a handed-out job, then removes the prepared file and
+// Waits (bounded) for a handed-out job, then removes the prepared files and
 // the old feature file.
 void discard_prepared_temps();
 // Start-up: removes <dir>/gfd-tmp left by a process that did not exit

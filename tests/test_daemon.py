@@ -116,21 +116,21 @@ def _split(tmp: Path):
     return ready, old
 
 
-def test_loop_keeps_one_prepared_file_and_at_most_one_old_file(binary, tmp_path):
-    """Loop mode: between cycles gfd-tmp/ holds one empty 0644 file made for
-    the next write, which that write swaps into place (RENAME_EXCHANGE), and
-    at most one old feature file swapped out, which the next cycle's worker
-    unlinks.  Exit removes everything (main.go:149-156)."""
+def test_loop_keeps_at_most_two_prepared_files_and_one_old_file(binary, tmp_path):
+    """Loop mode: between cycles gfd-tmp/ holds one or two empty 0644 files
+    made for the next writes, which swap them into place (RENAME_EXCHANGE),
+    and at most one old feature file swapped out, which the next cycle's
+    worker unlinks.  Exit removes everything (main.go:149-156)."""
     out = tmp_path / "gfd"
     tmp = tmp_path / "gfd-tmp"
     p = _start(binary, ["--sleep-interval=200ms", *_base(tmp_path, out)])
     try:
         assert _wait_for(out.exists), "first write"
-        assert _wait_for(lambda: len(_split(tmp)[0]) == 1), _temps(tmp)
+        assert _wait_for(lambda: len(_split(tmp)[0]) >= 1), _temps(tmp)
         for _ in range(3):
             ready, old = _split(tmp)
-            assert len(ready) <= 1 and len(old) <= 1, _temps(tmp)
-            assert len(_temps(tmp)) <= 2
+            assert len(ready) <= 2 and len(old) <= 1, _temps(tmp)
+            assert len(_temps(tmp)) <= 3
             for f, st in ready:
                 assert oct(st.st_mode & 0o777) == "0o644"
             inos = {st.st_ino for _, st in ready}
@@ -162,11 +162,11 @@ def test_sigkilled_daemons_leave_a_bounded_gfd_tmp(binary, tmp_path):
         finally:
             p.kill()
             p.wait(timeout=10)
-        assert 1 <= len(_temps(tmp)) <= 2, _temps(tmp)
+        assert 1 <= len(_temps(tmp)) <= 3, _temps(tmp)
     stale = {f for f, _ in _temps(tmp)}
+    m0 = out.stat().st_mtime_ns  # before the start: its first write may come at once
     p = _start(binary, ["--sleep-interval=10s", *_base(tmp_path, out)])
     try:
-        m0 = out.stat().st_mtime_ns
         assert _wait_for(lambda: out.stat().st_mtime_ns > m0), "first cycle"
         assert _wait_for(lambda: len(_temps(tmp)) == 1)  # the next write's file
         left = _temps(tmp)
@@ -198,7 +198,7 @@ def test_exchange_never_swaps_a_directory_into_gfd_tmp(binary, tmp_path):
     out = tmp_path / "gfd"
     p = _start(binary, ["--sleep-interval=100ms", *_base(tmp_path, out)])
     try:
-        assert _wait_for(lambda: out.exists() and len(_split(tmp_path / "gfd-tmp")[0]) == 1)
+        assert _wait_for(lambda: out.exists() and len(_split(tmp_path / "gfd-tmp")[0]) >= 1)
         out.unlink()
         out.mkdir()
         (out / "keep").write_text("user data")

@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <set>
 #include <thread>
 
 #include "lm/keys.h"
@@ -448,41 +449,51 @@ std::vector<std::string> prepared_files(const std::string& dir) {
 }
 }  // namespace
 
+namespace {
+ino_t inode(const std::string& p) {
+  struct stat st;
+  return ::stat(p.c_str(), &st) == 0 ? st.st_ino : 0;
+}
+}  // namespace
+
 TEST(WriteToFile_UsesPreparedTemporaryFiles) {
   char dir[] = "/tmp/gfd-write-XXXXXX";
   EXPECT_TRUE(mkdtemp(dir) != nullptr);
   std::string path = std::string(dir) + "/gfd", tmp = std::string(dir) + "/gfd-tmp";
   lm::write_to_file({{"k", "0"}}, path);  // creates gfd-tmp/
-  // One file is prepared ahead; further jobs have nothing to do.
-  for (int i = 0; i < 3; ++i)
-    if (auto job = lm::temp_preparer(path)) job();
-  auto ready = prepared_files(dir);
-  EXPECT_EQ(ready.size(), static_cast<size_t>(1));
+  // Two files are prepared ahead; further jobs have nothing to do.
+  if (auto job = lm::temp_preparer(path)) job();
+  auto first = prepared_files(dir);
+  EXPECT_EQ(first.size(), static_cast<size_t>(1));
+  if (auto job = lm::temp_preparer(path)) job();
+  auto both = prepared_files(dir);
+  EXPECT_EQ(both.size(), static_cast<size_t>(2));
   EXPECT_FALSE(static_cast<bool>(lm::temp_preparer(path)));
+  std::string a = first[0], b = both[0] == a ? both[1] : both[0];
   struct stat st;
-  EXPECT_TRUE(stat(ready[0].c_str(), &st) == 0);
+  EXPECT_TRUE(stat(a.c_str(), &st) == 0);
   EXPECT_EQ(static_cast<long>(st.st_size), 0L);
   EXPECT_EQ(static_cast<int>(st.st_mode & 0777), 0644);
-  ino_t ino = st.st_ino;
-  // A write takes it: its inode becomes the feature file, and the old
-  // feature file takes its name (RENAME_EXCHANGE) until the next preparer
-  // job unlinks it and makes the next file.
+  ino_t ino_a = inode(a), ino_b = inode(b);
+  // A write takes the oldest: its inode becomes the feature file, and the
+  // old feature file takes its name (RENAME_EXCHANGE) until the next
+  // preparer job unlinks it.
   lm::write_to_file({{"k", "1"}}, path);
   EXPECT_EQ(fs::read_file(path).data, std::string("k=1\n"));
+  EXPECT_EQ(inode(path), ino_a);
   EXPECT_TRUE(stat(path.c_str(), &st) == 0);
-  EXPECT_EQ(st.st_ino, ino);
   EXPECT_EQ(static_cast<int>(st.st_mode & 0777), 0644);
-  EXPECT_TRUE(prepared_files(dir) == ready);
-  EXPECT_EQ(fs::read_file(ready[0]).data, std::string("k=0\n"));
-  // Without a prepared file the next write renames over the feature file,
-  // and an old file waiting for its unlink is not displaced.
+  EXPECT_EQ(fs::read_file(a).data, std::string("k=0\n"));
+  // The next write takes the other one; an old file still waiting for its
+  // unlink is not displaced (a plain rename replaces the feature file).
   lm::write_to_file({{"k", "2"}}, path);
   EXPECT_EQ(fs::read_file(path).data, std::string("k=2\n"));
-  EXPECT_EQ(fs::read_file(ready[0]).data, std::string("k=0\n"));
+  EXPECT_EQ(inode(path), ino_b);
+  EXPECT_EQ(fs::read_file(a).data, std::string("k=0\n"));
   auto job = lm::temp_preparer(path);
   EXPECT_TRUE(static_cast<bool>(job));
   job();
-  EXPECT_FALSE(fs::exists(ready[0]));
+  EXPECT_FALSE(fs::exists(a));
   auto next = prepared_files(dir);
   EXPECT_EQ(next.size(), static_cast<size_t>(1));
   EXPECT_EQ(fs::read_file(next[0]).data, std::string());
@@ -494,13 +505,37 @@ TEST(WriteToFile_UsesPreparedTemporaryFiles) {
   fs::remove_all(dir);
 }
 
-TEST(WriteToFile_SteadyLoopKeepsAtMostTwoFilesInTheTemporaryDirectory) {
+TEST(WriteToFile_EveryLoopWriteFindsAPreparedFile) {
+  // The daemon's order: the job runs while its own cycle writes, so each
+  // write must find a file an earlier cycle's job made.  Here the job runs
+  // after the write (the latest it can run).
+  char dir[] = "/tmp/gfd-write-XXXXXX";
+  EXPECT_TRUE(mkdtemp(dir) != nullptr);
+  std::string path = std::string(dir) + "/gfd";
+  lm::write_to_file({{"k", "x"}}, path);
+  if (auto job = lm::temp_preparer(path)) job();
+  for (int i = 0; i < 10; ++i) {
+    auto job = lm::temp_preparer(path);
+    auto ready = prepared_files(dir);
+    std::set<ino_t> inos;
+    for (const auto& f : ready)
+      if (fs::read_file(f).data.empty()) inos.insert(inode(f));
+    lm::write_to_file({{"k", std::to_string(i)}}, path);
+    EXPECT_TRUE(inos.count(inode(path)) == 1);
+    if (job) job();
+    EXPECT_TRUE(prepared_files(dir).size() <= static_cast<size_t>(3));
+  }
+  lm::remove_output_file(path);
+  fs::remove_all(dir);
+}
+
+TEST(WriteToFile_SteadyLoopKeepsAtMostThreeFilesInTheTemporaryDirectory) {
   char dir[] = "/tmp/gfd-write-XXXXXX";
   EXPECT_TRUE(mkdtemp(dir) != nullptr);
   std::string path = std::string(dir) + "/gfd";
   for (int i = 0; i < 20; ++i) {
     prepare_then_write({{"k", std::to_string(i)}}, path);
-    EXPECT_TRUE(prepared_files(dir).size() <= static_cast<size_t>(2));
+    EXPECT_TRUE(prepared_files(dir).size() <= static_cast<size_t>(3));
     EXPECT_EQ(fs::read_file(path).data, "k=" + std::to_string(i) + "\n");
   }
   lm::remove_output_file(path);

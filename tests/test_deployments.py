@@ -142,3 +142,64 @@ def test_ci_workflow_runs_what_the_readme_claims(native):
     image = " ".join(s.get("run", "") for s in wf["jobs"]["image"]["steps"])
     assert "docker run" in image and "--oneshot --backend=null" in image
     assert "test -e /opt/rocm/.info/version" in image
+
+
+def test_chart_dependencies_are_in_the_repository(native):
+    """An offline `helm install` of the default values needs every
+    dependency in charts/ (the reference vendors NFD's chart as a .tgz;
+    Chart.yaml:10-15): no remote repository, and name/version match."""
+    chart = native.parse_yaml((CHART / "Chart.yaml").read_text())
+    for dep in chart["dependencies"]:
+        assert dep["repository"].startswith("file://"), dep
+        sub = CHART / dep["repository"][len("file://"):]
+        meta = native.parse_yaml((sub / "Chart.yaml").read_text())
+        assert (meta["name"], meta["version"]) == (dep["name"], dep["version"])
+    values = native.parse_yaml((CHART / "values.yaml").read_text())
+    assert values["nfd"]["deploy"] is True  # deployable by default: it is in the repository
+
+
+def test_nfd_subchart_renders_from_the_default_values(native):
+    """Render the NFD subchart as helm would with the parent's defaults (the
+    parent's `nfd:` block coalesced over the subchart's values.yaml) and
+    check what labeling depends on: the master publishes amd.com, the worker
+    reads the features.d hostPath the labeler writes and whitelists the
+    accelerator PCI class, both on the gRPC path."""
+    import helm_lite
+
+    sub = CHART / "charts" / "nfd-minimal"
+    values = helm_lite.merge(native.parse_yaml((sub / "values.yaml").read_text()),
+                             native.parse_yaml((CHART / "values.yaml").read_text())["nfd"])
+    docs = []
+    for t in sorted((sub / "templates").iterdir()):
+        text = helm_lite.render(t.read_text(), values)
+        docs += [native.parse_yaml(d) for d in re.split(r"^---\s*$", text, flags=re.M) if d.strip()]
+    kinds = sorted(d["kind"] for d in docs)
+    assert kinds == ["ClusterRole", "ClusterRoleBinding", "ConfigMap", "DaemonSet", "Deployment", "Service",
+                     "ServiceAccount"]
+    master = next(d for d in docs if d["kind"] == "Deployment")
+    args = master["spec"]["template"]["spec"]["containers"][0]["args"]
+    assert "-extra-label-ns=amd.com" in args and "-enable-nodefeature-api=false" in args
+    worker = next(d for d in docs if d["kind"] == "DaemonSet")
+    spec = worker["spec"]["template"]["spec"]
+    wargs = spec["containers"][0]["args"]
+    assert "-server=gfd-nfd-master:8080" in wargs and "-enable-nodefeature-api=false" in wargs
+    assert {"key": "amd.com/gpu", "operator": "Exists", "effect": "NoSchedule"} in spec["tolerations"]
+    vols = {v["name"]: v for v in spec["volumes"]}
+    assert vols["features-d"]["hostPath"]["path"] == "/etc/kubernetes/node-feature-discovery/features.d"
+    cm = next(d for d in docs if d["kind"] == "ConfigMap")
+    conf = native.parse_yaml(cm["data"]["nfd-worker.conf"])
+    assert "12" in conf["sources"]["pci"]["deviceClassWhitelist"]
+    svc = next(d for d in docs if d["kind"] == "Service")
+    assert svc["metadata"]["name"] == "gfd-nfd-master"
+    # Every value the templates use exists (an unknown one raises in render).
+    assert all(d["metadata"].get("namespace", "gpu-feature-discovery") == "gpu-feature-discovery" for d in docs)
+
+
+def test_helm_lite_refuses_what_it_does_not_implement():
+    import helm_lite
+
+    with pytest.raises(ValueError):
+        helm_lite.render('{{ include "x" . }}', {})
+    with pytest.raises(KeyError):
+        helm_lite.render("{{ .Values.missing }}", {})
+    assert helm_lite.render("a:{{- range .Values.l }} {{ . }}{{- end }}", {"l": [1, 2]}) == "a: 1 2"

@@ -1,0 +1,182 @@
+"""Run the daemon exactly as a deployment manifest would.
+
+The reference's container integration test runs its image privileged against
+a real node and matches the labels (tests/integration-tests.py:36-78).  There
+is no container runtime, helm or kubectl here or on the GPU box, so the
+stand-in takes the labeler container of a manifest - the static DaemonSet or
+Job template, or the Helm chart's DaemonSet with its default values - and
+runs the daemon binary with that container's argv and environment, its
+hostPath mounts reproduced under a scratch "container root":
+
+* features.d (hostPath /etc/kubernetes/node-feature-discovery/features.d):
+  an empty directory at the same container path;
+* the host's /opt (for --host-root): the node's /opt/rocm/.info/version
+  copied to the same container path;
+* /sys must be mounted at /sys (the daemon reads it there); the GPU run uses
+  the real one, the CPU rehearsal a synthetic tree (--sysfs-root, the one
+  setting that is added).
+
+Every path-valued setting (env or argument) is a container path and is
+re-rooted under the scratch root; nothing else is changed, so a manifest
+whose env names, arguments or mounts do not fit the daemon fails the run.
+"""
+
+from __future__ import annotations
+
+import os
+import re
+import shutil
+import signal
+import subprocess
+import time
+from dataclasses import dataclass, field
+from pathlib import Path
+
+FEATURES_D = "/etc/kubernetes/node-feature-discovery/features.d"
+DEFAULT_OUTPUT = FEATURES_D + "/gfd"
+# Settings whose value is a path inside the container.
+_PATH_ENV = ("GFD_OUTPUT_FILE", "GFD_HOST_ROOT", "GFD_CONFIG_FILE", "CONFIG_FILE", "GFD_ROCM_VERSION_FILE",
+             "GFD_MACHINE_TYPE_FILE")
+_PATH_ARGS = ("--output-file=", "--output=", "-o=", "--host-root=", "--config-file=", "--rocm-version-file=",
+              "--machine-type-file=")
+
+
+@dataclass
+class Pod:
+    kind: str                          # DaemonSet | Job
+    args: list[str] = field(default_factory=list)
+    env: dict[str, str] = field(default_factory=dict)
+    mounts: dict[str, str] = field(default_factory=dict)  # container path -> hostPath
+
+
+def from_static(native, path: Path) -> Pod:
+    docs = [native.parse_yaml(d) for d in re.split(r"^---\s*$", path.read_text(), flags=re.M) if d.strip()]
+    (obj,) = [d for d in docs if d.get("kind") in ("DaemonSet", "Job")]
+    spec = obj["spec"]["template"]["spec"]
+    (c,) = [c for c in spec["containers"] if c["name"] == "labeler"]
+    vols = {v["name"]: v["hostPath"]["path"] for v in spec["volumes"] if "hostPath" in v}
+    return Pod(kind=obj["kind"], args=[str(a) for a in c.get("args", [])],
+               env={e["name"]: str(e["value"]) for e in c.get("env", [])},
+               mounts={m["mountPath"]: vols[m["name"]] for m in c.get("volumeMounts", [])})
+
+
+def _value(values: dict, dotted: str):
+    node = values
+    for part in dotted.split("."):
+        node = node.get(part) if isinstance(node, dict) else None
+    return node
+
+
+def _helm_string(v) -> str:  # sprig's toString
+    return ("true" if v else "false") if isinstance(v, bool) else str(v)
+
+
+def from_helm(native, chart: Path) -> Pod:
+    """The chart's DaemonSet container under values.yaml's defaults: env from
+    the gfd-amd.env helper (templates/_helpers.tpl), mounts and volumes from
+    templates/daemonset.yml, `{{- if .Values.x }}` blocks evaluated."""
+    values = native.parse_yaml((chart / "values.yaml").read_text())
+    helpers = (chart / "templates" / "_helpers.tpl").read_text()
+    env: dict[str, str] = {}
+    for name, key in re.findall(r'"(GFD_[A-Z_]+)" \.Values\.([\w.]+)', helpers):
+        v = _value(values, key)
+        if v is not None and _helm_string(v) != "":
+            env[name] = _helm_string(v)
+    for cond, name, val in re.findall(r"\{\{- if \.Values\.([\w.]+) \}\}\s*- name: (GFD_\w+)\s*value: (\S+)", helpers):
+        if _value(values, cond):
+            env[name] = val
+    ds = (chart / "templates" / "daemonset.yml").read_text()
+    assert "args:" not in ds, "chart passes arguments: extend from_helm"
+
+    def active(text: str) -> list[str]:
+        # Lines outside false `{{- if .Values.x }}` blocks (no nesting/else).
+        out, keep = [], [True]
+        for line in text.splitlines():
+            m = re.search(r"\{\{-? if \.Values\.([\w.]+) \}\}", line)
+            if m:
+                keep.append(keep[-1] and bool(_value(values, m.group(1))))
+                continue
+            if re.search(r"\{\{-? end \}\}", line) and len(keep) > 1:
+                keep.pop()
+                continue
+            if keep[-1]:
+                out.append(re.sub(r"\{\{ \.Values\.([\w.]+) \}\}", lambda mm: str(_value(values, mm.group(1))), line))
+        return out
+
+    lines = "\n".join(active(ds))
+    vols = dict(re.findall(r"- name: ([\w-]+)\n\s+hostPath:\n\s+path: (\S+)", lines))
+    mounts = {mp.strip(): vols[n] for n, mp in re.findall(r"- \{name: ([\w-]+), mountPath: ([^,}]+)", lines)}
+    return Pod(kind="DaemonSet", env=env, mounts=mounts)
+
+
+def materialise(pod: Pod, croot: Path, host_opt: Path = Path("/opt")) -> None:
+    """Reproduce the pod's hostPath mounts under `croot`."""
+    for mpath, hpath in pod.mounts.items():
+        if mpath == "/sys":
+            assert hpath == "/sys", f"/sys is mounted from {hpath}"
+            continue
+        local = croot / mpath.lstrip("/")
+        local.mkdir(parents=True, exist_ok=True)
+        if hpath == FEATURES_D:
+            continue
+        if hpath == "/opt":
+            src = host_opt / "rocm" / ".info" / "version"
+            if src.exists():
+                dst = local / "rocm" / ".info" / "version"
+                dst.parent.mkdir(parents=True, exist_ok=True)
+                shutil.copyfile(os.path.realpath(src), dst)
+            continue
+        raise AssertionError(f"unknown hostPath {hpath} mounted at {mpath}")
+
+
+def plan(pod: Pod, binary: str, croot: Path, sysfs_root: str | None = None) -> tuple[list[str], dict[str, str], Path]:
+    """argv, environment and the output file (local path) of the pod's run."""
+    env = {k: v for k, v in os.environ.items()
+           if not k.startswith(("GFD_", "MIG_STRATEGY", "FAIL_ON_INIT", "CONFIG_FILE"))}
+    penv = dict(pod.env)
+    args = list(pod.args)
+    output = DEFAULT_OUTPUT
+    for k in _PATH_ENV:
+        if k in penv:
+            if k == "GFD_OUTPUT_FILE":
+                output = penv[k]
+            penv[k] = str(croot) + penv[k]
+    for i, a in enumerate(args):
+        for flag in _PATH_ARGS:
+            if a.startswith(flag):
+                if flag in ("--output-file=", "--output=", "-o="):
+                    output = a[len(flag):]
+                args[i] = flag + str(croot) + a[len(flag):]
+    if not any(a.startswith(("--output-file=", "--output=", "-o=")) for a in args) and "GFD_OUTPUT_FILE" not in pod.env:
+        penv["GFD_OUTPUT_FILE"] = str(croot) + output  # the default, re-rooted
+    assert any(output.startswith(m + "/") and h == FEATURES_D for m, h in pod.mounts.items()), \
+        f"the feature file {output} is not in the mounted features.d"
+    if sysfs_root:
+        penv["GFD_SYSFS_ROOT"] = sysfs_root
+        penv.setdefault("GFD_MACHINE_TYPE_FILE", sysfs_root + "/sys/class/dmi/id/product_name")
+    env.update(penv)
+    return [binary, *args], env, croot / output.lstrip("/")
+
+
+def run(pod: Pod, binary: str, croot: Path, sysfs_root: str | None = None, timeout: float = 120) -> dict:
+    """Run the pod's labeler: a Job to completion; a DaemonSet until its first
+    feature file, then SIGTERM (as a pod deletion does).  Returns the feature
+    file, stderr, exit code and whether the file was removed at exit."""
+    argv, env, out = plan(pod, binary, croot, sysfs_root)
+    if pod.kind == "Job":
+        cp = subprocess.run(argv, capture_output=True, text=True, timeout=timeout, env=env)
+        return {"text": out.read_text() if out.exists() else "", "stderr": cp.stderr, "rc": cp.returncode,
+                "removed_at_exit": not out.exists()}
+    p = subprocess.Popen(argv, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True, env=env)
+    text = ""
+    try:
+        end = time.monotonic() + timeout
+        while time.monotonic() < end and p.poll() is None:
+            if out.exists():
+                text = out.read_text()
+                break
+            time.sleep(0.01)
+    finally:
+        p.send_signal(signal.SIGTERM)
+        _, err = p.communicate(timeout=30)
+    return {"text": text, "stderr": err, "rc": p.returncode, "removed_at_exit": not out.exists()}

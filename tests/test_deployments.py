@@ -203,3 +203,68 @@ def test_helm_lite_refuses_what_it_does_not_implement():
     with pytest.raises(KeyError):
         helm_lite.render("{{ .Values.missing }}", {})
     assert helm_lite.render("a:{{- range .Values.l }} {{ . }}{{- end }}", {"l": [1, 2]}) == "a: 1 2"
+
+
+# ---- The manifests' own argv / env / mounts, run (tests/manifest_pods.py) --
+
+MANIFEST_PODS = [
+    ("static-daemonset", "gpu-feature-discovery-daemonset.yaml", "none"),
+    ("static-daemonset-single", "gpu-feature-discovery-daemonset-with-partition-single.yaml", "single"),
+    ("static-daemonset-mixed", "gpu-feature-discovery-daemonset-with-partition-mixed.yaml", "mixed"),
+    ("static-job", "gpu-feature-discovery-job.yaml.template", "none"),
+    ("helm", None, "none"),
+]
+
+
+def manifest_pod(native, source):
+    import manifest_pods
+
+    return manifest_pods.from_helm(native, CHART) if source is None else manifest_pods.from_static(native, STATIC / source)
+
+
+def check_manifest_run(r, pod, strategy, rocm: str):
+    """What every manifest run must show: exit 0, the full-GPU label set
+    (regex golden, both directions), the node's ROCm release, and the
+    DaemonSet removing its file at exit (main.go:149-156) / the Job not."""
+    from gpu_feature_discovery_amd.utils import golden
+
+    assert r["rc"] == 0, r["stderr"][-3000:]
+    assert r["text"], r["stderr"][-3000:]
+    labels = golden.parse_labels(r["text"])
+    assert labels.get("amd.com/partition.strategy", "none") == strategy
+    golden.check_regex_golden(r["text"], REPO / "tests" / "expected-output.txt",
+                              select=lambda ln: not ln.startswith("amd.com/partition.strategy="))
+    major, minor = rocm.split(".")[:2]
+    assert (labels["amd.com/rocm.runtime.major"], labels["amd.com/rocm.runtime.minor"]) == (major, minor)
+    assert r["removed_at_exit"] == (pod.kind == "DaemonSet")
+
+
+@pytest.mark.parametrize("name,source,strategy", MANIFEST_PODS, ids=[m[0] for m in MANIFEST_PODS])
+def test_manifest_pod_runs_on_a_synthetic_node(native, binary, tmp_path, name, source, strategy):
+    """CPU rehearsal of tests/test_gpu.py::test_manifest_pod_labels_the_real_node:
+    the same argv/env/mounts over a synthetic MI355X tree (the only added
+    setting is --sysfs-root, since this container's /sys has no GPU)."""
+    import manifest_pods
+    from gpu_feature_discovery_amd.utils import synth
+
+    pod = manifest_pod(native, source)
+    root = synth.make_mi355x_node(tmp_path / "node", n_gpus=1, rocm_version="6.4.2", seed=40)
+    croot = tmp_path / "container"
+    manifest_pods.materialise(pod, croot, host_opt=root / "opt")
+    r = manifest_pods.run(pod, binary, croot, sysfs_root=str(root), timeout=60)
+    check_manifest_run(r, pod, strategy, "6.4.2")
+
+
+def test_manifest_pod_catches_a_broken_mount(native, binary, tmp_path):
+    """The point of running the manifests: the host /opt mounted somewhere
+    --host-root does not look fails the run instead of dropping labels."""
+    import manifest_pods
+    from gpu_feature_discovery_amd.utils import synth
+
+    pod = manifest_pod(native, "gpu-feature-discovery-daemonset.yaml")
+    pod.mounts = {("/hostfs/opt" if m == "/host/opt" else m): h for m, h in pod.mounts.items()}
+    root = synth.make_mi355x_node(tmp_path / "node", n_gpus=1, seed=41)
+    croot = tmp_path / "container"
+    manifest_pods.materialise(pod, croot, host_opt=root / "opt")
+    r = manifest_pods.run(pod, binary, croot, sysfs_root=str(root), timeout=30)
+    assert r["rc"] == 1 and "has no opt/ directory" in r["stderr"]

@@ -17,6 +17,7 @@ import sys
 import pytest
 
 from conftest import REPO, TESTS, has_amd_gpu, run_daemon
+from test_deployments import MANIFEST_PODS, check_manifest_run, manifest_pod
 from gpu_feature_discovery_amd.utils import golden
 
 pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not has_amd_gpu(), reason="no /dev/kfd")]
@@ -45,10 +46,14 @@ def test_amdsmi_enumerates_mi355x(amdsmi_devices):
         assert 0 <= d["xgmi_links"] <= 7, d
         assert d["virtualization"] in ("baremetal", "host", "guest", "passthrough"), d
         assert d["vendor_id"] == 0x1002
-        if d["compute_partition"] == "SPX":
-            assert not d["partitioned"] and d["partitions"] == []
-        else:
-            assert d["partitioned"] and d["partitions"], d
+        # Against the driver's own attributes, whatever mode the box is in
+        # (the pool runs SPX/NPS1 and cannot switch; profiles/hw_probe.md).
+        pci = f"/sys/bus/pci/devices/{d['bdf']}"
+        mode = open(pci + "/current_compute_partition").read().strip().upper()
+        assert d["compute_partition"] == mode, (d, mode)
+        assert d["memory_partition"] == open(pci + "/current_memory_partition").read().strip().upper()
+        assert d["partitioned"] == (mode != "SPX")
+        assert len(d["partitions"]) == {"SPX": 0, "DPX": 2, "QPX": 4, "CPX": 8}[mode] or d["partitions"], d
 
 
 def test_sysfs_backend_agrees_with_amdsmi(amdsmi_devices, sysfs_devices):
@@ -204,13 +209,47 @@ def test_visible_devices_filter(native, amdsmi_devices):
     assert none == []
 
 
-def test_real_pci_scan_succeeds(native):
+def test_real_pci_scan_succeeds(native, amdsmi_devices):
+    """The SR-IOV scan on the box: it must find the allocated GPU's physical
+    function (an SR-IOV capable PF on the pool) and, as its VFs are not
+    enabled (sriov_numvfs 0, bare metal), emit no amd.com/sriov.* label -
+    the reference's vGPU labeler is silent on a passthrough GPU the same way
+    (internal/vgpu/vgpu_test.go:36-74).  On an SR-IOV node the labels must
+    match the SR-IOV golden instead."""
     r = native.Session(["--backend=sysfs", "--output-file="]).cycle(False)
     assert "sriov(overlapped)" in dict(r["phases"])
     sriov = {k: v for k, v in r["labels"].items() if "sriov" in k}
+    for d in amdsmi_devices:
+        pf = f"/sys/bus/pci/devices/{d['bdf']}"
+        assert os.path.exists(pf + "/vendor"), pf
+        assert open(pf + "/vendor").read().strip() == "0x1002"
+        numvfs = open(pf + "/sriov_numvfs").read().strip() if os.path.exists(pf + "/sriov_numvfs") else "0"
+        if d["virtualization"] == "baremetal" and numvfs == "0":
+            assert sriov == {}, sriov
     if sriov:
         golden.check_regex_golden("".join(f"{k}={v}\n" for k, v in sorted(sriov.items())),
                                   TESTS / "expected-output-sriov.txt")
+    assert r["labels"]["amd.com/gpu.virtualization-mode"] == amdsmi_devices[0]["virtualization"]
+
+
+def test_auto_backend_switch_with_library_values_keeps_the_labels(native):
+    """The daemon's default backend (auto) labels its first cycles from the
+    KFD topology and then from amd-smi; with the amd-smi backend's own sysfs
+    shortcuts off (amdsmi_library_only: every value through the library
+    calls), the label file must not change across the switch."""
+    import time
+
+    s = native.Session(["--backend=auto", "--no-timestamp", "--output-file="], amdsmi_library_only=True)
+    first = s.cycle(False)
+    assert s.backend == "sysfs", s.backend
+    for _ in range(500):
+        if s.backend.startswith("amdsmi"):
+            break
+        time.sleep(0.01)
+        s.cycle(False)
+    assert s.backend.startswith("amdsmi"), s.backend
+    after = s.cycle(False)
+    assert after["rendered"] == first["rendered"]
 
 
 def test_product_name_survives_torch_libdrm(tmp_path):
@@ -407,3 +446,31 @@ def test_daemon_pins_itself_to_one_l3_domain_only_when_asked(binary, tmp_path):
     lines = [ln for ln in on.stderr.splitlines() if "CPU affinity:" in ln]
     assert len(lines) == 1, on.stderr[-2000:]
     assert "sharing cpu" in lines[0] and "L3 cache" in lines[0], lines[0]
+
+
+# ---- The deployment manifests' own argv / env / mounts on the MI355X -------
+
+def _box_rocm() -> str:
+    text = open(os.path.realpath("/opt/rocm/.info/version")).read().strip()
+    return ".".join(text.split("-")[0].split(".")[:2])
+
+
+@pytest.mark.parametrize("name,source,strategy", MANIFEST_PODS, ids=[m[0] for m in MANIFEST_PODS])
+def test_manifest_pod_labels_the_real_node(native, binary, tmp_path, name, source, strategy):
+    """The stand-in for the reference's container integration test
+    (tests/integration-tests.py:36-78): each manifest's labeler container -
+    static DaemonSets, the Job template, the Helm chart's defaults - run with
+    exactly its argv and environment, its hostPath mounts reproduced (the
+    box's real /sys at /sys; a copy of the box's /opt/rocm/.info/version
+    under the --host-root mount).  The labels must match the regex golden in
+    both directions and carry the box's ROCm release; the DaemonSet must
+    remove its file on SIGTERM."""
+    import manifest_pods
+
+    pod = manifest_pod(native, source)
+    croot = tmp_path / "container"
+    manifest_pods.materialise(pod, croot)
+    r = manifest_pods.run(pod, binary, croot, timeout=120)
+    check_manifest_run(r, pod, strategy, _box_rocm())
+    if pod.env.get("GFD_BACKEND", "auto") == "auto" and pod.kind == "DaemonSet":
+        assert "failed to initialize" not in r["stderr"], r["stderr"][-3000:]

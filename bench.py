@@ -18,9 +18,9 @@ capabilities, versions, machine type - is read from the driver each step.
 
 The label set of every step is checked for correctness (count == N GPUs,
 gfx950/cdna4 arch, MI355 product, HBM size, valid Kubernetes label syntax)
-before timing is reported.  Like the daemon at start-up, the in-process
-session keeps its threads on the CPUs that share one L3 cache
-(src/util/affinity.h; GFD_CPU_AFFINITY=none to compare).
+before timing is reported.  The in-process session runs the daemon's default
+configuration: no CPU pinning (that is the daemon's opt-in
+--cpu-affinity=l3), workers that block when idle.
 
 N>1: launched by the driver as one process per GPU under torch.distributed
 (gloo, 127.0.0.1); rank 0 labels the node restricted to GPUs 0..N-1 (the
@@ -298,7 +298,9 @@ def main() -> int:
         if backend == "amdsmi" and fake:
             data = f"CPU rehearsal: fake amd-smi library ({os.path.basename(fake)}), {n} scripted MI355X GPU(s)"
         elif backend == "amdsmi":
-            data = "real MI355X via amd-smi (live driver queries every step)"
+            data = ("real MI355X, amd-smi backend: processor handles, KFD ids and identity from the persistent amd-smi "
+                    "session; memory, partition modes, xGMI links, capabilities and versions re-read from the amdgpu "
+                    "driver's attributes every step (the files amd-smi itself reads)")
         elif backend == "sysfs":
             data = f"real MI355X via KFD sysfs under {root}" if root else "real MI355X via KFD sysfs"
         else:

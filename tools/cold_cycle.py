@@ -24,10 +24,15 @@ def main() -> int:
     ap.add_argument("--interval", default="2s")
     ap.add_argument("--cycles", type=int, default=40)
     ap.add_argument("--backend", default="amdsmi")
+    ap.add_argument("--sysfs-root", default=None)
+    ap.add_argument("--visible-devices", default="")
     a = ap.parse_args()
+    extra = [f"--visible-devices={a.visible_devices}"]
+    if a.sysfs_root:
+        extra += [f"--sysfs-root={a.sysfs_root}", f"--machine-type-file={a.sysfs_root}/sys/class/dmi/id/product_name"]
     out = os.path.join(tempfile.mkdtemp(prefix="gfd-cold-"), "gfd")
     p = subprocess.Popen([os.path.join(REPO, "build", "gpu-feature-discovery"), f"--backend={a.backend}",
-                          f"--sleep-interval={a.interval}", "--trace-timing", f"--output-file={out}"],
+                          f"--sleep-interval={a.interval}", "--trace-timing", f"--output-file={out}", *extra],
                          stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
     totals, phases = [], {}
     try:

@@ -4,7 +4,8 @@ The reference's container integration test runs its image privileged against
 a real node and matches the labels (tests/integration-tests.py:36-78).  There
 is no container runtime, helm or kubectl here or on the GPU box, so the
 stand-in takes the labeler container of a manifest - the static DaemonSet or
-Job template, or the Helm chart's DaemonSet with its default values - and
+Job template, or the Helm chart's DaemonSet rendered with its default values
+(tests/helm_lite.py) - and
 runs the daemon binary with that container's argv and environment, its
 hostPath mounts reproduced under a scratch "container root":
 
@@ -52,61 +53,25 @@ class Pod:
 def from_static(native, path: Path) -> Pod:
     docs = [native.parse_yaml(d) for d in re.split(r"^---\s*$", path.read_text(), flags=re.M) if d.strip()]
     (obj,) = [d for d in docs if d.get("kind") in ("DaemonSet", "Job")]
-    spec = obj["spec"]["template"]["spec"]
+    return from_pod_spec(obj["kind"], obj["spec"]["template"]["spec"])
+
+
+def from_pod_spec(kind: str, spec: dict) -> Pod:
     (c,) = [c for c in spec["containers"] if c["name"] == "labeler"]
     vols = {v["name"]: v["hostPath"]["path"] for v in spec["volumes"] if "hostPath" in v}
-    return Pod(kind=obj["kind"], args=[str(a) for a in c.get("args", [])],
-               env={e["name"]: str(e["value"]) for e in c.get("env", [])},
-               mounts={m["mountPath"]: vols[m["name"]] for m in c.get("volumeMounts", [])})
+    return Pod(kind=kind, args=[str(a) for a in c.get("args", [])],
+               env={e["name"]: str(e["value"]) for e in c.get("env", []) or []},
+               mounts={m["mountPath"]: vols[m["name"]] for m in c.get("volumeMounts", []) if m["name"] in vols})
 
 
-def _value(values: dict, dotted: str):
-    node = values
-    for part in dotted.split("."):
-        node = node.get(part) if isinstance(node, dict) else None
-    return node
+def from_helm(chart: Path, values: dict | None = None) -> Pod:
+    """The chart's DaemonSet container as `helm template` renders it with
+    values.yaml's defaults (tests/helm_lite.py)."""
+    import helm_lite
 
-
-def _helm_string(v) -> str:  # sprig's toString
-    return ("true" if v else "false") if isinstance(v, bool) else str(v)
-
-
-def from_helm(native, chart: Path) -> Pod:
-    """The chart's DaemonSet container under values.yaml's defaults: env from
-    the gfd-amd.env helper (templates/_helpers.tpl), mounts and volumes from
-    templates/daemonset.yml, `{{- if .Values.x }}` blocks evaluated."""
-    values = native.parse_yaml((chart / "values.yaml").read_text())
-    helpers = (chart / "templates" / "_helpers.tpl").read_text()
-    env: dict[str, str] = {}
-    for name, key in re.findall(r'"(GFD_[A-Z_]+)" \.Values\.([\w.]+)', helpers):
-        v = _value(values, key)
-        if v is not None and _helm_string(v) != "":
-            env[name] = _helm_string(v)
-    for cond, name, val in re.findall(r"\{\{- if \.Values\.([\w.]+) \}\}\s*- name: (GFD_\w+)\s*value: (\S+)", helpers):
-        if _value(values, cond):
-            env[name] = val
-    ds = (chart / "templates" / "daemonset.yml").read_text()
-    assert "args:" not in ds, "chart passes arguments: extend from_helm"
-
-    def active(text: str) -> list[str]:
-        # Lines outside false `{{- if .Values.x }}` blocks (no nesting/else).
-        out, keep = [], [True]
-        for line in text.splitlines():
-            m = re.search(r"\{\{-? if \.Values\.([\w.]+) \}\}", line)
-            if m:
-                keep.append(keep[-1] and bool(_value(values, m.group(1))))
-                continue
-            if re.search(r"\{\{-? end \}\}", line) and len(keep) > 1:
-                keep.pop()
-                continue
-            if keep[-1]:
-                out.append(re.sub(r"\{\{ \.Values\.([\w.]+) \}\}", lambda mm: str(_value(values, mm.group(1))), line))
-        return out
-
-    lines = "\n".join(active(ds))
-    vols = dict(re.findall(r"- name: ([\w-]+)\n\s+hostPath:\n\s+path: (\S+)", lines))
-    mounts = {mp.strip(): vols[n] for n, mp in re.findall(r"- \{name: ([\w-]+), mountPath: ([^,}]+)", lines)}
-    return Pod(kind="DaemonSet", env=env, mounts=mounts)
+    docs = helm_lite.documents(helm_lite.render_chart(chart, values))
+    (ds,) = [d for d in docs if d["kind"] == "DaemonSet" and d["metadata"]["name"].endswith("gpu-feature-discovery-amd")]
+    return from_pod_spec("DaemonSet", ds["spec"]["template"]["spec"])
 
 
 def materialise(pod: Pod, croot: Path, host_opt: Path = Path("/opt")) -> None:

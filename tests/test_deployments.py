@@ -158,51 +158,91 @@ def test_chart_dependencies_are_in_the_repository(native):
     assert values["nfd"]["deploy"] is True  # deployable by default: it is in the repository
 
 
-def test_nfd_subchart_renders_from_the_default_values(native):
-    """Render the NFD subchart as helm would with the parent's defaults (the
-    parent's `nfd:` block coalesced over the subchart's values.yaml) and
-    check what labeling depends on: the master publishes amd.com, the worker
-    reads the features.d hostPath the labeler writes and whitelists the
-    accelerator PCI class, both on the gRPC path."""
+def _render(values=None, namespace="gpu-feature-discovery"):
     import helm_lite
 
-    sub = CHART / "charts" / "nfd-minimal"
-    values = helm_lite.merge(native.parse_yaml((sub / "values.yaml").read_text()),
-                             native.parse_yaml((CHART / "values.yaml").read_text())["nfd"])
-    docs = []
-    for t in sorted((sub / "templates").iterdir()):
-        text = helm_lite.render(t.read_text(), values)
-        docs += [native.parse_yaml(d) for d in re.split(r"^---\s*$", text, flags=re.M) if d.strip()]
+    return helm_lite.documents(helm_lite.render_chart(CHART, values, namespace=namespace))
+
+
+def test_chart_renders_offline_from_the_default_values(native):
+    """`helm template` of the chart's defaults, done by tests/helm_lite.py:
+    the labeler DaemonSet plus the in-repo NFD subchart, and what labeling
+    depends on - the labeler's env are daemon flags, it mounts features.d,
+    /sys and the host's /opt; NFD publishes amd.com, reads the same
+    features.d and whitelists the accelerator PCI class, on the gRPC path."""
+    docs = _render()
     kinds = sorted(d["kind"] for d in docs)
-    assert kinds == ["ClusterRole", "ClusterRoleBinding", "ConfigMap", "DaemonSet", "Deployment", "Service",
-                     "ServiceAccount"]
+    assert kinds == ["ClusterRole", "ClusterRoleBinding", "ConfigMap", "DaemonSet", "DaemonSet", "Deployment",
+                     "Service", "ServiceAccount"]
+    (gfd,) = [d for d in docs if d["kind"] == "DaemonSet" and d["metadata"]["name"] == "gfd-gpu-feature-discovery-amd"]
+    spec = gfd["spec"]["template"]["spec"]
+    (c,) = spec["containers"]
+    env = {e["name"]: e["value"] for e in c["env"]}
+    assert set(env) <= _env_vars(native), set(env) - _env_vars(native)
+    assert env["GFD_MIG_STRATEGY"] == "none" and env["GFD_HOST_ROOT"] == "/host"
+    assert c["image"].endswith(":" + _version())
+    vols = {v["name"]: v["hostPath"] for v in spec["volumes"]}
+    assert vols["host-opt"] == {"path": "/opt", "type": "Directory"}
+    assert spec["priorityClassName"] == "system-node-critical"
     master = next(d for d in docs if d["kind"] == "Deployment")
     args = master["spec"]["template"]["spec"]["containers"][0]["args"]
     assert "-extra-label-ns=amd.com" in args and "-enable-nodefeature-api=false" in args
-    worker = next(d for d in docs if d["kind"] == "DaemonSet")
-    spec = worker["spec"]["template"]["spec"]
-    wargs = spec["containers"][0]["args"]
-    assert "-server=gfd-nfd-master:8080" in wargs and "-enable-nodefeature-api=false" in wargs
-    assert {"key": "amd.com/gpu", "operator": "Exists", "effect": "NoSchedule"} in spec["tolerations"]
-    vols = {v["name"]: v for v in spec["volumes"]}
-    assert vols["features-d"]["hostPath"]["path"] == "/etc/kubernetes/node-feature-discovery/features.d"
+    (worker,) = [d for d in docs if d["kind"] == "DaemonSet" and d["metadata"]["name"] == "gfd-nfd-worker"]
+    wspec = worker["spec"]["template"]["spec"]
+    assert "-server=gfd-nfd-master:8080" in wspec["containers"][0]["args"]
+    assert {"key": "amd.com/gpu", "operator": "Exists", "effect": "NoSchedule"} in wspec["tolerations"]
+    wvols = {v["name"]: v for v in wspec["volumes"]}
+    assert wvols["features-d"]["hostPath"]["path"] == vols["features-d"]["path"]
     cm = next(d for d in docs if d["kind"] == "ConfigMap")
     conf = native.parse_yaml(cm["data"]["nfd-worker.conf"])
     assert "12" in conf["sources"]["pci"]["deviceClassWhitelist"]
-    svc = next(d for d in docs if d["kind"] == "Service")
-    assert svc["metadata"]["name"] == "gfd-nfd-master"
-    # Every value the templates use exists (an unknown one raises in render).
-    assert all(d["metadata"].get("namespace", "gpu-feature-discovery") == "gpu-feature-discovery" for d in docs)
+
+
+def test_chart_options_render(native):
+    """nfd.deploy=false drops the subchart; a config file becomes a ConfigMap,
+    a mount, GFD_CONFIG_FILE and a checksum annotation (pods restart when it
+    changes); an unprivileged pod (securityContext: null - an empty map would
+    be merged with the default) drops every capability."""
+    docs = _render({"nfd": {"deploy": False}, "config": {"version": "v1", "flags": {"migStrategy": "mixed"}},
+                    "securityContext": None})
+    assert sorted(d["kind"] for d in docs) == ["ConfigMap", "DaemonSet"]
+    (ds,) = [d for d in docs if d["kind"] == "DaemonSet"]
+    pod = ds["spec"]["template"]
+    assert "checksum/config" in pod["metadata"]["annotations"]
+    (c,) = pod["spec"]["containers"]
+    env = {e["name"]: e["value"] for e in c["env"]}
+    assert env["GFD_CONFIG_FILE"] == "/etc/gfd/config.yaml"
+    assert {"name": "gfd-config", "mountPath": "/etc/gfd", "readOnly": True} in c["volumeMounts"]
+    assert c["securityContext"] == {"allowPrivilegeEscalation": False, "capabilities": {"drop": ["ALL"]}}
+    cm = next(d for d in docs if d["kind"] == "ConfigMap")
+    assert native.parse_yaml(cm["data"]["config.yaml"])["flags"]["migStrategy"] == "mixed"
+
+
+@pytest.mark.parametrize("values,namespace,message", [
+    ({"namespace": "x"}, "gpu-feature-discovery", "'namespace' value is not supported"),
+    ({}, "default", "'default' namespace is not allowed"),
+    ({"migStrategy": "bogus"}, "gpu-feature-discovery", "migStrategy must be one of"),
+])
+def test_chart_validation_fails_like_the_reference(values, namespace, message):
+    """templates/validation.yml (reference: templates/validation.yml:1-16)."""
+    import helm_lite
+
+    with pytest.raises(helm_lite.HelmFail, match=message):
+        _render(values, namespace=namespace)
+    if namespace == "default":
+        _render({"allowDefaultNamespace": True}, namespace="default")
 
 
 def test_helm_lite_refuses_what_it_does_not_implement():
     import helm_lite
 
-    with pytest.raises(ValueError):
+    with pytest.raises(helm_lite.HelmFail, match="unsupported function"):
+        helm_lite.render("{{ lower .Values.x }}", {"x": "A"})
+    with pytest.raises(helm_lite.HelmFail, match="no template"):
         helm_lite.render('{{ include "x" . }}', {})
-    with pytest.raises(KeyError):
-        helm_lite.render("{{ .Values.missing }}", {})
+    assert helm_lite.render("{{ .Values.missing }}", {}) == ""  # Helm renders a missing key empty
     assert helm_lite.render("a:{{- range .Values.l }} {{ . }}{{- end }}", {"l": [1, 2]}) == "a: 1 2"
+    assert helm_lite.render('{{ if and .Values.a (not .Values.b) }}y{{ else }}n{{ end }}', {"a": 1, "b": 0}) == "y"
 
 
 # ---- The manifests' own argv / env / mounts, run (tests/manifest_pods.py) --
@@ -219,7 +259,7 @@ MANIFEST_PODS = [
 def manifest_pod(native, source):
     import manifest_pods
 
-    return manifest_pods.from_helm(native, CHART) if source is None else manifest_pods.from_static(native, STATIC / source)
+    return manifest_pods.from_helm(CHART) if source is None else manifest_pods.from_static(native, STATIC / source)
 
 
 def check_manifest_run(r, pod, strategy, rocm: str):

@@ -8,6 +8,8 @@ from --trace-timing, and what is left in the output directory after exit.
         [--backend auto|synthetic] [--variant VAR=val[,VAR=val]] ...
 
 DIR is where the output file goes (its file system is what is measured).
+A variant's BIN=path runs that daemon binary instead of build/'s (e.g. an
+earlier commit's build, to compare revisions on one box).
 """
 
 from __future__ import annotations
@@ -50,10 +52,12 @@ def main() -> int:
             for v in variants[1:]:
                 for kv in v.split(","):
                     env.pop(kv.split("=", 1)[0], None)
+            binary = os.path.join(REPO, "build", "gpu-feature-discovery")
             if var != "default":
                 env.update(kv.split("=", 1) for kv in var.split(","))
+                binary = os.path.join(REPO, env.pop("BIN", binary))
             out = os.path.join(d, f"out-{i}-{rep}", "gfd")
-            p = subprocess.Popen([os.path.join(REPO, "build", "gpu-feature-discovery"), *extra,
+            p = subprocess.Popen([binary, *extra,
                                   f"--sleep-interval={a.interval}", "--trace-timing", f"--output-file={out}"],
                                  stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True, env=env)
             tot, wr, ren = [], [], []

@@ -35,8 +35,12 @@ class CycleResult:
 class Labeler:
     """A configured daemon instance (flags as on the command line)."""
 
-    def __init__(self, args: Sequence[str] = (), env: dict[str, str] | None = None):
-        self._session = native().Session(list(args), env)
+    def __init__(self, args: Sequence[str] = (), env: dict[str, str] | None = None,
+                 amdsmi_library_only: bool = False):
+        """``env``: a private environment for flag resolution (instead of the
+        process's); ``amdsmi_library_only``: the amd-smi backend answers every
+        query through library calls (a cross-check of its attribute reads)."""
+        self._session = native().Session(list(args), env, amdsmi_library_only)
 
     @property
     def backend(self) -> str:

@@ -12,6 +12,7 @@ GPU node; not part of the CPU test-suite.
 from __future__ import annotations
 
 import argparse
+import re
 import subprocess
 import sys
 import tempfile
@@ -22,6 +23,27 @@ REPO = Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(REPO))
 
 from gpu_feature_discovery_amd.utils import golden  # noqa: E402
+
+
+def check(text: str, strategy: str) -> None:
+    """The labels against the regex golden of what the node is: an
+    unpartitioned node gets the full-GPU set under every strategy (plus the
+    strategy label under single/mixed); a partitioned one under `single`
+    the partition-single golden, under `mixed` per-profile resources."""
+    labels = golden.parse_labels(text)
+    assert labels.get("amd.com/partition.strategy", "none") == strategy, labels
+    partitioned = labels.get("amd.com/gpu.compute-partition", "SPX") != "SPX"
+    not_sriov = lambda ln: "sriov" not in ln  # noqa: E731
+    if not partitioned or strategy == "none":
+        golden.check_regex_golden(text, REPO / "tests" / "expected-output.txt",
+                                  select=lambda ln: not_sriov(ln) and not ln.startswith("amd.com/partition.strategy="))
+    elif strategy == "single":
+        golden.check_regex_golden(text, REPO / "tests" / "expected-output-partition-single.txt", select=not_sriov)
+    else:
+        per_profile = re.compile(r"amd\.com/partition-[a-z]+\.[0-9]+xcd\.[0-9]+gb\.(product|count|replicas|memory|"
+                                 r"compute-units|xcds|compute-partition|memory-partition|engines\.[a-z]+)=[A-Za-z0-9_.-]+")
+        keys = [k for k in labels if k.startswith("amd.com/partition-")]
+        assert keys and all(per_profile.fullmatch(f"{k}={labels[k]}") for k in keys), keys
 
 
 def main() -> int:
@@ -48,9 +70,7 @@ def main() -> int:
                 print("features.d/gfd never appeared", file=sys.stderr)
                 return 1
             text = out.read_text()
-            goldens = {"none": "expected-output.txt", "single": "expected-output-partition-single.txt",
-                       "mixed": "expected-output-partition-mixed.txt"}
-            golden.check_regex_golden(text, REPO / "tests" / goldens[a.strategy], select=lambda ln: "sriov" not in ln)
+            check(text, a.strategy)
             print(text, end="")
             print("integration test passed")
             return 0

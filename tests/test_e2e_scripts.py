@@ -1,0 +1,130 @@
+"""The counterparts of the reference's container integration test
+(tests/integration-tests.py) and cluster e2e test (tests/e2e-tests.py) -
+tests/e2e/integration_docker.py and tests/e2e/e2e_kubectl.py - run as they
+are, against a fake `docker` and a fake one-node `kubectl`
+(tests/e2e/fakes/): the labeler starts from the manifests' own argv, env
+and mounts, and the fake cluster publishes labels the way NFD would (its PCI
+source under the worker's class whitelist, its local source only in the
+master's -extra-label-ns namespaces).  On CPU the node is a synthetic
+MI355X tree; tests/test_gpu.py runs the same on the real MI355X.
+"""
+
+from __future__ import annotations
+
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+
+from conftest import REPO
+from gpu_feature_discovery_amd.utils import synth
+
+FAKES = REPO / "tests" / "e2e" / "fakes"
+
+
+def e2e_env(tmp_path, sysfs_root=None, host_opt=None) -> dict:
+    env = {k: v for k, v in os.environ.items() if not k.startswith(("GFD_", "FAKE_"))}
+    env["PATH"] = f"{FAKES}:{env['PATH']}"
+    env["FAKE_RUNTIME_STATE"] = str(tmp_path / "runtime")
+    if sysfs_root:
+        env["FAKE_SYSFS_ROOT"] = str(sysfs_root)
+    if host_opt:
+        env["FAKE_HOST_OPT"] = str(host_opt)
+    return env
+
+
+def stop_all(env):
+    """Stop whatever the fakes started (the e2e script leaves its DaemonSet)."""
+    sys.path.insert(0, str(FAKES))
+    os.environ["FAKE_RUNTIME_STATE"] = env["FAKE_RUNTIME_STATE"]
+    try:
+        import importlib
+
+        rt = importlib.reload(importlib.import_module("_runtime"))
+        for pid_file in rt.STATE.glob("*/pid"):
+            rt.stop(pid_file.parent.name)
+    finally:
+        os.environ.pop("FAKE_RUNTIME_STATE", None)
+        sys.path.remove(str(FAKES))
+
+
+def run_integration(env, strategy="none", timeout=60):
+    return subprocess.run([sys.executable, str(REPO / "tests/e2e/integration_docker.py"), "gfd-amd:test",
+                           f"--strategy={strategy}", "--timeout=30"], capture_output=True, text=True, env=env,
+                          timeout=timeout)
+
+
+def run_e2e(env, timeout=90):
+    return subprocess.run([sys.executable, str(REPO / "tests/e2e/e2e_kubectl.py"), "--timeout=40"],
+                          capture_output=True, text=True, env=env, timeout=timeout)
+
+
+@pytest.fixture()
+def node(tmp_path):
+    return synth.make_mi355x_node(tmp_path / "node", n_gpus=2, seed=50)
+
+
+@pytest.mark.parametrize("strategy", ["none", "single", "mixed"])
+def test_integration_script_against_fake_docker(tmp_path, node, strategy):
+    env = e2e_env(tmp_path, node, node / "opt")
+    try:
+        cp = run_integration(env, strategy)
+    finally:
+        stop_all(env)
+    assert cp.returncode == 0, cp.stdout + cp.stderr
+    assert "integration test passed" in cp.stdout
+    assert "amd.com/rocm.runtime.major=7" in cp.stdout
+
+
+def test_e2e_script_against_fake_cluster(tmp_path, node):
+    env = e2e_env(tmp_path, node, node / "opt")
+    try:
+        cp = run_e2e(env)
+    finally:
+        stop_all(env)
+    assert cp.returncode == 0, cp.stdout + cp.stderr
+    assert "e2e test passed" in cp.stdout
+    assert '"amd.com/gpu.count": "2"' in cp.stdout
+
+
+def test_fake_cluster_enforces_nfd_wiring(tmp_path, node):
+    """The fake cluster is strict where a real one is: without amd.com in
+    nfd-master's -extra-label-ns no amd.com label is published, and without
+    PCI class 12 in the worker's whitelist the labeler's node affinity never
+    matches an MI355X node."""
+    env = e2e_env(tmp_path, node, node / "opt")
+    nfd = (REPO / "deployments/static/nfd.yaml").read_text()
+    ds = REPO / "deployments/static/gpu-feature-discovery-daemonset.yaml"
+    kubectl = [str(FAKES / "kubectl")]
+
+    def labels():
+        import json
+
+        out = subprocess.run(kubectl + ["get", "nodes", "-o", "json"], capture_output=True, text=True, env=env,
+                             check=True).stdout
+        return json.loads(out)["items"][0]["metadata"]["labels"]
+
+    try:
+        bad = tmp_path / "nfd-no-ns.yaml"
+        bad.write_text(re.sub(r'^\s*- "-extra-label-ns=amd.com"\n', "", nfd, flags=re.M))
+        subprocess.run(kubectl + ["apply", "-f", str(bad)], check=True, env=env, capture_output=True)
+        subprocess.run(kubectl + ["apply", "-f", str(ds)], check=True, env=env, capture_output=True)
+        import time
+
+        time.sleep(1.0)
+        got = labels()
+        assert got.get("feature.node.kubernetes.io/pci-1002.present") == "true"
+        assert not any(k.startswith("amd.com/") for k in got), got
+    finally:
+        stop_all(env)
+    env2 = e2e_env(tmp_path / "b", node, node / "opt")
+    try:
+        bad = tmp_path / "nfd-no-class.yaml"
+        bad.write_text(nfd.replace('"12", "1200"', '"0b40"'))
+        subprocess.run(kubectl + ["apply", "-f", str(bad)], check=True, env=env2, capture_output=True)
+        cp = subprocess.run(kubectl + ["apply", "-f", str(ds)], env=env2, capture_output=True, text=True)
+        assert "no node matches its affinity" in cp.stderr
+    finally:
+        stop_all(env2)

@@ -474,3 +474,36 @@ def test_manifest_pod_labels_the_real_node(native, binary, tmp_path, name, sourc
     check_manifest_run(r, pod, strategy, _box_rocm())
     if pod.env.get("GFD_BACKEND", "auto") == "auto" and pod.kind == "DaemonSet":
         assert "failed to initialize" not in r["stderr"], r["stderr"][-3000:]
+
+
+# ---- tests/e2e scripts (the reference's integration / e2e tests) on the node -
+
+def test_integration_script_on_the_real_node(tmp_path):
+    """tests/e2e/integration_docker.py as it is, its `docker run` served by
+    the fake runtime (tests/e2e/fakes): the labeler with the host's real
+    /sys and /opt, labels checked against the regex golden."""
+    from test_e2e_scripts import e2e_env, run_integration, stop_all
+
+    env = e2e_env(tmp_path)
+    try:
+        cp = run_integration(env, "none", timeout=120)
+    finally:
+        stop_all(env)
+    assert cp.returncode == 0, cp.stdout + cp.stderr
+    assert "integration test passed" in cp.stdout and "amd.com/gpu.arch=gfx950" in cp.stdout
+
+
+def test_e2e_script_on_the_real_node(tmp_path):
+    """tests/e2e/e2e_kubectl.py as it is, against the fake one-node cluster
+    on the real MI355X: NFD's PCI source must match the node (class 0x12
+    whitelisted) for the DaemonSet to schedule, and its local source must
+    publish the amd.com labels."""
+    from test_e2e_scripts import e2e_env, run_e2e, stop_all
+
+    env = e2e_env(tmp_path)
+    try:
+        cp = run_e2e(env, timeout=150)
+    finally:
+        stop_all(env)
+    assert cp.returncode == 0, cp.stdout + cp.stderr
+    assert "e2e test passed" in cp.stdout and '"amd.com/gpu.family": "cdna4"' in cp.stdout

@@ -50,19 +50,18 @@ std::string render(const Labels& labels);
 // 0644).  An empty path writes to stdout.  Throws gfd::Error.  A temporary
 // file prepared by temp_preparer()'s job is used if one is ready; the write
 // that uses one (loop mode) swaps it with the old feature file
-// (RENAME_EXCHANGE) and leaves the old file for the next job to unlink.
+// (RENAME_EXCHANGE), leaving the old file for the next job to unlink.
 void write_to_file(const Labels& labels, const std::string& path);
 // Atomic write of arbitrary contents (labels.go:68-114).
 void write_file_atomically(const std::string& path, const std::string& contents, unsigned perm);
 // Loop mode: a job for a worker to run while a cycle enumerates - it unlinks
-// the old feature file the last write swapped out and creates the temporary
-// file of the next write to `path` (blocks preallocated for the last written
+// the old feature files earlier writes swapped out and creates the temporary
+// file of a later write to `path` (blocks preallocated for the last written
 // size where the write preallocates).  Empty when there is nothing to do or
-// a job is still out.  At most two prepared files and one old feature file
-// wait in <dir>/gfd-tmp.
+// a job is still out.
 std::function<void()> temp_preparer(const std::string& path);
 // Waits (bounded) for a handed-out job, then removes the prepared files and
-// the old feature file.
+// any swapped-out feature file not unlinked yet.
 void discard_prepared_temps();
 // Start-up: removes <dir>/gfd-tmp left by a process that did not exit
 // cleanly (one GFD per node writes there, as the reference assumes).

@@ -484,16 +484,19 @@ TEST(WriteToFile_UsesPreparedTemporaryFiles) {
   EXPECT_TRUE(stat(path.c_str(), &st) == 0);
   EXPECT_EQ(static_cast<int>(st.st_mode & 0777), 0644);
   EXPECT_EQ(fs::read_file(a).data, std::string("k=0\n"));
-  // The next write takes the other one; an old file still waiting for its
-  // unlink is not displaced (a plain rename replaces the feature file).
+  // The next write takes the other one and exchanges too, although the
+  // first old file still waits (no job ran in between).
   lm::write_to_file({{"k", "2"}}, path);
   EXPECT_EQ(fs::read_file(path).data, std::string("k=2\n"));
   EXPECT_EQ(inode(path), ino_b);
   EXPECT_EQ(fs::read_file(a).data, std::string("k=0\n"));
+  EXPECT_EQ(fs::read_file(b).data, std::string("k=1\n"));
+  // The job unlinks both and makes the next file.
   auto job = lm::temp_preparer(path);
   EXPECT_TRUE(static_cast<bool>(job));
   job();
   EXPECT_FALSE(fs::exists(a));
+  EXPECT_FALSE(fs::exists(b));
   auto next = prepared_files(dir);
   EXPECT_EQ(next.size(), static_cast<size_t>(1));
   EXPECT_EQ(fs::read_file(next[0]).data, std::string());
@@ -522,8 +525,8 @@ TEST(WriteToFile_EveryLoopWriteFindsAPreparedFile) {
       if (fs::read_file(f).data.empty()) inos.insert(inode(f));
     lm::write_to_file({{"k", std::to_string(i)}}, path);
     EXPECT_TRUE(inos.count(inode(path)) == 1);
-    if (job) job();
-    EXPECT_TRUE(prepared_files(dir).size() <= static_cast<size_t>(3));
+    if (job) job();  // after the write: it also unlinks this write's old file
+    EXPECT_TRUE(prepared_files(dir).size() <= static_cast<size_t>(2));
   }
   lm::remove_output_file(path);
   fs::remove_all(dir);
@@ -535,7 +538,7 @@ TEST(WriteToFile_SteadyLoopKeepsAtMostThreeFilesInTheTemporaryDirectory) {
   std::string path = std::string(dir) + "/gfd";
   for (int i = 0; i < 20; ++i) {
     prepare_then_write({{"k", std::to_string(i)}}, path);
-    EXPECT_TRUE(prepared_files(dir).size() <= static_cast<size_t>(3));
+    EXPECT_TRUE(prepared_files(dir).size() <= static_cast<size_t>(3));  // two prepared, one old
     EXPECT_EQ(fs::read_file(path).data, "k=" + std::to_string(i) + "\n");
   }
   lm::remove_output_file(path);

@@ -74,7 +74,8 @@ def main() -> int:
             p.wait(timeout=30)
             left = sorted(os.listdir(os.path.dirname(out)))
             print(f"rep {rep} {var:60s} cycle p50 {statistics.median(tot[1:]):.3f} ms  "
-                  f"write p50 {statistics.median(wr[1:]):.3f} ms  replace p50 {statistics.median(ren[1:]):.3f} ms  "
+                  f"write p50 {statistics.median(wr[1:]):.3f} ms  replace p50 {statistics.median(ren[1:]):.3f} ms "
+                  f"max {max(ren[1:]):.3f} ms  "
                   f"left after exit: {left}", flush=True)
     shutil.rmtree(d)
     return 0

@@ -135,9 +135,10 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
   lm::NodeFacts facts;
   lm::Labels sriov_labels;
   std::exception_ptr sriov_error;
-  int64_t facts_ns = 0, sriov_ns = 0;
+  int64_t facts_ns = 0, sriov_ns = 0, facts_start = 0, submitted = 0;
   std::function<void()> read_facts = [&] {
     int64_t s0 = trace::now_ns();
+    facts_start = s0;
     try {
       facts = lm::ReadNodeFacts(config, version_files);
     } catch (...) {
@@ -162,6 +163,7 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
   std::vector<std::function<void()>> fns{read_facts, scan_sriov};
   if (write && !config.oneshot())
     if (auto prepare = lm::temp_preparer(config.output_file())) fns.push_back(std::move(prepare));
+  submitted = trace::now_ns();
   auto seq = WorkerPool::instance().submit_sequence(std::move(fns));
   WorkerPool::Task facts_task = seq[0], sriov_task = seq[1];
   auto join_facts = [&]() -> const lm::NodeFacts& {
@@ -178,7 +180,13 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
     throw;
   }
   facts_task.cancel_or_wait();  // no devices: the labeler never needed them
+  int64_t j0 = trace::now_ns();
   sriov_task.run_or_wait();
+  // Where an overlapped cycle waits: how long after the hand-off the node
+  // facts started (a worker's wake-up, or this thread taking them over),
+  // and how long this thread then waited for the SR-IOV scan.
+  trace::record("sriov.join", trace::now_ns() - j0);
+  trace::record("facts.start", facts_start ? facts_start - submitted : 0);
   trace::record("facts(overlapped)", facts_ns);
   trace::record("sriov(overlapped)", sriov_ns);
   if (sriov_error) {

@@ -35,8 +35,8 @@ def _fds(pid: int) -> tuple[int, int]:
     # descriptors (the temp output file, an amd-smi device node), a leak
     # raises the floor.  The window must catch the daemon between cycles at
     # least once (see the per-cycle interval below).  Prepared temporary
-    # files (gfd-tmp/<a-e>/gfd-*, up to four kept open between cycles by design,
-    # src/lm/labels.cpp PreparedTemps) are counted apart: how many are ready
+    # files (gfd-tmp/gfd-*, up to two kept open between cycles by design,
+    # src/lm/labels.cpp WriterState) are counted apart: how many are ready
     # at a sample depends on timing, not on leaks - that made the floor
     # 15 or 16 from run to run.  Returns (floor without them, most of them).
     n, prepared = [], []
@@ -107,10 +107,10 @@ def _assert_steady(r: dict, min_cycles: int):
     assert r["rc"] == 0, r["tail"]
     assert r["cycles"] >= min_cycles, r
     assert r["fd1"] <= r["fd0"], f"file descriptors grew {r['fd0']} -> {r['fd1']}"
-    assert r["prepared"] <= 4, f"{r['prepared']} prepared temporary files open (at most four by design)"
-    # Four prepared + the swapped-out files no worker job has reached yet (one
+    assert r["prepared"] <= 2, f"{r['prepared']} prepared temporary files open (at most two by design)"
+    # Two prepared + the swapped-out files no worker job has reached yet (one
     # between cycles; two if a cycle's write beats the previous cycle's job).
-    assert r["tmp_files"] <= 6, f"{r['tmp_files']} files in gfd-tmp/: old feature files are not being unlinked"
+    assert r["tmp_files"] <= 4, f"{r['tmp_files']} files in gfd-tmp/: old feature files are not being unlinked"
     # Allocator noise only: a leak of even 100 bytes/cycle over thousands of
     # cycles would exceed this.
     assert r["rss1"] - r["rss0"] <= 1024, f"RSS grew {r['rss0']} -> {r['rss1']} KiB over {r['cycles']} cycles"

@@ -123,6 +123,7 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
                         const config::Config& config, const lm::LabelerPtr& timestamp, bool write) {
   trace::begin_cycle();
   int64_t t0 = trace::now_ns();
+  WorkerPool::instance().follow_caller();  // --cpu-affinity=follow
   // Work that does not depend on the device backend runs on workers while
   // the backend enumerates: the node facts the device labeler needs after
   // enumeration (machine type, file-backed versions) and the SR-IOV bus scan
@@ -338,8 +339,11 @@ int gfd_main(int argc, char** argv) {
   std::string placement = ctx.String("cpu-affinity");
   if (placement == "l3") {
     if (std::string pinned = affinity::pin_to_current_l3(); !pinned.empty()) log::printf("CPU affinity: %s", pinned.c_str());
+  } else if (placement == "follow") {
+    WorkerPool::instance().set_follow(true);
+    log::printf("CPU affinity: workers follow the labeling thread's L3 cache domain");
   } else if (placement != "none") {
-    log::printf("Error: unknown --cpu-affinity '%s' (expected none or l3)", placement.c_str());
+    log::printf("Error: unknown --cpu-affinity '%s' (expected none, follow or l3)", placement.c_str());
     return 1;
   }
   int rc = 0;

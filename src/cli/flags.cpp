@@ -184,8 +184,9 @@ std::vector<FlagDef> gfd_flags() {
       {"mock-file", {}, T::String, "", {"GFD_MOCK_FILE"}, "device fixture (YAML/JSON) for --backend=mock"},
       {"trace-timing", {}, T::Bool, "false", {"GFD_TRACE_TIMING"}, "log per-phase timing of every labeling cycle"},
       {"cpu-affinity", {}, T::String, "none", {"GFD_CPU_AFFINITY"},
-       "CPU placement of the daemon's threads: none (the scheduler decides) | l3 (the CPUs sharing the L3 cache of\n\t\t"
-       "the CPU it starts on: faster back-to-back cycles, for short --sleep-interval only)"},
+       "CPU placement of the daemon's threads: none (the scheduler decides) | follow (worker threads kept on the\n\t\t"
+       "CPUs sharing the L3 cache of the CPU each cycle starts on) | l3 (every thread on the L3 domain of the CPU\n\t\t"
+       "the daemon starts on)"},
   };
 }
 

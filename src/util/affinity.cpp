@@ -2,6 +2,9 @@
 
 #include <sched.h>
 
+#include <map>
+#include <mutex>
+#include <utility>
 #include <vector>
 
 #include "util/fs.h"
@@ -22,19 +25,40 @@ std::vector<int> parse_cpu_list(const std::string& s) {
   return out;
 }
 
+namespace {
+// "0-7,128-135" of the L3 cache of `cpu` (the cache index whose level is 3:
+// index3 on x86, but look), or "".
+std::string l3_list(int cpu, const std::string& sys_root) {
+  std::string base = fs::join(sys_root, "sys/devices/system/cpu/cpu" + std::to_string(cpu) + "/cache");
+  for (const auto& idx : fs::list_dir(base)) {
+    if (idx.rfind("index", 0) != 0) continue;
+    if (fs::read_trimmed(fs::join(base, idx + "/level")).value_or("") == "3")
+      return fs::read_trimmed(fs::join(base, idx + "/shared_cpu_list")).value_or("");
+  }
+  return "";
+}
+}  // namespace
+
+std::vector<int> l3_domain(int cpu, const std::string& sys_root) {
+  static std::mutex mu;
+  static std::map<std::pair<std::string, int>, std::vector<int>> known;
+  std::lock_guard<std::mutex> lk(mu);
+  auto key = std::make_pair(sys_root, cpu);
+  auto it = known.find(key);
+  if (it != known.end()) return it->second;
+  std::vector<int> out;
+  cpu_set_t allowed;
+  CPU_ZERO(&allowed);
+  if (cpu >= 0 && sched_getaffinity(0, sizeof(allowed), &allowed) == 0)
+    for (int c : parse_cpu_list(l3_list(cpu, sys_root)))
+      if (CPU_ISSET(c, &allowed)) out.push_back(c);
+  return known.emplace(key, std::move(out)).first->second;
+}
+
 std::string pin_to_current_l3(const std::string& sys_root) {
   int cpu = sched_getcpu();
   if (cpu < 0) return "";
-  // The L3 is the cache index whose level is 3 (index3 on x86, but look).
-  std::string base = fs::join(sys_root, "sys/devices/system/cpu/cpu" + std::to_string(cpu) + "/cache");
-  std::string list;
-  for (const auto& idx : fs::list_dir(base)) {
-    if (idx.rfind("index", 0) != 0) continue;
-    if (fs::read_trimmed(fs::join(base, idx + "/level")).value_or("") == "3") {
-      list = fs::read_trimmed(fs::join(base, idx + "/shared_cpu_list")).value_or("");
-      break;
-    }
-  }
+  std::string list = l3_list(cpu, sys_root);
   std::vector<int> l3 = parse_cpu_list(list);
   if (l3.empty()) return "";
   cpu_set_t allowed;

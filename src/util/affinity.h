@@ -22,6 +22,10 @@ namespace gfd::affinity {
 // Returns what was done, for the log ("" when nothing changed).
 std::string pin_to_current_l3(const std::string& sys_root = "/");
 
+// The CPUs sharing the L3 cache of `cpu` that this process may use (read
+// from sysfs once per CPU, then cached); empty if unknown.
+std::vector<int> l3_domain(int cpu, const std::string& sys_root = "/");
+
 // "0-7,128-135" -> CPU numbers; empty on a malformed list.
 std::vector<int> parse_cpu_list(const std::string& s);
 

@@ -1,16 +1,29 @@
 #include "util/pool.h"
 
+#include <pthread.h>
+#include <sched.h>
+
 #include <algorithm>
 #include <atomic>
 
+#include "util/affinity.h"
+
 namespace gfd {
+
+namespace {
+void pin(std::thread& t, const std::vector<int>& cpus) {
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  for (int c : cpus) CPU_SET(c, &set);
+  pthread_setaffinity_np(t.native_handle(), sizeof(set), &set);
+}
+}  // namespace
 
 WorkerPool& WorkerPool::instance() {
   // Leaked on purpose: workers may still be parked at exit.
   static WorkerPool* pool = new WorkerPool(8);
   return *pool;
 }
-
 
 WorkerPool::WorkerPool(size_t max_workers) : max_workers_(max_workers ? max_workers : 1) {}
 
@@ -37,7 +50,25 @@ void WorkerPool::ensure_workers(size_t n) {
     workers_.push_back(std::make_unique<Worker>());
     Worker* w = workers_.back().get();
     threads_.emplace_back([this, w] { loop(w); });
+    if (!domain_.empty()) pin(threads_.back(), domain_);
   }
+}
+
+void WorkerPool::set_follow(bool on) {
+  std::lock_guard<std::mutex> g(mu_);
+  follow_ = on;
+}
+
+void WorkerPool::follow_caller() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (!follow_) return;
+  }
+  std::vector<int> domain = affinity::l3_domain(sched_getcpu());
+  std::lock_guard<std::mutex> g(mu_);
+  if (domain.empty() || domain == domain_) return;
+  domain_ = std::move(domain);
+  for (auto& t : threads_) pin(t, domain_);
 }
 
 void WorkerPool::wake_one() {

@@ -75,6 +75,13 @@ class WorkerPool {
 
   size_t workers() const;
 
+  // Workers follow the caller: follow_caller() (called by the thread about
+  // to hand out work) keeps every worker on the CPUs that share the L3 cache
+  // of the CPU the caller runs on, re-pinning them only when that changed.
+  // The caller is left where the scheduler put it.  Off until enabled.
+  void set_follow(bool on);
+  void follow_caller();
+
  private:
   struct Worker {
     std::condition_variable cv;
@@ -93,6 +100,8 @@ class WorkerPool {
   size_t waking_ = 0;          // woken, not yet running
   size_t spawning_ = 0;        // threads created but not yet parked
   bool stop_ = false;
+  bool follow_ = false;
+  std::vector<int> domain_;  // CPUs the workers are kept on (follow mode; empty: anywhere)
 };
 
 // Lanes for per-GPU work in one cycle: one GPU per lane, at most 8 (the

@@ -247,7 +247,8 @@ TEST(LabelCycle_RecordsPhases) {
   auto r = label_cycle(m, sriov::new_empty_sriov(), c, ts, false);
   std::vector<std::string> names;
   for (const auto& p : r.phases) names.push_back(p.first);
-  EXPECT_EQ(names, (std::vector<std::string>{"init", "enumerate", "label", "facts(overlapped)", "sriov(overlapped)"}));
+  EXPECT_EQ(names, (std::vector<std::string>{"init", "enumerate", "label", "sriov.join", "facts.start",
+                                             "facts(overlapped)", "sriov(overlapped)"}));
   EXPECT_TRUE(r.total_ns > 0);
   EXPECT_EQ(r.labels["amd.com/gfd.timestamp"], std::string("1"));
 }

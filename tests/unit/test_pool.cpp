@@ -173,3 +173,29 @@ TEST(Affinity_PinsToTheCurrentL3DomainWithinTheAllowedSet) {
   EXPECT_TRUE(sched_setaffinity(0, sizeof(before), &before) == 0);
   fs::remove_all(root);
 }
+
+TEST(Pool_WorkersFollowTheCallersL3Domain) {
+  // --cpu-affinity=follow: every worker is kept on the CPUs sharing the L3
+  // of the CPU the calling thread runs on; the caller itself is untouched.
+  int cpu = sched_getcpu();
+  std::vector<int> domain = affinity::l3_domain(cpu);
+  if (domain.empty()) return;  // no cache topology in sysfs here
+  cpu_set_t before;
+  EXPECT_TRUE(sched_getaffinity(0, sizeof(before), &before) == 0);
+  gfd::WorkerPool pool(2);
+  pool.set_follow(true);
+  pool.follow_caller();
+  std::vector<int> seen;
+  pool.submit([&] {
+        cpu_set_t s;
+        CPU_ZERO(&s);
+        sched_getaffinity(0, sizeof(s), &s);
+        for (int c = 0; c < CPU_SETSIZE; ++c)
+          if (CPU_ISSET(c, &s)) seen.push_back(c);
+      })
+      .wait();
+  EXPECT_TRUE(seen == affinity::l3_domain(sched_getcpu()) || seen == domain);
+  cpu_set_t after;
+  EXPECT_TRUE(sched_getaffinity(0, sizeof(after), &after) == 0);
+  EXPECT_TRUE(CPU_EQUAL(&before, &after));
+}

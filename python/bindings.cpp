@@ -27,6 +27,7 @@
 #include "util/duration.h"
 #include "util/error.h"
 #include "util/log.h"
+#include "util/pool.h"
 
 namespace py = pybind11;
 using namespace gfd;
@@ -102,14 +103,17 @@ py::dict device_to_dict(const resource::Device& d) {
 // exactly as `start` does, then any number of labeling cycles.
 class Session {
  public:
-  // A library leaves the host process's CPU placement alone: the daemon's
-  // opt-in --cpu-affinity is applied by gfd_main only, never here.
+  // A library leaves the host process's CPU placement alone: --cpu-affinity=l3
+  // is applied by gfd_main only, never here.  The default, follow, moves
+  // only the pool's own worker threads (to the L3 domain of the thread that
+  // runs a cycle), as in the daemon.
   Session(const std::vector<std::string>& args, const std::map<std::string, std::string>& env, bool use_env,
           bool amdsmi_library_only) {
     auto ctx = cli::Context::parse(cli::gfd_flags(), args, use_env ? &env : nullptr);
     config_ = cli::load_config(ctx);
     config::disable_resource_renaming(config_);
     config_.amdsmi_library_only = amdsmi_library_only;
+    WorkerPool::instance().set_follow(ctx.String("cpu-affinity") == "follow");
     manager_ = resource::new_manager(config_);
     sriov_ = sriov::new_sriov_lib(config_.sysfs_root());
     timestamp_ = lm::NewTimestampLabeler(config_);

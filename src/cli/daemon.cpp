@@ -334,8 +334,13 @@ int gfd_main(int argc, char** argv) {
     return 0;
   }
   g_timeline.main_ns = trace::now_ns();
-  // Opt-in (--cpu-affinity=l3), before any thread exists: workers inherit
-  // the mask (util/affinity.h).
+  // CPU placement (util/affinity.h, util/pool.h).  The default, follow,
+  // leaves the cycle thread to the scheduler and keeps only the pool's
+  // workers on the L3 cache domain it runs on, so a hand-off never crosses
+  // the fabric: back to back 0.027-0.050 -> 0.025-0.027 ms, after an idle
+  // second 0.24-0.32 -> 0.25-0.28 ms (profiles/affinity_r3.txt).  l3 pins
+  // the whole process to the domain it starts on (before any thread exists:
+  // workers inherit the mask); none changes nothing.
   std::string placement = ctx.String("cpu-affinity");
   if (placement == "l3") {
     if (std::string pinned = affinity::pin_to_current_l3(); !pinned.empty()) log::printf("CPU affinity: %s", pinned.c_str());

@@ -183,7 +183,7 @@ std::vector<FlagDef> gfd_flags() {
        "amd-smi session lifetime: persistent (initialise once, re-init on topology change) | per-cycle"},
       {"mock-file", {}, T::String, "", {"GFD_MOCK_FILE"}, "device fixture (YAML/JSON) for --backend=mock"},
       {"trace-timing", {}, T::Bool, "false", {"GFD_TRACE_TIMING"}, "log per-phase timing of every labeling cycle"},
-      {"cpu-affinity", {}, T::String, "none", {"GFD_CPU_AFFINITY"},
+      {"cpu-affinity", {}, T::String, "follow", {"GFD_CPU_AFFINITY"},
        "CPU placement of the daemon's threads: none (the scheduler decides) | follow (worker threads kept on the\n\t\t"
        "CPUs sharing the L3 cache of the CPU each cycle starts on) | l3 (every thread on the L3 domain of the CPU\n\t\t"
        "the daemon starts on)"},

@@ -570,11 +570,14 @@ def test_concurrent_reader_never_sees_a_partial_file(binary, tmp_path, mi355x_no
         p.communicate(timeout=30)
 
 
-def test_cpu_affinity_is_opt_in(binary, tmp_path):
-    """No CPU placement change unless asked (--cpu-affinity=l3); an unknown
-    value is an error."""
+def test_cpu_placement_modes(binary, tmp_path):
+    """--cpu-affinity: follow (default: only the pool's workers move, to the
+    labeling thread's L3 domain), none (nothing changed), l3 (the whole
+    process pinned at start); an unknown value is an error."""
     args = ["--oneshot", *_base(tmp_path, tmp_path / "gfd")]
-    assert "CPU affinity:" not in run_daemon(binary, *args, check=True).stderr
+    err = run_daemon(binary, *args, check=True).stderr
+    assert "workers follow the labeling thread's L3 cache domain" in err and "sharing cpu" not in err
+    assert "CPU affinity:" not in run_daemon(binary, "--cpu-affinity=none", *args, check=True).stderr
     run_daemon(binary, "--cpu-affinity=l3", *args, check=True)
     cp = run_daemon(binary, "--cpu-affinity=numa", *args)
     assert cp.returncode == 1 and "unknown --cpu-affinity 'numa'" in cp.stderr

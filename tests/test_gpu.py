@@ -428,10 +428,11 @@ def test_runtime_visibility_masks_do_not_hide_gpus(binary, tmp_path, var):
 
 
 def test_daemon_pins_itself_to_one_l3_domain_only_when_asked(binary, tmp_path):
-    """CPU placement is opt-in: by default the daemon leaves its threads to
-    the scheduler; with --cpu-affinity=l3 (GFD_CPU_AFFINITY=l3) it keeps them
-    on the CPUs sharing one L3 cache (util/affinity.h), within the allowed
-    set.  (Started with every CPU of the box allowed.)"""
+    """CPU placement: by default (follow) the process is not pinned - only
+    the pool's workers are kept on the labeling thread's L3 domain; with
+    --cpu-affinity=l3 (GFD_CPU_AFFINITY=l3) every thread stays on the CPUs
+    sharing one L3 cache (util/affinity.h), within the allowed set.
+    (Started with every CPU of the box allowed.)"""
     def run(env):
         def widen():
             os.sched_setaffinity(0, range(os.cpu_count()))  # the kernel keeps the cgroup's share
@@ -441,7 +442,9 @@ def test_daemon_pins_itself_to_one_l3_domain_only_when_asked(binary, tmp_path):
         return subprocess.run([binary, "--oneshot", "--backend=null", "--output-file="], capture_output=True,
                               text=True, timeout=60, env=e, preexec_fn=widen, check=True)
 
-    assert "CPU affinity:" not in run({}).stderr
+    default = run({}).stderr
+    assert "sharing cpu" not in default and "workers follow" in default
+    assert "CPU affinity:" not in run({"GFD_CPU_AFFINITY": "none"}).stderr
     on = run({"GFD_CPU_AFFINITY": "l3"})
     lines = [ln for ln in on.stderr.splitlines() if "CPU affinity:" in ln]
     assert len(lines) == 1, on.stderr[-2000:]

@@ -128,3 +128,51 @@ def test_fake_cluster_enforces_nfd_wiring(tmp_path, node):
         assert "no node matches its affinity" in cp.stderr
     finally:
         stop_all(env2)
+
+
+def helm_install(env, tmp_path, values=None):
+    """`helm install` of the chart's rendering (tests/helm_lite.py) into the
+    fake cluster: every rendered document applied with the fake kubectl."""
+    import helm_lite
+    import yaml
+
+    docs = helm_lite.documents(helm_lite.render_chart(REPO / "deployments/helm/gpu-feature-discovery-amd", values))
+    # NFD first, as the e2e script applies it (the labeler's affinity needs
+    # the node's PCI labels).
+    docs.sort(key=lambda d: 0 if "nfd" in d["metadata"]["name"] else 1)
+    manifest = tmp_path / "rendered.yaml"
+    manifest.write_text(yaml.safe_dump_all(docs))
+    return subprocess.run([str(FAKES / "kubectl"), "apply", "-f", str(manifest)], capture_output=True, text=True,
+                          env=env, timeout=60)
+
+
+def wait_for_node_labels(env, timeout=30.0) -> dict:
+    import json
+    import time
+
+    end = time.monotonic() + timeout
+    labels = {}
+    while time.monotonic() < end:
+        out = subprocess.run([str(FAKES / "kubectl"), "get", "nodes", "-o", "json"], capture_output=True, text=True,
+                             env=env, check=True).stdout
+        labels = json.loads(out)["items"][0]["metadata"]["labels"]
+        if "amd.com/gfd.timestamp" in labels:
+            break
+        time.sleep(0.2)
+    return labels
+
+
+def test_helm_chart_installs_into_the_fake_cluster(tmp_path, node):
+    """The chart's defaults, rendered and applied: its NFD subchart's worker
+    reaches the master Service it names, the node gets its PCI vendor label,
+    the labeler DaemonSet schedules on it, and NFD publishes the amd.com
+    labels the labeler writes."""
+    env = e2e_env(tmp_path, node, node / "opt")
+    try:
+        cp = helm_install(env, tmp_path)
+        assert cp.returncode == 0, cp.stderr
+        labels = wait_for_node_labels(env)
+    finally:
+        stop_all(env)
+    assert labels.get("feature.node.kubernetes.io/pci-1002.present") == "true", labels
+    assert labels.get("amd.com/gpu.count") == "2" and labels.get("amd.com/gpu.arch") == "gfx950", labels

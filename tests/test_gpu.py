@@ -510,3 +510,21 @@ def test_e2e_script_on_the_real_node(tmp_path):
         stop_all(env)
     assert cp.returncode == 0, cp.stdout + cp.stderr
     assert "e2e test passed" in cp.stdout and '"amd.com/gpu.family": "cdna4"' in cp.stdout
+
+
+def test_helm_chart_installs_on_the_real_node(tmp_path):
+    """The Helm chart's defaults rendered (tests/helm_lite.py) and applied to
+    the fake one-node cluster backed by the real MI355X: NFD's PCI source
+    must see the GPU for the DaemonSet to schedule, and the published
+    amd.com labels must describe it."""
+    from test_e2e_scripts import e2e_env, helm_install, stop_all, wait_for_node_labels
+
+    env = e2e_env(tmp_path)
+    try:
+        cp = helm_install(env, tmp_path)
+        assert cp.returncode == 0, cp.stderr
+        labels = wait_for_node_labels(env, timeout=90)
+    finally:
+        stop_all(env)
+    assert labels.get("feature.node.kubernetes.io/pci-1002.present") == "true", labels
+    assert labels.get("amd.com/gpu.arch") == "gfx950" and labels.get("amd.com/gpu.family") == "cdna4", labels

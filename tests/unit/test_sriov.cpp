@@ -43,6 +43,27 @@ TEST(Pci_CapabilityWalkFindsExpressCapability) {
   }
 }
 
+TEST(Pci_ReferenceConfigDumpsVendorCapability) {
+  // internal/vgpu/pciutil_test.go:26-42 on the reference's own two
+  // configuration-space dumps (tests/fixtures/pci/README.md): the generic
+  // capability walk finds the vendor-specific capability with the lengths
+  // the reference expects, and the vGPU one carries the 'VF' signature.
+  struct Case {
+    const char* file;
+    size_t length;
+  };
+  for (const Case& c : {Case{"nvidia-passthrough.cfg", 20}, Case{"nvidia-vgpu.cfg", 27}}) {
+    PCIDevice d;
+    d.config = fs::read_file(std::string(GFD_SOURCE_DIR) + "/tests/fixtures/pci/" + c.file).data;
+    EXPECT_EQ(d.config.size(), static_cast<size_t>(256));
+    EXPECT_EQ(GetWord(d.config, 0), static_cast<uint16_t>(0x10de));
+    auto cap = d.GetVendorSpecificCapability();
+    EXPECT_TRUE(cap.has_value());
+    EXPECT_EQ(cap->size(), c.length);
+    EXPECT_EQ(cap->substr(3, 2) == "VF", std::string(c.file) == "nvidia-vgpu.cfg");
+  }
+}
+
 TEST(Pci_CapabilityWalkRequiresFullConfig) {
   PCIDevice d = find("passthrough");
   d.config.resize(64);  // what an unprivileged reader sees

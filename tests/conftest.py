@@ -43,6 +43,16 @@ def binary() -> str:
     return str(gfd.binary_path())
 
 
+@pytest.fixture(scope="session")
+def image():
+    """The labeler image's root file system: deployments/container/Dockerfile's
+    runtime stage assembled offline (tests/e2e/fakes/_image.py)."""
+    sys.path.insert(0, str(TESTS / "e2e" / "fakes"))
+    import _image
+
+    return _image.build()
+
+
 @pytest.fixture()
 def machine_file(tmp_path) -> str:
     """Fake DMI product name (main_test.go setupMachineFile)."""

@@ -11,7 +11,10 @@ scripts - run against these two stand-ins, put first on PATH:
   /sys and writes its feature file exactly where the container would;
 * /sys is the host's own unless FAKE_SYSFS_ROOT names a synthetic tree (CPU
   runs); the host's /opt is FAKE_HOST_OPT or /opt;
-* "the image" is the daemon binary built in-tree (FAKE_IMAGE_BINARY).
+* "the image" is the Dockerfile's runtime stage assembled offline
+  (`_image.py`): the daemon starts from the image's own files, through the
+  image's loader, with only the image's libraries to load; the loader's
+  library trace is kept in <state>/<name>/ld.<pid>.
 """
 
 from __future__ import annotations
@@ -22,6 +25,8 @@ import signal
 import subprocess
 import time
 from pathlib import Path
+
+import _image
 
 REPO = Path(__file__).resolve().parents[3]
 STATE = Path(os.environ.get("FAKE_RUNTIME_STATE", "/tmp/gfd-fake-runtime"))
@@ -82,10 +87,9 @@ def start(name: str, mounts: list[tuple[str, str]], env: dict[str, str], args: l
     if sys_root:
         cenv["GFD_SYSFS_ROOT"] = sys_root
         cenv.setdefault("GFD_MACHINE_TYPE_FILE", sys_root + "/sys/class/dmi/id/product_name")
-    penv.update(cenv)
-    binary = os.environ.get("FAKE_IMAGE_BINARY", str(REPO / "build" / "gpu-feature-discovery"))
+    argv, penv = _image.command(_image.build(), args, cenv, base=penv, trace=STATE / name / "ld")
     log = open(STATE / name / "log", "w")
-    p = subprocess.Popen([binary, *args], env=penv, stdout=log, stderr=subprocess.STDOUT, start_new_session=True)
+    p = subprocess.Popen(argv, env=penv, stdout=log, stderr=subprocess.STDOUT, start_new_session=True)
     (STATE / name / "pid").write_text(str(p.pid))
     return p.pid
 

@@ -6,8 +6,10 @@ is no container runtime, helm or kubectl here or on the GPU box, so the
 stand-in takes the labeler container of a manifest - the static DaemonSet or
 Job template, or the Helm chart's DaemonSet rendered with its default values
 (tests/helm_lite.py) - and
-runs the daemon binary with that container's argv and environment, its
-hostPath mounts reproduced under a scratch "container root":
+runs the labeler image (the Dockerfile's runtime stage assembled offline,
+tests/e2e/fakes/_image.py: the daemon started from the image's own files and
+libraries) with that container's argv and environment, its hostPath mounts
+reproduced under a scratch "container root":
 
 * features.d (hostPath /etc/kubernetes/node-feature-discovery/features.d):
   an empty directory at the same container path;
@@ -29,9 +31,13 @@ import re
 import shutil
 import signal
 import subprocess
+import sys
 import time
 from dataclasses import dataclass, field
 from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent / "e2e" / "fakes"))
+import _image  # noqa: E402
 
 FEATURES_D = "/etc/kubernetes/node-feature-discovery/features.d"
 DEFAULT_OUTPUT = FEATURES_D + "/gfd"
@@ -94,8 +100,10 @@ def materialise(pod: Pod, croot: Path, host_opt: Path = Path("/opt")) -> None:
         raise AssertionError(f"unknown hostPath {hpath} mounted at {mpath}")
 
 
-def plan(pod: Pod, binary: str, croot: Path, sysfs_root: str | None = None) -> tuple[list[str], dict[str, str], Path]:
-    """argv, environment and the output file (local path) of the pod's run."""
+def plan(pod: Pod, image: Path, croot: Path, sysfs_root: str | None = None,
+         trace: Path | None = None) -> tuple[list[str], dict[str, str], Path]:
+    """argv, environment and the output file (local path) of the pod's run
+    from the image rooted at `image` (`_image.build()`)."""
     env = {k: v for k, v in os.environ.items()
            if not k.startswith(("GFD_", "MIG_STRATEGY", "FAIL_ON_INIT", "CONFIG_FILE"))}
     penv = dict(pod.env)
@@ -119,19 +127,26 @@ def plan(pod: Pod, binary: str, croot: Path, sysfs_root: str | None = None) -> t
     if sysfs_root:
         penv["GFD_SYSFS_ROOT"] = sysfs_root
         penv.setdefault("GFD_MACHINE_TYPE_FILE", sysfs_root + "/sys/class/dmi/id/product_name")
-    env.update(penv)
-    return [binary, *args], env, croot / output.lstrip("/")
+    argv, env = _image.command(image, args, penv, base=env, trace=trace)
+    return argv, env, croot / output.lstrip("/")
 
 
-def run(pod: Pod, binary: str, croot: Path, sysfs_root: str | None = None, timeout: float = 120) -> dict:
+def run(pod: Pod, image: Path, croot: Path, sysfs_root: str | None = None, timeout: float = 120) -> dict:
     """Run the pod's labeler: a Job to completion; a DaemonSet until its first
     feature file, then SIGTERM (as a pod deletion does).  Returns the feature
-    file, stderr, exit code and whether the file was removed at exit."""
-    argv, env, out = plan(pod, binary, croot, sysfs_root)
+    file, stderr, exit code, whether the file was removed at exit, and the
+    shared objects the process loaded: all of them, and those that came from
+    the host's library directories instead of the image."""
+    trace = croot.parent / (croot.name + ".ld")
+    argv, env, out = plan(pod, image, croot, sysfs_root, trace)
+
+    def libraries() -> dict:
+        return {"loaded": _image.loaded_objects(trace), "foreign": _image.foreign_libraries(image, trace)}
+
     if pod.kind == "Job":
         cp = subprocess.run(argv, capture_output=True, text=True, timeout=timeout, env=env)
         return {"text": out.read_text() if out.exists() else "", "stderr": cp.stderr, "rc": cp.returncode,
-                "removed_at_exit": not out.exists()}
+                "removed_at_exit": not out.exists(), **libraries()}
     p = subprocess.Popen(argv, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True, env=env)
     text = ""
     try:
@@ -144,4 +159,4 @@ def run(pod: Pod, binary: str, croot: Path, sysfs_root: str | None = None, timeo
     finally:
         p.send_signal(signal.SIGTERM)
         _, err = p.communicate(timeout=30)
-    return {"text": text, "stderr": err, "rc": p.returncode, "removed_at_exit": not out.exists()}
+    return {"text": text, "stderr": err, "rc": p.returncode, "removed_at_exit": not out.exists(), **libraries()}

@@ -6,6 +6,7 @@ Helm templates may only reference values that exist."""
 
 from __future__ import annotations
 
+import os
 import re
 from pathlib import Path
 
@@ -122,6 +123,59 @@ def test_dockerfile(native):
     assert "gfd_unit_tests" in text  # the build stage runs the unit tests
     # The image must not carry a ROCm version of its own (node-true labels).
     assert not re.search(r"^COPY .*\.info/version", text, re.M)
+
+
+def test_image_holds_what_the_dockerfile_copies(image):
+    """The runtime stage assembled from the Dockerfile (tests/e2e/fakes/_image.py):
+    the daemon at its ENTRYPOINT, amd-smi under ROCM_PATH, libdrm_amdgpu and
+    its marketing-name table, a base C/C++ runtime - and no ROCm version
+    file, so rocm.runtime.* can only come from the host mount."""
+    assert (image / "usr/bin/gpu-feature-discovery").is_file()
+    assert list((image / "opt/rocm/lib").glob("libamd_smi.so.*"))
+    assert (image / "usr/share/libdrm/amdgpu.ids").is_file()
+    for lib in ("libdrm_amdgpu.so.1", "libdrm.so.2", "libc.so.6", "libstdc++.so.6", "libgcc_s.so.1"):
+        assert (image / "usr/lib/x86_64-linux-gnu" / lib).exists(), lib
+    assert not (image / "opt/rocm/.info/version").exists()
+    assert (image / ".image.entrypoint").read_text().split() == ["/usr/bin/gpu-feature-discovery"]
+
+
+def test_image_lacking_a_library_is_caught(image, tmp_path):
+    """What the image check relies on: with libstdc++ removed from (a copy
+    of) the image, loading amd-smi has to reach past the image - the loader's
+    last resort is the host's system directories, there being no mount
+    namespace - and the loader trace names that library as foreign."""
+    import shutil
+    import subprocess
+    import sys
+
+    sys.path.insert(0, str(REPO / "tests" / "e2e" / "fakes"))
+    import _image
+
+    broken = tmp_path / "image"
+    shutil.copytree(image, broken, symlinks=True)
+    for f in (broken / "usr/lib/x86_64-linux-gnu").glob("libstdc++.so.6*"):
+        f.unlink()
+    trace = tmp_path / "ld"
+    argv, env = _image.command(broken, ["--oneshot", "--backend=amdsmi", "--output-file=-"], {},
+                               base={"PATH": "/usr/bin:/bin"}, trace=trace)
+    subprocess.run(argv, env=env, capture_output=True, text=True, timeout=60)
+    assert [os.path.basename(o) for o in _image.foreign_libraries(broken, trace)] == ["libstdc++.so.6"]
+    assert not _image.foreign_libraries(image, _trace_of_intact_run(image, tmp_path))
+
+
+def _trace_of_intact_run(image, tmp_path):
+    import subprocess
+    import sys
+
+    sys.path.insert(0, str(REPO / "tests" / "e2e" / "fakes"))
+    import _image
+
+    trace = tmp_path / "ld-intact"
+    argv, env = _image.command(image, ["--oneshot", "--backend=amdsmi", "--output-file=-"], {},
+                               base={"PATH": "/usr/bin:/bin"}, trace=trace)
+    subprocess.run(argv, env=env, capture_output=True, text=True, timeout=60)
+    assert _image.matches(_image.loaded_objects(trace), "libamd_smi.so*")
+    return trace
 
 
 def test_helm_mounts_host_opt(native):
@@ -277,10 +331,13 @@ def check_manifest_run(r, pod, strategy, rocm: str):
     major, minor = rocm.split(".")[:2]
     assert (labels["amd.com/rocm.runtime.major"], labels["amd.com/rocm.runtime.minor"]) == (major, minor)
     assert r["removed_at_exit"] == (pod.kind == "DaemonSet")
+    # Started from the image's own files: every library it loaded is the
+    # image's (none came from the host's library directories).
+    assert r["loaded"] and not r["foreign"], r["foreign"]
 
 
 @pytest.mark.parametrize("name,source,strategy", MANIFEST_PODS, ids=[m[0] for m in MANIFEST_PODS])
-def test_manifest_pod_runs_on_a_synthetic_node(native, binary, tmp_path, name, source, strategy):
+def test_manifest_pod_runs_on_a_synthetic_node(native, image, tmp_path, name, source, strategy):
     """CPU rehearsal of tests/test_gpu.py::test_manifest_pod_labels_the_real_node:
     the same argv/env/mounts over a synthetic MI355X tree (the only added
     setting is --sysfs-root, since this container's /sys has no GPU)."""
@@ -291,11 +348,11 @@ def test_manifest_pod_runs_on_a_synthetic_node(native, binary, tmp_path, name, s
     root = synth.make_mi355x_node(tmp_path / "node", n_gpus=1, rocm_version="6.4.2", seed=40)
     croot = tmp_path / "container"
     manifest_pods.materialise(pod, croot, host_opt=root / "opt")
-    r = manifest_pods.run(pod, binary, croot, sysfs_root=str(root), timeout=60)
+    r = manifest_pods.run(pod, image, croot, sysfs_root=str(root), timeout=60)
     check_manifest_run(r, pod, strategy, "6.4.2")
 
 
-def test_manifest_pod_catches_a_broken_mount(native, binary, tmp_path):
+def test_manifest_pod_catches_a_broken_mount(native, image, tmp_path):
     """The point of running the manifests: the host /opt mounted somewhere
     --host-root does not look fails the run instead of dropping labels."""
     import manifest_pods
@@ -306,5 +363,5 @@ def test_manifest_pod_catches_a_broken_mount(native, binary, tmp_path):
     root = synth.make_mi355x_node(tmp_path / "node", n_gpus=1, seed=41)
     croot = tmp_path / "container"
     manifest_pods.materialise(pod, croot, host_opt=root / "opt")
-    r = manifest_pods.run(pod, binary, croot, sysfs_root=str(root), timeout=30)
+    r = manifest_pods.run(pod, image, croot, sysfs_root=str(root), timeout=30)
     assert r["rc"] == 1 and "has no opt/ directory" in r["stderr"]

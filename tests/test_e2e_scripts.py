@@ -15,6 +15,7 @@ import os
 import re
 import subprocess
 import sys
+from pathlib import Path
 
 import pytest
 
@@ -50,6 +51,27 @@ def stop_all(env):
         sys.path.remove(str(FAKES))
 
 
+def image_libraries(env) -> tuple[list[str], list[str]]:
+    """Shared objects the fakes' labeler containers loaded (from the loader
+    traces the fake runtime keeps), and those not from the image."""
+    sys.path.insert(0, str(FAKES))
+    try:
+        import _image
+    finally:
+        sys.path.remove(str(FAKES))
+    root = _image.build()
+    loaded, foreign = [], []
+    for c in Path(env["FAKE_RUNTIME_STATE"]).glob("*/"):
+        loaded += _image.loaded_objects(c / "ld")
+        foreign += _image.foreign_libraries(root, c / "ld")
+    return loaded, foreign
+
+
+def assert_ran_from_the_image(env):
+    loaded, foreign = image_libraries(env)
+    assert loaded and not foreign, (loaded, foreign)
+
+
 def run_integration(env, strategy="none", timeout=60):
     return subprocess.run([sys.executable, str(REPO / "tests/e2e/integration_docker.py"), "gfd-amd:test",
                            f"--strategy={strategy}", "--timeout=30"], capture_output=True, text=True, env=env,
@@ -76,6 +98,7 @@ def test_integration_script_against_fake_docker(tmp_path, node, strategy):
     assert cp.returncode == 0, cp.stdout + cp.stderr
     assert "integration test passed" in cp.stdout
     assert "amd.com/rocm.runtime.major=7" in cp.stdout
+    assert_ran_from_the_image(env)
 
 
 def test_e2e_script_against_fake_cluster(tmp_path, node):
@@ -87,6 +110,7 @@ def test_e2e_script_against_fake_cluster(tmp_path, node):
     assert cp.returncode == 0, cp.stdout + cp.stderr
     assert "e2e test passed" in cp.stdout
     assert '"amd.com/gpu.count": "2"' in cp.stdout
+    assert_ran_from_the_image(env)
 
 
 def test_fake_cluster_enforces_nfd_wiring(tmp_path, node):

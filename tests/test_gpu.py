@@ -459,7 +459,7 @@ def _box_rocm() -> str:
 
 
 @pytest.mark.parametrize("name,source,strategy", MANIFEST_PODS, ids=[m[0] for m in MANIFEST_PODS])
-def test_manifest_pod_labels_the_real_node(native, binary, tmp_path, name, source, strategy):
+def test_manifest_pod_labels_the_real_node(native, image, tmp_path, name, source, strategy):
     """The stand-in for the reference's container integration test
     (tests/integration-tests.py:36-78): each manifest's labeler container -
     static DaemonSets, the Job template, the Helm chart's defaults - run with
@@ -473,10 +473,33 @@ def test_manifest_pod_labels_the_real_node(native, binary, tmp_path, name, sourc
     pod = manifest_pod(native, source)
     croot = tmp_path / "container"
     manifest_pods.materialise(pod, croot)
-    r = manifest_pods.run(pod, binary, croot, timeout=120)
+    r = manifest_pods.run(pod, image, croot, timeout=120)
     check_manifest_run(r, pod, strategy, _box_rocm())
     if pod.env.get("GFD_BACKEND", "auto") == "auto" and pod.kind == "DaemonSet":
         assert "failed to initialize" not in r["stderr"], r["stderr"][-3000:]
+
+
+def test_image_labels_the_real_node_with_its_own_libraries(binary, image, tmp_path):
+    """The image (the Dockerfile's runtime stage, tests/e2e/fakes/_image.py)
+    on the MI355X with the amd-smi backend: amd-smi and the libdrm_amdgpu it
+    loads for the marketing names come from the image (its COPY --from=build
+    and apt-get lines), nothing from the host's library directories, and the
+    labels equal the in-tree build's."""
+    sys.path.insert(0, str(TESTS / "e2e" / "fakes"))
+    import _image
+
+    args = ["--oneshot", "--backend=amdsmi", "--no-timestamp", "--host-root=/"]
+    trace = tmp_path / "ld"
+    argv, env = _image.command(image, [*args, f"--output-file={tmp_path / 'image'}"], {}, base=dict(os.environ),
+                               trace=trace)
+    cp = subprocess.run(argv, env=env, capture_output=True, text=True, timeout=60)
+    assert cp.returncode == 0, cp.stderr[-3000:]
+    run_daemon(binary, *args, f"--output-file={tmp_path / 'host'}", check=True)
+    assert (tmp_path / "image").read_text() == (tmp_path / "host").read_text()
+    loaded = _image.loaded_objects(trace)
+    for lib in ("libamd_smi.so*", "libdrm_amdgpu.so*"):
+        assert [o for o in _image.matches(loaded, lib) if o.startswith(str(image))], (lib, loaded)
+    assert not _image.foreign_libraries(image, trace)
 
 
 # ---- tests/e2e scripts (the reference's integration / e2e tests) on the node -
@@ -485,7 +508,7 @@ def test_integration_script_on_the_real_node(tmp_path):
     """tests/e2e/integration_docker.py as it is, its `docker run` served by
     the fake runtime (tests/e2e/fakes): the labeler with the host's real
     /sys and /opt, labels checked against the regex golden."""
-    from test_e2e_scripts import e2e_env, run_integration, stop_all
+    from test_e2e_scripts import assert_ran_from_the_image, e2e_env, run_integration, stop_all
 
     env = e2e_env(tmp_path)
     try:
@@ -494,6 +517,7 @@ def test_integration_script_on_the_real_node(tmp_path):
         stop_all(env)
     assert cp.returncode == 0, cp.stdout + cp.stderr
     assert "integration test passed" in cp.stdout and "amd.com/gpu.arch=gfx950" in cp.stdout
+    assert_ran_from_the_image(env)
 
 
 def test_e2e_script_on_the_real_node(tmp_path):
@@ -501,7 +525,7 @@ def test_e2e_script_on_the_real_node(tmp_path):
     on the real MI355X: NFD's PCI source must match the node (class 0x12
     whitelisted) for the DaemonSet to schedule, and its local source must
     publish the amd.com labels."""
-    from test_e2e_scripts import e2e_env, run_e2e, stop_all
+    from test_e2e_scripts import assert_ran_from_the_image, e2e_env, run_e2e, stop_all
 
     env = e2e_env(tmp_path)
     try:
@@ -510,6 +534,7 @@ def test_e2e_script_on_the_real_node(tmp_path):
         stop_all(env)
     assert cp.returncode == 0, cp.stdout + cp.stderr
     assert "e2e test passed" in cp.stdout and '"amd.com/gpu.family": "cdna4"' in cp.stdout
+    assert_ran_from_the_image(env)
 
 
 def test_helm_chart_installs_on_the_real_node(tmp_path):

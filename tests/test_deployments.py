@@ -156,7 +156,7 @@ def test_image_lacking_a_library_is_caught(image, tmp_path):
     for f in (broken / "usr/lib/x86_64-linux-gnu").glob("libstdc++.so.6*"):
         f.unlink()
     trace = tmp_path / "ld"
-    argv, env = _image.command(broken, ["--oneshot", "--backend=amdsmi", "--output-file=-"], {},
+    argv, env = _image.command(broken, ["--oneshot", "--backend=amdsmi", f"--output-file={tmp_path / 'out'}"], {},
                                base={"PATH": "/usr/bin:/bin"}, trace=trace)
     subprocess.run(argv, env=env, capture_output=True, text=True, timeout=60)
     assert [os.path.basename(o) for o in _image.foreign_libraries(broken, trace)] == ["libstdc++.so.6"]
@@ -171,7 +171,7 @@ def _trace_of_intact_run(image, tmp_path):
     import _image
 
     trace = tmp_path / "ld-intact"
-    argv, env = _image.command(image, ["--oneshot", "--backend=amdsmi", "--output-file=-"], {},
+    argv, env = _image.command(image, ["--oneshot", "--backend=amdsmi", f"--output-file={tmp_path / 'out-intact'}"], {},
                                base={"PATH": "/usr/bin:/bin"}, trace=trace)
     subprocess.run(argv, env=env, capture_output=True, text=True, timeout=60)
     assert _image.matches(_image.loaded_objects(trace), "libamd_smi.so*")

@@ -165,38 +165,102 @@ def _copy(src_pattern: str, dst: str, src_root: Path, root: Path) -> None:
         _place(s, root, d)
 
 
-def _map_build_path(path: str, workdir: str | None) -> tuple[str, Path]:
-    """Where a build-stage path is: under its WORKDIR, the repository (the
-    stage's `COPY . .`); anywhere else, this machine."""
+def _map_build_path(path: str, workdir: str | None, src: Path) -> tuple[str, Path]:
+    """Where a build-stage path is: under its WORKDIR, `src` (the stage's
+    `COPY . .` and what its RUN built there); anywhere else, this machine."""
     if workdir and (path == workdir or path.startswith(workdir.rstrip("/") + "/")):
-        return path[len(workdir.rstrip("/")):], REPO
+        return path[len(workdir.rstrip("/")):], src
     return path, Path("/")
 
 
-def _key() -> str:
+def _ignore_patterns(context: Path) -> list[re.Pattern]:
+    """.dockerignore's patterns (no `!` exceptions: this one has none)."""
+    f = context / ".dockerignore"
+    out = []
+    for line in (f.read_text().splitlines() if f.exists() else []):
+        line = line.strip()
+        if not line or line.startswith("#"):
+            continue
+        if line.startswith("!"):
+            raise ValueError(".dockerignore exceptions are not emulated")
+        rx = re.escape(line.strip("/")).replace(r"\*\*/", "(.*/)?").replace(r"\*", "[^/]*").replace(r"\?", "[^/]")
+        out.append(re.compile(rx + "$"))
+    return out
+
+
+def context_files(context: Path = REPO) -> list[str]:
+    """The build context `docker build` would send: every file under
+    `context` (relative paths) that .dockerignore does not exclude; an
+    excluded directory excludes everything under it."""
+    pats = _ignore_patterns(context)
+    out = []
+    for d, dirs, files in os.walk(context):
+        rel = os.path.relpath(d, context)
+        rel = "" if rel == "." else rel + "/"
+        dirs[:] = [x for x in dirs if not any(p.match(rel + x) for p in pats)]
+        out += [rel + f for f in files if not any(p.match(rel + f) for p in pats)]
+    return sorted(out)
+
+
+def run_build_stage(work: Path, log=print) -> Path:
+    """Run the Dockerfile's build stage: the build context copied to
+    work/<WORKDIR> (`COPY . .`), then each RUN there, package installs
+    skipped (no network; this machine is the stage's base image).  Raises
+    on the first failing step; returns the WORKDIR."""
+    stages = _stages(DOCKERFILE.read_text())
+    stage = next(s for s in stages if s["name"] == "build")
+    src = work
+    for ins, arg in stage["steps"]:
+        if ins == "WORKDIR":
+            src = work / arg.lstrip("/")
+            src.mkdir(parents=True, exist_ok=True)
+        elif ins == "COPY":
+            if arg.split() != [".", "."]:
+                raise ValueError(f"COPY {arg} in the build stage is not emulated")
+            for rel in context_files():
+                (src / rel).parent.mkdir(parents=True, exist_ok=True)
+                shutil.copy2(REPO / rel, src / rel, follow_symlinks=False)
+        elif ins == "RUN":
+            steps = [c.strip() for c in arg.split("&&")]
+            steps = [c for c in steps if not c.startswith(("apt-get", "rm -rf /var/lib/apt"))]
+            if not steps:
+                continue
+            cmd = " && ".join(steps)
+            log(f"RUN {cmd}")
+            subprocess.run(["bash", "-e", "-c", cmd], cwd=src, check=True)
+        elif ins in ("ARG", "ENV", "LABEL"):
+            pass
+        else:
+            raise ValueError(f"{ins} in the build stage is not emulated")
+    return src
+
+
+def _key(src: Path) -> str:
     h = hashlib.sha256(DOCKERFILE.read_bytes())
-    for f in (REPO / "build" / "gpu-feature-discovery", Path("/opt/rocm/lib")):
+    for f in (src / "build" / "gpu-feature-discovery", Path("/opt/rocm/lib")):
         st = f.stat()
         h.update(f"{f}:{st.st_mtime_ns}:{st.st_size}".encode())
     return h.hexdigest()[:16]
 
 
-def build(dest: Path = DEFAULT_DEST) -> Path:
+def build(dest: Path = DEFAULT_DEST, build_src: Path = REPO) -> Path:
     """Assemble the runtime stage under `dest` (reused while the Dockerfile,
     the daemon binary and the ROCm libraries are unchanged; concurrent
-    builders wait for each other); returns the image's root."""
+    builders wait for each other); returns the image's root.  The build
+    stage's WORKDIR is `build_src`: by default the repository with its
+    in-tree build, or what `run_build_stage` produced."""
     dest.mkdir(parents=True, exist_ok=True)
-    root = dest / f"rootfs-{_key()}"
+    root = dest / f"rootfs-{_key(build_src)}"
     with open(dest / ".lock", "w") as lock:
         fcntl.flock(lock, fcntl.LOCK_EX)
         if not (root / ".complete").exists():
             for old in dest.glob("rootfs-*"):
                 shutil.rmtree(old, ignore_errors=True)
-            _assemble(root)
+            _assemble(root, build_src)
     return root
 
 
-def _assemble(root: Path) -> None:
+def _assemble(root: Path, build_src: Path) -> None:
     stages = _stages(DOCKERFILE.read_text())
     build_stage = next(s for s in stages if s["name"] == "build")
     workdir = next((a for i, a in build_stage["steps"] if i == "WORKDIR"), None)
@@ -226,7 +290,7 @@ def _assemble(root: Path) -> None:
             *srcs, dst = words
             for s in srcs:
                 if frm == "build":
-                    path, src_root = _map_build_path(s, workdir)
+                    path, src_root = _map_build_path(s, workdir, build_src)
                     _copy(path, dst, src_root, root)
                 elif frm is None:
                     _copy(s, dst, REPO, root)

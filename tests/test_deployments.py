@@ -125,6 +125,21 @@ def test_dockerfile(native):
     assert not re.search(r"^COPY .*\.info/version", text, re.M)
 
 
+def test_docker_context_leaves_build_trees_out():
+    """`make image` sends the repository root as the build context; a local
+    build tree in it would reach the build stage's /src, where CMake refuses
+    a cache made for another source path (`cmake -B build` fails)."""
+    import sys
+
+    sys.path.insert(0, str(REPO / "tests" / "e2e" / "fakes"))
+    import _image
+
+    files = _image.context_files()
+    assert "CMakeLists.txt" in files and "deployments/container/Dockerfile" in files
+    assert not [f for f in files if f.split("/")[0].startswith(("build", ".git", "gpurun_out"))]
+    assert not [f for f in files if f.endswith((".so", ".o", ".a", ".pyc"))]
+
+
 def test_image_holds_what_the_dockerfile_copies(image):
     """The runtime stage assembled from the Dockerfile (tests/e2e/fakes/_image.py):
     the daemon at its ENTRYPOINT, amd-smi under ROCM_PATH, libdrm_amdgpu and

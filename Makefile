@@ -5,7 +5,7 @@ BUILD_DIR ?= build
 JOBS ?= $(shell nproc 2>/dev/null || echo 8)
 PYTHON ?= python3
 
-.PHONY: all build cmds test test-unit test-gpu coverage asan tsan fuzz bench fmt assert-fmt lint check-yamls image clean
+.PHONY: all build cmds test test-unit test-gpu coverage asan tsan fuzz bench fmt assert-fmt lint check-yamls image image-offline clean
 
 all: build
 
@@ -86,6 +86,12 @@ check-yamls:
 
 image:
 	$(MAKE) -C deployments/container image VERSION=$(VERSION) IMAGE_NAME=$(IMAGE_NAME)
+
+# The same Dockerfile built without docker (no image builder on the GPU pool):
+# its build stage run in a copy of the build context, the runtime stage
+# assembled from the result and its entrypoint run (tools/image_build.py).
+image-offline:
+	$(PYTHON) tools/image_build.py
 
 clean:
 	rm -rf $(BUILD_DIR) build-asan build-tsan build-cov gpu_feature_discovery_amd/_gfd*.so

@@ -5,7 +5,7 @@ BUILD_DIR ?= build
 JOBS ?= $(shell nproc 2>/dev/null || echo 8)
 PYTHON ?= python3
 
-.PHONY: all build cmds test test-unit test-gpu coverage asan tsan fuzz bench fmt assert-fmt lint check-yamls image image-offline clean
+.PHONY: all build cmds test test-unit test-gpu coverage asan tsan fuzz bench fmt assert-fmt lint check-yamls image image-offline shell clean
 
 all: build
 
@@ -92,6 +92,22 @@ image:
 # assembled from the result and its entrypoint run (tools/image_build.py).
 image-offline:
 	$(PYTHON) tools/image_build.py
+
+# Any target inside the development image (reference analogue: the
+# docker-% targets, Makefile:119-150): `make docker-test`, `make docker-asan`...
+DOCKER ?= docker
+BUILDIMAGE ?= $(IMAGE_NAME)-devel:$(VERSION)
+
+.build-image: docker/Dockerfile.devel
+	$(DOCKER) build --build-arg ROCM_VERSION=$(basename $(ROCM_VERSION)) \
+	  --build-arg UBUNTU_VERSION=$(UBUNTU_VERSION) --tag $(BUILDIMAGE) -f docker/Dockerfile.devel docker
+
+docker-%: .build-image
+	$(DOCKER) run --rm -v $(CURDIR):/work -w /work --user $$(id -u):$$(id -g) -e HOME=/tmp \
+	  $(BUILDIMAGE) make $*
+
+shell: .build-image
+	$(DOCKER) run --rm -ti -v $(CURDIR):/work -w /work --user $$(id -u):$$(id -g) -e HOME=/tmp $(BUILDIMAGE)
 
 clean:
 	rm -rf $(BUILD_DIR) build-asan build-tsan build-cov gpu_feature_discovery_amd/_gfd*.so

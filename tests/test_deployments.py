@@ -125,6 +125,26 @@ def test_dockerfile(native):
     assert not re.search(r"^COPY .*\.info/version", text, re.M)
 
 
+def test_devel_image_has_what_the_make_targets_run():
+    """docker/Dockerfile.devel (the `make docker-<target>` / `make shell`
+    image) starts from the image build stage's base and installs every tool
+    a Makefile target calls."""
+    import sys
+
+    sys.path.insert(0, str(REPO / "tests" / "e2e" / "fakes"))
+    import _image
+
+    (devel,) = _image._stages((REPO / "docker" / "Dockerfile.devel").read_text())
+    build_stage = _image._stages((DEPLOY / "container" / "Dockerfile").read_text())[0]
+    assert devel["base"] == build_stage["base"]
+    runs = " ".join(a for i, a in devel["steps"] if i == "RUN")
+    for tool in ("cmake", "ninja-build", "g++", "clang", "clang-format", "python3-pybind11", "pytest",
+                 "pytest-timeout", "pyyaml", "hypothesis", "pyflakes"):
+        assert re.search(r"(^|\s)" + re.escape(tool) + r"(\s|$)", runs), tool
+    make = (REPO / "Makefile").read_text()
+    assert "docker-%: .build-image" in make and "shell: .build-image" in make
+
+
 def test_docker_context_leaves_build_trees_out():
     """`make image` sends the repository root as the build context; a local
     build tree in it would reach the build stage's /src, where CMake refuses

@@ -52,7 +52,8 @@ fuzz:
 	cmake --build build-fuzz -j $(JOBS)
 	for t in config pci values flags sysfs amdsmi; do mkdir -p build-fuzz/corpus-$$t && \
 	  UBSAN_OPTIONS=halt_on_error=1 ./build-fuzz/fuzz_$$t -max_total_time=$(FUZZ_SECONDS) -timeout=10 \
-	    -rss_limit_mb=2048 build-fuzz/corpus-$$t tests/fuzz/corpus/$$t || exit 1; done
+	    -rss_limit_mb=2048 $$([ -f tests/fuzz/$$t.dict ] && echo -dict=tests/fuzz/$$t.dict) \
+	    build-fuzz/corpus-$$t tests/fuzz/corpus/$$t || exit 1; done
 
 coverage:
 	cmake -S . -B build-cov -G Ninja -DCMAKE_BUILD_TYPE=Debug -DGFD_BUILD_PYTHON=OFF \

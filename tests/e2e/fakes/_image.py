@@ -51,11 +51,11 @@ DEFAULT_DEST = Path(os.environ.get("TMPDIR", "/tmp")) / "gfd-image"
 LIB_DIRS = ("lib/x86_64-linux-gnu", "usr/lib/x86_64-linux-gnu", "lib", "usr/lib", "lib64")
 
 
-def _stages(text: str) -> list[dict]:
+def _stages(text: str, build_args: dict[str, str] | None = None) -> list[dict]:
     """The Dockerfile's stages: name, base and (instruction, argument) list,
-    ARGs substituted with their defaults."""
+    ARGs substituted (`build_args` over the declared defaults)."""
     text = re.sub(r"\\\n", " ", text)
-    args: dict[str, str] = {}
+    args: dict[str, str] = dict(build_args or {})
     stages: list[dict] = []
 
     def subst(s: str) -> str:
@@ -202,12 +202,12 @@ def context_files(context: Path = REPO) -> list[str]:
     return sorted(out)
 
 
-def run_build_stage(work: Path, log=print) -> Path:
+def run_build_stage(work: Path, log=print, build_args: dict[str, str] | None = None) -> Path:
     """Run the Dockerfile's build stage: the build context copied to
     work/<WORKDIR> (`COPY . .`), then each RUN there, package installs
     skipped (no network; this machine is the stage's base image).  Raises
     on the first failing step; returns the WORKDIR."""
-    stages = _stages(DOCKERFILE.read_text())
+    stages = _stages(DOCKERFILE.read_text(), build_args)
     stage = next(s for s in stages if s["name"] == "build")
     src = work
     for ins, arg in stage["steps"]:

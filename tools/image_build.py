@@ -35,7 +35,11 @@ def main() -> int:
     work = Path(a.work or tempfile.mkdtemp(prefix="gfd-docker-build-"))
     print(f"# build context: {len(_image.context_files())} files after .dockerignore", flush=True)
     t0 = time.monotonic()
-    src = _image.run_build_stage(work / "build-stage", log=lambda m: print(f"# {m}", flush=True))
+    # As the container Makefile passes it (versions.mk's GIT_COMMIT).
+    commit = subprocess.run(["git", "-C", str(REPO), "describe", "--match=", "--dirty", "--long", "--always"],
+                            capture_output=True, text=True).stdout.strip() or "unknown"
+    src = _image.run_build_stage(work / "build-stage", log=lambda m: print(f"# {m}", flush=True),
+                                 build_args={"GIT_COMMIT": commit})
     print(f"# build stage: ok in {time.monotonic() - t0:.0f} s", flush=True)
     root = _image.build(work / "image", build_src=src)
     size = subprocess.run(["du", "-sh", str(root)], capture_output=True, text=True).stdout.split()[0]
@@ -58,6 +62,7 @@ def main() -> int:
         ok &= cp.returncode == 0 and not foreign
         if name == "--version":
             print("   " + cp.stdout.strip().replace("\n", "\n   "))
+            ok &= f"commit: {commit}" in cp.stdout
     labels = (work / "labels").read_text().splitlines()
     print(f"oneshot labels ({len(labels)}): " + ", ".join(x for x in labels if "gpu.count" in x or "product" in x))
     if not a.work:

@@ -4,6 +4,7 @@ sampled every --every seconds for --seconds: a leak grows linearly with
 cycles, allocator warm-up plateaus.
 
     python tools/rss_series.py [--seconds 300] [--every 20] [--backend amdsmi]
+        [--backend sysfs --sysfs-root synthetic|PATH]
 """
 
 from __future__ import annotations
@@ -19,12 +20,17 @@ import time
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def rss_kib(pid: int) -> int:
+def mem_kib(pid: int) -> dict[str, int]:
+    """VmRSS and its split: RssAnon (heap, stacks: what a leak grows) and
+    RssFile (mapped code and data touched so far: grows as rarely taken paths
+    of the binary and its libraries run for the first time, then stops)."""
+    out = {}
     with open(f"/proc/{pid}/status") as f:
         for line in f:
-            if line.startswith("VmRSS:"):
-                return int(line.split()[1])
-    return 0
+            k = line.split(":")[0]
+            if k in ("VmRSS", "RssAnon", "RssFile"):
+                out[k] = int(line.split()[1])
+    return out
 
 
 def main() -> int:
@@ -32,9 +38,21 @@ def main() -> int:
     ap.add_argument("--seconds", type=float, default=300)
     ap.add_argument("--every", type=float, default=20)
     ap.add_argument("--backend", default="amdsmi")
+    ap.add_argument("--sysfs-root", default=None, help="a synthetic node (utils/synth.py) instead of the host")
     a = ap.parse_args()
-    out = os.path.join(tempfile.mkdtemp(prefix="gfd-rss-"), "gfd")
-    p = subprocess.Popen([os.path.join(REPO, "build", "gpu-feature-discovery"), f"--backend={a.backend}",
+    d = tempfile.mkdtemp(prefix="gfd-rss-")
+    out = os.path.join(d, "gfd")
+    extra = []
+    if a.sysfs_root == "synthetic":
+        import sys
+
+        sys.path.insert(0, REPO)
+        from gpu_feature_discovery_amd.utils import synth
+
+        a.sysfs_root = str(synth.make_mi355x_node(os.path.join(d, "node"), n_gpus=8, seed=3))
+    if a.sysfs_root:
+        extra = [f"--sysfs-root={a.sysfs_root}", f"--machine-type-file={a.sysfs_root}/sys/class/dmi/id/product_name"]
+    p = subprocess.Popen([os.path.join(REPO, "build", "gpu-feature-discovery"), f"--backend={a.backend}", *extra,
                           "--sleep-interval=1ms", "--trace-timing", f"--output-file={out}"],
                          stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
     cycles = [0]
@@ -49,8 +67,10 @@ def main() -> int:
     try:
         while time.monotonic() - t0 < a.seconds and p.poll() is None:
             time.sleep(a.every)
-            print(f"t={time.monotonic() - t0:6.0f}s cycles={cycles[0]:8d} rss={rss_kib(p.pid)} KiB "
-                  f"fds={len(os.listdir(f'/proc/{p.pid}/fd'))}", flush=True)
+            m = mem_kib(p.pid)
+            print(f"t={time.monotonic() - t0:6.0f}s cycles={cycles[0]:8d} rss={m.get('VmRSS')} KiB "
+                  f"(anon {m.get('RssAnon')}, file {m.get('RssFile')}) fds={len(os.listdir(f'/proc/{p.pid}/fd'))}",
+                  flush=True)
     finally:
         p.send_signal(signal.SIGTERM)
         p.wait(timeout=30)

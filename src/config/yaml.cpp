@@ -130,21 +130,23 @@ Node resolve_plain(const std::string& s) {
     // ^[-+]?(\.[0-9]+|[0-9]+(\.[0-9]*)?)([eE][-+]?[0-9]+)?$
     size_t i = 0;
     if (i < t.size() && (t[i] == '-' || t[i] == '+')) i++;
-    size_t digits = 0, frac = 0;
-    while (i < t.size() && isdigit(static_cast<unsigned char>(t[i]))) i++, digits++;
+    auto digit_run = [&] {  // digits at i, skipped; how many
+      size_t n = 0;
+      for (; i < t.size() && isdigit(static_cast<unsigned char>(t[i])); ++i) ++n;
+      return n;
+    };
+    size_t digits = digit_run(), frac = 0;
     bool dot = false;
     if (i < t.size() && t[i] == '.') {
       dot = true;
       i++;
-      while (i < t.size() && isdigit(static_cast<unsigned char>(t[i]))) i++, frac++;
+      frac = digit_run();
     }
     bool ok = digits > 0 || (dot && frac > 0);
     if (ok && i < t.size() && (t[i] == 'e' || t[i] == 'E')) {
       i++;
       if (i < t.size() && (t[i] == '-' || t[i] == '+')) i++;
-      size_t ed = 0;
-      while (i < t.size() && isdigit(static_cast<unsigned char>(t[i]))) i++, ed++;
-      ok = ed > 0;
+      ok = digit_run() > 0;
     }
     if (ok && i == t.size()) {
       auto f = str::parse_float(t);

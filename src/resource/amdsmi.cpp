@@ -687,6 +687,11 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
       }
     }
   }
+  if (!opts_.filter.all()) {
+    std::vector<std::string> bdfs;
+    for (const auto& procs : physical) bdfs.push_back(procs[0].gpu_bdf);
+    opts_.filter.check_selection(bdfs);
+  }
   const bool sysfs_values = opts_.sysfs_values;
 
   // One GPU's values and capabilities, always on one thread: amdgpu

@@ -348,6 +348,11 @@ std::vector<DevicePtr> SysfsManager::enumerate() {
   for (size_t i = 0; i < topo->gpus.size(); ++i)
     if (opts_.filter.matches(static_cast<int>(i), topo->gpus[i].bdf))
       visible.emplace_back(static_cast<int>(i), &topo->gpus[i]);
+  if (!opts_.filter.all()) {
+    std::vector<std::string> bdfs;
+    for (const auto& g : topo->gpus) bdfs.push_back(g.bdf);
+    opts_.filter.check_selection(bdfs);
+  }
   std::vector<DevicePtr> out(visible.size());
   trace::Span span("sysfs.gpus");
   // Unpartitioned GPUs: ~10 attribute preads each, two GPUs per lane (see

@@ -5,6 +5,7 @@
 #include <unistd.h>
 
 #include <chrono>
+#include <cstdio>
 #include <condition_variable>
 #include <mutex>
 
@@ -19,6 +20,7 @@
 #include "resource/versions.h"
 #include "test.h"
 #include "util/fs.h"
+#include "util/log.h"
 #include "util/strings.h"
 
 using namespace gfd;
@@ -204,6 +206,47 @@ TEST(Filter_Parse) {
   EXPECT_TRUE(DeviceFilter::parse("all").all());
   EXPECT_THROW_MSG(DeviceFilter::parse("3-1"), "invalid device range");
   EXPECT_THROW_MSG(DeviceFilter::parse("x"), "invalid device");
+  EXPECT_THROW_MSG(DeviceFilter::parse("0000:zz"), "invalid PCI address '0000:zz'");
+  EXPECT_THROW_MSG(DeviceFilter::parse("d9:20.0"), "invalid PCI address");  // device > 0x1f
+  EXPECT_THROW_MSG(DeviceFilter::parse("d9:00.8"), "invalid PCI address");  // function > 7
+  EXPECT_TRUE(DeviceFilter::parse("10000:d9:00.0").matches(0, "10000:d9:00.0"));  // 5-digit domain
+}
+
+namespace {
+// stderr of `f` (the logger writes there; the test binary silences it).
+template <typename F>
+std::string stderr_of(F&& f) {
+  bool was_quiet = gfd::log::set_quiet(false);
+  std::fflush(stderr);
+  FILE* tmp = std::tmpfile();
+  int saved = ::dup(2);
+  ::dup2(::fileno(tmp), 2);
+  f();
+  std::fflush(stderr);
+  ::dup2(saved, 2);
+  ::close(saved);
+  gfd::log::set_quiet(was_quiet);
+  std::string out;
+  std::rewind(tmp);
+  for (int c; (c = std::fgetc(tmp)) != EOF;) out.push_back(static_cast<char>(c));
+  std::fclose(tmp);
+  return out;
+}
+}  // namespace
+
+TEST(Filter_ItemsSelectingNoGpuAreLoggedOnce) {
+  auto f = DeviceFilter::parse("1,5,0000:aa:00.0");
+  std::vector<std::string> node{"0000:23:00.0", "0000:d9:00.0"};
+  std::string first = stderr_of([&] { f.check_selection(node); });
+  EXPECT_TRUE(first.find("--visible-devices '1,5,0000:aa:00.0': 5, 0000:aa:00.0 select none of the node's 2 GPU(s)") !=
+              std::string::npos);
+  // Every cycle checks; the same outcome is not logged again, a new one is.
+  EXPECT_EQ(stderr_of([&] { f.check_selection(node); }), std::string());
+  node.push_back("0000:aa:00.0");
+  EXPECT_TRUE(stderr_of([&] { f.check_selection(node); }).find("5 selects none of the node's 3 GPU(s)") !=
+              std::string::npos);
+  // Everything selected something: nothing to say.
+  EXPECT_EQ(stderr_of([&] { DeviceFilter::parse("0-1").check_selection(node); }), std::string());
 }
 
 TEST(GfxTarget_Parsing) {

@@ -333,11 +333,13 @@ std::shared_ptr<const SysfsManager::Topology> SysfsManager::read_topology() cons
 
 std::vector<DevicePtr> SysfsManager::enumerate() {
   std::shared_ptr<const Topology> topo;
+  bool fresh = false;
   if (!generation_.empty() && generation_ == cached_generation_ && cached_) {
     topo = cached_;
   } else {
     if (!cached_generation_.empty()) fs::attrs().clear();  // paths of the old topology
     topo = read_topology();
+    fresh = true;
     cached_ = generation_.empty() ? nullptr : topo;
     cached_generation_ = generation_;
   }
@@ -348,7 +350,7 @@ std::vector<DevicePtr> SysfsManager::enumerate() {
   for (size_t i = 0; i < topo->gpus.size(); ++i)
     if (opts_.filter.matches(static_cast<int>(i), topo->gpus[i].bdf))
       visible.emplace_back(static_cast<int>(i), &topo->gpus[i]);
-  if (!opts_.filter.all()) {
+  if (fresh && !opts_.filter.all()) {  // the GPUs can only change with the topology
     std::vector<std::string> bdfs;
     for (const auto& g : topo->gpus) bdfs.push_back(g.bdf);
     opts_.filter.check_selection(bdfs);

@@ -41,9 +41,11 @@ Job-mode process from spawn to exit, and per-phase p50s of the timed steps.
 from __future__ import annotations
 
 import argparse
+import atexit
 import gc
 import json
 import os
+import shutil
 import statistics
 import subprocess
 import sys
@@ -209,6 +211,7 @@ def main() -> int:
     n = a.gpus
 
     tmp = tempfile.mkdtemp(prefix="gfd-bench-")
+    atexit.register(shutil.rmtree, tmp, True)
     out = os.path.join(tmp, "features.d", "gfd")
     os.makedirs(os.path.dirname(out), exist_ok=True)
 

@@ -265,7 +265,7 @@ class Parser {
       t = t.substr(3);
     int no = 0;
     size_t start = 0;
-    bool seen_content = false;
+    bool seen_content = false, ended = false;  // ended: a "..." closed the document
     while (start <= t.size()) {
       size_t end = t.find('\n', start);
       if (end == std::string::npos) end = t.size();
@@ -282,13 +282,20 @@ class Parser {
       l.indent = static_cast<int>(ind);
       std::string body = str::trim(strip_comment(raw.substr(ind)));
       // Directives / document markers before the first content.
-      if (!seen_content && (body == "---" || str::starts_with(body, "%"))) body.clear();
-      if (!seen_content && str::starts_with(body, "--- ")) {
+      // Markers and directives count only at the start of a line; indented,
+      // "---" and "..." are plain text.
+      bool col0 = ind == 0;
+      if (ended && !body.empty()) fail_no(no, "multiple YAML documents are not supported");
+      if (col0 && !seen_content && (body == "---" || str::starts_with(body, "%"))) body.clear();
+      if (col0 && !seen_content && str::starts_with(body, "--- ")) {
         body = str::trim(body.substr(4));
         l.indent = static_cast<int>(ind + 4);
       }
-      if (seen_content && body == "...") body.clear();
-      if (seen_content && (body == "---" || str::starts_with(body, "--- ")))
+      if (col0 && body == "...") {
+        body.clear();
+        ended = seen_content;
+      }
+      if (col0 && seen_content && (body == "---" || str::starts_with(body, "--- ")))
         fail_no(no, "multiple YAML documents are not supported");
       l.content = body;
       if (!body.empty()) seen_content = true;
@@ -769,8 +776,12 @@ class Parser {
       if (c == '-') chomp = 's';
       else if (c == '+') chomp = 'k';
       else if (c >= '1' && c <= '9') explicit_indent = c - '0';
-      else if (c == ' ' || c == '\t') break;
-      else fail_no(lineno, "invalid block scalar header");
+      else if (c == ' ' || c == '\t') {
+        if (!str::trim(header.substr(k)).empty()) fail_no(lineno, "did not find expected comment or line break");
+        break;
+      } else {
+        fail_no(lineno, "invalid block scalar header");
+      }
     }
     std::vector<std::string> raw;
     int block_indent = explicit_indent ? parent_indent + explicit_indent : -1;
@@ -863,6 +874,14 @@ class Parser {
       return parse_flow_text(text, lineno);
     }
     char c = rest[0];
+    // Characters that cannot start a block value (go-yaml/libyaml's scanner
+    // and parser errors): flow terminators, reserved indicators, and a
+    // sequence entry or complex key on the line of a mapping key.
+    if (c == ',' || c == ']' || c == '}') fail_no(lineno, "did not find expected node content");
+    if (c == '%' || c == '@' || c == '`') fail_no(lineno, "found character that cannot start any token");
+    if (is_map_value && (c == '-' || c == '?') && (rest.size() == 1 || rest[1] == ' ' || rest[1] == '\t'))
+      fail_no(lineno, c == '-' ? "block sequence entries are not allowed in this context"
+                               : "mapping keys are not allowed in this context");
     if (c == '[' || c == '{') return parse_flow_text(gather_flow(rest, idx, lineno), lineno);
     if (c == '"' || c == '\'') {
       std::string text = rest;
@@ -906,13 +925,26 @@ class Parser {
   }
 
   // Plain scalar text starting with `rest`, continued on more-indented lines.
+  // A ':' followed by a blank or the end of the line ends a block plain
+  // scalar and would start a mapping value where none may be ("a: b: c",
+  // go-yaml/PyYAML: "mapping values are not allowed in this context").
   std::string gather_plain(const std::string& rest, size_t& idx, int parent_indent) {
+    auto mapping_indicator = [](const std::string& t) {
+      for (size_t k = 0; k < t.size(); ++k)
+        if (t[k] == ':' && (k + 1 == t.size() || t[k + 1] == ' ' || t[k + 1] == '\t')) return true;
+      return false;
+    };
+    if (mapping_indicator(rest)) {
+      int no = idx > 0 && idx <= lines_.size() ? lines_[idx - 1].no : 0;
+      fail_no(no, "mapping values are not allowed in this context");
+    }
     std::string text = rest;
     for (;;) {
       size_t j = next_content(idx);
       if (j >= lines_.size() || lines_[j].indent <= parent_indent) break;
       const Line& l = lines_[j];
-      if (split_key(l.content, l.no) || is_seq_entry(l.content)) fail(l, "mapping values are not allowed in this context");
+      // "- x" here is text ("b - x", as libyaml reads it); "x: y" is not.
+      if (split_key(l.content, l.no)) fail(l, "mapping values are not allowed in this context");
       text += " " + l.content;
       idx = j + 1;
     }

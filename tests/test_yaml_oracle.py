@@ -122,6 +122,42 @@ def test_pinned_cases(native, text, expected):
     assert yaml.safe_load(text) == expected
 
 
+@pytest.mark.parametrize("text", ["a: b: c\n", "a: b:\n", "a: x:\ty\n", "- x: y: z\n", "a: !!str b: c\n",
+                                  "a: &x b: c\n", "a:\n  - b: c: d\n", "run: x | grep -q 'commit: '\n"])
+def test_mapping_value_inside_a_plain_value_is_rejected_like_pyyaml(native, text):
+    """': ' ends a block plain scalar; both readers refuse what follows (the
+    native one accepted it as text until round 3 - found when this repo's
+    own CI file carried such a line)."""
+    with pytest.raises(yaml.YAMLError):
+        yaml.safe_load(text)
+    with pytest.raises(native.GfdError, match="mapping values are not allowed"):
+        native.parse_yaml(text)
+
+
+@pytest.mark.parametrize("text,message", [
+    ("a: ]\n", "did not find expected node content"), ("a: , x\n", "did not find expected node content"),
+    ("a: @x\n", "cannot start any token"), ("a: `x`\n", "cannot start any token"),
+    ("a: %x\n", "cannot start any token"), ("a: - x\n", "block sequence entries are not allowed"),
+    ("a: ? x\n", "mapping keys are not allowed"), ("a: | x\n", "expected comment or line break"),
+    ("a: 1\n...\nb: 2\n", "multiple YAML documents"),
+])
+def test_what_cannot_start_a_block_value_is_rejected_like_pyyaml(native, text, message):
+    """Found by a differential run of random token soups against PyYAML
+    (round 3): the native reader took these as plain text."""
+    with pytest.raises(yaml.YAMLError):
+        yaml.safe_load(text)
+    with pytest.raises(native.GfdError, match=message):
+        native.parse_yaml(text)
+
+
+@pytest.mark.parametrize("text,expected", [
+    ("a:\n  ...\n", {"a": "..."}), ("a:\n  ---\n", {"a": "---"}),  # markers count at column 0 only
+    ("a: b\n  - c\n", {"a": "b - c"}),                                # "- " continuing a plain scalar
+])
+def test_indented_markers_and_dashes_are_text(native, text, expected):
+    assert native.parse_yaml(text) == expected == yaml.safe_load(text)
+
+
 def test_integer_prefixes_follow_go_yaml_not_pyyaml(native):
     """Where the reference's parser and PyYAML disagree, go-yaml v2 wins:
     it resolves plain integers with Go's strconv.ParseInt(s, 0, 64), which

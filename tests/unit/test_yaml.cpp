@@ -88,6 +88,42 @@ TEST(Yaml_Errors) {
   EXPECT_THROW_MSG(parse("\ta: 1\n"), "tab");
 }
 
+TEST(Yaml_MappingIndicatorInsidePlainValueIsAnError) {
+  // ": " (or ":" at the end) ends a block plain scalar; go-yaml and PyYAML
+  // reject what follows.  A ':' inside a word, or inside quotes, is text.
+  for (const char* doc : {"a: b: c\n", "a: b:\n", "a: x:\ty\n", "- x: y: z\n", "a: !!str b: c\n", "a: &x b: c\n",
+                          "a:\n  - b: c: d\n", "run: x | grep -q 'commit: '\n"})
+    EXPECT_THROW_MSG(parse(doc), "mapping values are not allowed in this context");
+  EXPECT_EQ(parse("a: http://h:80/p\n").get("a")->text(), std::string("http://h:80/p"));
+  EXPECT_EQ(parse("a: b :c\n").get("a")->text(), std::string("b :c"));
+  EXPECT_EQ(parse("a: 'q: r'\n").get("a")->text(), std::string("q: r"));
+  EXPECT_EQ(parse("a: b #c: d\n").get("a")->text(), std::string("b"));
+}
+
+TEST(Yaml_WhatCannotStartABlockValue) {
+  EXPECT_THROW_MSG(parse("a: ]\n"), "did not find expected node content");
+  EXPECT_THROW_MSG(parse("a: , x\n"), "did not find expected node content");
+  EXPECT_THROW_MSG(parse("a: @x\n"), "cannot start any token");
+  EXPECT_THROW_MSG(parse("a: `x`\n"), "cannot start any token");
+  EXPECT_THROW_MSG(parse("a: %x\n"), "cannot start any token");
+  EXPECT_THROW_MSG(parse("a: - x\n"), "block sequence entries are not allowed");
+  EXPECT_THROW_MSG(parse("a: ? x\n"), "mapping keys are not allowed");
+  EXPECT_THROW_MSG(parse("a: | x\n"), "did not find expected comment or line break");
+  // Still fine: indicators inside a word, compact nested sequences, a block
+  // scalar header with a comment, "- " continuing a plain scalar.
+  EXPECT_EQ(parse("a: -x\n").get("a")->text(), std::string("-x"));
+  EXPECT_EQ(parse("- - a\n  - b\n").items()[0].items().size(), static_cast<size_t>(2));
+  EXPECT_EQ(parse("a: | # note\n  t\n").get("a")->text(), std::string("t\n"));
+  EXPECT_EQ(parse("a: b\n  - c\n").get("a")->text(), std::string("b - c"));
+}
+
+TEST(Yaml_DocumentMarkersOnlyAtColumnZero) {
+  EXPECT_EQ(parse("a:\n  ...\n").get("a")->text(), std::string("..."));
+  EXPECT_EQ(parse("a:\n  ---\n").get("a")->text(), std::string("---"));
+  EXPECT_EQ(parse("a: 1\n...\n").get("a")->text(), std::string("1"));
+  EXPECT_THROW_MSG(parse("a: 1\n...\nb: 2\n"), "multiple YAML documents");
+}
+
 TEST(Yaml_JsonPrettyPrint) {
   Node n = parse("a: 1\nb: [x]\nc: {}\n");
   EXPECT_EQ(to_json(n, 2), std::string("{\n  \"a\": 1,\n  \"b\": [\n    \"x\"\n  ],\n  \"c\": {}\n}"));

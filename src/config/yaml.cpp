@@ -185,6 +185,7 @@ struct Line {
   int indent = 0;       // leading spaces
   std::string raw;      // full raw line (no newline)
   std::string content;  // after indent, comment stripped, right-trimmed
+  bool comment = false; // the line ends in a comment
 };
 
 class Parser {
@@ -228,6 +229,7 @@ class Parser {
   static std::string strip_comment(const std::string& in) {
     std::string s = in;
     bool sq = false, dq = false;
+    size_t closed = std::string::npos;  // just past the last closing quote
     for (size_t i = 0; i < s.size(); ++i) {
       char c = s[i];
       if (dq) {
@@ -235,19 +237,24 @@ class Parser {
           ++i;
         } else if (c == '"') {
           dq = false;
+          closed = i + 1;
         }
       } else if (sq) {
         if (c == '\'') {
-          if (i + 1 < s.size() && s[i + 1] == '\'')
+          if (i + 1 < s.size() && s[i + 1] == '\'') {
             ++i;
-          else
+          } else {
             sq = false;
+            closed = i + 1;
+          }
         }
       } else if (c == '"' && (i == 0 || strchr(" \t\n[{,:", s[i - 1]))) {
         dq = true;
       } else if (c == '\'' && (i == 0 || strchr(" \t\n[{,:", s[i - 1]))) {
         sq = true;
-      } else if (c == '#' && (i == 0 || s[i - 1] == ' ' || s[i - 1] == '\t' || s[i - 1] == '\n')) {
+      } else if (c == '#' && (i == 0 || i == closed || s[i - 1] == ' ' || s[i - 1] == '\t' || s[i - 1] == '\n')) {
+        // (Right after a closing quote too: the scalar has ended, libyaml and
+        // PyYAML read the rest of the line as a comment.)
         size_t nl = s.find('\n', i);
         if (nl == std::string::npos) return s.substr(0, i);
         s.erase(i, nl - i);
@@ -280,7 +287,9 @@ class Parser {
       if (ind < raw.size() && raw[ind] == '\t' && str::trim(raw).size() > 0 && str::trim(raw)[0] != '#')
         fail_no(no, "found character that cannot start any token (tab indentation)");
       l.indent = static_cast<int>(ind);
-      std::string body = str::trim(strip_comment(raw.substr(ind)));
+      std::string uncommented = strip_comment(raw.substr(ind));
+      l.comment = uncommented.size() < raw.size() - ind;
+      std::string body = str::trim(uncommented);
       // Directives / document markers before the first content.
       // Markers and directives count only at the start of a line; indented,
       // "---" and "..." are plain text.
@@ -340,6 +349,8 @@ class Parser {
       if (s[i] == ':' && (i + 1 == s.size() || s[i + 1] == ' ' || s[i + 1] == '\t')) {
         key = str::trim(s.substr(0, i));
         if (key.empty()) return std::nullopt;
+        // A plain key cannot start with these either (see parse_inline_value).
+        if (strchr(",]}%@`|>", key[0])) fail_no(lineno, "found character that cannot start a mapping key");
         return std::make_pair(key, str::trim(s.substr(i + 1)));
       }
     }
@@ -771,12 +782,15 @@ class Parser {
     bool literal = header[0] == '|';
     char chomp = 'c';  // clip
     int explicit_indent = 0;
+    bool chomp_seen = false;
     for (size_t k = 1; k < header.size(); ++k) {
       char c = header[k];
-      if (c == '-') chomp = 's';
-      else if (c == '+') chomp = 'k';
-      else if (c >= '1' && c <= '9') explicit_indent = c - '0';
-      else if (c == ' ' || c == '\t') {
+      if ((c == '-' || c == '+') && !chomp_seen) {
+        chomp = c == '-' ? 's' : 'k';
+        chomp_seen = true;
+      } else if (c >= '1' && c <= '9' && !explicit_indent) {
+        explicit_indent = c - '0';
+      } else if (c == ' ' || c == '\t') {
         if (!str::trim(header.substr(k)).empty()) fail_no(lineno, "did not find expected comment or line break");
         break;
       } else {
@@ -842,6 +856,18 @@ class Parser {
     return Node::string(out);
   }
 
+  // Characters that cannot start a block value (go-yaml/libyaml's scanner
+  // and parser errors): flow terminators, reserved indicators, and a
+  // sequence entry or complex key on the line of a mapping key.
+  static void check_value_start(const std::string& rest, bool is_map_value, int lineno) {
+    char c = rest[0];
+    if (c == ',' || c == ']' || c == '}') fail_no(lineno, "did not find expected node content");
+    if (c == '%' || c == '@' || c == '`') fail_no(lineno, "found character that cannot start any token");
+    if (is_map_value && (c == '-' || c == '?') && (rest.size() == 1 || rest[1] == ' ' || rest[1] == '\t'))
+      fail_no(lineno, c == '-' ? "block sequence entries are not allowed in this context"
+                               : "mapping keys are not allowed in this context");
+  }
+
   // Value text appearing inline after "key:" or "- ".  idx points at the line
   // after the one holding `rest`.
   Node parse_inline_value(const std::string& rest, size_t& idx, int parent_indent, bool is_map_value) {
@@ -874,14 +900,7 @@ class Parser {
       return parse_flow_text(text, lineno);
     }
     char c = rest[0];
-    // Characters that cannot start a block value (go-yaml/libyaml's scanner
-    // and parser errors): flow terminators, reserved indicators, and a
-    // sequence entry or complex key on the line of a mapping key.
-    if (c == ',' || c == ']' || c == '}') fail_no(lineno, "did not find expected node content");
-    if (c == '%' || c == '@' || c == '`') fail_no(lineno, "found character that cannot start any token");
-    if (is_map_value && (c == '-' || c == '?') && (rest.size() == 1 || rest[1] == ' ' || rest[1] == '\t'))
-      fail_no(lineno, c == '-' ? "block sequence entries are not allowed in this context"
-                               : "mapping keys are not allowed in this context");
+    check_value_start(rest, is_map_value, lineno);
     if (c == '[' || c == '{') return parse_flow_text(gather_flow(rest, idx, lineno), lineno);
     if (c == '"' || c == '\'') {
       std::string text = rest;
@@ -916,6 +935,7 @@ class Parser {
         return v;
       }
       if (!after.empty() && !strchr("[{\"'|>&*!", after[0])) {
+        check_value_start(after, true, lineno);
         std::string text = gather_plain(after, idx, parent_indent);
         return apply_tag(name, resolve_plain(text), true, text, lineno);
       }
@@ -940,12 +960,25 @@ class Parser {
     }
     std::string text = rest;
     for (;;) {
-      size_t j = next_content(idx);
+      // Line folding: one break is a space, a break and n empty lines are n
+      // newlines.  A comment line ends the scalar.
+      size_t j = idx, empties = 0;
+      while (j < lines_.size() && lines_[j].content.empty()) {
+        if (str::trim(lines_[j].raw).empty()) {
+          ++empties;
+        } else {
+          return text;  // a comment line
+        }
+        ++j;
+      }
       if (j >= lines_.size() || lines_[j].indent <= parent_indent) break;
       const Line& l = lines_[j];
-      // "- x" here is text ("b - x", as libyaml reads it); "x: y" is not.
-      if (split_key(l.content, l.no)) fail(l, "mapping values are not allowed in this context");
-      text += " " + l.content;
+      // A comment on the previous line ended the scalar.
+      if (idx > 0 && lines_[idx - 1].comment) fail(l, "could not find expected ':'");
+      // "- x" here is text ("b - x", as libyaml reads it); "x: y" or ": y" is not.
+      if (mapping_indicator(l.content)) fail(l, "mapping values are not allowed in this context");
+      text += empties ? std::string(empties, '\n') : std::string(" ");
+      text += l.content;
       idx = j + 1;
     }
     return text;

@@ -117,6 +117,19 @@ TEST(Yaml_WhatCannotStartABlockValue) {
   EXPECT_EQ(parse("a: b\n  - c\n").get("a")->text(), std::string("b - c"));
 }
 
+TEST(Yaml_PlainScalarFoldingAndEnds) {
+  // Pinned against PyYAML (tools/yaml_diff.py found the differences).
+  EXPECT_EQ(parse("a: x\n  y\n\n\n  z\n").get("a")->text(), std::string("x y\n\nz"));  // n empty lines: n newlines
+  EXPECT_THROW_MSG(parse("a: x # c\n  y\n"), "could not find expected ':'");     // a comment ends the scalar
+  EXPECT_THROW_MSG(parse("a: x\n  : y\n"), "mapping values are not allowed");  // ':' on a continuation line
+  EXPECT_EQ(parse("a: \"d\"#c\n").get("a")->text(), std::string("d"));           // comment right after a quote
+  EXPECT_EQ(parse("a: 'it''s'#c\n").get("a")->text(), std::string("it's"));
+  EXPECT_EQ(parse("a: \"x#y\"\n").get("a")->text(), std::string("x#y"));
+  EXPECT_THROW_MSG(parse("a: !!str ]\n"), "did not find expected node content");  // after a tag, too
+  EXPECT_THROW_MSG(parse("a: |--\n  x\n"), "invalid block scalar header");       // one chomping indicator
+  EXPECT_THROW_MSG(parse("a:\n  }: 1\n"), "cannot start a mapping key");
+}
+
 TEST(Yaml_DocumentMarkersOnlyAtColumnZero) {
   EXPECT_EQ(parse("a:\n  ...\n").get("a")->text(), std::string("..."));
   EXPECT_EQ(parse("a:\n  ---\n").get("a")->text(), std::string("---"));

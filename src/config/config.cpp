@@ -1,6 +1,8 @@
 #include "config/config.h"
 
+#include <cctype>
 #include <cmath>
+#include <cstring>
 #include <limits>
 
 #include "util/error.h"
@@ -54,6 +56,23 @@ std::string default_shared_rename(const std::string& resource_name) {
 // Typed decoding with json-like error messages.
 
 namespace {
+
+// A struct field's key, matched the way the reference's decoder matches it
+// (sigs.k8s.io/yaml -> encoding/json): any key equal to the field's name
+// ignoring ASCII case ("MigStrategy", "MIGSTRATEGY"), the last one in the
+// document winning.  (A key repeated verbatim keeps its first position here,
+// so "a, A, a" picks A where Go picks the second a.)
+const Node* field(const Node& n, const char* name) {
+  const Node* found = nullptr;
+  for (const auto& [k, v] : n.entries()) {
+    if (k.size() != std::strlen(name)) continue;
+    bool eq = true;
+    for (size_t i = 0; i < k.size() && eq; ++i)
+      eq = std::tolower(static_cast<unsigned char>(k[i])) == std::tolower(static_cast<unsigned char>(name[i]));
+    if (eq) found = &v;
+  }
+  return found;
+}
 
 [[noreturn]] void type_error(const Node& n, const std::string& path, const std::string& want) {
   throw Error("json: cannot unmarshal " + n.kind_name() + " into Go struct field " + path + " of type " + want);
@@ -188,20 +207,20 @@ ReplicatedDevices decode_devices(const Node& n) {
 ReplicatedResource decode_replicated_resource(const Node& n, const std::string& path) {
   require_map(n, path, "ReplicatedResource");
   ReplicatedResource r;
-  const Node* name = n.get("name");
+  const Node* name = field(n, "name");
   if (!name) throw Error("no resource name specified");
   auto name_s = opt_string(name, path + ".name");
   r.name = new_resource_name(name_s.value_or(""));
-  const Node* devices = n.get("devices");
+  const Node* devices = field(n, "devices");
   if (devices && !devices->is_null())
     r.devices = decode_devices(*devices);
   else
     r.devices.all = true;
-  const Node* replicas = n.get("replicas");
+  const Node* replicas = field(n, "replicas");
   if (!replicas) throw Error("no replicas specified");
   r.replicas = to_int(*replicas, path + ".replicas");
   if (r.replicas < 2) throw Error("number of replicas must be >= 2");
-  if (const Node* rename = n.get("rename")) {
+  if (const Node* rename = field(n, "rename")) {
     auto rs = opt_string(rename, path + ".rename");
     if (rs) r.rename = new_resource_name(*rs);
   }
@@ -211,10 +230,10 @@ ReplicatedResource decode_replicated_resource(const Node& n, const std::string& 
 TimeSlicing decode_time_slicing(const Node& n, const std::string& path) {
   require_map(n, path, "TimeSlicing");
   TimeSlicing ts;
-  ts.rename_by_default = opt_bool(n.get("renameByDefault"), path + ".renameByDefault").value_or(false);
+  ts.rename_by_default = opt_bool(field(n, "renameByDefault"), path + ".renameByDefault").value_or(false);
   ts.fail_requests_greater_than_one =
-      opt_bool(n.get("failRequestsGreaterThanOne"), path + ".failRequestsGreaterThanOne").value_or(false);
-  const Node* res = n.get("resources");
+      opt_bool(field(n, "failRequestsGreaterThanOne"), path + ".failRequestsGreaterThanOne").value_or(false);
+  const Node* res = field(n, "resources");
   if (!res || res->is_null()) throw Error("no resources specified");
   if (!res->is_seq()) type_error(*res, path + ".resources", "[]ReplicatedResource");
   for (const auto& item : res->items()) ts.resources.push_back(decode_replicated_resource(item, path + ".resources"));
@@ -230,8 +249,8 @@ std::vector<Resource> decode_resource_list(const Node* n, const std::string& pat
   if (!n->is_seq()) type_error(*n, path, "[]Resource");
   for (const auto& item : n->items()) {
     require_map(item, path, "Resource");
-    const Node* pattern = item.get("pattern");
-    const Node* name = item.get("name");
+    const Node* pattern = field(item, "pattern");
+    const Node* name = field(item, "name");
     if (!pattern) throw Error("resources must have a 'pattern' field set");
     if (!name) throw Error("resources must have a 'name' field set");
     Resource r;
@@ -245,19 +264,19 @@ std::vector<Resource> decode_resource_list(const Node* n, const std::string& pat
 GFDFlags decode_gfd_flags(const Node& n) {
   GFDFlags g;
   require_map(n, "Config.flags.gfd", "GFDCommandLineFlags");
-  g.oneshot = opt_bool(n.get("oneshot"), "Config.flags.gfd.oneshot");
-  g.no_timestamp = opt_bool(n.get("noTimestamp"), "Config.flags.gfd.noTimestamp");
-  g.sleep_interval = opt_duration(n.get("sleepInterval"), "Config.flags.gfd.sleepInterval");
-  g.output_file = opt_string(n.get("outputFile"), "Config.flags.gfd.outputFile");
-  g.machine_type_file = opt_string(n.get("machineTypeFile"), "Config.flags.gfd.machineTypeFile");
-  g.backend = opt_string(n.get("backend"), "Config.flags.gfd.backend");
-  g.sysfs_root = opt_string(n.get("sysfsRoot"), "Config.flags.gfd.sysfsRoot");
-  g.host_root = opt_string(n.get("hostRoot"), "Config.flags.gfd.hostRoot");
-  g.rocm_version_file = opt_string(n.get("rocmVersionFile"), "Config.flags.gfd.rocmVersionFile");
-  g.visible_devices = opt_string(n.get("visibleDevices"), "Config.flags.gfd.visibleDevices");
-  g.mock_file = opt_string(n.get("mockFile"), "Config.flags.gfd.mockFile");
-  g.amdsmi_session = opt_string(n.get("amdsmiSession"), "Config.flags.gfd.amdsmiSession");
-  g.trace_timing = opt_bool(n.get("traceTiming"), "Config.flags.gfd.traceTiming");
+  g.oneshot = opt_bool(field(n, "oneshot"), "Config.flags.gfd.oneshot");
+  g.no_timestamp = opt_bool(field(n, "noTimestamp"), "Config.flags.gfd.noTimestamp");
+  g.sleep_interval = opt_duration(field(n, "sleepInterval"), "Config.flags.gfd.sleepInterval");
+  g.output_file = opt_string(field(n, "outputFile"), "Config.flags.gfd.outputFile");
+  g.machine_type_file = opt_string(field(n, "machineTypeFile"), "Config.flags.gfd.machineTypeFile");
+  g.backend = opt_string(field(n, "backend"), "Config.flags.gfd.backend");
+  g.sysfs_root = opt_string(field(n, "sysfsRoot"), "Config.flags.gfd.sysfsRoot");
+  g.host_root = opt_string(field(n, "hostRoot"), "Config.flags.gfd.hostRoot");
+  g.rocm_version_file = opt_string(field(n, "rocmVersionFile"), "Config.flags.gfd.rocmVersionFile");
+  g.visible_devices = opt_string(field(n, "visibleDevices"), "Config.flags.gfd.visibleDevices");
+  g.mock_file = opt_string(field(n, "mockFile"), "Config.flags.gfd.mockFile");
+  g.amdsmi_session = opt_string(field(n, "amdsmiSession"), "Config.flags.gfd.amdsmiSession");
+  g.trace_timing = opt_bool(field(n, "traceTiming"), "Config.flags.gfd.traceTiming");
   return g;
 }
 
@@ -273,25 +292,25 @@ Config parse_config_text(const std::string& text) {
     root = yaml::parse(text);
     if (!root.is_null()) {
       require_map(root, "Config", "Config");
-      if (auto v = opt_string(root.get("version"), "Config.version")) c.version = *v;
-      if (const Node* flags = root.get("flags"); flags && !flags->is_null()) {
+      if (auto v = opt_string(field(root, "version"), "Config.version")) c.version = *v;
+      if (const Node* flags = field(root, "flags"); flags && !flags->is_null()) {
         require_map(*flags, "Config.flags", "Flags");
-        c.flags.mig_strategy = opt_string(flags->get("migStrategy"), "Config.flags.migStrategy");
-        c.flags.fail_on_init_error = opt_bool(flags->get("failOnInitError"), "Config.flags.failOnInitError");
-        c.flags.driver_root = opt_string(flags->get("driverRoot"), "Config.flags.driverRoot");
-        if (const Node* p = flags->get("plugin"); p && !p->is_null()) c.flags.plugin_present = true;
-        if (const Node* g = flags->get("gfd"); g && !g->is_null()) c.flags.gfd = decode_gfd_flags(*g);
+        c.flags.mig_strategy = opt_string(field(*flags, "migStrategy"), "Config.flags.migStrategy");
+        c.flags.fail_on_init_error = opt_bool(field(*flags, "failOnInitError"), "Config.flags.failOnInitError");
+        c.flags.driver_root = opt_string(field(*flags, "driverRoot"), "Config.flags.driverRoot");
+        if (const Node* p = field(*flags, "plugin"); p && !p->is_null()) c.flags.plugin_present = true;
+        if (const Node* g = field(*flags, "gfd"); g && !g->is_null()) c.flags.gfd = decode_gfd_flags(*g);
       }
-      if (const Node* res = root.get("resources"); res && !res->is_null()) {
+      if (const Node* res = field(root, "resources"); res && !res->is_null()) {
         require_map(*res, "Config.resources", "Resources");
-        c.resources.gpus = decode_resource_list(res->get("gpus"), "Config.resources.gpus");
-        c.resources.partitions = decode_resource_list(res->get("mig"), "Config.resources.mig");
+        c.resources.gpus = decode_resource_list(field(*res, "gpus"), "Config.resources.gpus");
+        c.resources.partitions = decode_resource_list(field(*res, "mig"), "Config.resources.mig");
         if (c.resources.partitions.empty())
-          c.resources.partitions = decode_resource_list(res->get("partitions"), "Config.resources.partitions");
+          c.resources.partitions = decode_resource_list(field(*res, "partitions"), "Config.resources.partitions");
       }
-      if (const Node* sh = root.get("sharing"); sh && !sh->is_null()) {
+      if (const Node* sh = field(root, "sharing"); sh && !sh->is_null()) {
         require_map(*sh, "Config.sharing", "Sharing");
-        if (const Node* ts = sh->get("timeSlicing"); ts && !ts->is_null())
+        if (const Node* ts = field(*sh, "timeSlicing"); ts && !ts->is_null())
           c.sharing.time_slicing = decode_time_slicing(*ts, "Config.sharing.timeSlicing");
       }
     }

@@ -168,7 +168,7 @@ def test_sigkilled_daemons_leave_a_bounded_gfd_tmp(binary, tmp_path):
     p = _start(binary, ["--sleep-interval=10s", *_base(tmp_path, out)])
     try:
         assert _wait_for(lambda: out.stat().st_mtime_ns > m0), "first cycle"
-        assert _wait_for(lambda: len(_temps(tmp)) == 1)  # the next write's file
+        time.sleep(0.2)  # the cycle's preparer job has run (whether its file is left depends on timing)
         left = _temps(tmp)
         assert len(left) <= 2, left
         assert not stale & {f for f, _ in left}, left

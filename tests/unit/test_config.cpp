@@ -13,6 +13,22 @@ TEST(Config_EmptyDocumentDefaultsToV1) {
   EXPECT_FALSE(c.flags.mig_strategy.has_value());
 }
 
+TEST(Config_KeysMatchIgnoringCaseLikeEncodingJson) {
+  // The reference decodes through encoding/json, which takes a key that
+  // equals a field's name ignoring case; the last such key wins.
+  Config c = parse_config_text(
+      "Version: v1\nFLAGS:\n  MigStrategy: single\n  migstrategy: mixed\n  Gfd:\n    SleepInterval: 5s\n"
+      "Sharing:\n  timeslicing:\n    Resources:\n    - NAME: amd.com/gpu\n      Replicas: 4\n");
+  EXPECT_EQ(c.mig_strategy(), std::string("mixed"));
+  EXPECT_EQ(*c.flags.gfd.sleep_interval, parse_duration("5s"));
+  EXPECT_EQ(c.sharing.time_slicing.resources.size(), static_cast<size_t>(1));
+  EXPECT_EQ(c.sharing.time_slicing.resources[0].replicas, 4);
+  EXPECT_EQ(parse_config_text("flags:\n  migStrategy: single\n  MIGSTRATEGY: mixed\n").mig_strategy(),
+            std::string("mixed"));
+  EXPECT_EQ(parse_config_text("flags:\n  MIGSTRATEGY: mixed\n  migStrategy: single\n").mig_strategy(),
+            std::string("single"));
+}
+
 TEST(Config_UnknownVersionRejected) {
   EXPECT_THROW_MSG(parse_config_text("version: v2\n"), "unknown version: v2");
 }

@@ -61,7 +61,10 @@ namespace {
 // (sigs.k8s.io/yaml -> encoding/json): any key equal to the field's name
 // ignoring ASCII case ("MigStrategy", "MIGSTRATEGY"), the last one in the
 // document winning.  (A key repeated verbatim keeps its first position here,
-// so "a, A, a" picks A where Go picks the second a.)
+// so "a, A, a" picks A where Go picks the second a.)  Not for the bodies the
+// reference decodes with its own UnmarshalJSON - TimeSlicing,
+// ReplicatedResource, Resource (replicas.go:121-200, resources.go:94-122) -
+// which look their keys up exactly in a map.
 const Node* field(const Node& n, const char* name) {
   const Node* found = nullptr;
   for (const auto& [k, v] : n.entries()) {
@@ -207,20 +210,20 @@ ReplicatedDevices decode_devices(const Node& n) {
 ReplicatedResource decode_replicated_resource(const Node& n, const std::string& path) {
   require_map(n, path, "ReplicatedResource");
   ReplicatedResource r;
-  const Node* name = field(n, "name");
+  const Node* name = n.get("name");
   if (!name) throw Error("no resource name specified");
   auto name_s = opt_string(name, path + ".name");
   r.name = new_resource_name(name_s.value_or(""));
-  const Node* devices = field(n, "devices");
+  const Node* devices = n.get("devices");
   if (devices && !devices->is_null())
     r.devices = decode_devices(*devices);
   else
     r.devices.all = true;
-  const Node* replicas = field(n, "replicas");
+  const Node* replicas = n.get("replicas");
   if (!replicas) throw Error("no replicas specified");
   r.replicas = to_int(*replicas, path + ".replicas");
   if (r.replicas < 2) throw Error("number of replicas must be >= 2");
-  if (const Node* rename = field(n, "rename")) {
+  if (const Node* rename = n.get("rename")) {
     auto rs = opt_string(rename, path + ".rename");
     if (rs) r.rename = new_resource_name(*rs);
   }
@@ -230,10 +233,10 @@ ReplicatedResource decode_replicated_resource(const Node& n, const std::string& 
 TimeSlicing decode_time_slicing(const Node& n, const std::string& path) {
   require_map(n, path, "TimeSlicing");
   TimeSlicing ts;
-  ts.rename_by_default = opt_bool(field(n, "renameByDefault"), path + ".renameByDefault").value_or(false);
+  ts.rename_by_default = opt_bool(n.get("renameByDefault"), path + ".renameByDefault").value_or(false);
   ts.fail_requests_greater_than_one =
-      opt_bool(field(n, "failRequestsGreaterThanOne"), path + ".failRequestsGreaterThanOne").value_or(false);
-  const Node* res = field(n, "resources");
+      opt_bool(n.get("failRequestsGreaterThanOne"), path + ".failRequestsGreaterThanOne").value_or(false);
+  const Node* res = n.get("resources");
   if (!res || res->is_null()) throw Error("no resources specified");
   if (!res->is_seq()) type_error(*res, path + ".resources", "[]ReplicatedResource");
   for (const auto& item : res->items()) ts.resources.push_back(decode_replicated_resource(item, path + ".resources"));
@@ -249,8 +252,8 @@ std::vector<Resource> decode_resource_list(const Node* n, const std::string& pat
   if (!n->is_seq()) type_error(*n, path, "[]Resource");
   for (const auto& item : n->items()) {
     require_map(item, path, "Resource");
-    const Node* pattern = field(item, "pattern");
-    const Node* name = field(item, "name");
+    const Node* pattern = item.get("pattern");
+    const Node* name = item.get("name");
     if (!pattern) throw Error("resources must have a 'pattern' field set");
     if (!name) throw Error("resources must have a 'name' field set");
     Resource r;

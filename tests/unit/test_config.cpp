@@ -18,7 +18,7 @@ TEST(Config_KeysMatchIgnoringCaseLikeEncodingJson) {
   // equals a field's name ignoring case; the last such key wins.
   Config c = parse_config_text(
       "Version: v1\nFLAGS:\n  MigStrategy: single\n  migstrategy: mixed\n  Gfd:\n    SleepInterval: 5s\n"
-      "Sharing:\n  timeslicing:\n    Resources:\n    - NAME: amd.com/gpu\n      Replicas: 4\n");
+      "Sharing:\n  timeslicing:\n    resources:\n    - name: amd.com/gpu\n      replicas: 4\n");
   EXPECT_EQ(c.mig_strategy(), std::string("mixed"));
   EXPECT_EQ(*c.flags.gfd.sleep_interval, parse_duration("5s"));
   EXPECT_EQ(c.sharing.time_slicing.resources.size(), static_cast<size_t>(1));
@@ -27,6 +27,11 @@ TEST(Config_KeysMatchIgnoringCaseLikeEncodingJson) {
             std::string("mixed"));
   EXPECT_EQ(parse_config_text("flags:\n  MIGSTRATEGY: mixed\n  migStrategy: single\n").mig_strategy(),
             std::string("single"));
+  // Not inside the bodies the reference decodes itself (TimeSlicing,
+  // ReplicatedResource, Resource: exact map lookups).
+  EXPECT_THROW_MSG(parse_config_text("sharing:\n  timeSlicing:\n    Resources:\n    - name: amd.com/gpu\n"
+                                     "      replicas: 2\n"),
+                   "no resources specified");
 }
 
 TEST(Config_UnknownVersionRejected) {

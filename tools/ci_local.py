@@ -64,8 +64,9 @@ def main() -> int:
                             print(f"{label}: skip  {cmd.strip()}")
                             continue
                         t0 = time.monotonic()
+                        # errors="replace": a fuzzer's log holds raw input bytes.
                         cp = subprocess.run(["bash", "-e", "-c", cmd], cwd=work, capture_output=True, text=True,
-                                            env={**os.environ, "CI": os.environ.get("CI", "")})
+                                            errors="replace", env={**os.environ, "CI": os.environ.get("CI", "")})
                         dt = time.monotonic() - t0
                         tail = (cp.stdout + cp.stderr).strip().splitlines()[-1:] or [""]
                         print(f"{label}: {'ok  ' if cp.returncode == 0 else 'FAIL'}  {cmd.strip()}  "

@@ -181,16 +181,18 @@ ReplicatedDevices decode_devices(const Node& n) {
     d.all = true;
     return d;
   }
-  if (n.kind() == Node::Kind::Int) {
-    if (n.as_int() <= 0)
-      throw Error("devices set as '" + std::to_string(n.as_int()) + "' but a count of devices must be > 0");
-    d.count = static_cast<int>(n.as_int());
+  // Numbers reach the reference's decoder as JSON written by sigs.k8s.io/yaml,
+  // where an integral float is an integer (2.0 -> 2): counts and indices
+  // take either.
+  if (auto count = integral_in(n, std::numeric_limits<int>::min(), std::numeric_limits<int>::max())) {
+    if (*count <= 0) throw Error("devices set as '" + std::to_string(*count) + "' but a count of devices must be > 0");
+    d.count = static_cast<int>(*count);
     return d;
   }
   if (n.is_seq()) {
     for (const auto& item : n.items()) {
-      if (item.kind() == Node::Kind::Int && item.as_int() >= 0) {
-        d.list.push_back(std::to_string(item.as_int()));
+      if (auto index = integral_in(item, 0, std::numeric_limits<int>::max())) {
+        d.list.push_back(std::to_string(*index));
         continue;
       }
       if (item.kind() == Node::Kind::String) {

@@ -116,6 +116,20 @@ TEST(Config_TimeSlicingValidation) {
                    "unsupported type for device");
 }
 
+TEST(Config_IntegralFloatsAreIntegersLikeTheReferencesJson) {
+  // sigs.k8s.io/yaml hands the reference's decoder JSON in which 2.0 is 2.
+  auto devices = [](const std::string& v) {
+    return parse_config_text("sharing:\n  timeSlicing:\n    resources:\n    - name: gpu\n      replicas: 2.0\n"
+                             "      devices: " + v + "\n")
+        .sharing.time_slicing.resources[0];
+  };
+  EXPECT_EQ(devices("2.0").devices.count, 2);
+  EXPECT_EQ(devices("2.0").replicas, 2);
+  EXPECT_EQ(devices("[1.0, 0]").devices.list, (std::vector<std::string>{"1", "0"}));
+  EXPECT_THROW_MSG(devices("2.5"), "unrecognized type for devices spec");
+  EXPECT_THROW_MSG(devices("[-1]"), "unsupported type for device");
+}
+
 TEST(Config_OutOfRangeNumbersAreTypeErrors) {
   // Found by tests/fuzz/fuzz_config.cpp: a float beyond the integer range
   // was converted with undefined behaviour, a large int silently truncated.

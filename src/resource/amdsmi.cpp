@@ -687,10 +687,14 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
       }
     }
   }
-  if (!opts_.filter.all()) {
-    std::vector<std::string> bdfs;
-    for (const auto& procs : physical) bdfs.push_back(procs[0].gpu_bdf);
-    opts_.filter.check_selection(bdfs);
+  if (!opts_.filter.all()) {  // checked when the set of GPUs changes, not every cycle
+    bool same = selected_from_.size() == physical.size();
+    for (size_t i = 0; same && i < physical.size(); ++i) same = selected_from_[i] == physical[i][0].gpu_bdf;
+    if (!same) {
+      selected_from_.clear();
+      for (const auto& procs : physical) selected_from_.push_back(procs[0].gpu_bdf);
+      opts_.filter.check_selection(selected_from_);
+    }
   }
   const bool sysfs_values = opts_.sysfs_values;
 

@@ -129,6 +129,8 @@ class AmdSmiManager : public Manager {
   // it could not load libdrm_amdgpu, returns uninitialised bytes with
   // success (measured on the pool).  Also saves the call on every cycle.
   std::map<void*, std::string> proc_bdf_;
+  // The physical GPUs (BDFs, index order) the device filter was last checked against.
+  std::vector<std::string> selected_from_;
 };
 
 }  // namespace gfd::resource

@@ -179,6 +179,16 @@ def test_sigkilled_daemons_leave_a_bounded_gfd_tmp(binary, tmp_path):
     assert not out.exists() and not tmp.exists()
 
 
+def test_labels_on_stdout_that_cannot_be_written_fail_the_run(binary):
+    """--output-file="" prints the labels (labels.go:38-41); a stdout that
+    refuses them (a full disk, a closed pipe) is an error, not a silent
+    success."""
+    with open("/dev/full", "w") as full:
+        cp = subprocess.run([binary, "--oneshot", "--backend=null", "--output-file="], stdout=full,
+                            stderr=subprocess.PIPE, text=True, timeout=30)
+    assert cp.returncode == 1 and "error writing labels to stdout" in cp.stderr, cp.stderr[-2000:]
+
+
 def test_oneshot_leaves_gfd_tmp_alone(binary, tmp_path):
     """Only the loop daemon sweeps gfd-tmp/ at start: a oneshot Job may share
     the directory with a running DaemonSet."""

@@ -1,11 +1,13 @@
 // Labeler unit tests.  Ports of internal/lm/resource_test.go:27-304 and
 // internal/lm/nvml_test.go:11-77, re-expressed for the amd.com schema.
 #include <fcntl.h>
+#include <sys/resource.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
+#include <csignal>
 #include <cstdio>
 #include <set>
 #include <thread>
@@ -406,6 +408,34 @@ TEST(WriteToFile_ReplaceKeepsExactContentsAndStaysFast) {
 
 TEST(WriteToFile_UnwritableDirectoryErrors) {
   EXPECT_THROW_MSG(lm::write_to_file({{"k", "v"}}, "/proc/gfd-cannot-write/here/gfd"), "error atomically writing file");
+}
+
+TEST(WriteToFile_FailedWriteLeavesNoTemporaries) {
+  // A write that fails part-way (here: the file size limit, EFBIG - as a
+  // full disk gives ENOSPC) throws and removes gfd-tmp/, like the
+  // reference's deferred cleanup (labels.go:81-96); the old file stays.
+  char dir[] = "/tmp/gfd-write-XXXXXX";
+  EXPECT_TRUE(mkdtemp(dir) != nullptr);
+  std::string path = std::string(dir) + "/gfd";
+  lm::write_to_file({{"k", "old"}}, path);
+  struct rlimit old_limit;
+  ::getrlimit(RLIMIT_FSIZE, &old_limit);
+  struct rlimit small = old_limit;
+  small.rlim_cur = 64;
+  auto old_handler = ::signal(SIGXFSZ, SIG_IGN);
+  ::setrlimit(RLIMIT_FSIZE, &small);
+  std::string err;
+  try {
+    lm::write_to_file({{"k", std::string(4096, 'v')}}, path);
+  } catch (const std::exception& e) {
+    err = e.what();
+  }
+  ::setrlimit(RLIMIT_FSIZE, &old_limit);
+  ::signal(SIGXFSZ, old_handler);
+  EXPECT_TRUE(err.find("error writing temporary file") != std::string::npos);
+  EXPECT_FALSE(fs::exists(std::string(dir) + "/gfd-tmp"));
+  EXPECT_EQ(fs::read_file(path, 64).data, std::string("k=old\n"));
+  fs::remove_all(dir);
 }
 
 TEST(WriteToFile_RenameFailureLeavesNoTemporaries) {

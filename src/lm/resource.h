@@ -39,7 +39,6 @@ class ResourceLabeler {
   // product: non-empty parts joined by '-', spaces replaced, "-SHARED" if
   // replicated (>1) and not renamed (resource.go:159-176).
   Labels product_label(const std::vector<std::string>& parts) const;
-  Labels count_label(int count) const { return single("count", std::to_string(count)); }
   Labels replicas_label() const;
   Labels base_labels(int count, const std::vector<std::string>& parts) const;
 

@@ -212,14 +212,6 @@ MockManager& MockManager::with_error_on_init(std::string msg) {
   init_error = std::move(msg);
   return *this;
 }
-MockManager& MockManager::with_driver_version(std::string v) {
-  driver_version = std::move(v);
-  return *this;
-}
-MockManager& MockManager::with_runtime_version(RuntimeVersion v) {
-  runtime_version = v;
-  return *this;
-}
 
 // ---------------------------------------------------------------------------
 // Builders

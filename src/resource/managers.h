@@ -143,8 +143,6 @@ class MockManager : public Manager {
   std::string Name() const override { return "mock"; }
 
   MockManager& with_error_on_init(std::string msg);
-  MockManager& with_driver_version(std::string v);
-  MockManager& with_runtime_version(RuntimeVersion v);
 
   std::vector<DevicePtr> devices;
   std::optional<std::string> init_error;

@@ -22,7 +22,6 @@ class DynLib {
   // Try each candidate path in order (RTLD_LAZY | RTLD_LOCAL).  Returns false
   // and records the last dlerror() if none loads.
   bool open(const std::vector<std::string>& candidates);
-  bool is_open() const { return handle_ != nullptr; }
   void close();
 
   void* symbol(const char* name) const;

@@ -51,12 +51,6 @@ std::optional<std::string> read_trimmed(const std::string& path) {
   return str::trim(r.data);
 }
 
-std::string read_file_or_throw(const std::string& path) {
-  auto r = read_file(path);
-  if (!r.ok()) throw Error("open " + path + ": " + errno_str(r.err));
-  return r.data;
-}
-
 bool exists(const std::string& path) {
   struct stat st;
   return ::stat(path.c_str(), &st) == 0;
@@ -351,12 +345,6 @@ std::string resolve_in_root(const std::string& root, const std::string& rel) {
     push_path(target);
   }
   return path_of(cur);
-}
-
-std::string real_basename(const std::string& path) {
-  char buf[PATH_MAX];
-  if (!::realpath(path.c_str(), buf)) return {};
-  return basename(buf);
 }
 
 std::string join(const std::string& a, const std::string& b) {

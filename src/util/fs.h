@@ -24,8 +24,6 @@ struct ReadResult {
 ReadResult read_file(const std::string& path, size_t max_bytes = 1 << 20);
 // read_file + trim; nullopt on any error.
 std::optional<std::string> read_trimmed(const std::string& path);
-// Throws gfd::Error("<what> '<path>': <strerror>") on failure.
-std::string read_file_or_throw(const std::string& path);
 
 bool exists(const std::string& path);
 bool is_dir(const std::string& path);
@@ -127,8 +125,6 @@ AttrReader& attrs();
 
 // readlink(2); empty on failure.
 std::string read_link(const std::string& path);
-// Final path component of realpath(path), or empty.
-std::string real_basename(const std::string& path);
 // Resolve `rel` under `root` the way a process chrooted at `root` would:
 // component by component, following symlinks, with absolute link targets
 // re-rooted under `root` (a host's /opt/rocm -> /opt/rocm-7.2.0 seen through

@@ -48,9 +48,4 @@ void printf(const char* fmt, ...) {
   emit(buf, static_cast<size_t>(n));
 }
 
-void line(const std::string& msg) {
-  if (quiet()) return;
-  emit(msg.data(), msg.size());
-}
-
 }  // namespace gfd::log

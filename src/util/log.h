@@ -12,7 +12,6 @@ namespace gfd::log {
 
 // printf-style log line; a trailing newline is added if missing.
 void printf(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
-void line(const std::string& msg);
 
 // Silence all log output (used by the in-process benchmark binding so that
 // timing is not dominated by stderr writes).  Returns the previous setting.

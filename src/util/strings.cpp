@@ -20,13 +20,6 @@ std::string trim(std::string_view s) {
   return std::string(s.substr(b, e - b));
 }
 
-std::string trim_chars(std::string_view s, std::string_view chars) {
-  size_t b = 0, e = s.size();
-  while (b < e && chars.find(s[b]) != std::string_view::npos) ++b;
-  while (e > b && chars.find(s[e - 1]) != std::string_view::npos) --e;
-  return std::string(s.substr(b, e - b));
-}
-
 std::vector<std::string> split(std::string_view s, char sep) {
   std::vector<std::string> out;
   size_t start = 0;
@@ -85,9 +78,6 @@ std::string to_upper(std::string s) {
 }
 
 bool starts_with(std::string_view s, std::string_view p) { return s.size() >= p.size() && s.compare(0, p.size(), p) == 0; }
-bool ends_with(std::string_view s, std::string_view p) {
-  return s.size() >= p.size() && s.compare(s.size() - p.size(), p.size(), p) == 0;
-}
 
 std::optional<int64_t> parse_int(std::string_view sv, int base) {
   std::string s = trim(sv);

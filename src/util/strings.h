@@ -11,7 +11,6 @@
 namespace gfd::str {
 
 std::string trim(std::string_view s);
-std::string trim_chars(std::string_view s, std::string_view chars);
 std::vector<std::string> split(std::string_view s, char sep);
 std::vector<std::string> split_n(std::string_view s, char sep, size_t n);
 std::string join(const std::vector<std::string>& parts, std::string_view sep);
@@ -19,7 +18,6 @@ std::string replace_all(std::string s, std::string_view from, std::string_view t
 std::string to_lower(std::string s);
 std::string to_upper(std::string s);
 bool starts_with(std::string_view s, std::string_view prefix);
-bool ends_with(std::string_view s, std::string_view suffix);
 
 // Strict parses: the whole (trimmed) string must be consumed.
 std::optional<int64_t> parse_int(std::string_view s, int base = 10);

@@ -287,6 +287,25 @@ def test_chart_renders_offline_from_the_default_values(native):
     assert "12" in conf["sources"]["pci"]["deviceClassWhitelist"]
 
 
+def test_chart_takes_the_references_nfd_values(native):
+    """A values file written for the reference's chart names its bundled NFD
+    objects with nfd.nameOverride and nfd.master.serviceAccount.name
+    (deployments/helm/gpu-feature-discovery/values.yaml:68-74); the in-repo
+    NFD subchart takes both."""
+    docs = _render({"nfd": {"nameOverride": "node-feature-discovery",
+                            "master": {"serviceAccount": {"name": "node-feature-discovery"}}}})
+    names = {(d["kind"], d["metadata"]["name"]) for d in docs}
+    assert ("Deployment", "gfd-node-feature-discovery-master") in names
+    assert ("DaemonSet", "gfd-node-feature-discovery-worker") in names
+    assert ("ServiceAccount", "node-feature-discovery") in names
+    master = next(d for d in docs if d["kind"] == "Deployment")
+    assert master["spec"]["template"]["spec"]["serviceAccountName"] == "node-feature-discovery"
+    binding = next(d for d in docs if d["kind"] == "ClusterRoleBinding")
+    assert binding["subjects"][0]["name"] == "node-feature-discovery"
+    (worker,) = [d for d in docs if d["kind"] == "DaemonSet" and "worker" in d["metadata"]["name"]]
+    assert "-server=gfd-node-feature-discovery-master:8080" in worker["spec"]["template"]["spec"]["containers"][0]["args"]
+
+
 def test_chart_options_render(native):
     """nfd.deploy=false drops the subchart; a config file becomes a ConfigMap,
     a mount, GFD_CONFIG_FILE and a checksum annotation (pods restart when it

@@ -304,6 +304,10 @@ def test_chart_takes_the_references_nfd_values(native):
     assert binding["subjects"][0]["name"] == "node-feature-discovery"
     (worker,) = [d for d in docs if d["kind"] == "DaemonSet" and "worker" in d["metadata"]["name"]]
     assert "-server=gfd-node-feature-discovery-master:8080" in worker["spec"]["template"]["spec"]["containers"][0]["args"]
+    # The reference's extraLabelNs (nvidia.com) still lets amd.com through.
+    docs = _render({"nfd": {"master": {"extraLabelNs": ["nvidia.com"]}}})
+    args = next(d for d in docs if d["kind"] == "Deployment")["spec"]["template"]["spec"]["containers"][0]["args"]
+    assert "-extra-label-ns=nvidia.com" in args and "-extra-label-ns=amd.com" in args
 
 
 def test_chart_options_render(native):

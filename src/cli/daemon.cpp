@@ -272,7 +272,6 @@ struct ProcessTimeline {
 }  // namespace
 
 void start(const Context& ctx, SignalWatcher& sigs) {
-  bool swept = false;
   for (;;) {
     log::printf("Loading configuration.");
     config::Config c;
@@ -286,9 +285,10 @@ void start(const Context& ctx, SignalWatcher& sigs) {
     // A process killed without its exit cleanup (OOM, SIGKILL, node crash)
     // left its temporary files in <dir>/gfd-tmp: remove them before the
     // first write.  Loop mode only - a oneshot Job leaves the directory to
-    // the DaemonSet that may share it.
-    if (!swept && !c.oneshot() && !c.output_file().empty()) {
-      swept = true;
+    // the DaemonSet that may share it.  Every (re)start: a SIGHUP may have
+    // moved the output file to a directory a crashed daemon wrote to (the
+    // previous run's own gfd-tmp/ is already gone with its exit cleanup).
+    if (!c.oneshot() && !c.output_file().empty()) {
       try {
         lm::sweep_temp_dir(c.output_file());
       } catch (const std::exception& e) {

@@ -5,7 +5,7 @@ BUILD_DIR ?= build
 JOBS ?= $(shell nproc 2>/dev/null || echo 8)
 PYTHON ?= python3
 
-.PHONY: all build cmds test test-unit test-gpu coverage asan tsan fuzz bench fmt assert-fmt lint check-yamls image image-offline shell clean
+.PHONY: all build cmds test test-unit test-gpu coverage asan tsan fuzz bench fmt assert-fmt vet lint check-yamls image image-offline shell clean
 
 all: build
 
@@ -79,6 +79,15 @@ fmt:
 assert-fmt:
 	find src tests/unit python -name '*.cpp' -o -name '*.h' | xargs clang-format --dry-run --Werror
 
+# Static checks of the C++ (reference analogue: `go vet`, Makefile:102-103):
+# the whole tree built by clang with extra diagnostics, every warning an error.
+VET_FLAGS = -Werror -Wshadow -Wnon-virtual-dtor -Wnull-dereference -Wformat=2 -Wdeprecated -Wcomma -Wloop-analysis \
+  -Wunused-member-function -Wconditional-uninitialized -Wextra-semi -Wunreachable-code -Wimplicit-fallthrough
+vet:
+	cmake -S . -B build-vet -G Ninja -DCMAKE_BUILD_TYPE=Release -DCMAKE_CXX_COMPILER=$(FUZZ_CXX) \
+	  -DGFD_BUILD_PYTHON=OFF -DCMAKE_CXX_FLAGS="$(VET_FLAGS)"
+	cmake --build build-vet -j $(JOBS)
+
 LINT_PY = gpu_feature_discovery_amd tests tools bench.py __graft_entry__.py
 lint:
 	@if $(PYTHON) -c "import pyflakes" 2>/dev/null; then $(PYTHON) -m pyflakes $(LINT_PY); \
@@ -114,4 +123,4 @@ shell: .build-image
 	$(DOCKER) run --rm -ti -v $(CURDIR):/work -w /work --user $$(id -u):$$(id -g) -e HOME=/tmp $(BUILDIMAGE)
 
 clean:
-	rm -rf $(BUILD_DIR) build-asan build-tsan build-cov gpu_feature_discovery_amd/_gfd*.so
+	rm -rf $(BUILD_DIR) build-asan build-tsan build-cov build-vet gpu_feature_discovery_amd/_gfd*.so

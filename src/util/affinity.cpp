@@ -40,19 +40,24 @@ std::string l3_list(int cpu, const std::string& sys_root) {
 }  // namespace
 
 std::vector<int> l3_domain(int cpu, const std::string& sys_root) {
-  static std::mutex mu;
-  static std::map<std::pair<std::string, int>, std::vector<int>> known;
-  std::lock_guard<std::mutex> lk(mu);
-  auto key = std::make_pair(sys_root, cpu);
-  auto it = known.find(key);
-  if (it != known.end()) return it->second;
+  if (cpu < 0) return {};
+  std::vector<int> l3;
+  {
+    static std::mutex mu;
+    static std::map<std::pair<std::string, int>, std::vector<int>> known;
+    std::lock_guard<std::mutex> lk(mu);
+    auto key = std::make_pair(sys_root, cpu);
+    auto it = known.find(key);
+    if (it == known.end()) it = known.emplace(key, parse_cpu_list(l3_list(cpu, sys_root))).first;
+    l3 = it->second;
+  }
   std::vector<int> out;
   cpu_set_t allowed;
   CPU_ZERO(&allowed);
-  if (cpu >= 0 && sched_getaffinity(0, sizeof(allowed), &allowed) == 0)
-    for (int c : parse_cpu_list(l3_list(cpu, sys_root)))
+  if (sched_getaffinity(0, sizeof(allowed), &allowed) == 0)
+    for (int c : l3)
       if (CPU_ISSET(c, &allowed)) out.push_back(c);
-  return known.emplace(key, std::move(out)).first->second;
+  return out;
 }
 
 std::string pin_to_current_l3(const std::string& sys_root) {

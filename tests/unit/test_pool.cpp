@@ -12,11 +12,13 @@
 #include "util/affinity.h"
 #include "util/fs.h"
 #include "util/pool.h"
+#include "util/strings.h"
 
 using gfd::WorkerPool;
 namespace affinity = gfd::affinity;
 namespace fs = gfd::fs;
 namespace lm = gfd::lm;
+namespace str = gfd::str;
 
 TEST(Pool_ParallelForVisitsEveryIndexOnce) {
   WorkerPool pool(4);
@@ -171,6 +173,40 @@ TEST(Affinity_PinsToTheCurrentL3DomainWithinTheAllowedSet) {
   // Already within one domain: nothing changes.
   EXPECT_EQ(affinity::pin_to_current_l3(root), std::string(""));
   EXPECT_TRUE(sched_setaffinity(0, sizeof(before), &before) == 0);
+  fs::remove_all(root);
+}
+
+TEST(Affinity_L3DomainFollowsTheAllowedSetAsItChanges) {
+  // A cpuset changed under a running pod (CPU manager): the domain is the
+  // cached cache topology intersected with what the thread may use now.
+  cpu_set_t before;
+  CPU_ZERO(&before);
+  EXPECT_TRUE(sched_getaffinity(0, sizeof(before), &before) == 0);
+  if (CPU_COUNT(&before) < 2) return;
+  std::vector<int> allowed;
+  for (int c = 0; c < CPU_SETSIZE; ++c)
+    if (CPU_ISSET(c, &before)) allowed.push_back(c);
+  // One L3 shared by every allowed CPU.
+  char d[] = "/tmp/gfd-aff-XXXXXX";
+  EXPECT_TRUE(mkdtemp(d) != nullptr);
+  std::string root = d;
+  std::vector<std::string> names;
+  for (int c : allowed) names.push_back(std::to_string(c));
+  for (int c : allowed) {
+    std::string idx = root + "/sys/devices/system/cpu/cpu" + std::to_string(c) + "/cache/index3";
+    fs::mkdir_all(idx);
+    lm::write_file_atomically(idx + "/level", "3\n", 0644);
+    lm::write_file_atomically(idx + "/shared_cpu_list", str::join(names, ",") + "\n", 0644);
+  }
+  int cpu = allowed.front();
+  EXPECT_TRUE(affinity::l3_domain(cpu, root) == allowed);
+  cpu_set_t one;
+  CPU_ZERO(&one);
+  CPU_SET(allowed.back(), &one);
+  EXPECT_TRUE(sched_setaffinity(0, sizeof(one), &one) == 0);
+  EXPECT_TRUE(affinity::l3_domain(cpu, root) == std::vector<int>{allowed.back()});
+  EXPECT_TRUE(sched_setaffinity(0, sizeof(before), &before) == 0);
+  EXPECT_TRUE(affinity::l3_domain(cpu, root) == allowed);
   fs::remove_all(root);
 }
 

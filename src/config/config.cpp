@@ -303,7 +303,20 @@ Config parse_config_text(const std::string& text) {
         c.flags.mig_strategy = opt_string(field(*flags, "migStrategy"), "Config.flags.migStrategy");
         c.flags.fail_on_init_error = opt_bool(field(*flags, "failOnInitError"), "Config.flags.failOnInitError");
         c.flags.driver_root = opt_string(field(*flags, "driverRoot"), "Config.flags.driverRoot");
-        if (const Node* p = field(*flags, "plugin"); p && !p->is_null()) c.flags.plugin_present = true;
+        // A config file shared with the device plugin carries the plugin's
+        // keys too (vendored api/config/v1/flags.go:48-63).  They do not
+        // configure this daemon, but they are decoded and type-checked as the
+        // reference decodes them, so a file it rejects is rejected here.
+        (void)opt_string(field(*flags, "nvidiaDriverRoot"), "Config.flags.nvidiaDriverRoot");
+        (void)opt_bool(field(*flags, "gdsEnabled"), "Config.flags.gdsEnabled");
+        (void)opt_bool(field(*flags, "mofedEnabled"), "Config.flags.mofedEnabled");
+        if (const Node* p = field(*flags, "plugin"); p && !p->is_null()) {
+          require_map(*p, "Config.flags.plugin", "PluginCommandLineFlags");
+          (void)opt_bool(field(*p, "passDeviceSpecs"), "Config.flags.plugin.passDeviceSpecs");
+          (void)opt_string(field(*p, "deviceListStrategy"), "Config.flags.plugin.deviceListStrategy");
+          (void)opt_string(field(*p, "deviceIDStrategy"), "Config.flags.plugin.deviceIDStrategy");
+          c.flags.plugin_present = true;
+        }
         if (const Node* g = field(*flags, "gfd"); g && !g->is_null()) c.flags.gfd = decode_gfd_flags(*g);
       }
       if (const Node* res = field(root, "resources"); res && !res->is_null()) {

@@ -79,6 +79,39 @@ sharing:
   EXPECT_EQ(rs[1].devices.list, (std::vector<std::string>{"0", "1", "0:3"}));
 }
 
+TEST(Config_FileSharedWithTheDevicePlugin) {
+  // The reference README's config shared with the device plugin: the
+  // plugin's keys are accepted (and dropped) ...
+  Config c = parse_config_text(R"(
+version: v1
+flags:
+  migStrategy: "none"
+  failOnInitError: true
+  nvidiaDriverRoot: "/"
+  gdsEnabled: false
+  plugin:
+    passDeviceSpecs: false
+    deviceListStrategy: "envvar"
+    deviceIDStrategy: "uuid"
+  gfd:
+    oneshot: false
+    noTimestamp: false
+    outputFile: /etc/kubernetes/node-feature-discovery/features.d/gfd
+    sleepInterval: 60s
+)");
+  EXPECT_TRUE(c.flags.plugin_present);
+  EXPECT_EQ(*c.flags.gfd.sleep_interval, 60 * kSecond);
+  EXPECT_EQ(c.mig_strategy(), std::string("none"));
+  // ... and type-checked as the reference decodes them.
+  EXPECT_THROW_MSG(parse_config_text("flags:\n  plugin:\n    passDeviceSpecs: sometimes\n"),
+                   "Go struct field Config.flags.plugin.passDeviceSpecs of type bool");
+  EXPECT_THROW_MSG(parse_config_text("flags:\n  plugin: [envvar]\n"),
+                   "Go struct field Config.flags.plugin of type PluginCommandLineFlags");
+  EXPECT_THROW_MSG(parse_config_text("flags:\n  mofedEnabled: 1\n"), "Config.flags.mofedEnabled of type bool");
+  EXPECT_THROW_MSG(parse_config_text("flags:\n  nvidiaDriverRoot: {a: b}\n"),
+                   "Config.flags.nvidiaDriverRoot of type string");
+}
+
 TEST(Config_JsonFile) {
   Config c = parse_config_text(R"({"version":"v1","flags":{"migStrategy":"single","gfd":{"sleepInterval":5000000000}}})");
   EXPECT_EQ(*c.flags.mig_strategy, std::string("single"));

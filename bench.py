@@ -139,11 +139,12 @@ def _daemon_loop(binary: str, args: list[str], cycles: int, interval: str = "2ms
 
     p = subprocess.Popen([binary, f"--sleep-interval={interval}", "--trace-timing", *args], stdout=subprocess.DEVNULL,
                          stderr=subprocess.PIPE, text=True, env={**os.environ, **(env or {})})
-    totals, phases = [], {}
+    totals, phases, cpus = [], {}, []
     try:
         for line in p.stderr:
             if "Timing:" in line:
                 fields = dict(kv.split("=", 1) for kv in line.split("Timing:", 1)[1].split())
+                cpus.append(fields.pop("cpu", ""))
                 totals.append(float(fields["total"].rstrip("ms")))
                 if len(totals) > 1:
                     for k, v in fields.items():
@@ -157,9 +158,15 @@ def _daemon_loop(binary: str, args: list[str], cycles: int, interval: str = "2ms
         except subprocess.TimeoutExpired:
             p.kill()
     steady = totals[1:] or totals
+    # "start,end" CPU of each cycle's thread: where the scheduler woke it.
+    starts = [c.split(",")[0] for c in cpus if c]
     return {"interval": interval, "first_cycle_ms": round(totals[0], 3) if totals else None,
             "p50_ms": round(_percentile(steady, 0.5), 4), "p90_ms": round(_percentile(steady, 0.9), 4),
             "cycles": len(totals),
+            # Time no phase names (total minus the top-level phases).
+            "other_p50_ms": round(_percentile(phases.get("other", []), 0.5), 4),
+            "cycle_cpus": cpus,
+            "cpu_moves": sum(1 for a, b in zip(starts, starts[1:]) if a != b),
             "phases_p50_ms": {k: round(_percentile(v, 0.5), 4) for k, v in phases.items() if k != "total"}}
 
 

@@ -1,5 +1,6 @@
 #include "cli/daemon.h"
 
+#include <sched.h>
 #include <signal.h>
 #include <time.h>
 
@@ -123,7 +124,12 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
                         const config::Config& config, const lm::LabelerPtr& timestamp, bool write) {
   trace::begin_cycle();
   int64_t t0 = trace::now_ns();
-  WorkerPool::instance().follow_caller();  // --cpu-affinity=follow
+  CycleResult r;
+  r.cpu_start = sched_getcpu();
+  {
+    trace::Span span("placement");
+    WorkerPool::instance().follow_caller();  // --cpu-affinity=follow
+  }
   // Work that does not depend on the device backend runs on workers while
   // the backend enumerates: the node facts the device labeler needs after
   // enumeration (machine type, file-backed versions) and the SR-IOV bus scan
@@ -132,14 +138,20 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
   // the time it is needed runs on this thread instead (run_or_wait).  The
   // tasks never throw; an SR-IOV error is handed back and raised after the
   // device labeler.
-  std::optional<resource::VersionSources> version_files = manager.VersionFiles();
+  std::optional<resource::VersionSources> version_files;
+  {
+    trace::Span span("versions");
+    version_files = manager.VersionFiles();
+  }
   lm::NodeFacts facts;
   lm::Labels sriov_labels;
   std::exception_ptr sriov_error;
   int64_t facts_ns = 0, sriov_ns = 0, facts_start = 0, submitted = 0;
+
   std::function<void()> read_facts = [&] {
     int64_t s0 = trace::now_ns();
     facts_start = s0;
+    r.cpu_facts = sched_getcpu();
     try {
       facts = lm::ReadNodeFacts(config, version_files);
     } catch (...) {
@@ -161,11 +173,15 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
   // Loop mode: the same worker then unlinks the old feature file and creates
   // the temporary file of a later cycle's write (lm::temp_preparer) - never
   // waited for, so it runs after the two even if this thread took them over.
-  std::vector<std::function<void()>> fns{read_facts, scan_sriov};
-  if (write && !config.oneshot())
-    if (auto prepare = lm::temp_preparer(config.output_file())) fns.push_back(std::move(prepare));
-  submitted = trace::now_ns();
-  auto seq = WorkerPool::instance().submit_sequence(std::move(fns));
+  std::vector<WorkerPool::Task> seq;
+  {
+    trace::Span span("submit");
+    std::vector<std::function<void()>> fns{read_facts, scan_sriov};
+    if (write && !config.oneshot())
+      if (auto prepare = lm::temp_preparer(config.output_file())) fns.push_back(std::move(prepare));
+    submitted = trace::now_ns();
+    seq = WorkerPool::instance().submit_sequence(std::move(fns));
+  }
   WorkerPool::Task facts_task = seq[0], sriov_task = seq[1];
   auto join_facts = [&]() -> const lm::NodeFacts& {
     facts_task.run_or_wait();
@@ -180,13 +196,13 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
     sriov_task.cancel_or_wait();
     throw;
   }
-  facts_task.cancel_or_wait();  // no devices: the labeler never needed them
   int64_t j0 = trace::now_ns();
+  facts_task.cancel_or_wait();  // no devices: the labeler never needed them
   sriov_task.run_or_wait();
   // Where an overlapped cycle waits: how long after the hand-off the node
   // facts started (a worker's wake-up, or this thread taking them over),
   // and how long this thread then waited for the SR-IOV scan.
-  trace::record("sriov.join", trace::now_ns() - j0);
+  trace::record_top("sriov.join", trace::now_ns() - j0);
   trace::record("facts.start", facts_start ? facts_start - submitted : 0);
   trace::record("facts(overlapped)", facts_ns);
   trace::record("sriov(overlapped)", sriov_ns);
@@ -197,16 +213,22 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
       throw Error(std::string("error generating labels: ") + e.what());
     }
   }
-  lm::LabelerPtr labelers = lm::merge({timestamp, device, lm::from_labels(std::move(sriov_labels))});
-  CycleResult r;
-  try {
-    r.labels = labelers->GetLabels();
-  } catch (const std::exception& e) {
-    throw Error(std::string("error generating labels: ") + e.what());
+  {
+    trace::Span span("merge");
+    lm::LabelerPtr labelers = lm::merge({timestamp, device, lm::from_labels(std::move(sriov_labels))});
+    try {
+      r.labels = labelers->GetLabels();
+    } catch (const std::exception& e) {
+      throw Error(std::string("error generating labels: ") + e.what());
+    }
+    device.reset();
   }
   if (r.labels.size() <= 1) log::printf("Warning: no labels generated from any source");
   if (write) {
-    log::printf("Writing labels to output file");
+    {
+      trace::Span span("log");
+      log::printf("Writing labels to output file");
+    }
     trace::Span span("write");
     try {
       lm::write_to_file(r.labels, config.output_file());
@@ -215,7 +237,9 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
     }
   }
   r.total_ns = trace::now_ns() - t0;
+  r.other_ns = r.total_ns - trace::top_level_ns();
   r.phases = trace::phases();
+  r.cpu_end = sched_getcpu();
   return r;
 }
 
@@ -237,7 +261,8 @@ bool run(resource::Manager& manager, const std::shared_ptr<sriov::Interface>& sr
   lm::LabelerPtr timestamp = lm::NewTimestampLabeler(config);
   for (;;) {
     CycleResult r = label_cycle(manager, sriov, config, timestamp, true);
-    if (config.trace_timing()) log::printf("Timing: %s", trace::summary(r.total_ns).c_str());
+    if (config.trace_timing())
+      log::printf("Timing: %s cpu=%d,%d,%d", trace::summary(r.total_ns).c_str(), r.cpu_start, r.cpu_end, r.cpu_facts);
     if (config.oneshot()) return false;
 
     log::printf("Sleeping for %s", format_duration(config.sleep_interval()).c_str());

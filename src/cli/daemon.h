@@ -39,7 +39,11 @@ class SignalWatcher {
 struct CycleResult {
   lm::Labels labels;
   int64_t total_ns = 0;
+  int64_t other_ns = 0;  // total minus the top-level phases (unattributed)
   std::vector<trace::Phase> phases;
+  // CPU the cycle thread started / ended on, and the one the node facts ran
+  // on (a worker's, or the cycle thread's if it took them over).
+  int cpu_start = -1, cpu_end = -1, cpu_facts = -1;
 };
 
 // One labeling cycle: build labelers (device + SR-IOV), merge with the

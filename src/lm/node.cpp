@@ -188,6 +188,7 @@ class ShutdownGuard {
  public:
   explicit ShutdownGuard(resource::Manager& m) : m_(m) {}
   ~ShutdownGuard() {
+    trace::Span span("shutdown");
     try {
       m_.Shutdown();
     } catch (const std::exception& e) {

@@ -1,0 +1,136 @@
+#include "sriov/bound.h"
+
+#include <algorithm>
+#include <set>
+
+#include "util/error.h"
+#include "util/fs.h"
+#include "util/strings.h"
+#include "util/trace.h"
+
+namespace gfd::sriov {
+
+namespace {
+
+// "DDDD:BB:DD.F" (a driver directory also holds bind, unbind, new_id,
+// module, uevent...).
+bool is_pci_address(const std::string& name) {
+  size_t n = name.size();
+  if (n < 12 || name[n - 2] != '.' || name[n - 5] != ':' || name[n - 8] != ':') return false;
+  for (size_t i = 0; i < n; ++i) {
+    if (i == n - 2 || i == n - 5 || i == n - 8) continue;
+    char c = name[i];
+    if (!((c >= '0' && c <= '9') || (c >= 'a' && c <= 'f') || (c >= 'A' && c <= 'F'))) return false;
+  }
+  return true;
+}
+
+// The function at `dir` as SysfsAmdPCI reports it, or nullopt when it is not
+// a display (0x03) or processing-accelerator (0x12) function.  Every function
+// reached here is AMD's: amdgpu's and gim's ID tables name vendor 0x1002 only,
+// and a PF's VFs carry its vendor.
+std::optional<PCIDevice> read_function(const std::string& dir, const std::string& addr, const std::string& physfn) {
+  auto cls = fs::read_file(fs::join(dir, "class"), 64);
+  if (!cls.ok()) throw Error("unable to read PCI device class for " + addr + ": " + fs::errno_str(cls.err));
+  std::string c = str::trim(cls.data);
+  if (!str::starts_with(c, "0x03") && !str::starts_with(c, "0x12")) return std::nullopt;
+  PCIDevice d;
+  d.path = dir;
+  d.address = addr;
+  d.vendor = kAmdVendorId;
+  d.class_code = c.substr(0, 4);
+  d.device = fs::read_trimmed(fs::join(dir, "device")).value_or("");
+  if (auto t = fs::read_trimmed(fs::join(dir, "sriov_totalvfs")))
+    d.sriov_totalvfs = static_cast<int>(str::parse_uint(*t).value_or(0));
+  if (d.sriov_totalvfs == 0) {
+    d.sriov_numvfs = 0;  // SR-IOV capable in name only
+  } else if (d.sriov_totalvfs > 0) {
+    if (auto n = fs::read_trimmed(fs::join(dir, "sriov_numvfs")))
+      d.sriov_numvfs = static_cast<int>(str::parse_uint(*n).value_or(0));
+    if (d.sriov_numvfs > 0) d.sriov_vf_device = fs::read_trimmed(fs::join(dir, "sriov_vf_device")).value_or("");
+  }
+  if (!physfn.empty()) {
+    d.physfn = physfn;
+  } else {
+    std::string link = fs::read_link(fs::join(dir, "physfn"));
+    if (!link.empty()) d.physfn = fs::basename(link);
+  }
+  // Configuration space only where sysfs publishes no SR-IOV state.
+  if (d.sriov_totalvfs < 0 && d.physfn.empty()) {
+    auto cfg = fs::read_file(fs::join(dir, "config"), kPciExpressConfigSpaceSize);
+    if (!cfg.ok()) throw Error("unable to read PCI configuration space for " + addr + ": " + fs::errno_str(cfg.err));
+    d.config = std::move(cfg.data);
+  }
+  return d;
+}
+
+}  // namespace
+
+const std::vector<std::string>& BoundAmdPCI::drivers() {
+  static const std::vector<std::string> names{"amdgpu", "gim"};
+  return names;
+}
+
+std::vector<PCIDevice> BoundAmdPCI::scan_bound(const std::vector<std::string>& bound) {
+  std::string devices = fs::join(root_, kPciDevicesRoot);
+  std::vector<PCIDevice> out;
+  std::set<std::string> seen(bound.begin(), bound.end());
+  std::vector<std::pair<std::string, std::string>> vfs;  // VF address, its PF
+  for (const auto& addr : bound) {
+    std::string dir = fs::join(devices, addr);
+    auto d = read_function(dir, addr, "");
+    if (!d) continue;
+    if (d->sriov_numvfs > 0) {
+      // The PF's enabled VFs, bound to whatever hands them to VMs (or
+      // nothing): "virtfn0" -> "../0000:d9:00.1".
+      for (const auto& e : fs::list_dir(dir)) {
+        if (e.rfind("virtfn", 0) != 0) continue;
+        std::string vf = fs::basename(fs::read_link(fs::join(dir, e)));
+        if (is_pci_address(vf) && seen.insert(vf).second) vfs.emplace_back(vf, addr);
+      }
+    }
+    out.push_back(std::move(*d));
+  }
+  for (const auto& [vf, pf] : vfs)
+    if (auto d = read_function(fs::join(devices, vf), vf, pf)) out.push_back(std::move(*d));
+  std::sort(out.begin(), out.end(), [](const PCIDevice& a, const PCIDevice& b) { return a.address < b.address; });
+  return out;
+}
+
+std::vector<PCIDevice> BoundAmdPCI::Devices() {
+  int64_t t0 = trace::now_ns();
+  // A booted kernel has sent thousands of uevents; "" or "0" is an emulated
+  // sysfs that never counts, and is not trusted.
+  auto seqnum = fs::attrs().read_trimmed(fs::join(root_, "sys/kernel/uevent_seqnum"));
+  if (seqnum && (seqnum->empty() || *seqnum == "0")) seqnum.reset();
+  if (have_ && seqnum && *seqnum == seqnum_) {
+    trace::record("pci.bound(kept)", trace::now_ns() - t0);
+    return fell_back_ && fallback_ ? fallback_->Devices() : last_;
+  }
+  std::vector<std::string> bound;
+  for (const auto& drv : drivers())
+    for (auto& name : fs::list_dir(fs::join(root_, "sys/bus/pci/drivers/" + drv)))
+      if (is_pci_address(name)) bound.push_back(std::move(name));
+  std::sort(bound.begin(), bound.end());
+  bound.erase(std::unique(bound.begin(), bound.end()), bound.end());
+  trace::record("pci.drivers", trace::now_ns() - t0);
+  std::vector<PCIDevice> out;
+  if (bound.empty()) {
+    // Nothing bound: a guest whose amdgpu is not loaded still shows its VF
+    // on the bus.
+    fell_back_ = true;
+    last_.clear();
+    if (fallback_) out = fallback_->Devices();
+  } else {
+    int64_t t1 = trace::now_ns();
+    out = scan_bound(bound);
+    trace::record("pci.bound", trace::now_ns() - t1);
+    fell_back_ = false;
+    last_ = out;
+  }
+  have_ = true;
+  seqnum_ = seqnum.value_or("");
+  return out;
+}
+
+}  // namespace gfd::sriov

@@ -1,0 +1,59 @@
+// SR-IOV discovery through the drivers that bind AMD GPU functions.
+//
+// Reference: internal/vgpu/pciutil.go:70-112 lists every function on the PCI
+// bus and reads the vendor of each - 367 functions on an 8xMI355X host, most
+// of a oneshot Job's cycle (~1 ms cold, profiles/oneshot_breakdown_r3.txt).
+// The functions that matter are far fewer and the kernel already knows
+// them: every AMD GPU function a node uses is bound to amdgpu (bare metal, a
+// passthrough guest, an SR-IOV guest's VF) or, on an MxGPU host, its physical
+// functions to the GIM host driver, whose enabled VFs are the PF's
+// `virtfn<N>` links.  So this source lists
+//   <root>/sys/bus/pci/drivers/{amdgpu,gim}/<address>
+// reads the identity and SR-IOV attributes of those functions only (about
+// six small sysfs reads per GPU), adds the VFs their `virtfn*` links name,
+// and returns them in the same form as the full-bus scan (SysfsAmdPCI), so
+// sriov::Lib classifies them identically.
+//
+// When neither driver binds anything - an SR-IOV guest whose amdgpu is not
+// loaded, or a node without AMD GPUs - it falls back to the full-bus scan.
+// Not seen without the fallback: an AMD function bound to some other driver
+// (vfio-pci, say) that is itself a PF with VFs enabled; GIM hosts bind their
+// PFs to gim.
+//
+// Like the full scan, the result is kept while /sys/kernel/uevent_seqnum is
+// unchanged: binding, unbinding, adding or removing a function (VFs
+// included, so any NumVFs change) sends a uevent.
+#pragma once
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "sriov/pci.h"
+
+namespace gfd::sriov {
+
+class BoundAmdPCI : public AmdPCI {
+ public:
+  // `fallback`: the full-bus scan used when no function is bound (may be null:
+  // then nothing is reported in that case).
+  explicit BoundAmdPCI(std::string root = "/", std::shared_ptr<AmdPCI> fallback = nullptr)
+      : root_(std::move(root)), fallback_(std::move(fallback)) {}
+  std::vector<PCIDevice> Devices() override;
+  // Whether the last Devices() came from the fallback scan.
+  bool used_fallback() const { return fell_back_; }
+
+  // The drivers whose bound functions are the node's AMD GPU functions.
+  static const std::vector<std::string>& drivers();
+
+ private:
+  std::vector<PCIDevice> scan_bound(const std::vector<std::string>& bound);
+  std::string root_;
+  std::shared_ptr<AmdPCI> fallback_;
+  bool have_ = false;
+  bool fell_back_ = false;
+  std::string seqnum_;  // /sys/kernel/uevent_seqnum of the kept result
+  std::vector<PCIDevice> last_;
+};
+
+}  // namespace gfd::sriov

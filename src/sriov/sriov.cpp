@@ -1,5 +1,7 @@
 #include "sriov/sriov.h"
 
+#include "sriov/bound.h"
+
 #include "resource/pci_ids.h"
 #include "util/error.h"
 #include "util/strings.h"
@@ -96,7 +98,9 @@ class EmptyLib : public Interface {
 }  // namespace
 
 std::shared_ptr<Interface> new_sriov_lib(const std::string& root) {
-  return std::make_shared<Lib>(std::make_shared<SysfsAmdPCI>(root), root);
+  // The functions amdgpu / gim bind, and the VFs of those PFs; the whole bus
+  // only when neither binds anything (sriov/bound.h).
+  return std::make_shared<Lib>(std::make_shared<BoundAmdPCI>(root, std::make_shared<SysfsAmdPCI>(root)), root);
 }
 
 std::shared_ptr<Interface> new_mock_sriov() { return std::make_shared<Lib>(std::make_shared<MockAmdPCI>()); }

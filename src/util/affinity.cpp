@@ -4,6 +4,7 @@
 
 #include <map>
 #include <mutex>
+#include <optional>
 #include <utility>
 #include <vector>
 
@@ -26,18 +27,80 @@ std::vector<int> parse_cpu_list(const std::string& s) {
 }
 
 namespace {
-// "0-7,128-135" of the L3 cache of `cpu` (the cache index whose level is 3:
-// index3 on x86, but look), or "".
-std::string l3_list(int cpu, const std::string& sys_root) {
-  std::string base = fs::join(sys_root, "sys/devices/system/cpu/cpu" + std::to_string(cpu) + "/cache");
+
+std::string cache_dir(const std::string& sys_root, int cpu) {
+  return fs::join(sys_root, "sys/devices/system/cpu/cpu" + std::to_string(cpu) + "/cache");
+}
+
+// The cache index directory ("index3" on x86) whose level is 3, or "".
+std::string l3_index(const std::string& base) {
   for (const auto& idx : fs::list_dir(base)) {
     if (idx.rfind("index", 0) != 0) continue;
-    if (fs::read_trimmed(fs::join(base, idx + "/level")).value_or("") == "3")
-      return fs::read_trimmed(fs::join(base, idx + "/shared_cpu_list")).value_or("");
+    if (fs::read_trimmed(fs::join(base, idx + "/level")).value_or("") == "3") return idx;
   }
   return "";
 }
+
+// "0-7,128-135" of the L3 cache of `cpu`, or "".
+std::string l3_list(int cpu, const std::string& sys_root) {
+  std::string base = cache_dir(sys_root, cpu);
+  std::string idx = l3_index(base);
+  return idx.empty() ? "" : fs::read_trimmed(fs::join(base, idx + "/shared_cpu_list")).value_or("");
+}
+
 }  // namespace
+
+L3Map L3Map::read(const std::string& sys_root) {
+  L3Map m;
+  std::vector<int> cpus = parse_cpu_list(
+      fs::read_trimmed(fs::join(sys_root, "sys/devices/system/cpu/online")).value_or(""));
+  std::string idx;  // the L3's index name, found once (the same on every CPU of a host)
+  for (int cpu : cpus) {
+    if (static_cast<size_t>(cpu) < m.domain_of_.size() && m.domain_of_[cpu] >= 0) continue;
+    std::string base = cache_dir(sys_root, cpu);
+    std::optional<std::string> list;
+    if (!idx.empty()) list = fs::read_trimmed(fs::join(base, idx + "/shared_cpu_list"));
+    if (!list) {  // first CPU, or one whose index layout differs
+      idx = l3_index(base);
+      if (idx.empty()) continue;
+      list = fs::read_trimmed(fs::join(base, idx + "/shared_cpu_list"));
+    }
+    std::vector<int> members = parse_cpu_list(list.value_or(""));
+    if (members.empty()) continue;
+    int id = static_cast<int>(m.domains_.size());
+    for (int c : members) {
+      if (static_cast<size_t>(c) >= m.domain_of_.size()) m.domain_of_.resize(static_cast<size_t>(c) + 1, -1);
+      m.domain_of_[c] = id;
+    }
+    m.domains_.push_back(std::move(members));
+  }
+  return m;
+}
+
+int L3Map::id(int cpu) const {
+  if (cpu < 0 || static_cast<size_t>(cpu) >= domain_of_.size()) return -1;
+  return domain_of_[cpu];
+}
+
+const std::vector<int>& L3Map::cpus(int id) const {
+  static const std::vector<int> none;
+  return id >= 0 && static_cast<size_t>(id) < domains_.size() ? domains_[id] : none;
+}
+
+const L3Map& L3Map::host() {
+  static const L3Map m = read("/");
+  return m;
+}
+
+std::vector<int> allowed_subset(const std::vector<int>& cpus) {
+  std::vector<int> out;
+  cpu_set_t allowed;
+  CPU_ZERO(&allowed);
+  if (sched_getaffinity(0, sizeof(allowed), &allowed) == 0)
+    for (int c : cpus)
+      if (CPU_ISSET(c, &allowed)) out.push_back(c);
+  return out;
+}
 
 std::vector<int> l3_domain(int cpu, const std::string& sys_root) {
   if (cpu < 0) return {};
@@ -51,13 +114,7 @@ std::vector<int> l3_domain(int cpu, const std::string& sys_root) {
     if (it == known.end()) it = known.emplace(key, parse_cpu_list(l3_list(cpu, sys_root))).first;
     l3 = it->second;
   }
-  std::vector<int> out;
-  cpu_set_t allowed;
-  CPU_ZERO(&allowed);
-  if (sched_getaffinity(0, sizeof(allowed), &allowed) == 0)
-    for (int c : l3)
-      if (CPU_ISSET(c, &allowed)) out.push_back(c);
-  return out;
+  return allowed_subset(l3);
 }
 
 std::string pin_to_current_l3(const std::string& sys_root) {

@@ -55,20 +55,46 @@ void WorkerPool::ensure_workers(size_t n) {
 }
 
 void WorkerPool::set_follow(bool on) {
+  const affinity::L3Map* map = on ? &affinity::L3Map::host() : nullptr;
   std::lock_guard<std::mutex> g(mu_);
-  follow_ = on;
+  follow_.store(on);
+  l3_ = map;
+  domain_id_.store(-1);
+  if (!on && !domain_.empty()) unpin_locked();
+}
+
+void WorkerPool::unpin_locked() {
+  // Back to wherever the caller may run (the process's placement).
+  cpu_set_t allowed;
+  CPU_ZERO(&allowed);
+  if (sched_getaffinity(0, sizeof(allowed), &allowed) == 0)
+    for (auto& t : threads_) pthread_setaffinity_np(t.native_handle(), sizeof(allowed), &allowed);
+  domain_.clear();
 }
 
 void WorkerPool::follow_caller() {
-  {
-    std::lock_guard<std::mutex> g(mu_);
-    if (!follow_) return;
-  }
-  std::vector<int> domain = affinity::l3_domain(sched_getcpu());
+  if (!follow_.load(std::memory_order_relaxed)) return;
+  // The common case - the cycle woke on the L3 domain it last ran on - is a
+  // vDSO getcpu and a table lookup.
+  int cpu = sched_getcpu();
   std::lock_guard<std::mutex> g(mu_);
-  if (domain.empty() || domain == domain_) return;
+  if (!l3_) return;
+  int id = l3_->id(cpu);
+  if (id < 0 || id == domain_id_.load(std::memory_order_relaxed)) return;
+  domain_id_.store(id, std::memory_order_relaxed);
+  std::vector<int> domain = affinity::allowed_subset(l3_->cpus(id));
+  if (domain.size() < 2) {
+    // A pod whose cpuset holds one CPU of this L3: pinning would put every
+    // lane on that core.  Leave the workers to the scheduler.
+    if (domain_.empty()) return;
+    unpin_locked();
+    ++repins_;
+    return;
+  }
+  if (domain == domain_) return;
   domain_ = std::move(domain);
   for (auto& t : threads_) pin(t, domain_);
+  ++repins_;
 }
 
 void WorkerPool::wake_one() {

@@ -22,6 +22,8 @@
 #include <thread>
 #include <vector>
 
+#include "util/affinity.h"
+
 namespace gfd {
 
 class WorkerPool {
@@ -77,10 +79,16 @@ class WorkerPool {
 
   // Workers follow the caller: follow_caller() (called by the thread about
   // to hand out work) keeps every worker on the CPUs that share the L3 cache
-  // of the CPU the caller runs on, re-pinning them only when that changed.
-  // The caller is left where the scheduler put it.  Off until enabled.
+  // of the CPU the caller runs on, re-pinning them only when that domain
+  // changed.  The caller is left where the scheduler put it.  Off until
+  // enabled; set_follow(true) reads the host's L3 map (once per process),
+  // so a cycle only looks its CPU up.  A domain of which fewer than two CPUs
+  // are allowed is not pinned to (every lane on one core).  set_follow(false)
+  // returns pinned workers to the caller's allowed set.
   void set_follow(bool on);
   void follow_caller();
+  // Re-pins done by follow_caller (tests / benchmarks).
+  size_t repins() const { return repins_.load(std::memory_order_relaxed); }
 
  private:
   struct Worker {
@@ -88,6 +96,7 @@ class WorkerPool {
     bool woken = false;  // set by wake_one (guarded by mu_)
   };
   void ensure_workers(size_t n);
+  void unpin_locked();  // caller holds mu_
   void wake_one();
   void loop(Worker* w);
 
@@ -100,8 +109,11 @@ class WorkerPool {
   size_t waking_ = 0;          // woken, not yet running
   size_t spawning_ = 0;        // threads created but not yet parked
   bool stop_ = false;
-  bool follow_ = false;
+  std::atomic<bool> follow_{false};
+  const affinity::L3Map* l3_ = nullptr;  // set with follow_
+  std::atomic<int> domain_id_{-1};        // L3 domain the workers follow (-1: none yet)
   std::vector<int> domain_;  // CPUs the workers are kept on (follow mode; empty: anywhere)
+  std::atomic<size_t> repins_{0};
 };
 
 // Lanes for per-GPU work in one cycle: one GPU per lane, at most 8 (the

@@ -6,10 +6,14 @@ namespace gfd::trace {
 
 namespace {
 thread_local std::vector<Phase> t_phases;
+thread_local int64_t t_top_ns = 0;
+thread_local int t_depth = 0;
 // Only threads that run labeling cycles record; spans executed on pool
 // workers would otherwise accumulate forever.
 thread_local bool t_active = false;
-}
+}  // namespace
+
+int& detail::depth() { return t_depth; }
 
 int64_t now_ns() {
   return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
@@ -18,12 +22,19 @@ int64_t now_ns() {
 
 void begin_cycle() {
   t_phases.clear();
+  t_top_ns = 0;
   t_active = true;
 }
 const std::vector<Phase>& phases() { return t_phases; }
 void record(const std::string& name, int64_t ns) {
   if (t_active) t_phases.emplace_back(name, ns);
 }
+void record_top(const std::string& name, int64_t ns) {
+  if (!t_active) return;
+  t_phases.emplace_back(name, ns);
+  t_top_ns += ns;
+}
+int64_t top_level_ns() { return t_top_ns; }
 
 std::string summary(int64_t total_ns) {
   std::string out;
@@ -32,7 +43,9 @@ std::string summary(int64_t total_ns) {
     snprintf(buf, sizeof(buf), "%s=%.3fms ", p.first.c_str(), static_cast<double>(p.second) / 1e6);
     out += buf;
   }
-  snprintf(buf, sizeof(buf), "total=%.3fms", static_cast<double>(total_ns) / 1e6);
+  int64_t other = total_ns - t_top_ns;
+  snprintf(buf, sizeof(buf), "other=%.3fms total=%.3fms", static_cast<double>(other) / 1e6,
+           static_cast<double>(total_ns) / 1e6);
   out += buf;
   return out;
 }

@@ -29,7 +29,7 @@ def check(text: str, strategy: str) -> None:
     """The labels against the regex golden of what the node is: an
     unpartitioned node gets the full-GPU set under every strategy (plus the
     strategy label under single/mixed); a partitioned one under `single`
-    the partition-single golden, under `mixed` per-profile resources."""
+    the node partition-single golden, under `mixed` per-profile resources."""
     labels = golden.parse_labels(text)
     assert labels.get("amd.com/partition.strategy", "none") == strategy, labels
     partitioned = labels.get("amd.com/gpu.compute-partition", "SPX") != "SPX"
@@ -38,7 +38,9 @@ def check(text: str, strategy: str) -> None:
         golden.check_regex_golden(text, REPO / "tests" / "expected-output.txt",
                                   select=lambda ln: not_sriov(ln) and not ln.startswith("amd.com/partition.strategy="))
     elif strategy == "single":
-        golden.check_regex_golden(text, REPO / "tests" / "expected-output-partition-single.txt", select=not_sriov)
+        # The node golden: a real node keeps its ISA/topology labels (the
+        # mock fixture's expected-output-partition-single.txt has none).
+        golden.check_regex_golden(text, REPO / "tests" / "expected-output-partition-single-node.txt", select=not_sriov)
     else:
         per_profile = re.compile(r"amd\.com/partition-[a-z]+\.[0-9]+xcd\.[0-9]+gb\.(product|count|replicas|memory|"
                                  r"compute-units|xcds|compute-partition|memory-partition|engines\.[a-z]+)=[A-Za-z0-9_.-]+")

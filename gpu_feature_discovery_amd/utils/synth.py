@@ -62,6 +62,10 @@ class GpuSpec:
     # Partition indices whose KFD nodes the container may read (None: all),
     # e.g. [3] for a pod that was allocated one CPX partition.
     visible_partitions: list[int] | None = None
+    # PCI driver bound to the function (sys/bus/pci/drivers/<driver>/<bdf>):
+    # "auto" = gim for an SR-IOV PF on a GIM host, else amdgpu; None = none
+    # (a guest whose amdgpu is not loaded).
+    driver: str | None = "auto"
 
 
 @dataclass
@@ -249,6 +253,15 @@ def make_node(root: str | os.PathLike, spec: NodeSpec) -> Path:
             for res, total in (("xcc", g.xcds), ("dma", 16), ("dec", 4), ("jpeg", 32)):
                 _write(d / f"compute_partition_config/{res}/num_inst", f"{max(1, total // parts)}\n")
                 _write(d / f"compute_partition_config/{res}/num_shared", f"{max(1, parts // total)}\n")
+        driver = g.driver
+        if driver == "auto":
+            driver = "gim" if g.sriov and spec.gim_version else "amdgpu"
+        if driver:
+            drv = root / "sys/bus/pci/drivers" / driver
+            drv.mkdir(parents=True, exist_ok=True)
+            for f in ("bind", "unbind", "new_id", "remove_id", "uevent"):
+                (drv / f).touch()
+            (drv / bdf).symlink_to(f"../../devices/{bdf}")
         for v in range(sriov.get("num", 0)):
             vf_bdf = f"0000:{bus:02x}:00.{v + 1}"
             vd = root / "sys/bus/pci/devices" / vf_bdf
@@ -257,6 +270,7 @@ def make_node(root: str | os.PathLike, spec: NodeSpec) -> Path:
             _write(vd / "class", "0x120000\n")
             _write(vd / "config", config_space(sriov.get("vf_device", 0x75B3), None, 4096 if spec.privileged else 64))
             (vd / "physfn").symlink_to(f"../{bdf}")
+            (d / f"virtfn{v}").symlink_to(f"../{vf_bdf}")
     # An unrelated non-AMD PCI function (the scanner must skip it).
     other = root / "sys/bus/pci/devices/0000:00:00.0"
     _write(other / "vendor", "0x1022\n")

@@ -3,6 +3,7 @@
 // PCIe SR-IOV.
 #include "lm/labels.h"
 #include "lm/node.h"
+#include "sriov/bound.h"
 #include "sriov/pci.h"
 #include "sriov/sriov.h"
 #include "test.h"
@@ -618,5 +619,122 @@ TEST(Sriov_FailedScanLeavesStateForTheNextOne) {
   auto devs = pci.Devices();
   EXPECT_EQ(devs.size(), static_cast<size_t>(6));
   for (const auto& d : devs) EXPECT_EQ(d.device, std::string("0x75a3"));
+  fs::remove_all(root);
+}
+
+// ---------------------------------------------------------------------------
+// Driver-directed discovery (sriov/bound.h)
+
+namespace {
+void bind_driver(const std::string& root, const std::string& driver, const std::string& bdf) {
+  std::string dir = root + "/sys/bus/pci/drivers/" + driver;
+  fs::mkdir_all(dir);
+  put_file(dir + "/bind", "");
+  put_file(dir + "/unbind", "");
+  if (symlink(("../../devices/" + bdf).c_str(), (dir + "/" + bdf).c_str()) != 0) throw std::runtime_error("symlink");
+}
+
+// pci_host() as a GIM host binds it: the 4 plain PFs to amdgpu, the PF with
+// VFs to gim, its VFs named by virtfn links (and bound to nothing).
+std::string bound_host(int filler, int vfs) {
+  std::string root = pci_host(filler, vfs);
+  for (int g = 0; g < 4; ++g) bind_driver(root, "amdgpu", str::format("0000:%02x:00.0", 0x11 + 0x10 * g));
+  bind_driver(root, "gim", "0000:c1:00.0");
+  std::string pf = root + "/sys/bus/pci/devices/0000:c1:00.0/";
+  for (int v = 0; v < vfs; ++v)
+    if (symlink(str::format("../0000:c1:00.%d", v + 1).c_str(), (pf + "virtfn" + std::to_string(v)).c_str()) != 0)
+      throw std::runtime_error("symlink");
+  return root;
+}
+
+std::string describe(const std::vector<PCIDevice>& devs) {
+  std::string out;
+  for (const auto& d : devs)
+    out += d.address + " " + d.vendor + " " + d.device + " " + d.class_code + " " + std::to_string(d.sriov_totalvfs) +
+           " " + std::to_string(d.sriov_numvfs) + " " + d.sriov_vf_device + " " + d.physfn + " cfg" +
+           std::to_string(d.config.size()) + "\n";
+  return out;
+}
+}  // namespace
+
+TEST(Bound_SameFunctionsAsTheFullBusScan) {
+  // The full scan reads 300 + 9 functions; the bound scan 5 + 3 VFs - and
+  // both hand sriov::Lib the same functions, field for field.
+  std::string root = bound_host(300, 3);
+  BoundAmdPCI bound(root);
+  SysfsAmdPCI full(root);
+  auto b = bound.Devices();
+  EXPECT_FALSE(bound.used_fallback());
+  EXPECT_EQ(b.size(), static_cast<size_t>(8));
+  EXPECT_EQ(describe(b), describe(full.Devices()));
+  auto labels = lm::NewSriovLabeler(std::make_shared<Lib>(std::make_shared<BoundAmdPCI>(root)))->GetLabels();
+  auto want = lm::NewSriovLabeler(std::make_shared<Lib>(std::make_shared<SysfsAmdPCI>(root)))->GetLabels();
+  EXPECT_EQ(labels, want);
+  EXPECT_EQ(labels["amd.com/sriov.num-vfs"], std::string("3"));
+  fs::remove_all(root);
+}
+
+TEST(Bound_NeverReadsFunctionsNoDriverBinds) {
+  // An unbound AMD function whose class cannot be read: the full scan fails
+  // on it, the bound scan never looks.
+  std::string root = bound_host(10, 0);
+  std::string odd = root + "/sys/bus/pci/devices/0000:e1:00.0";
+  put_file(odd + "/vendor", "0x1002\n");
+  fs::mkdir_all(odd + "/class");  // reads fail (EISDIR)
+  BoundAmdPCI bound(root);
+  EXPECT_EQ(bound.Devices().size(), static_cast<size_t>(5));
+  EXPECT_THROW_MSG(SysfsAmdPCI(root).Devices(), "unable to read PCI device class for 0000:e1:00.0");
+  fs::remove_all(root);
+}
+
+TEST(Bound_FallsBackToTheBusWhenNothingIsBound) {
+  // A guest whose amdgpu is not loaded: its VF is on the bus, bound to nothing.
+  std::string root = pci_host(5, 0);
+  fs::mkdir_all(root + "/sys/bus/pci/drivers/amdgpu");  // module loaded, nothing bound
+  BoundAmdPCI bound(root, std::make_shared<SysfsAmdPCI>(root));
+  auto devs = bound.Devices();
+  EXPECT_TRUE(bound.used_fallback());
+  EXPECT_EQ(devs.size(), static_cast<size_t>(5));
+  EXPECT_EQ(BoundAmdPCI(root).Devices().size(), static_cast<size_t>(0));  // no fallback given
+  fs::remove_all(root);
+}
+
+TEST(Bound_GuestVFOnAmdgpu) {
+  // Inside a VM: the VF is an ordinary function to the guest kernel - no
+  // physfn link, no SR-IOV attributes - bound to amdgpu; its VF device ID
+  // makes it a VF, and its (unprivileged, 64-byte) config space is read
+  // because sysfs publishes no SR-IOV state for it.
+  char d[] = "/tmp/gfd-pci-XXXXXX";
+  EXPECT_TRUE(mkdtemp(d) != nullptr);
+  std::string root = d;
+  std::string p = root + "/sys/bus/pci/devices/0000:00:05.0";
+  put_file(p + "/vendor", "0x1002\n");
+  put_file(p + "/class", "0x120000\n");
+  put_file(p + "/device", "0x75b3\n");
+  put_file(p + "/config", std::string(64, '\x02'));
+  bind_driver(root, "amdgpu", "0000:00:05.0");
+  auto fns = Lib(std::make_shared<BoundAmdPCI>(root)).Devices();
+  EXPECT_EQ(fns.size(), static_cast<size_t>(1));
+  EXPECT_EQ(fns[0].GetInfo().role, std::string("vf"));
+  EXPECT_EQ(fns[0].pci().config.size(), static_cast<size_t>(64));
+  fs::remove_all(root);
+}
+
+TEST(Bound_KeptWhileUeventSeqnumUnchanged) {
+  std::string root = bound_host(3, 2);
+  put_file(root + "/sys/kernel/uevent_seqnum", "4242\n");
+  BoundAmdPCI bound(root);
+  EXPECT_EQ(bound.Devices().size(), static_cast<size_t>(7));
+  // A VF removed behind a constant seqnum (impossible on a real kernel: the
+  // removal sends a uevent) is not noticed...
+  fs::remove_all(root + "/sys/bus/pci/devices/0000:c1:00.0/virtfn1");
+  EXPECT_EQ(bound.Devices().size(), static_cast<size_t>(7));
+  // ...until the seqnum moves.
+  put_file(root + "/sys/kernel/uevent_seqnum", "4243\n");
+  EXPECT_EQ(bound.Devices().size(), static_cast<size_t>(6));
+  // An emulated sysfs that never counts ("0") is re-read every time.
+  put_file(root + "/sys/kernel/uevent_seqnum", "0\n");
+  fs::remove_all(root + "/sys/bus/pci/devices/0000:c1:00.0/virtfn0");
+  EXPECT_EQ(bound.Devices().size(), static_cast<size_t>(5));
   fs::remove_all(root);
 }

@@ -167,7 +167,10 @@ namespace {
 //     write p50 0.055-0.090 ms vs 0.147-0.282 ms creating in the write
 //     (profiles/writer_ab_r3.txt).  Two, not one: the job runs while its own
 //     cycle writes, so the file a write uses must come from an earlier
-//     cycle's job - with one, every other write made its own file.
+//     cycle's job - with one, every other write made its own file.  Each
+//     job tops the queue up to two (and makes gfd-tmp/ if the first cycle's
+//     write has not yet), so every write after the first takes one
+//     (tests/test_daemon.py::test_loop_writes_take_prepared_files).
 //   * The exchange: a rename over the old feature file frees its inode
 //     inside rename(2); on ext4 (the usual file system of NFD's features.d
 //     hostPath) that is most of a cold replace, 0.34-0.58 ms vs 0.03 ms for
@@ -350,25 +353,38 @@ std::function<void()> temp_preparer(const std::string& path) {
   return [tmp_dir, hint, ticket] {
     WriterState& q = writer();
     std::vector<std::string> old;
-    bool make;
+    size_t want;
     {
       std::lock_guard<std::mutex> lk(q.mu);
       old.swap(q.retired);
-      make = q.dir != tmp_dir || q.ready.size() < kMaxPrepared;
+      size_t have = q.dir == tmp_dir ? q.ready.size() : 0;
+      want = have < kMaxPrepared ? kMaxPrepared - have : 0;
     }
     for (const auto& name : old) ::unlink(name.c_str());
-    if (!make) return;
-    // gfd-tmp/ itself is not re-created: a missing one is the next write's
-    // business.
-    Prepared f;
-    f.fd = create_temp(tmp_dir, 0644, &f.name);
-    if (f.fd < 0) return;
-    if (hint > 0 && wants_prealloc(f.fd) && ::fallocate(f.fd, FALLOC_FL_KEEP_SIZE, 0, static_cast<off_t>(hint)) == 0)
-      f.allocated = hint;
-    std::lock_guard<std::mutex> lk(q.mu);
-    if (q.dir != tmp_dir) drop_ready(q);
-    q.dir = tmp_dir;
-    q.ready.push_back(std::move(f));
+    // Top the queue up to kMaxPrepared, not one file per job: a job that
+    // runs after its own cycle's write (the worker is free only after the
+    // node facts and the SR-IOV scan) must still leave the next write one.
+    for (size_t i = 0; i < want; ++i) {
+      // The first cycle's job usually runs before gfd-tmp/ exists: make it
+      // (and the output directory), as that cycle's write is about to.
+      Prepared f;
+      f.fd = create_temp(tmp_dir, 0644, &f.name);
+      if (f.fd < 0 && errno == ENOENT) {
+        try {
+          fs::mkdir_all(tmp_dir);
+        } catch (const std::exception&) {
+          return;  // the write reports it
+        }
+        f.fd = create_temp(tmp_dir, 0644, &f.name);
+      }
+      if (f.fd < 0) return;
+      if (hint > 0 && wants_prealloc(f.fd) && ::fallocate(f.fd, FALLOC_FL_KEEP_SIZE, 0, static_cast<off_t>(hint)) == 0)
+        f.allocated = hint;
+      std::lock_guard<std::mutex> lk(q.mu);
+      if (q.dir != tmp_dir) drop_ready(q);
+      q.dir = tmp_dir;
+      q.ready.push_back(std::move(f));
+    }
   };
 }
 

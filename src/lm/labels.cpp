@@ -324,9 +324,15 @@ std::string temp_dir_of(const std::string& path) { return fs::join(fs::dirname(f
 void write_file_atomically(const std::string& path, const std::string& contents, unsigned perm) {
   std::string tmp_dir = temp_dir_of(path);
   // Prepared files are created 0644 - the feature file's mode.
-  if (!write_atomically_once(path, tmp_dir, contents, perm, perm == 0644))
-    write_atomically_once(path, tmp_dir, contents, perm, false);
   WriterState& w = writer();
+  if (!write_atomically_once(path, tmp_dir, contents, perm, perm == 0644)) {
+    {
+      // gfd-tmp/ was removed under us: the other prepared files went with it.
+      std::lock_guard<std::mutex> lk(w.mu);
+      drop_ready(w);
+    }
+    write_atomically_once(path, tmp_dir, contents, perm, false);
+  }
   std::lock_guard<std::mutex> lk(w.mu);
   w.last_size = contents.size();
 }

@@ -90,14 +90,21 @@ mode_t process_umask() {
   return mask;
 }
 
-// mkstemp with the final permission bits: "<dir>/gfd-XXXXXX" with a random
-// suffix, O_EXCL.  Returns the fd (name in *name) or -1 with errno set.
+// Prefix of this daemon's temporary files in gfd-tmp/.  NVIDIA's GFD, which
+// may run on the same node (GPUs of both vendors), keeps its own files there
+// as gfd-XXXXXX (labels.go:90): everything here that removes temporary files
+// removes only names with this prefix, never the other daemon's in-flight
+// file.
+constexpr const char kTempPrefix[] = "gfd-amd-";
+
+// mkstemp with the final permission bits: "<dir>/gfd-amd-XXXXXX" with a
+// random suffix, O_EXCL.  Returns the fd (name in *name) or -1 with errno set.
 int create_temp(const std::string& dir, unsigned perm, std::string* name) {
   static const char kChars[] = "abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789";
   static thread_local uint64_t state = static_cast<uint64_t>(::getpid()) * 0x9E3779B97F4A7C15ULL ^
                                        static_cast<uint64_t>(reinterpret_cast<uintptr_t>(&state));
   for (int attempt = 0; attempt < 100; ++attempt) {
-    *name = dir + "/gfd-";
+    *name = dir + "/" + kTempPrefix;
     for (int i = 0; i < 6; ++i) {
       state ^= state << 13;
       state ^= state >> 7;
@@ -127,6 +134,33 @@ bool wants_prealloc(int fd) {
   if (::fstatfs(fd, &sf) != 0) return false;
   constexpr unsigned long kExt4 = 0xEF53, kOverlay = 0x794c7630;
   return static_cast<unsigned long>(sf.f_type) == kExt4 || static_cast<unsigned long>(sf.f_type) == kOverlay;
+}
+
+// Removes this daemon's files from gfd-tmp/ (kTempPrefix) and any
+// subdirectory (only this daemon's round-2 layout made them; NVIDIA's GFD
+// keeps plain files there), then the directory if nothing else is left in
+// it.  Something that is not a directory where gfd-tmp/ belongs blocks
+// every write, and is removed.  Returns 0 or an errno.
+int remove_own_temps(const std::string& tmp_dir) {
+  int err = 0;
+  auto names = fs::list_dir(tmp_dir, &err);
+  if (err == ENOENT) return 0;
+  if (err == ENOTDIR) return ::unlink(tmp_dir.c_str()) == 0 || errno == ENOENT ? 0 : errno;
+  if (err != 0) return err;
+  int first = 0;
+  for (const auto& n : names) {
+    std::string p = tmp_dir + "/" + n;
+    int e = 0;
+    if (n.rfind(kTempPrefix, 0) == 0) {
+      e = ::unlink(p.c_str()) == 0 || errno == ENOENT ? 0 : errno;
+      if (e == EISDIR || e == EPERM) e = fs::remove_all(p);
+    } else if (fs::is_dir(p)) {
+      e = fs::remove_all(p);
+    }
+    if (e && !first) first = e;
+  }
+  if (::rmdir(tmp_dir.c_str()) != 0 && errno != ENOTEMPTY && errno != EEXIST && errno != ENOENT && !first) first = errno;
+  return first;
 }
 
 }  // namespace
@@ -279,13 +313,13 @@ bool write_atomically_once(const std::string& path, const std::string& tmp_dir, 
   // prepared file lost with it is a vanished prepared file (retried).
   if (fd < 0) {
     int e = errno;
-    fs::remove_all(tmp_dir);
+    remove_own_temps(tmp_dir);
     throw Error("fail to create temporary output file: " + fs::errno_str(e));
   }
   auto fail = [&](const std::string& msg) {
     ::close(fd);
     ::unlink(tmpl.c_str());
-    fs::remove_all(tmp_dir);
+    remove_own_temps(tmp_dir);
     throw Error(msg);
   };
   int64_t t1 = trace::now_ns();
@@ -300,7 +334,7 @@ bool write_atomically_once(const std::string& path, const std::string& tmp_dir, 
   if (::close(fd) != 0) {
     int e = errno;
     ::unlink(tmpl.c_str());
-    fs::remove_all(tmp_dir);
+    remove_own_temps(tmp_dir);
     throw Error("error writing temporary file '" + tmpl + "': " + fs::errno_str(e));
   }
   int64_t t2 = trace::now_ns();
@@ -310,7 +344,7 @@ bool write_atomically_once(const std::string& path, const std::string& tmp_dir, 
     // A prepared file removed behind our back (gfd-tmp/ deleted between
     // cycles): not an error of this cycle.
     if (prepared_fd && e == ENOENT) return false;
-    fs::remove_all(tmp_dir);
+    remove_own_temps(tmp_dir);
     throw Error("error moving temporary file to '" + path + "': " + fs::errno_str(e));
   }
   trace::record("write.rename", trace::now_ns() - t2);
@@ -411,8 +445,8 @@ void discard_prepared_temps() {
 void sweep_temp_dir(const std::string& path) {
   if (path.empty()) return;
   std::string tmp_dir = temp_dir_of(path);
-  if (int e = fs::remove_all(tmp_dir))
-    throw Error("failed to remove stale temporary directory '" + tmp_dir + "': " + fs::errno_str(e));
+  if (int e = remove_own_temps(tmp_dir))
+    throw Error("failed to remove stale temporary files in '" + tmp_dir + "': " + fs::errno_str(e));
 }
 
 void write_to_file(const Labels& labels, const std::string& path) {
@@ -433,7 +467,7 @@ void remove_output_file(const std::string& path) {
   discard_prepared_temps();
   std::string abs = fs::absolute(path);
   std::string tmp_dir = temp_dir_of(abs);
-  if (int e = fs::remove_all(tmp_dir)) throw Error("failed to remove temporary output directory: " + fs::errno_str(e));
+  if (int e = remove_own_temps(tmp_dir)) throw Error("failed to remove temporary output directory: " + fs::errno_str(e));
   if (::unlink(abs.c_str()) != 0) throw Error("failed to remove output file: " + fs::errno_str(errno));
 }
 

@@ -17,13 +17,18 @@
 //     queries run in parallel across physical GPUs on multi-GPU nodes.
 //   * the virtualization mode, fixed at driver probe, is queried once per
 //     session instead of every cycle.
-//   * an unpartitioned (SPX) GPU's per-cycle values come straight from the
-//     sysfs attributes the library would read for them (GFD_AMDSMI_SYSFS=0
-//     turns this off); partitioned GPUs are queried through amd-smi.
+//   * per-cycle values (memory, partition modes, xGMI links, available
+//     modes) come straight from the amdgpu sysfs attributes the library
+//     itself reads for them - for an unpartitioned GPU and for the parent
+//     function of a partitioned one, whose partitions' KFD nodes and counts
+//     are kept per session; everything else goes through amd-smi.  The
+//     test-only Config::amdsmi_library_only (AmdSmiOptions::sysfs_values =
+//     false) sends every query through the library instead.
 //   * compute partitions (DPX/QPX/CPX) are separate amd-smi processors on
 //     one PCI slot (their function bits may carry the partition index); they
-//     are regrouped into parent GPUs by slot and ASIC serial
-//     (resource/physical.h).
+//     are regrouped into parent GPUs by PCI slot and device ID, and split
+//     by ASIC serial only for SR-IOV functions (resource/physical.h,
+//     split_by_identity).
 #pragma once
 
 #include <cstdint>

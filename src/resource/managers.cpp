@@ -60,6 +60,32 @@ struct WarmStartManager::Warmer {
   int64_t ns = 0;
 };
 
+namespace {
+// The warmer a torn-down manager left running (its library init wedged), if
+// any.  A wedged amdsmi_init holds the library's process-wide lock, so a new
+// warmer would only block behind it: a reloaded daemon waits for this one to
+// finish before starting its own, and at most one warmer is ever left
+// behind, however many SIGHUPs come.
+std::mutex g_orphan_mu;
+std::shared_ptr<WarmStartManager::Warmer> g_orphan;
+
+bool orphan_running() {
+  std::shared_ptr<WarmStartManager::Warmer> w;
+  {
+    std::lock_guard<std::mutex> g(g_orphan_mu);
+    w = g_orphan;
+  }
+  if (!w) return false;
+  std::lock_guard<std::mutex> lk(w->mu);
+  if (!w->done) return true;
+  std::lock_guard<std::mutex> g(g_orphan_mu);
+  if (g_orphan == w) g_orphan.reset();
+  return false;
+}
+}  // namespace
+
+bool warmer_left_running() { return orphan_running(); }
+
 WarmStartManager::WarmStartManager(ManagerPtr preferred, ManagerPtr quick)
     : preferred_(std::move(preferred)), quick_(std::move(quick)), current_(quick_) {}
 
@@ -76,6 +102,10 @@ WarmStartManager::~WarmStartManager() {
   lk.unlock();
   log::printf("Warning: the %s manager is still initializing after %lld ms; not waiting for it",
               preferred_->Name().c_str(), static_cast<long long>(teardown_wait_ms));
+  {
+    std::lock_guard<std::mutex> g(g_orphan_mu);
+    g_orphan = warmer_;
+  }
   thread_.detach();  // it owns what it uses (the manager and its state)
 }
 
@@ -93,7 +123,15 @@ std::vector<DevicePtr> WarmStartManager::GetDevices() {
 }
 
 void WarmStartManager::Init() {
-  if (state_ == State::cold) {
+  if (state_ == State::cold && orphan_running()) {
+    // An earlier manager's warmer is still stuck in the library's init:
+    // label from the quick manager and look again next cycle.
+    if (!waited_logged_) {
+      log::printf("The %s manager of the previous configuration is still initializing; labeling from the %s "
+                  "manager until it finishes", preferred_->Name().c_str(), quick_->Name().c_str());
+      waited_logged_ = true;
+    }
+  } else if (state_ == State::cold) {
     // A persistent session stays initialised after Shutdown: the warmer
     // opens it and takes one snapshot - the library's first queries of a
     // device (~1.2 ms on MI355X: ASIC info, KFD node, virtualization mode)

@@ -107,11 +107,12 @@ class WarmStartManager : public Manager {
   // The preferred manager is the one in use.
   bool warmed() const { return state_ == State::preferred; }
   int64_t teardown_wait_ms = 5000;
+  struct Warmer;
 
  private:
   enum class State { cold, warming, preferred, quick_only };
   void fall_back(const std::string& why);
-  struct Warmer;
+  bool waited_logged_ = false;
 
   ManagerPtr preferred_, quick_, current_;
   State state_ = State::cold;
@@ -119,6 +120,12 @@ class WarmStartManager : public Manager {
   std::shared_ptr<Warmer> warmer_;
   std::string quick_devices_;  // the quick manager's last devices (device_summary), while warming
 };
+
+// Whether a WarmStartManager was torn down while its warmer was still
+// initialising the preferred manager and that warmer has not finished: the
+// process must then not run static destructors (the warmer may be inside
+// the library), so main() leaves with _exit.
+bool warmer_left_running();
 
 // What the labels of `devices` depend on, one line per device (and
 // partition): compared when the daemon switches backends, so a difference

@@ -268,7 +268,7 @@ def test_sighup_to_a_new_output_file_leaves_nothing_in_the_old_directory(binary,
     old_dir, new_dir = tmp_path / "old", tmp_path / "new"
     old_dir.mkdir()
     (new_dir / "gfd-tmp").mkdir(parents=True)
-    (new_dir / "gfd-tmp" / "gfd-stale1").write_text("left by a killed daemon")
+    (new_dir / "gfd-tmp" / "gfd-amd-stale1").write_text("left by a killed daemon")
     cfg = tmp_path / "config.yaml"
     cfg.write_text(f"version: v1\nflags:\n  gfd:\n    outputFile: {old_dir / 'gfd'}\n")
     base = [a for a in _base(tmp_path, old_dir / "gfd") if not a.startswith("--output-file")]
@@ -278,7 +278,7 @@ def test_sighup_to_a_new_output_file_leaves_nothing_in_the_old_directory(binary,
         cfg.write_text(f"version: v1\nflags:\n  gfd:\n    outputFile: {new_dir / 'gfd'}\n")
         p.send_signal(signal.SIGHUP)
         assert _wait_for(lambda: (new_dir / "gfd").exists(), timeout=10)
-        assert not (new_dir / "gfd-tmp" / "gfd-stale1").exists()
+        assert not (new_dir / "gfd-tmp" / "gfd-amd-stale1").exists()
         assert _wait_for(lambda: not (old_dir / "gfd").exists() and not (old_dir / "gfd-tmp").exists(), timeout=5), \
             list(old_dir.rglob("*"))
         assert golden.parse_labels((new_dir / "gfd").read_text())["amd.com/gpu.product"] == "MOCKMODEL"

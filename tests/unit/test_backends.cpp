@@ -597,6 +597,40 @@ TEST(WarmStart_DestructorDoesNotWaitForeverForAWedgedInit) {
   EXPECT_EQ(smi.use_count(), 1L);
 }
 
+TEST(WarmStart_ReloadWaitsForTheWedgedWarmerInsteadOfStartingAnother) {
+  // a library init wedged while holding amd-smi's process-wide
+  // lock; every SIGHUP used to start (and then abandon) one more warmer
+  // blocked behind it.  Now a reloaded manager labels from the quick one
+  // until the old warmer finishes, and only then starts its own.
+  auto wedged = std::make_shared<BlockingManager>();
+  auto kfd = std::make_shared<MockManager>(std::vector<DevicePtr>{new_full_gpu()});
+  {
+    WarmStartManager w(wedged, kfd);
+    w.teardown_wait_ms = 20;
+    w.Init();
+    w.Shutdown();
+  }  // SIGHUP: torn down with its warmer stuck
+  EXPECT_TRUE(warmer_left_running());
+  auto smi = std::make_shared<MockManager>(std::vector<DevicePtr>{new_full_gpu(), new_full_gpu()});
+  {
+    WarmStartManager w2(smi, kfd);
+    for (int i = 0; i < 5; ++i) {  // reloads' cycles: no second warmer
+      w2.Init();
+      EXPECT_EQ(w2.GetDevices().size(), static_cast<size_t>(1));
+      w2.Shutdown();
+    }
+    EXPECT_EQ(smi->init_calls, 0);
+    wedged->release();
+    for (int i = 0; i < 2000 && warmer_left_running(); ++i) usleep(1000);
+    EXPECT_FALSE(warmer_left_running());
+    auto seen = cycle_until_warm(w2);
+    EXPECT_TRUE(w2.warmed());
+    EXPECT_EQ(seen.front(), static_cast<size_t>(1));
+  }
+  for (int i = 0; i < 2000 && wedged.use_count() > 1; ++i) usleep(1000);
+  EXPECT_EQ(wedged.use_count(), 1L);
+}
+
 TEST(DeviceSummary_ShowsWhatTheLabelsDependOn) {
   auto a = device_summary({new_full_gpu()});
   EXPECT_EQ(a, device_summary({new_full_gpu()}));

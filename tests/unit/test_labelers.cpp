@@ -583,10 +583,19 @@ TEST(SweepTempDir_RemovesWhatACrashLeft) {
   EXPECT_TRUE(mkdtemp(dir) != nullptr);
   std::string path = std::string(dir) + "/gfd", tmp = std::string(dir) + "/gfd-tmp";
   fs::mkdir_all(tmp + "/a");  // round-2 layout: subdirectories
-  for (const char* n : {"/gfd-abc123", "/a/gfd-def456"})
+  for (const char* n : {"/gfd-amd-abc123", "/a/gfd-def456"})
     EXPECT_TRUE(::close(::open((tmp + n).c_str(), O_CREAT | O_WRONLY, 0644)) == 0);
   lm::sweep_temp_dir(path);
   EXPECT_FALSE(fs::exists(tmp));
+  // NVIDIA's GFD on the same node keeps its in-flight file there as
+  // gfd-XXXXXX: a sweep leaves it (and so the directory) alone.
+  fs::mkdir_all(tmp);
+  for (const char* n : {"/gfd-amd-abc123", "/gfd-xyz789"})
+    EXPECT_TRUE(::close(::open((tmp + n).c_str(), O_CREAT | O_WRONLY, 0644)) == 0);
+  lm::sweep_temp_dir(path);
+  EXPECT_FALSE(fs::exists(tmp + "/gfd-amd-abc123"));
+  EXPECT_TRUE(fs::exists(tmp + "/gfd-xyz789"));
+  fs::remove_all(tmp);
   lm::sweep_temp_dir(path);  // nothing there: fine
   lm::sweep_temp_dir("");    // stdout mode: nothing to do
   fs::remove_all(dir);

@@ -1,10 +1,12 @@
 #include "sriov/bound.h"
 
 #include <algorithm>
+#include <optional>
 #include <set>
 
 #include "util/error.h"
 #include "util/fs.h"
+#include "util/pool.h"
 #include "util/strings.h"
 #include "util/trace.h"
 
@@ -73,26 +75,43 @@ const std::vector<std::string>& BoundAmdPCI::drivers() {
 
 std::vector<PCIDevice> BoundAmdPCI::scan_bound(const std::vector<std::string>& bound) {
   std::string devices = fs::join(root_, kPciDevicesRoot);
+  // Two functions per lane: the 8 GPUs of an MI355X host are ~40 small
+  // reads, 0.23 ms on one thread of a process that just started.
+  constexpr size_t kChunk = 2;
+  std::vector<std::optional<PCIDevice>> found(bound.size());
+  auto read_all = [&](const std::vector<std::string>& addrs, const std::vector<std::string>& pfs) {
+    size_t chunks = (addrs.size() + kChunk - 1) / kChunk;
+    found.assign(addrs.size(), std::nullopt);
+    WorkerPool::instance().parallel_for(chunks, [&](size_t c) {
+      for (size_t i = c * kChunk; i < std::min(addrs.size(), (c + 1) * kChunk); ++i)
+        found[i] = read_function(fs::join(devices, addrs[i]), addrs[i], pfs.empty() ? "" : pfs[i]);
+    });
+  };
+  read_all(bound, {});
   std::vector<PCIDevice> out;
   std::set<std::string> seen(bound.begin(), bound.end());
-  std::vector<std::pair<std::string, std::string>> vfs;  // VF address, its PF
-  for (const auto& addr : bound) {
-    std::string dir = fs::join(devices, addr);
-    auto d = read_function(dir, addr, "");
-    if (!d) continue;
-    if (d->sriov_numvfs > 0) {
+  std::vector<std::string> vfs, vf_pfs;  // VF addresses and their PFs
+  for (size_t i = 0; i < bound.size(); ++i) {
+    if (!found[i]) continue;
+    if (found[i]->sriov_numvfs > 0) {
       // The PF's enabled VFs, bound to whatever hands them to VMs (or
       // nothing): "virtfn0" -> "../0000:d9:00.1".
-      for (const auto& e : fs::list_dir(dir)) {
+      for (const auto& e : fs::list_dir(found[i]->path)) {
         if (e.rfind("virtfn", 0) != 0) continue;
-        std::string vf = fs::basename(fs::read_link(fs::join(dir, e)));
-        if (is_pci_address(vf) && seen.insert(vf).second) vfs.emplace_back(vf, addr);
+        std::string vf = fs::basename(fs::read_link(fs::join(found[i]->path, e)));
+        if (is_pci_address(vf) && seen.insert(vf).second) {
+          vfs.push_back(vf);
+          vf_pfs.push_back(bound[i]);
+        }
       }
     }
-    out.push_back(std::move(*d));
+    out.push_back(std::move(*found[i]));
   }
-  for (const auto& [vf, pf] : vfs)
-    if (auto d = read_function(fs::join(devices, vf), vf, pf)) out.push_back(std::move(*d));
+  if (!vfs.empty()) {
+    read_all(vfs, vf_pfs);
+    for (auto& d : found)
+      if (d) out.push_back(std::move(*d));
+  }
   std::sort(out.begin(), out.end(), [](const PCIDevice& a, const PCIDevice& b) { return a.address < b.address; });
   return out;
 }

@@ -167,6 +167,7 @@ def _daemon_loop(binary: str, args: list[str], cycles: int, interval: str = "2ms
             "other_p50_ms": round(_percentile(phases.get("other", []), 0.5), 4),
             "cycle_cpus": cpus,
             "cpu_moves": sum(1 for a, b in zip(starts, starts[1:]) if a != b),
+            "totals_ms": totals,
             "phases_p50_ms": {k: round(_percentile(v, 0.5), 4) for k, v in phases.items() if k != "total"}}
 
 
@@ -195,7 +196,7 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--backend", default="auto", help="auto | amdsmi | sysfs | synthetic")
     ap.add_argument("--no-extras", action="store_true", help="skip the secondary measurements")
-    ap.add_argument("--cold-cycles", type=int, default=env_int("GFD_BENCH_COLD_CYCLES", 8),
+    ap.add_argument("--cold-cycles", type=int, default=env_int("GFD_BENCH_COLD_CYCLES", 12),
                     help="daemon cycles 1 s apart for the cold-cycle measurement (0: skip)")
     ap.add_argument("--sysfs-root", default=None,
                     help="with --backend sysfs: read this root instead of / (tools/hybrid_root.py builds one that "

@@ -260,12 +260,16 @@ bool run(resource::Manager& manager, const std::shared_ptr<sriov::Interface>& sr
 
   lm::LabelerPtr timestamp = lm::NewTimestampLabeler(config);
   for (;;) {
+    // The cycle's log lines ("Writing labels to output file", ...) go out
+    // together once the feature file is in place (and on any error).
+    log::Hold hold;
     CycleResult r = label_cycle(manager, sriov, config, timestamp, true);
     if (config.trace_timing())
       log::printf("Timing: %s cpu=%d,%d,%d", trace::summary(r.total_ns).c_str(), r.cpu_start, r.cpu_end, r.cpu_facts);
     if (config.oneshot()) return false;
 
     log::printf("Sleeping for %s", format_duration(config.sleep_interval()).c_str());
+    hold.flush();
     std::optional<int> sig;
     if (sigs) {
       sig = sigs->wait(config.sleep_interval());

@@ -9,6 +9,7 @@ namespace gfd::log {
 
 namespace {
 std::atomic<bool> g_quiet{false};
+thread_local std::string* t_held = nullptr;  // the innermost Hold's buffer
 
 void emit(const char* msg, size_t len) {
   char stamp[32];
@@ -22,11 +23,32 @@ void emit(const char* msg, size_t len) {
   out.append(stamp);
   out.append(msg, len);
   if (len == 0 || msg[len - 1] != '\n') out.push_back('\n');
+  if (t_held) {
+    t_held->append(out);
+    return;
+  }
   fwrite(out.data(), 1, out.size(), stderr);
 }
 }  // namespace
 
 bool set_quiet(bool q) { return g_quiet.exchange(q); }
+
+Hold::Hold() : prev_(t_held) { t_held = &buf_; }
+
+Hold::~Hold() {
+  flush();
+  t_held = prev_;
+}
+
+void Hold::flush() {
+  if (buf_.empty()) return;
+  if (prev_) {
+    prev_->append(buf_);  // nested: the outer Hold writes it
+  } else {
+    fwrite(buf_.data(), 1, buf_.size(), stderr);
+  }
+  buf_.clear();
+}
 bool quiet() { return g_quiet.load(std::memory_order_relaxed); }
 
 void printf(const char* fmt, ...) {

@@ -18,4 +18,22 @@ void printf(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
 bool set_quiet(bool quiet);
 bool quiet();
 
+// While a Hold lives, this thread's log lines (each stamped when logged)
+// are collected and written together - in log order, one write(2) - when it
+// is flushed or destroyed.  The daemon holds a cycle's lines until the
+// feature file is in place: a line to stderr, usually a pipe to the
+// container runtime, is a syscall the labels do not wait for.
+class Hold {
+ public:
+  Hold();
+  ~Hold();
+  Hold(const Hold&) = delete;
+  Hold& operator=(const Hold&) = delete;
+  void flush();
+
+ private:
+  std::string buf_;
+  std::string* prev_;
+};
+
 }  // namespace gfd::log

@@ -179,7 +179,11 @@ def _cold_process(binary: str, args: list[str], runs: int) -> dict:
     from gpu_feature_discovery_amd.utils.proc import spawn_wait_ms
 
     ms = [spawn_wait_ms([binary, "--oneshot", *args], timeout=60) for _ in range(runs)]
+    # The first spawns after the cold-cycle measurement land on idle,
+    # down-clocked cores (2-3 ms where later ones take 1.3-1.4 ms,
+    # profiles/oneshot_series_r4.jsonl): the first run is reported on its own.
     return {"p50_ms": round(_percentile(ms, 0.5), 3), "p90_ms": round(_percentile(ms, 0.9), 3), "runs": runs,
+            "first_ms": round(ms[0], 3), "runs_ms": [round(x, 3) for x in ms],
             "args": " ".join(a for a in args if not a.startswith(("--output-file", "--sysfs-root", "--machine")))}
 
 
@@ -287,7 +291,7 @@ def main() -> int:
             loop_args = _session_args("auto", n, out, root, [])
             try:
                 binary = str(gfd.binary_path())
-                runs = max(5, min(30, a.steps // 10))
+                runs = max(15, min(30, a.steps // 10))
                 extras["daemon_loop"] = _daemon_loop(binary, loop_args, max(20, min(a.steps, 300)))
                 first_cycle = extras["daemon_loop"]["first_cycle_ms"]
                 # Deployed cadence: cycles after >= 1 s of idle (the daemon

@@ -114,6 +114,7 @@ class Session {
     config::disable_resource_renaming(config_);
     config_.amdsmi_library_only = amdsmi_library_only;
     WorkerPool::instance().set_follow(ctx.String("cpu-affinity") == "follow");
+    if (!config_.oneshot()) WorkerPool::instance().load_topology();
     manager_ = resource::new_manager(config_);
     sriov_ = sriov::new_sriov_lib(config_.sysfs_root());
     timestamp_ = lm::NewTimestampLabeler(config_);

@@ -127,8 +127,9 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
   CycleResult r;
   r.cpu_start = sched_getcpu();
   {
+    // --cpu-affinity=follow, loop mode only: a oneshot Job has one cycle.
     trace::Span span("placement");
-    WorkerPool::instance().follow_caller();  // --cpu-affinity=follow
+    if (!config.oneshot()) WorkerPool::instance().follow_caller();
   }
   // Work that does not depend on the device backend runs on workers while
   // the backend enumerates: the node facts the device labeler needs after
@@ -324,6 +325,7 @@ void start(const Context& ctx, SignalWatcher& sigs) {
         log::printf("Warning: %s", e.what());
       }
     }
+    if (!c.oneshot()) WorkerPool::instance().load_topology();  // before the first cycle
     g_timeline.enabled = c.trace_timing();
     if (!g_timeline.configured_ns) g_timeline.configured_ns = trace::now_ns();
 

@@ -55,12 +55,17 @@ void WorkerPool::ensure_workers(size_t n) {
 }
 
 void WorkerPool::set_follow(bool on) {
-  const affinity::L3Map* map = on ? &affinity::L3Map::host() : nullptr;
   std::lock_guard<std::mutex> g(mu_);
   follow_.store(on);
-  l3_ = map;
   domain_id_.store(-1);
   if (!on && !domain_.empty()) unpin_locked();
+}
+
+void WorkerPool::load_topology() {
+  if (!follow_.load()) return;
+  const affinity::L3Map* map = &affinity::L3Map::host();  // sysfs reads: outside the lock
+  std::lock_guard<std::mutex> g(mu_);
+  l3_ = map;
 }
 
 void WorkerPool::unpin_locked() {
@@ -78,7 +83,7 @@ void WorkerPool::follow_caller() {
   // vDSO getcpu and a table lookup.
   int cpu = sched_getcpu();
   std::lock_guard<std::mutex> g(mu_);
-  if (!l3_) return;
+  if (!l3_) l3_ = &affinity::L3Map::host();  // load_topology() was not called
   int id = l3_->id(cpu);
   if (id < 0 || id == domain_id_.load(std::memory_order_relaxed)) return;
   domain_id_.store(id, std::memory_order_relaxed);

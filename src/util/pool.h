@@ -81,11 +81,14 @@ class WorkerPool {
   // to hand out work) keeps every worker on the CPUs that share the L3 cache
   // of the CPU the caller runs on, re-pinning them only when that domain
   // changed.  The caller is left where the scheduler put it.  Off until
-  // enabled; set_follow(true) reads the host's L3 map (once per process),
-  // so a cycle only looks its CPU up.  A domain of which fewer than two CPUs
-  // are allowed is not pinned to (every lane on one core).  set_follow(false)
-  // returns pinned workers to the caller's allowed set.
+  // enabled.  load_topology() reads the host's L3 map (once per process;
+  // the daemon calls it at start-up in loop mode, so a cycle only looks its
+  // CPU up; a oneshot Job never follows and never reads it).  A domain of
+  // which fewer than two CPUs are allowed is not pinned to (every lane on
+  // one core).  set_follow(false) returns pinned workers to the caller's
+  // allowed set.
   void set_follow(bool on);
+  void load_topology();
   void follow_caller();
   // Re-pins done by follow_caller (tests / benchmarks).
   size_t repins() const { return repins_.load(std::memory_order_relaxed); }

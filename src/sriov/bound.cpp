@@ -75,17 +75,22 @@ const std::vector<std::string>& BoundAmdPCI::drivers() {
 
 std::vector<PCIDevice> BoundAmdPCI::scan_bound(const std::vector<std::string>& bound) {
   std::string devices = fs::join(root_, kPciDevicesRoot);
-  // Two functions per lane: the 8 GPUs of an MI355X host are ~40 small
-  // reads, 0.23 ms on one thread of a process that just started.
+  // Two functions per lane - the 8 GPUs of an MI355X host are ~40 small
+  // reads, 0.23 ms on one cold thread - but only on workers already parked:
+  // in a oneshot Job, creating threads for them made the scan slower (0.39
+  // ms), and it is overlapped with enumeration anyway.
   constexpr size_t kChunk = 2;
   std::vector<std::optional<PCIDevice>> found(bound.size());
   auto read_all = [&](const std::vector<std::string>& addrs, const std::vector<std::string>& pfs) {
     size_t chunks = (addrs.size() + kChunk - 1) / kChunk;
     found.assign(addrs.size(), std::nullopt);
-    WorkerPool::instance().parallel_for(chunks, [&](size_t c) {
-      for (size_t i = c * kChunk; i < std::min(addrs.size(), (c + 1) * kChunk); ++i)
-        found[i] = read_function(fs::join(devices, addrs[i]), addrs[i], pfs.empty() ? "" : pfs[i]);
-    });
+    WorkerPool::instance().parallel_for(
+        chunks,
+        [&](size_t c) {
+          for (size_t i = c * kChunk; i < std::min(addrs.size(), (c + 1) * kChunk); ++i)
+            found[i] = read_function(fs::join(devices, addrs[i]), addrs[i], pfs.empty() ? "" : pfs[i]);
+        },
+        1 + WorkerPool::instance().idle_workers());
   };
   read_all(bound, {});
   std::vector<PCIDevice> out;

@@ -41,6 +41,11 @@ size_t WorkerPool::workers() const {
   return threads_.size();
 }
 
+size_t WorkerPool::idle_workers() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return idle_.size();
+}
+
 void WorkerPool::ensure_workers(size_t n) {
   // Caller holds mu_.  `n` tasks are queued: make sure that many workers are
   // parked, being woken or starting (busy workers may be blocked in a nested

@@ -76,6 +76,9 @@ class WorkerPool {
   void parallel_for(size_t n, const std::function<void(size_t)>& fn, size_t max_parallel = 0);
 
   size_t workers() const;
+  // Workers parked right now (a lane given to one of them needs no thread
+  // to be created: in a fresh process that costs more than short work).
+  size_t idle_workers() const;
 
   // Workers follow the caller: follow_caller() (called by the thread about
   // to hand out work) keeps every worker on the CPUs that share the L3 cache

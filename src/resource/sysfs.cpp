@@ -275,9 +275,10 @@ std::shared_ptr<const SysfsManager::Topology> SysfsManager::read_topology() cons
   }
   std::vector<char> usable(nodes.size(), 0);
   constexpr size_t kChunk = 8;
+  fs::Dir top(topology_);  // "<id>/properties" relative to it: no path walk per node
   auto read_chunk = [&](size_t c) {
     for (size_t i = c * kChunk; i < std::min(nodes.size(), (c + 1) * kChunk); ++i) {
-      auto r = fs::read_file(fs::join(nodes[i].dir, "properties"));
+      auto r = top.read_attr((std::to_string(nodes[i].id) + "/properties").c_str());
       if (!r.ok()) continue;  // EPERM: GPU not allocated to this container
       parse_properties(r.data, nodes[i]);
       usable[i] = nodes[i].gfx_target_version != 0 && nodes[i].simd_count != 0;  // else a CPU node

@@ -31,35 +31,34 @@ bool is_pci_address(const std::string& name) {
 // a display (0x03) or processing-accelerator (0x12) function.  Every function
 // reached here is AMD's: amdgpu's and gim's ID tables name vendor 0x1002 only,
 // and a PF's VFs carry its vendor.
-std::optional<PCIDevice> read_function(const std::string& dir, const std::string& addr, const std::string& physfn) {
-  auto cls = fs::read_file(fs::join(dir, "class"), 64);
+std::optional<PCIDevice> read_function(const std::string& path, const std::string& addr, const std::string& physfn) {
+  fs::Dir dir(path);
+  auto cls = dir.read_attr("class", 64);
   if (!cls.ok()) throw Error("unable to read PCI device class for " + addr + ": " + fs::errno_str(cls.err));
   std::string c = str::trim(cls.data);
   if (!str::starts_with(c, "0x03") && !str::starts_with(c, "0x12")) return std::nullopt;
   PCIDevice d;
-  d.path = dir;
+  d.path = path;
   d.address = addr;
   d.vendor = kAmdVendorId;
   d.class_code = c.substr(0, 4);
-  d.device = fs::read_trimmed(fs::join(dir, "device")).value_or("");
-  if (auto t = fs::read_trimmed(fs::join(dir, "sriov_totalvfs")))
-    d.sriov_totalvfs = static_cast<int>(str::parse_uint(*t).value_or(0));
+  d.device = dir.read_trimmed("device").value_or("");
+  if (auto t = dir.read_trimmed("sriov_totalvfs")) d.sriov_totalvfs = static_cast<int>(str::parse_uint(*t).value_or(0));
   if (d.sriov_totalvfs == 0) {
     d.sriov_numvfs = 0;  // SR-IOV capable in name only
   } else if (d.sriov_totalvfs > 0) {
-    if (auto n = fs::read_trimmed(fs::join(dir, "sriov_numvfs")))
-      d.sriov_numvfs = static_cast<int>(str::parse_uint(*n).value_or(0));
-    if (d.sriov_numvfs > 0) d.sriov_vf_device = fs::read_trimmed(fs::join(dir, "sriov_vf_device")).value_or("");
+    if (auto n = dir.read_trimmed("sriov_numvfs")) d.sriov_numvfs = static_cast<int>(str::parse_uint(*n).value_or(0));
+    if (d.sriov_numvfs > 0) d.sriov_vf_device = dir.read_trimmed("sriov_vf_device").value_or("");
   }
   if (!physfn.empty()) {
     d.physfn = physfn;
   } else {
-    std::string link = fs::read_link(fs::join(dir, "physfn"));
+    std::string link = dir.read_link("physfn");
     if (!link.empty()) d.physfn = fs::basename(link);
   }
   // Configuration space only where sysfs publishes no SR-IOV state.
   if (d.sriov_totalvfs < 0 && d.physfn.empty()) {
-    auto cfg = fs::read_file(fs::join(dir, "config"), kPciExpressConfigSpaceSize);
+    auto cfg = dir.read_attr("config", kPciExpressConfigSpaceSize);
     if (!cfg.ok()) throw Error("unable to read PCI configuration space for " + addr + ": " + fs::errno_str(cfg.err));
     d.config = std::move(cfg.data);
   }

@@ -303,6 +303,55 @@ AttrReader& attrs() {
   return *reader;
 }
 
+Dir::Dir(const std::string& path) {
+  fd_ = ::open(path.c_str(), O_PATH | O_DIRECTORY | O_CLOEXEC);
+  if (fd_ < 0) err_ = errno;
+}
+
+Dir::~Dir() {
+  if (fd_ >= 0) ::close(fd_);
+}
+
+ReadResult Dir::read_attr(const char* name, size_t max_bytes) const {
+  ReadResult r;
+  if (fd_ < 0) {
+    r.err = err_;
+    return r;
+  }
+  int fd = ::openat(fd_, name, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) {
+    r.err = errno;
+    return r;
+  }
+  r.data.resize(max_bytes);
+  ssize_t n;
+  do {
+    n = ::read(fd, r.data.data(), max_bytes);
+  } while (n < 0 && errno == EINTR);
+  if (n < 0) {
+    r.err = errno;
+    r.data.clear();
+  } else {
+    r.data.resize(static_cast<size_t>(n));
+  }
+  ::close(fd);
+  return r;
+}
+
+std::optional<std::string> Dir::read_trimmed(const char* name) const {
+  auto r = read_attr(name);
+  if (!r.ok()) return std::nullopt;
+  return str::trim(r.data);
+}
+
+std::string Dir::read_link(const char* name) const {
+  if (fd_ < 0) return {};
+  char buf[PATH_MAX];
+  ssize_t n = ::readlinkat(fd_, name, buf, sizeof(buf) - 1);
+  if (n < 0) return {};
+  return std::string(buf, static_cast<size_t>(n));
+}
+
 std::string read_link(const std::string& path) {
   char buf[PATH_MAX];
   ssize_t n = ::readlink(path.c_str(), buf, sizeof(buf) - 1);

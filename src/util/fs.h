@@ -125,6 +125,28 @@ AttrReader& attrs();
 
 // readlink(2); empty on failure.
 std::string read_link(const std::string& path);
+
+// A directory opened once (O_PATH) whose entries are then read relative to
+// it: no path walk per attribute - a PCI function's sysfs path goes through
+// a symlink and a dozen components, which is most of a cold attribute read.
+class Dir {
+ public:
+  explicit Dir(const std::string& path);
+  ~Dir();
+  Dir(const Dir&) = delete;
+  Dir& operator=(const Dir&) = delete;
+  int err() const { return err_; }  // 0 if the directory was opened
+  // A sysfs attribute in one read(2): kernfs hands over the whole value (at
+  // most a page; a binary attribute up to `max_bytes`) in the first read,
+  // so no second read for end-of-file.
+  ReadResult read_attr(const char* name, size_t max_bytes = 4096) const;
+  std::optional<std::string> read_trimmed(const char* name) const;
+  std::string read_link(const char* name) const;
+
+ private:
+  int fd_ = -1;
+  int err_ = 0;
+};
 // Resolve `rel` under `root` the way a process chrooted at `root` would:
 // component by component, following symlinks, with absolute link targets
 // re-rooted under `root` (a host's /opt/rocm -> /opt/rocm-7.2.0 seen through

@@ -5,6 +5,7 @@
 #include <time.h>
 
 #include <cerrno>
+#include <cstdlib>
 #include <functional>
 #include <cstdio>
 
@@ -120,6 +121,19 @@ std::string SignalWatcher::name(int sig) {
 // ---------------------------------------------------------------------------
 // Labeling
 
+namespace {
+// GFD_CYCLE_TASKS=inline (an experiment switch, read once): the node facts
+// and the SR-IOV lookup run on the cycle thread instead of a worker, and
+// the preparer job is handed out after the write.
+bool cycle_tasks_inline() {
+  static const bool on = [] {
+    const char* v = std::getenv("GFD_CYCLE_TASKS");
+    return v && std::string(v) == "inline";
+  }();
+  return on;
+}
+}  // namespace
+
 CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov::Interface>& sriov,
                         const config::Config& config, const lm::LabelerPtr& timestamp, bool write) {
   trace::begin_cycle();
@@ -175,13 +189,20 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
   // the temporary file of a later cycle's write (lm::temp_preparer) - never
   // waited for, so it runs after the two even if this thread took them over.
   std::vector<WorkerPool::Task> seq;
+  std::function<void()> prepare_later;  // inline mode: handed out after the write
   {
     trace::Span span("submit");
-    std::vector<std::function<void()>> fns{read_facts, scan_sriov};
-    if (write && !config.oneshot())
-      if (auto prepare = lm::temp_preparer(config.output_file())) fns.push_back(std::move(prepare));
+    std::function<void()> prepare;
+    if (write && !config.oneshot()) prepare = lm::temp_preparer(config.output_file());
     submitted = trace::now_ns();
-    seq = WorkerPool::instance().submit_sequence(std::move(fns));
+    if (cycle_tasks_inline()) {
+      seq = {WorkerPool::local(read_facts), WorkerPool::local(scan_sriov)};
+      prepare_later = std::move(prepare);
+    } else {
+      std::vector<std::function<void()>> fns{read_facts, scan_sriov};
+      if (prepare) fns.push_back(std::move(prepare));
+      seq = WorkerPool::instance().submit_sequence(std::move(fns));
+    }
   }
   WorkerPool::Task facts_task = seq[0], sriov_task = seq[1];
   auto join_facts = [&]() -> const lm::NodeFacts& {
@@ -239,6 +260,7 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
   }
   r.total_ns = trace::now_ns() - t0;
   r.other_ns = r.total_ns - trace::top_level_ns();
+  if (prepare_later) WorkerPool::instance().submit(std::move(prepare_later));  // for a later cycle's write
   r.phases = trace::phases();
   r.cpu_end = sched_getcpu();
   return r;

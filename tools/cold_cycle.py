@@ -6,7 +6,8 @@
                                [--variants follow,none,l3] [--reps 3]
 
 Each variant is a daemon flag set (`--cpu-affinity=<v>` for a bare name, or
-a literal flag list with spaces); variants are run alternately, `reps`
+a literal list of flags and NAME=value environment settings, space-separated,
+e.g. "GFD_CYCLE_TASKS=inline"); variants are run alternately, `reps`
 times each, so a box-wide drift hits all of them alike.  Prints one JSON
 line per run and a summary per variant: p50 of the cycle total, of the
 unattributed time (`other`) and of every phase, over the cycles after the
@@ -29,8 +30,14 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def run_once(binary: str, flags: list[str], interval: str, cycles: int, extra: list[str]) -> dict:
     out = os.path.join(tempfile.mkdtemp(prefix="gfd-cold-"), "gfd")
+    # NAME=value tokens of a variant are environment variables.
+    env = dict(os.environ)
+    for f in [f for f in flags if not f.startswith("-") and "=" in f]:
+        k, v = f.split("=", 1)
+        env[k] = v
+    flags = [f for f in flags if f.startswith("-")]
     p = subprocess.Popen([binary, f"--sleep-interval={interval}", "--trace-timing", f"--output-file={out}", *extra,
-                          *flags], stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+                          *flags], stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True, env=env)
     rows = []
     try:
         for line in p.stderr:
@@ -82,7 +89,7 @@ def main() -> int:
     per: dict[str, list[dict]] = {v: [] for v in variants}
     for rep in range(a.reps):
         for v in variants:
-            flags = v.split() if " " in v or v.startswith("--") else [f"--cpu-affinity={v}"]
+            flags = v.split() if " " in v or v.startswith("--") or "=" in v else [f"--cpu-affinity={v}"]
             r = run_once(a.binary, flags, a.interval, a.cycles, extra)
             per[v].append(r)
             print(json.dumps({"variant": v, "rep": rep, **r}), flush=True)

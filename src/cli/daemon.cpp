@@ -121,19 +121,6 @@ std::string SignalWatcher::name(int sig) {
 // ---------------------------------------------------------------------------
 // Labeling
 
-namespace {
-// GFD_CYCLE_TASKS=inline (an experiment switch, read once): the node facts
-// and the SR-IOV lookup run on the cycle thread instead of a worker, and
-// the preparer job is handed out after the write.
-bool cycle_tasks_inline() {
-  static const bool on = [] {
-    const char* v = std::getenv("GFD_CYCLE_TASKS");
-    return v && std::string(v) == "inline";
-  }();
-  return on;
-}
-}  // namespace
-
 CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov::Interface>& sriov,
                         const config::Config& config, const lm::LabelerPtr& timestamp, bool write) {
   trace::begin_cycle();
@@ -188,21 +175,17 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
   // Loop mode: the same worker then unlinks the old feature file and creates
   // the temporary file of a later cycle's write (lm::temp_preparer) - never
   // waited for, so it runs after the two even if this thread took them over.
+  // On this thread instead (no hand-off; the preparer job after the write)
+  // measured slower both ways: cycles 1 s apart 0.362 vs 0.2555 ms, back to
+  // back 0.0295 vs 0.023 ms (profiles/cycle_tasks_ab_r4.txt).
   std::vector<WorkerPool::Task> seq;
-  std::function<void()> prepare_later;  // inline mode: handed out after the write
   {
     trace::Span span("submit");
-    std::function<void()> prepare;
-    if (write && !config.oneshot()) prepare = lm::temp_preparer(config.output_file());
+    std::vector<std::function<void()>> fns{read_facts, scan_sriov};
+    if (write && !config.oneshot())
+      if (auto prepare = lm::temp_preparer(config.output_file())) fns.push_back(std::move(prepare));
     submitted = trace::now_ns();
-    if (cycle_tasks_inline()) {
-      seq = {WorkerPool::local(read_facts), WorkerPool::local(scan_sriov)};
-      prepare_later = std::move(prepare);
-    } else {
-      std::vector<std::function<void()>> fns{read_facts, scan_sriov};
-      if (prepare) fns.push_back(std::move(prepare));
-      seq = WorkerPool::instance().submit_sequence(std::move(fns));
-    }
+    seq = WorkerPool::instance().submit_sequence(std::move(fns));
   }
   WorkerPool::Task facts_task = seq[0], sriov_task = seq[1];
   auto join_facts = [&]() -> const lm::NodeFacts& {
@@ -260,7 +243,6 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
   }
   r.total_ns = trace::now_ns() - t0;
   r.other_ns = r.total_ns - trace::top_level_ns();
-  if (prepare_later) WorkerPool::instance().submit(std::move(prepare_later));  // for a later cycle's write
   r.phases = trace::phases();
   r.cpu_end = sched_getcpu();
   return r;

@@ -177,13 +177,6 @@ WorkerPool::Task WorkerPool::submit(std::function<void()> fn) {
   return t;
 }
 
-WorkerPool::Task WorkerPool::local(std::function<void()> fn) {
-  Task t;
-  t.state_ = std::make_shared<Task::State>();
-  t.state_->fn = std::move(fn);
-  return t;
-}
-
 std::vector<WorkerPool::Task> WorkerPool::submit_sequence(std::vector<std::function<void()>> fns) {
   std::vector<Task> tasks(fns.size());
   std::vector<std::shared_ptr<Task::State>> states;

@@ -65,8 +65,6 @@ class WorkerPool {
 
   // Run fn on a worker (or on the thread that calls run_or_wait first).
   Task submit(std::function<void()> fn);
-  // A task no worker will run: it runs on the thread that calls run_or_wait.
-  static Task local(std::function<void()> fn);
   // Run fns in order on ONE worker (same core, warm cache); each is still a
   // Task of its own that the caller may run itself (run_or_wait) or drop
   // (cancel_or_wait) if the worker has not reached it yet.

@@ -1,8 +1,11 @@
 #!/bin/bash
 # The driver's headline (bench.py --steps 20 --warmup 5, in-process) for a
-# few variants, alternated: the round-3 tree (abtree/r3, when staged) and
-# the current tree with GFD_PREPARE_PER_JOB=2 (top up) / 1 (one file per
-# preparer job).  One JSON line per run: value and the write phases.
+# few variants, alternated: an older tree staged under abtree/<name>/
+# (bench.py, gpu_feature_discovery_amd/ with its _gfd .so, build/ daemon)
+# and the current tree.  Round 4 also ran the current tree with an
+# experiment switch (GFD_PREPARE_PER_JOB, since removed):
+# profiles/headline_ab_r4.txt.  One JSON line per run: value and the write
+# phases.
 # Usage (GPU box): tools/headline_ab.sh [reps] [steps] [warmup]
 set -o pipefail
 reps=${1:-4}; steps=${2:-20}; warm=${3:-5}
@@ -16,7 +19,8 @@ print(json.dumps({'variant': '$name', 'value': d['value'], 'p90': d['p90_ms'], '
   'create': p.get('write.create'), 'rename': p.get('write.rename')}))"
 }
 for i in $(seq $reps); do
-  [ -d abtree/r3 ] && { run r3 abtree/r3 X=1 || exit 1; }
-  run top2 . GFD_PREPARE_PER_JOB=2 || exit 1
-  run one . GFD_PREPARE_PER_JOB=1 || exit 1
+  for d in abtree/*/; do
+    [ -d "$d" ] && { run "$(basename "$d")" "$d" X=1 || exit 1; }
+  done
+  run current . X=1 || exit 1
 done

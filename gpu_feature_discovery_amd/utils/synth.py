@@ -256,6 +256,10 @@ def make_node(root: str | os.PathLike, spec: NodeSpec) -> Path:
         driver = g.driver
         if driver == "auto":
             driver = "gim" if g.sriov and spec.gim_version else "amdgpu"
+        _write(d / "uevent", (f"DRIVER={driver}\n" if driver else "") +
+               f"PCI_CLASS=120000\nPCI_ID=1002:{device_id:04X}\nPCI_SUBSYS_ID=1002:{device_id:04X}\n"
+               f"PCI_SLOT_NAME={bdf}\nMODALIAS=pci:v00001002d0000{device_id:04X}sv00001002sd0000{device_id:04X}"
+               "bc12sc00i00\n")
         if driver:
             drv = root / "sys/bus/pci/drivers" / driver
             drv.mkdir(parents=True, exist_ok=True)

@@ -31,18 +31,39 @@ bool is_pci_address(const std::string& name) {
 // a display (0x03) or processing-accelerator (0x12) function.  Every function
 // reached here is AMD's: amdgpu's and gim's ID tables name vendor 0x1002 only,
 // and a PF's VFs carry its vendor.
+// Class and device ID from the function's `uevent` (PCI_CLASS=120000,
+// PCI_ID=1002:75A3): one read instead of `class` and `device`.
+bool from_uevent(const fs::Dir& dir, std::string* cls, std::string* device) {
+  auto r = dir.read_attr("uevent");
+  if (!r.ok()) return false;
+  std::string c, id;
+  for (const auto& line : str::split(r.data, '\n')) {
+    if (str::starts_with(line, "PCI_CLASS=")) c = line.substr(10);
+    if (str::starts_with(line, "PCI_ID=")) id = line.substr(7);
+  }
+  auto colon = id.find(':');
+  if (c.empty() || colon == std::string::npos) return false;
+  *cls = "0x" + str::to_lower(c);
+  *device = "0x" + str::to_lower(id.substr(colon + 1));
+  return true;
+}
+
 std::optional<PCIDevice> read_function(const std::string& path, const std::string& addr, const std::string& physfn) {
   fs::Dir dir(path);
-  auto cls = dir.read_attr("class", 64);
-  if (!cls.ok()) throw Error("unable to read PCI device class for " + addr + ": " + fs::errno_str(cls.err));
-  std::string c = str::trim(cls.data);
+  std::string c, device;
+  bool have_device = from_uevent(dir, &c, &device);
+  if (!have_device) {
+    auto cls = dir.read_attr("class", 64);
+    if (!cls.ok()) throw Error("unable to read PCI device class for " + addr + ": " + fs::errno_str(cls.err));
+    c = str::trim(cls.data);
+  }
   if (!str::starts_with(c, "0x03") && !str::starts_with(c, "0x12")) return std::nullopt;
   PCIDevice d;
   d.path = path;
   d.address = addr;
   d.vendor = kAmdVendorId;
   d.class_code = c.substr(0, 4);
-  d.device = dir.read_trimmed("device").value_or("");
+  d.device = have_device ? device : dir.read_trimmed("device").value_or("");
   if (auto t = dir.read_trimmed("sriov_totalvfs")) d.sriov_totalvfs = static_cast<int>(str::parse_uint(*t).value_or(0));
   if (d.sriov_totalvfs == 0) {
     d.sriov_numvfs = 0;  // SR-IOV capable in name only
@@ -52,7 +73,9 @@ std::optional<PCIDevice> read_function(const std::string& path, const std::strin
   }
   if (!physfn.empty()) {
     d.physfn = physfn;
-  } else {
+  } else if (d.sriov_totalvfs < 0) {
+    // Only a function without an SR-IOV capability of its own can be a VF
+    // (a PF's VFs have none; every PF that has one publishes sriov_totalvfs).
     std::string link = dir.read_link("physfn");
     if (!link.empty()) d.physfn = fs::basename(link);
   }

@@ -638,7 +638,14 @@ void bind_driver(const std::string& root, const std::string& driver, const std::
 // VFs to gim, its VFs named by virtfn links (and bound to nothing).
 std::string bound_host(int filler, int vfs) {
   std::string root = pci_host(filler, vfs);
-  for (int g = 0; g < 4; ++g) bind_driver(root, "amdgpu", str::format("0000:%02x:00.0", 0x11 + 0x10 * g));
+  for (int g = 0; g < 4; ++g) {
+    std::string bdf = str::format("0000:%02x:00.0", 0x11 + 0x10 * g);
+    bind_driver(root, "amdgpu", bdf);
+    // The 4 plain PFs carry a uevent (class and ID in one read); the PF with
+    // VFs does not, so both ways of reading them are compared below.
+    put_file(root + "/sys/bus/pci/devices/" + bdf + "/uevent",
+             "DRIVER=amdgpu\nPCI_CLASS=120000\nPCI_ID=1002:75A3\nPCI_SLOT_NAME=" + bdf + "\n");
+  }
   bind_driver(root, "gim", "0000:c1:00.0");
   std::string pf = root + "/sys/bus/pci/devices/0000:c1:00.0/";
   for (int v = 0; v < vfs; ++v)

@@ -10,17 +10,19 @@ scan) and atomically rewrite the NFD feature file.  Nothing is cached across
 steps except what the daemon itself keeps between its cycles, listed with
 the reason each is safe in docs/ARCHITECTURE.md ("What is kept between
 cycles"): the loaded library, the persistent amd-smi session's handles and
-the facts fixed until the KFD topology generation changes (virtualization
-mode, KFD node id and XCD count), open descriptors of sysfs attributes, and
-the PCI bus listing while no device was added or removed.  Every other
+the facts fixed until the KFD topology generation changes (ASIC identity,
+virtualization mode, KFD node id and XCD count), open descriptors of sysfs
+attributes, and the SR-IOV functions while no uevent was sent (no device
+added, removed, bound or unbound).  Every other
 device value - memory, partition modes, xGMI links, partition
 capabilities, versions, machine type - is read from the driver each step.
 
 The label set of every step is checked for correctness (count == N GPUs,
 gfx950/cdna4 arch, MI355 product, HBM size, valid Kubernetes label syntax)
 before timing is reported.  The in-process session runs the daemon's default
-configuration: no CPU pinning (that is the daemon's opt-in
---cpu-affinity=l3), workers that block when idle.
+configuration: workers follow the cycle thread's L3 domain
+(--cpu-affinity=follow), block when idle, and prepare the next writes'
+temporary files.
 
 N>1: launched by the driver as one process per GPU under torch.distributed
 (gloo, 127.0.0.1); rank 0 labels the node restricted to GPUs 0..N-1 (the

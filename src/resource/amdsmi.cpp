@@ -479,9 +479,27 @@ std::string checked_bdf(AmdSmiLib& L, const std::string& root, amdsmi_processor_
 // as amd-smi listed it), ordered by parent PCI function; every processor's
 // gpu_bdf set.  `parents` caches the parent function per group for the
 // session (resolve_parent_bdf reads sysfs).
+using IdentityCache = std::map<void*, AmdSmiManager::Identity>;
+
+// Fills p's identity from the session cache; true if it was there.
+static bool identity_from_cache(const IdentityCache& cache, ProcInfo& p) {
+  auto it = cache.find(p.h);
+  if (it == cache.end()) return false;
+  const auto& id = it->second;
+  p.market_name = id.market_name;
+  p.vendor_id = id.vendor_id;
+  p.device_id = id.device_id;
+  p.cus = id.cus;
+  p.gfx = id.gfx;
+  p.uuid = id.uuid;
+  p.identified = true;
+  return true;
+}
+
 static std::vector<std::vector<ProcInfo>> collect_physical_gpus(AmdSmiLib& L, const std::string& root,
                                                                 std::map<std::string, std::string>& parents,
-                                                                std::map<void*, std::string>& proc_bdfs) {
+                                                                std::map<void*, std::string>& proc_bdfs,
+                                                                const IdentityCache& identities) {
   uint32_t ns = 0;
   amdsmi_status_t st = L.get_socket_handles(&ns, nullptr);
   if (st != AMDSMI_STATUS_SUCCESS) call_failed(L, "amdsmi_get_socket_handles", st);
@@ -520,6 +538,7 @@ static std::vector<std::vector<ProcInfo>> collect_physical_gpus(AmdSmiLib& L, co
       ProcInfo p;
       p.h = h;
       p.bdf = known->second;
+      identity_from_cache(identities, p);
       slots[bdf_slot(p.bdf)].push_back(p);
     }
   }
@@ -589,6 +608,7 @@ void AmdSmiManager::library_init() {
   partition_facts_.clear();
   parent_bdf_.clear();
   proc_bdf_.clear();
+  identity_.clear();
   ++init_count_;
 }
 
@@ -654,7 +674,7 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
   AmdSmiLib& L = *lib_;
   trace::Span span("amdsmi.snapshot");
   int64_t handles_t0 = trace::now_ns();
-  std::vector<std::vector<ProcInfo>> physical = collect_physical_gpus(L, opts_.root, parent_bdf_, proc_bdf_);
+  std::vector<std::vector<ProcInfo>> physical = collect_physical_gpus(L, opts_.root, parent_bdf_, proc_bdf_, identity_);
   trace::record("amdsmi.handles", trace::now_ns() - handles_t0);
 
   // Apply the visible-device filter on physical GPUs (index = parent BDF order).
@@ -764,6 +784,9 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
   trace::record("amdsmi.proc", proc_ns);
   trace::record("amdsmi.extras", caps_ns);
   for (const auto& g : gpus) {
+    for (const auto& p : *g.procs)
+      if (p.identified && !identity_.count(p.h))
+        identity_[p.h] = Identity{p.market_name, p.vendor_id, p.device_id, p.cus, p.gfx, p.uuid};
     if (!g.extras.virtualization.empty()) virt_mode_[g.bdf] = g.extras.virtualization;
     if (g.kfd.node_id != kNoNode) kfd_node_[g.bdf] = g.kfd;
     for (const auto& f : g.parts)

@@ -85,6 +85,13 @@ class AmdSmiManager : public Manager {
     int sdma = -1;
     uint64_t mem_bytes = 0;
   };
+  // Per-session ASIC identity of one processor (see identity_).
+  struct Identity {
+    std::string market_name;
+    uint32_t vendor_id = 0, device_id = 0, cus = 0;
+    uint64_t gfx = 0;
+    std::string uuid;
+  };
 
  private:
   std::vector<DevicePtr> snapshot();
@@ -134,6 +141,14 @@ class AmdSmiManager : public Manager {
   // it could not load libdrm_amdgpu, returns uninitialised bytes with
   // success (measured on the pool).  Also saves the call on every cycle.
   std::map<void*, std::string> proc_bdf_;
+  // ASIC identity of each processor (by handle) for the lifetime of one
+  // session: market name (after the FRU fallback), vendor / device ID, CU
+  // count, gfx target and the UUID derived from the ASIC serial - read-only
+  // properties of the ASIC, and a partition's CU count changes only with a
+  // partition switch, which re-initialises the session.  amdsmi_get_gpu_asic_info
+  // was the costliest call left in a cycle (17-28 us after an idle second,
+  // profiles/amdsmi_calls_cold_r4.txt).
+  std::map<void*, Identity> identity_;
   // The physical GPUs (BDFs, index order) the device filter was last checked against.
   std::vector<std::string> selected_from_;
 };

@@ -16,6 +16,7 @@
 #include "config/config.h"
 #include "lm/resource.h"
 #include "resource/amdsmi.h"
+#include "resource/managers.h"
 #include "resource/factory.h"
 #include "test.h"
 #include "util/fs.h"
@@ -271,6 +272,35 @@ TEST(AmdSmiFake_VirtualizationModeQueriedOncePerSession) {
     pc.Shutdown();
   }
   EXPECT_EQ(fake().virt_calls() - v0, 5);
+  fs::remove_all(root);
+}
+
+TEST(AmdSmiFake_AsicIdentityQueriedOncePerSession) {
+  // amdsmi_get_gpu_asic_info (market name, IDs, CUs, gfx target, serial):
+  // once per processor per session - 1 + 8 processors here - not per cycle,
+  // and again after a re-initialisation.
+  REQUIRE_FAKE();
+  fake().configure(kTwoGpus);
+  std::string root = temp_root();
+  set_generation(root, "1");
+  long a0 = fake().calls("amdsmi_get_gpu_asic_info");
+  AmdSmiManager m(opts(root, true));
+  std::string first;
+  for (int c = 0; c < 4; ++c) {
+    m.Init();
+    auto devs = m.GetDevices();
+    m.Shutdown();
+    std::string d = device_summary(devs);
+    if (c == 0) first = d;
+    EXPECT_EQ(d, first);  // the cached identity describes the GPUs the same way
+    EXPECT_EQ(devs[1]->GetName(), devs[1]->Info().name);
+  }
+  EXPECT_EQ(fake().calls("amdsmi_get_gpu_asic_info") - a0, 9L);
+  set_generation(root, "2");  // partition switch / driver reload: new session
+  m.Init();
+  m.GetDevices();
+  m.Shutdown();
+  EXPECT_EQ(fake().calls("amdsmi_get_gpu_asic_info") - a0, 18L);
   fs::remove_all(root);
 }
 

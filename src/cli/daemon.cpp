@@ -189,7 +189,9 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
   }
   WorkerPool::Task facts_task = seq[0], sriov_task = seq[1];
   auto join_facts = [&]() -> const lm::NodeFacts& {
+    int64_t w0 = trace::now_ns();
     facts_task.run_or_wait();
+    trace::record("facts.wait", trace::now_ns() - w0);  // inside "label"
     return facts;
   };
   lm::LabelerPtr device;

@@ -224,6 +224,12 @@ LabelerPtr NewDeviceLabeler(resource::Manager& manager, const config::Config& co
   if (devices.empty()) return empty();
 
   trace::Span span("label");
+  // The device-derived labelers first: the node facts are read on a worker
+  // meanwhile (daemon.cpp label_cycle), and are joined only when this
+  // thread has nothing else to do.
+  auto capability = GFD_WRAP("error creating partition capability labeler", NewPartitionCapabilityLabeler(manager));
+  auto topology = GFD_WRAP("error creating topology labeler", NewTopologyLabeler(manager));
+  auto resources = GFD_WRAP("error creating resource labeler", NewResourceLabeler(manager, config));
   const NodeFacts* pre = facts ? &facts() : nullptr;
   LabelerPtr machine, version;
   if (pre) {
@@ -242,9 +248,6 @@ LabelerPtr NewDeviceLabeler(resource::Manager& manager, const config::Config& co
   } else {
     version = GFD_WRAP("failed to construct version labeler", NewVersionLabeler(manager));
   }
-  auto capability = GFD_WRAP("error creating partition capability labeler", NewPartitionCapabilityLabeler(manager));
-  auto topology = GFD_WRAP("error creating topology labeler", NewTopologyLabeler(manager));
-  auto resources = GFD_WRAP("error creating resource labeler", NewResourceLabeler(manager, config));
   return merge({machine, version, capability, topology, resources});
 }
 

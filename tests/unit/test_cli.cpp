@@ -247,8 +247,8 @@ TEST(LabelCycle_RecordsPhases) {
   auto r = label_cycle(m, sriov::new_empty_sriov(), c, ts, false);
   std::vector<std::string> names;
   for (const auto& p : r.phases) names.push_back(p.first);
-  EXPECT_EQ(names, (std::vector<std::string>{"placement", "versions", "submit", "init", "enumerate", "label",
-                                             "shutdown", "sriov.join", "facts.start", "facts(overlapped)",
+  EXPECT_EQ(names, (std::vector<std::string>{"placement", "versions", "submit", "init", "enumerate", "facts.wait",
+                                             "label", "shutdown", "sriov.join", "facts.start", "facts(overlapped)",
                                              "sriov(overlapped)", "merge"}));
   // Every top-level phase is named: what is left is bookkeeping.
   EXPECT_TRUE(r.other_ns >= 0 && r.other_ns < r.total_ns);

@@ -30,11 +30,15 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def run_once(binary: str, flags: list[str], interval: str, cycles: int, extra: list[str]) -> dict:
     out = os.path.join(tempfile.mkdtemp(prefix="gfd-cold-"), "gfd")
-    # NAME=value tokens of a variant are environment variables.
+    # NAME=value tokens of a variant are environment variables; BIN=<path>
+    # runs another daemon binary (e.g. an older build staged for an A/B).
     env = dict(os.environ)
     for f in [f for f in flags if not f.startswith("-") and "=" in f]:
         k, v = f.split("=", 1)
-        env[k] = v
+        if k == "BIN":
+            binary = v
+        else:
+            env[k] = v
     flags = [f for f in flags if f.startswith("-")]
     p = subprocess.Popen([binary, f"--sleep-interval={interval}", "--trace-timing", f"--output-file={out}", *extra,
                           *flags], stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True, env=env)

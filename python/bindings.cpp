@@ -115,14 +115,27 @@ class Session {
     config_.amdsmi_library_only = amdsmi_library_only;
     WorkerPool::instance().set_follow(ctx.String("cpu-affinity") == "follow");
     if (!config_.oneshot()) WorkerPool::instance().load_topology();
-    manager_ = resource::new_manager(config_);
+    // As cli::start does: the first SR-IOV scan runs on a worker while the
+    // backend is selected (and, here, while the caller does whatever it does
+    // before the first cycle).
     sriov_ = sriov::new_sriov_lib(config_.sysfs_root());
+    auto lib = sriov_;
+    prefetch_ = WorkerPool::instance().submit([lib] {
+      try {
+        lib->Devices();
+      } catch (...) {
+      }
+    });
+    manager_ = resource::new_manager(config_);
     timestamp_ = lm::NewTimestampLabeler(config_);
   }
   // A loop-mode session's cycles leave the next cycle's temporary file
   // prepared and the old feature file to unlink (lm::temp_preparer); do not
   // leave them behind.
-  ~Session() { lm::discard_prepared_temps(); }
+  ~Session() {
+    prefetch_.cancel_or_wait();
+    lm::discard_prepared_temps();
+  }
   Session(const Session&) = delete;
   Session& operator=(const Session&) = delete;
 
@@ -188,6 +201,7 @@ class Session {
 
  private:
   config::Config config_;
+  WorkerPool::Task prefetch_;
   resource::ManagerPtr manager_;
   std::shared_ptr<sriov::Interface> sriov_;
   lm::LabelerPtr timestamp_;

@@ -317,6 +317,20 @@ void start(const Context& ctx, SignalWatcher& sigs) {
       throw Error(std::string("unable to load config: ") + e.what());
     }
     config::disable_resource_renaming(c);
+    // The first SR-IOV scan (every amdgpu/gim-bound function, ~0.3 ms in a
+    // fresh process) starts now, on a worker, while this thread logs the
+    // configuration and selects the backend; the first cycle then finds its
+    // result kept (unchanged uevent counter) or waits for it to finish.
+    auto sriov = sriov::new_sriov_lib(c.sysfs_root());
+    struct Prefetch {  // never outlives this iteration (an error exits the process)
+      WorkerPool::Task task;
+      ~Prefetch() { task.cancel_or_wait(); }
+    } prefetch{WorkerPool::instance().submit([sriov] {
+      try {
+        sriov->Devices();
+      } catch (...) {  // the cycle's own scan reports it
+      }
+    })};
     log::printf("\nRunning with config:\n%s", config::to_json(c).c_str());
     // A process killed without its exit cleanup (OOM, SIGKILL, node crash)
     // left its temporary files in <dir>/gfd-tmp: remove them before the
@@ -338,7 +352,6 @@ void start(const Context& ctx, SignalWatcher& sigs) {
     bool restart;
     {
       resource::ManagerPtr manager = resource::new_manager(c);
-      auto sriov = sriov::new_sriov_lib(c.sysfs_root());
       if (!g_timeline.manager_ns) g_timeline.manager_ns = trace::now_ns();
 
       log::printf("Start running");

@@ -65,6 +65,7 @@ std::optional<Info> Lib::Classify(const PCIDevice& d) {
 
 std::vector<Function> Lib::Devices() {
   std::vector<PCIDevice> devices;
+  std::lock_guard<std::mutex> lk(mu_);
   try {
     devices = pci_->Devices();
   } catch (const std::exception& e) {

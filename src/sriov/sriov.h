@@ -23,6 +23,7 @@
 #pragma once
 
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -77,6 +78,8 @@ class Interface {
 class Lib : public Interface {
  public:
   explicit Lib(std::shared_ptr<AmdPCI> pci, std::string root = "") : pci_(std::move(pci)), root_(std::move(root)) {}
+  // Thread-safe (one scan at a time): the daemon may start the first scan on
+  // a worker while it selects the backend (cli::start).
   std::vector<Function> Devices() override;
   // <root>/sys/module/gim/version (no root: not looked up).
   std::optional<std::string> HostDriverVersion() override;
@@ -86,6 +89,7 @@ class Lib : public Interface {
  private:
   std::shared_ptr<AmdPCI> pci_;
   std::string root_;
+  std::mutex mu_;
 };
 
 std::shared_ptr<Interface> new_sriov_lib(const std::string& root);

@@ -131,6 +131,10 @@ def _time_variant(args: list[str], steps: int, warmup: int) -> dict:
             "mean_ms": round(statistics.fmean(ms), 4), "backend": r["backend"]}
 
 
+_ROW_PHASES = ("submit", "init", "enumerate", "label", "facts.wait", "sriov.join", "merge", "log", "write", "other",
+               "facts.start", "facts(overlapped)", "total")
+
+
 def _daemon_loop(binary: str, args: list[str], cycles: int, interval: str = "2ms",
                  env: dict | None = None) -> dict:
     """The production path: the daemon binary in loop mode, timing every
@@ -141,13 +145,17 @@ def _daemon_loop(binary: str, args: list[str], cycles: int, interval: str = "2ms
 
     p = subprocess.Popen([binary, f"--sleep-interval={interval}", "--trace-timing", *args], stdout=subprocess.DEVNULL,
                          stderr=subprocess.PIPE, text=True, env={**os.environ, **(env or {})})
-    totals, phases, cpus = [], {}, []
+    totals, phases, cpus, rows = [], {}, [], []
     try:
         for line in p.stderr:
             if "Timing:" in line:
                 fields = dict(kv.split("=", 1) for kv in line.split("Timing:", 1)[1].split())
                 cpus.append(fields.pop("cpu", ""))
                 totals.append(float(fields["total"].rstrip("ms")))
+                # Per cycle: the cycle thread's top-level phases and the
+                # overlapped node facts (where a slow cycle spent its time).
+                rows.append({k: float(v.rstrip("ms")) for k, v in fields.items()
+                             if k in _ROW_PHASES})
                 if len(totals) > 1:
                     for k, v in fields.items():
                         phases.setdefault(k, []).append(float(v.rstrip("ms")))
@@ -170,6 +178,7 @@ def _daemon_loop(binary: str, args: list[str], cycles: int, interval: str = "2ms
             "cycle_cpus": cpus,
             "cpu_moves": sum(1 for a, b in zip(starts, starts[1:]) if a != b),
             "totals_ms": totals,
+            "rows_ms": rows if interval != "2ms" else None,
             "phases_p50_ms": {k: round(_percentile(v, 0.5), 4) for k, v in phases.items() if k != "total"}}
 
 

@@ -143,6 +143,38 @@ std::vector<PCIDevice> BoundAmdPCI::scan_bound(const std::vector<std::string>& b
   return out;
 }
 
+std::vector<std::pair<std::string, uint64_t>> BoundAmdPCI::list_bound() const {
+  std::vector<std::pair<std::string, uint64_t>> bound;
+  for (const auto& drv : drivers())
+    for (auto& e : fs::list_dir_ino(fs::join(root_, "sys/bus/pci/drivers/" + drv)))
+      if (is_pci_address(e.first)) bound.push_back(std::move(e));
+  std::sort(bound.begin(), bound.end());
+  bound.erase(std::unique(bound.begin(), bound.end(),
+                          [](const auto& a, const auto& b) { return a.first == b.first; }),
+              bound.end());
+  return bound;
+}
+
+bool BoundAmdPCI::still_valid(const std::vector<std::pair<std::string, uint64_t>>& bound) const {
+  if (!have_ || fell_back_ || bound != bound_) return false;
+  for (const auto& d : last_) {
+    if (d.sriov_totalvfs <= 0) continue;
+    auto n = fs::attrs().read_trimmed(fs::join(d.path, "sriov_numvfs"));
+    if (!n || static_cast<int>(str::parse_uint(*n).value_or(0)) != d.sriov_numvfs) return false;
+    if (d.sriov_numvfs <= 0) continue;
+    // Its VFs: one of them removed on its own (`remove`) leaves NumVFs as it was.
+    std::vector<std::string> now, kept;
+    for (const auto& e : fs::list_dir(d.path))
+      if (e.rfind("virtfn", 0) == 0) now.push_back(fs::basename(fs::read_link(fs::join(d.path, e))));
+    for (const auto& v : last_)
+      if (v.physfn == d.address) kept.push_back(v.address);
+    std::sort(now.begin(), now.end());
+    std::sort(kept.begin(), kept.end());
+    if (now != kept) return false;
+  }
+  return true;
+}
+
 std::vector<PCIDevice> BoundAmdPCI::Devices() {
   int64_t t0 = trace::now_ns();
   // A booted kernel has sent thousands of uevents; "" or "0" is an emulated
@@ -153,12 +185,13 @@ std::vector<PCIDevice> BoundAmdPCI::Devices() {
     trace::record("pci.bound(kept)", trace::now_ns() - t0);
     return fell_back_ && fallback_ ? fallback_->Devices() : last_;
   }
-  std::vector<std::string> bound;
-  for (const auto& drv : drivers())
-    for (auto& name : fs::list_dir(fs::join(root_, "sys/bus/pci/drivers/" + drv)))
-      if (is_pci_address(name)) bound.push_back(std::move(name));
-  std::sort(bound.begin(), bound.end());
-  bound.erase(std::unique(bound.begin(), bound.end()), bound.end());
+  auto bound = list_bound();
+  if (seqnum && still_valid(bound)) {
+    // The counter moved for some other device (a container's veth...).
+    seqnum_ = *seqnum;
+    trace::record("pci.bound(checked)", trace::now_ns() - t0);
+    return last_;
+  }
   trace::record("pci.drivers", trace::now_ns() - t0);
   std::vector<PCIDevice> out;
   if (bound.empty()) {
@@ -169,12 +202,15 @@ std::vector<PCIDevice> BoundAmdPCI::Devices() {
     if (fallback_) out = fallback_->Devices();
   } else {
     int64_t t1 = trace::now_ns();
-    out = scan_bound(bound);
+    std::vector<std::string> names;
+    for (const auto& e : bound) names.push_back(e.first);
+    out = scan_bound(names);
     trace::record("pci.bound", trace::now_ns() - t1);
     fell_back_ = false;
     last_ = out;
   }
   have_ = true;
+  bound_ = std::move(bound);
   seqnum_ = seqnum.value_or("");
   return out;
 }

@@ -22,7 +22,13 @@
 //
 // Like the full scan, the result is kept while /sys/kernel/uevent_seqnum is
 // unchanged: binding, unbinding, adding or removing a function (VFs
-// included, so any NumVFs change) sends a uevent.
+// included, so any NumVFs change) sends a uevent.  A moved counter is not
+// enough to re-read everything - every container start on a node (veth,
+// loop and cgroup devices) sends uevents too: measured on the pool, 4 of 11
+// cycles 1 s apart found it moved and paid a 0.25 ms re-read.  So the
+// driver directories are re-listed (names and inode numbers: a function
+// removed and re-added under the same address gets a new entry) and the
+// PFs' NumVFs re-read; only a difference in either re-reads the functions.
 #pragma once
 
 #include <memory>
@@ -48,11 +54,16 @@ class BoundAmdPCI : public AmdPCI {
 
  private:
   std::vector<PCIDevice> scan_bound(const std::vector<std::string>& bound);
+  // (address, inode) of every function in the driver directories, sorted.
+  std::vector<std::pair<std::string, uint64_t>> list_bound() const;
+  // Whether last_ still describes the node: same bound functions, same NumVFs.
+  bool still_valid(const std::vector<std::pair<std::string, uint64_t>>& bound) const;
   std::string root_;
   std::shared_ptr<AmdPCI> fallback_;
   bool have_ = false;
   bool fell_back_ = false;
   std::string seqnum_;  // /sys/kernel/uevent_seqnum of the kept result
+  std::vector<std::pair<std::string, uint64_t>> bound_;  // list_bound() of the kept result
   std::vector<PCIDevice> last_;
 };
 

@@ -739,6 +739,28 @@ TEST(Bound_KeptWhileUeventSeqnumUnchanged) {
   // ...until the seqnum moves.
   put_file(root + "/sys/kernel/uevent_seqnum", "4243\n");
   EXPECT_EQ(bound.Devices().size(), static_cast<size_t>(6));
+  // A counter that moved for another device (a container's veth, say):
+  // the functions are not read again - here one whose class has become
+  // unreadable would make a re-read fail.
+  fs::remove_all(root + "/sys/bus/pci/devices/0000:11:00.0/class");
+  fs::mkdir_all(root + "/sys/bus/pci/devices/0000:11:00.0/class");
+  put_file(root + "/sys/kernel/uevent_seqnum", "4300\n");
+  EXPECT_EQ(bound.Devices().size(), static_cast<size_t>(6));
+  fs::remove_all(root + "/sys/bus/pci/devices/0000:11:00.0/class");
+  put_file(root + "/sys/bus/pci/devices/0000:11:00.0/class", "0x120000\n");
+  // A function removed and re-added under the same address (a new entry in
+  // the driver directory) is read again.
+  fs::remove_all(root + "/sys/bus/pci/drivers/amdgpu/0000:21:00.0");
+  put_file(root + "/sys/bus/pci/drivers/amdgpu/placeholder", "");  // takes the freed inode number (kernfs never reuses one)
+  bind_driver(root, "amdgpu", "0000:21:00.0");
+  put_file(root + "/sys/bus/pci/devices/0000:21:00.0/device", "0x75a0\n");
+  fs::remove_all(root + "/sys/bus/pci/devices/0000:21:00.0/uevent");
+  put_file(root + "/sys/kernel/uevent_seqnum", "4301\n");
+  auto devs = bound.Devices();
+  EXPECT_EQ(devs.size(), static_cast<size_t>(6));
+  bool seen = false;
+  for (const auto& d : devs) seen |= d.address == "0000:21:00.0" && d.device == "0x75a0";
+  EXPECT_TRUE(seen);
   // An emulated sysfs that never counts ("0") is re-read every time.
   put_file(root + "/sys/kernel/uevent_seqnum", "0\n");
   fs::remove_all(root + "/sys/bus/pci/devices/0000:c1:00.0/virtfn0");

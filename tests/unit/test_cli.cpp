@@ -10,6 +10,7 @@
 #include "sriov/sriov.h"
 #include "test.h"
 #include "util/fs.h"
+#include "util/log.h"
 
 using namespace gfd;
 using namespace gfd::cli;
@@ -254,4 +255,57 @@ TEST(LabelCycle_RecordsPhases) {
   EXPECT_TRUE(r.other_ns >= 0 && r.other_ns < r.total_ns);
   EXPECT_TRUE(r.total_ns > 0);
   EXPECT_EQ(r.labels["amd.com/gfd.timestamp"], std::string("1"));
+}
+
+namespace {
+// Runs fn with stderr redirected to a temporary file; returns what it wrote
+// so far each time `peek` is called, and everything at the end.
+struct StderrCapture {
+  char path[32] = "/tmp/gfd-stderr-XXXXXX";
+  int fd = -1, saved = -1;
+  StderrCapture() {
+    fd = mkstemp(path);
+    fflush(stderr);
+    saved = dup(2);
+    dup2(fd, 2);
+  }
+  std::string peek() {
+    fflush(stderr);
+    return fs::read_file(path).data;
+  }
+  ~StderrCapture() {
+    fflush(stderr);
+    dup2(saved, 2);
+    close(saved);
+    close(fd);
+    unlink(path);
+  }
+};
+}  // namespace
+
+TEST(LogHold_WritesTheCycleLinesTogetherInOrder) {
+  bool was = log::set_quiet(false);
+  std::string held, after, nested;
+  {
+    StderrCapture cap;
+    {
+      log::Hold hold;
+      log::printf("Writing labels to output file");
+      log::printf("Sleeping for %s", "60s");
+      held = cap.peek();  // nothing yet
+      hold.flush();
+      after = cap.peek();
+      {
+        log::Hold inner;  // nested: the outer one writes
+        log::printf("inner");
+      }
+      nested = cap.peek();
+    }
+    nested = cap.peek();
+  }
+  log::set_quiet(was);
+  EXPECT_EQ(held, std::string(""));
+  auto a = after.find("Writing labels to output file"), b = after.find("Sleeping for 60s");
+  EXPECT_TRUE(a != std::string::npos && b != std::string::npos && a < b);
+  EXPECT_TRUE(nested.find("inner") != std::string::npos);
 }

@@ -23,6 +23,7 @@
 #include "resource/factory.h"
 #include "resource/managers.h"
 #include "resource/sysfs.h"
+#include "sriov/bound.h"
 #include "sriov/sriov.h"
 #include "util/duration.h"
 #include "util/error.h"
@@ -225,6 +226,39 @@ PYBIND11_MODULE(_gfd, m) {
     bool ok = resource::has_amdsmi(&reason);
     return py::make_tuple(ok, reason);
   });
+  // The SR-IOV function sources side by side: "bound" (the daemon's: the
+  // functions amdgpu / gim bind and their VFs) or "bus" (every function on
+  // the PCI bus, the reference's approach and the daemon's fallback).
+  m.def(
+      "pci_functions",
+      [](const std::string& root, const std::string& source) {
+        std::vector<sriov::PCIDevice> devs;
+        {
+          py::gil_scoped_release nogil;
+          if (source == "bound") {
+            devs = sriov::BoundAmdPCI(root).Devices();
+          } else if (source == "bus") {
+            devs = sriov::SysfsAmdPCI(root).Devices();
+          } else {
+            throw Error("unknown PCI function source '" + source + "' (expected bound or bus)");
+          }
+        }
+        py::list out;
+        for (const auto& d : devs) {
+          py::dict o;
+          o["address"] = d.address;
+          o["device"] = d.device;
+          o["class"] = d.class_code;
+          o["sriov_totalvfs"] = d.sriov_totalvfs;
+          o["sriov_numvfs"] = d.sriov_numvfs;
+          o["sriov_vf_device"] = d.sriov_vf_device;
+          o["physfn"] = d.physfn;
+          o["config_bytes"] = d.config.size();
+          out.append(o);
+        }
+        return out;
+      },
+      py::arg("root") = "/", py::arg("source") = "bound");
   m.def("parse_duration", &parse_duration);
   m.def("format_duration", &format_duration);
   m.def("parse_yaml", [](const std::string& text) { return node_to_py(yaml::parse(text)); });

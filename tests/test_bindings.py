@@ -90,3 +90,30 @@ def test_session_errors_surface(native, tmp_path):
     s = native.Session(["--backend=sysfs", f"--sysfs-root={tmp_path}", "--output-file="])
     with pytest.raises(native.GfdError, match="KFD topology not available"):
         s.cycle(False)
+
+
+@pytest.mark.parametrize("kind", ["spx8", "sriov-host", "sriov-host-privileged", "guest-vf", "guest-vf-unbound"])
+def test_bound_sriov_source_matches_the_whole_bus(native, tmp_path, kind):
+    """The daemon's SR-IOV source (the functions amdgpu / gim bind, plus
+    their VFs) hands the labeler the same functions, field for field, as the
+    reference-style scan of the whole PCI bus - on nodes of every SR-IOV
+    shape (sriov/bound.h).  A guest whose amdgpu is not loaded has nothing
+    bound: the daemon then falls back to the bus scan, which this source on
+    its own reports as nothing."""
+    gim = None
+    if kind == "spx8":
+        gpus = [synth.GpuSpec() for _ in range(8)]
+    elif kind.startswith("sriov-host"):
+        gpus = [synth.GpuSpec(sriov={"total": 8, "num": 3, "vf_device": 0x75B3}), synth.GpuSpec()]
+        gim = "8.1.0.K"
+    else:
+        gpus = [synth.GpuSpec(vf=True, driver=None if kind.endswith("unbound") else "auto")]
+    root = synth.make_node(tmp_path / "node", synth.NodeSpec(gpus=gpus, gim_version=gim, seed=11,
+                                                              privileged=kind.endswith("privileged")))
+    bound = native.pci_functions(str(root), "bound")
+    bus = native.pci_functions(str(root), "bus")
+    if kind == "guest-vf-unbound":
+        assert bound == [] and len(bus) == 1
+        return
+    assert bound == bus
+    assert len(bound) == {"spx8": 8, "guest-vf": 1}.get(kind, 2 + 3)

@@ -232,6 +232,28 @@ def test_real_pci_scan_succeeds(native, amdsmi_devices):
     assert r["labels"]["amd.com/gpu.virtualization-mode"] == amdsmi_devices[0]["virtualization"]
 
 
+def test_bound_sriov_source_matches_the_whole_bus_on_the_box(native, amdsmi_devices):
+    """Round 4 reads SR-IOV state only from the functions amdgpu / gim bind
+    (plus their VFs) instead of every function on the bus.  On the real
+    host - 8 MI355X bound to amdgpu, ~370 PCI functions, the allocated GPU
+    among them - both sources must hand the labeler the same functions,
+    field for field, and the bound one must be much cheaper."""
+    import time
+
+    def timed(source):
+        t0 = time.perf_counter()
+        r = native.pci_functions("/", source)
+        return r, (time.perf_counter() - t0) * 1e3
+
+    bus, bus_ms = timed("bus")
+    bound, bound_ms = timed("bound")
+    assert bound == bus, (bound, bus)
+    addrs = {f["address"] for f in bound}
+    for d in amdsmi_devices:
+        assert d["bdf"] in addrs, (d["bdf"], addrs)
+    print(f"bound {len(bound)} functions in {bound_ms:.3f} ms, whole bus {bus_ms:.3f} ms")
+
+
 def test_auto_backend_switch_with_library_values_keeps_the_labels(native):
     """The daemon's default backend (auto) labels its first cycles from the
     KFD topology and then from amd-smi; with the amd-smi backend's own sysfs

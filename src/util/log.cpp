@@ -12,11 +12,17 @@ std::atomic<bool> g_quiet{false};
 thread_local std::string* t_held = nullptr;  // the innermost Hold's buffer
 
 void emit(const char* msg, size_t len) {
-  char stamp[32];
+  // The stamp only changes once a second: the lines of one cycle share one
+  // localtime_r/strftime (per thread).
+  thread_local time_t stamp_sec = -1;
+  thread_local char stamp[32];
   time_t now = time(nullptr);
-  struct tm tmv;
-  localtime_r(&now, &tmv);
-  strftime(stamp, sizeof(stamp), "%Y/%m/%d %H:%M:%S ", &tmv);
+  if (now != stamp_sec) {
+    struct tm tmv;
+    localtime_r(&now, &tmv);
+    strftime(stamp, sizeof(stamp), "%Y/%m/%d %H:%M:%S ", &tmv);
+    stamp_sec = now;
+  }
   // One fwrite per piece; stderr is unbuffered so keep the pieces few.
   std::string out;
   out.reserve(len + 24);

@@ -17,7 +17,8 @@ for g in 1 2 4 8; do
     --interval 1s --cycles 10 > $out/cold_$g.json 2> $out/cold_$g.err ||
     { echo "cold $g failed"; tail -5 $out/cold_$g.err; exit 1; }
   python3 -c "
-import json; r=json.load(open('$out/sysfs_$g.json')); c=json.load(open('$out/cold_$g.json'))
-print('%d GPU(s): back to back p50 %.4f ms p90 %.4f ms | 1 s apart p50 %.3f ms p90 %.3f ms | labels_ok=%s count=%s' % (
-  $g, r['value'], r['p90_ms'], c['p50_ms'], c['p90_ms'], r['labels_ok'], r['n_gpus']))"
+import json; r=json.load(open('$out/sysfs_$g.json'))
+c=[json.loads(l) for l in open('$out/cold_$g.json') if l.startswith('{')][0]  # the run's line
+print('%d GPU(s): back to back p50 %.4f ms p90 %.4f ms | 1 s apart p50 %.3f ms | labels_ok=%s count=%s | enumerate %s ms' % (
+  $g, r['value'], r['p90_ms'], c['p50_ms'], r['labels_ok'], r['n_gpus'], r['phases_p50_ms'].get('enumerate')))"
 done | tee $out/curve.txt

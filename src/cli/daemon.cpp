@@ -150,7 +150,7 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
   std::exception_ptr sriov_error;
   int64_t facts_ns = 0, sriov_ns = 0, facts_start = 0, submitted = 0;
 
-  std::function<void()> read_facts = [&] {
+  auto read_facts = [&] {
     int64_t s0 = trace::now_ns();
     facts_start = s0;
     r.cpu_facts = sched_getcpu();
@@ -161,7 +161,7 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
     }
     facts_ns = trace::now_ns() - s0;
   };
-  std::function<void()> scan_sriov = [&] {
+  auto scan_sriov = [&] {
     int64_t s0 = trace::now_ns();
     try {
       sriov_labels = lm::NewSriovLabeler(sriov)->GetLabels();
@@ -181,7 +181,10 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
   std::vector<WorkerPool::Task> seq;
   {
     trace::Span span("submit");
-    std::vector<std::function<void()>> fns{read_facts, scan_sriov};
+    std::vector<std::function<void()>> fns;
+    fns.reserve(3);
+    fns.emplace_back(read_facts);
+    fns.emplace_back(scan_sriov);
     if (write && !config.oneshot())
       if (auto prepare = lm::temp_preparer(config.output_file())) fns.push_back(std::move(prepare));
     submitted = trace::now_ns();

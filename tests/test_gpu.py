@@ -254,6 +254,37 @@ def test_bound_sriov_source_matches_the_whole_bus_on_the_box(native, amdsmi_devi
     print(f"bound {len(bound)} functions in {bound_ms:.3f} ms, whole bus {bus_ms:.3f} ms")
 
 
+def test_idle_cycles_on_hardware_are_attributed_and_take_prepared_files(binary, tmp_path):
+    """The deployed daemon (auto backend) with idle time between cycles, on
+    the real node: every cycle's named phases account for all but a few
+    microseconds of it (round-3 verdict: 0.369 ms of a 0.683 ms cycle were
+    unnamed), and every write after the first takes a prepared file."""
+    import signal
+    import statistics
+
+    from test_daemon import TOP_LEVEL, _timing_fields
+
+    out = tmp_path / "features.d" / "gfd"
+    p = subprocess.Popen([binary, "--sleep-interval=300ms", "--trace-timing", f"--output-file={out}"],
+                         stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True,
+                         env={k: v for k, v in os.environ.items() if not k.startswith("GFD_")})
+    rows = []
+    try:
+        for line in p.stderr:
+            if "Timing:" in line:
+                rows.append(_timing_fields(line))
+                if len(rows) >= 8:
+                    break
+    finally:
+        p.send_signal(signal.SIGTERM)
+        p.communicate(timeout=30)
+    assert len(rows) == 8
+    for r in rows:
+        assert abs(sum(v for k, v in r.items() if k in TOP_LEVEL) + r["other"] - r["total"]) <= 0.013, r
+    assert statistics.median(r["other"] for r in rows[1:]) <= 0.02, rows
+    assert all("write.take" in r for r in rows[1:]), rows
+
+
 def test_auto_backend_switch_with_library_values_keeps_the_labels(native):
     """The daemon's default backend (auto) labels its first cycles from the
     KFD topology and then from amd-smi; with the amd-smi backend's own sysfs

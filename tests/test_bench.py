@@ -52,6 +52,17 @@ def test_single_process_contract():
     assert r["first_cycle_ms"] > 0
     assert r["cold_cycle"]["interval"] == "1s" and r["cold_cycle"]["cycles"] == 2
     assert r["cold_cycle"]["p50_ms"] > 0 and "write" in r["cold_cycle"]["phases_p50_ms"]
+    # Attribution and per-cycle records (round 4): the unattributed time, the
+    # CPUs of every cycle, and one row per cycle whose phases add up.
+    c = r["cold_cycle"]
+    assert c["other_p50_ms"] is not None and c["other_p50_ms"] < 0.05
+    assert len(c["cycle_cpus"]) == len(c["totals_ms"]) == len(c["rows_ms"]) == 2
+    for row in c["rows_ms"]:
+        top = sum(row.get(k, 0) for k in ("submit", "init", "enumerate", "label", "sriov.join", "merge", "log", "write",
+                                           "other"))
+        assert top <= row["total"] + 0.02, row
+    job = r["extras"]["oneshot_process"]
+    assert job["runs"] >= 15 and len(job["runs_ms"]) == job["runs"] and job["first_ms"] == job["runs_ms"][0]
 
 
 @pytest.mark.parametrize("n", [2, 4, 8])

@@ -161,13 +161,16 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
     }
     facts_ns = trace::now_ns() - s0;
   };
+  std::vector<trace::Phase> sriov_detail;  // the lookup's own records, made on a worker
   auto scan_sriov = [&] {
     int64_t s0 = trace::now_ns();
+    trace::Capture capture;
     try {
       sriov_labels = lm::NewSriovLabeler(sriov)->GetLabels();
     } catch (...) {
       sriov_error = std::current_exception();
     }
+    sriov_detail = capture.take();
     sriov_ns = trace::now_ns() - s0;
   };
   // Both on one worker, in that order: two workers measured slower (each
@@ -216,6 +219,8 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
   trace::record("facts.start", facts_start ? facts_start - submitted : 0);
   trace::record("facts(overlapped)", facts_ns);
   trace::record("sriov(overlapped)", sriov_ns);
+  // Which way the lookup went (kept / checked / re-read), wherever it ran.
+  for (const auto& p : sriov_detail) trace::record(p.first, p.second);
   if (sriov_error) {
     try {
       std::rethrow_exception(sriov_error);

@@ -143,11 +143,15 @@ std::vector<PCIDevice> BoundAmdPCI::scan_bound(const std::vector<std::string>& b
   return out;
 }
 
-std::vector<std::pair<std::string, uint64_t>> BoundAmdPCI::list_bound() const {
+std::vector<std::pair<std::string, uint64_t>> BoundAmdPCI::list_bound() {
   std::vector<std::pair<std::string, uint64_t>> bound;
-  for (const auto& drv : drivers())
-    for (auto& e : fs::list_dir_ino(fs::join(root_, "sys/bus/pci/drivers/" + drv)))
+  for (size_t i = 0; i < listings_.size(); ++i) {
+    bool changed = false;
+    // A driver that is not loaded has no directory: nothing bound to it.
+    if (listings_[i].read(fs::join(root_, "sys/bus/pci/drivers/" + drivers()[i]), &changed) != 0) continue;
+    for (auto& e : listings_[i].entries())
       if (is_pci_address(e.first)) bound.push_back(std::move(e));
+  }
   std::sort(bound.begin(), bound.end());
   bound.erase(std::unique(bound.begin(), bound.end(),
                           [](const auto& a, const auto& b) { return a.first == b.first; }),
@@ -186,10 +190,14 @@ std::vector<PCIDevice> BoundAmdPCI::Devices() {
     return fell_back_ && fallback_ ? fallback_->Devices() : last_;
   }
   auto bound = list_bound();
+  int64_t t_list = trace::now_ns();
   if (seqnum && still_valid(bound)) {
     // The counter moved for some other device (a container's veth...).
     seqnum_ = *seqnum;
-    trace::record("pci.bound(checked)", trace::now_ns() - t0);
+    int64_t t_end = trace::now_ns();
+    trace::record("pci.list", t_list - t0);
+    trace::record("pci.numvfs", t_end - t_list);
+    trace::record("pci.bound(checked)", t_end - t0);
     return last_;
   }
   trace::record("pci.drivers", trace::now_ns() - t0);

@@ -29,13 +29,17 @@
 // driver directories are re-listed (names and inode numbers: a function
 // removed and re-added under the same address gets a new entry) and the
 // PFs' NumVFs re-read; only a difference in either re-reads the functions.
+// The driver directories are read through descriptors kept open
+// (fs::DirListing): no path walk, open or close per check.
 #pragma once
 
+#include <array>
 #include <memory>
 #include <string>
 #include <vector>
 
 #include "sriov/pci.h"
+#include "util/fs.h"
 
 namespace gfd::sriov {
 
@@ -55,7 +59,7 @@ class BoundAmdPCI : public AmdPCI {
  private:
   std::vector<PCIDevice> scan_bound(const std::vector<std::string>& bound);
   // (address, inode) of every function in the driver directories, sorted.
-  std::vector<std::pair<std::string, uint64_t>> list_bound() const;
+  std::vector<std::pair<std::string, uint64_t>> list_bound();
   // Whether last_ still describes the node: same bound functions, same NumVFs.
   bool still_valid(const std::vector<std::pair<std::string, uint64_t>>& bound) const;
   std::string root_;
@@ -65,6 +69,7 @@ class BoundAmdPCI : public AmdPCI {
   std::string seqnum_;  // /sys/kernel/uevent_seqnum of the kept result
   std::vector<std::pair<std::string, uint64_t>> bound_;  // list_bound() of the kept result
   std::vector<PCIDevice> last_;
+  std::array<fs::DirListing, 2> listings_;  // one per drivers() entry
 };
 
 }  // namespace gfd::sriov

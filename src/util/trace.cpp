@@ -36,6 +36,26 @@ void record_top(const std::string& name, int64_t ns) {
 }
 int64_t top_level_ns() { return t_top_ns; }
 
+Capture::Capture() : own_(!t_active) {
+  if (!own_) return;
+  t_phases.clear();
+  top_ns_ = t_top_ns;
+  t_active = true;
+}
+
+std::vector<Phase> Capture::take() {
+  std::vector<Phase> out;
+  if (own_) out.swap(t_phases);
+  return out;
+}
+
+Capture::~Capture() {
+  if (!own_) return;
+  t_phases.clear();
+  t_top_ns = top_ns_;
+  t_active = false;
+}
+
 std::string summary(int64_t total_ns) {
   std::string out;
   char buf[96];

@@ -42,6 +42,23 @@ namespace detail {
 int& depth();
 }
 
+// The records a task makes on a pool worker (a thread that runs no cycle and
+// so records nothing), to be re-recorded by the cycle thread as details once
+// it has joined the task.  On the cycle thread itself (a task it took over)
+// the records already are the cycle's, and take() returns none.
+class Capture {
+ public:
+  Capture();
+  ~Capture();
+  std::vector<Phase> take();
+  Capture(const Capture&) = delete;
+  Capture& operator=(const Capture&) = delete;
+
+ private:
+  bool own_;  // this thread was not recording: the records are ours to hand over
+  int64_t top_ns_ = 0;
+};
+
 class Span {
  public:
   explicit Span(const char* name) : name_(name), start_(now_ns()) { ++detail::depth(); }

@@ -3,6 +3,8 @@
 // matrix (cmd/gpu-feature-discovery/main_test.go:273-380).
 #include <unistd.h>
 
+#include <thread>
+
 #include "cli/daemon.h"
 #include "cli/flags.h"
 #include "lm/node.h"
@@ -11,6 +13,7 @@
 #include "test.h"
 #include "util/fs.h"
 #include "util/log.h"
+#include "util/trace.h"
 
 using namespace gfd;
 using namespace gfd::cli;
@@ -255,6 +258,52 @@ TEST(LabelCycle_RecordsPhases) {
   EXPECT_TRUE(r.other_ns >= 0 && r.other_ns < r.total_ns);
   EXPECT_TRUE(r.total_ns > 0);
   EXPECT_EQ(r.labels["amd.com/gfd.timestamp"], std::string("1"));
+}
+
+TEST(Trace_CaptureHandsAWorkersRecordsToTheCycleOnce) {
+  trace::begin_cycle();
+  std::vector<trace::Phase> got;
+  std::thread worker([&] {
+    trace::record("dropped", 1);  // a worker records nothing of its own
+    trace::Capture c;
+    { trace::Span s("pci.x"); }
+    trace::record("pci.y", 2);
+    got = c.take();
+  });
+  worker.join();
+  EXPECT_EQ(got.size(), static_cast<size_t>(2));
+  EXPECT_EQ(got[0].first, std::string("pci.x"));
+  EXPECT_EQ(got[1].first, std::string("pci.y"));
+  {
+    // On the cycle thread the records are already the cycle's.
+    trace::Capture c;
+    trace::record("pci.z", 3);
+    EXPECT_TRUE(c.take().empty());
+  }
+  EXPECT_EQ(trace::phases().size(), static_cast<size_t>(1));
+  EXPECT_EQ(trace::phases()[0].first, std::string("pci.z"));
+}
+
+namespace {
+// An SR-IOV source that records a detail, as BoundAmdPCI does.
+struct RecordingSriov : sriov::Interface {
+  std::vector<sriov::Function> Devices() override {
+    trace::record("pci.test", 5000);
+    return {};
+  }
+};
+}  // namespace
+
+TEST(LabelCycle_RecordsTheSriovLookupsDetailOnceWhereverItRan) {
+  auto c = run_config("", "none", true, true);
+  resource::MockManager m({resource::new_full_gpu()});
+  auto ts = lm::NewTimestampLabeler(c, 1);
+  for (int i = 0; i < 20; ++i) {
+    auto r = label_cycle(m, std::make_shared<RecordingSriov>(), c, ts, false);
+    int n = 0;
+    for (const auto& p : r.phases) n += p.first == "pci.test";
+    EXPECT_EQ(n, 1);
+  }
 }
 
 namespace {

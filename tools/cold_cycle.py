@@ -3,7 +3,7 @@
 (cores idle, workers parked, caches cold), read from its own --trace-timing.
 
     python tools/cold_cycle.py [--interval 1s] [--cycles 9] [--backend auto]
-                               [--variants follow,none,l3] [--reps 3]
+                               [--variants follow,none,l3] [--reps 3] [--rows]
 
 Each variant is a daemon flag set (`--cpu-affinity=<v>` for a bare name, or
 a literal list of flags and NAME=value environment settings, space-separated,
@@ -25,6 +25,7 @@ import subprocess
 import sys
 import tempfile
 
+ROWS = False  # --rows: every cycle's full Timing fields in the per-run line
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -70,6 +71,7 @@ def run_once(binary: str, flags: list[str], interval: str, cycles: int, extra: l
             "cpu_moves": sum(1 for a, b in zip(starts, starts[1:]) if a != b),
             "cpus": [r["cpu"] for r in rows],
             "totals": [r["total"] for r in rows],
+            "rows": rows if ROWS else None,
             "phases_p50_ms": {k: round(statistics.median(v), 4) for k, v in phases.items()}}
 
 
@@ -82,8 +84,11 @@ def main() -> int:
     ap.add_argument("--visible-devices", default="")
     ap.add_argument("--variants", default="follow", help="comma-separated --cpu-affinity values or flag lists")
     ap.add_argument("--reps", type=int, default=1)
+    ap.add_argument("--rows", action="store_true", help="print every cycle's phases")
     ap.add_argument("--binary", default=os.path.join(REPO, "build", "gpu-feature-discovery"))
     a = ap.parse_args()
+    global ROWS
+    ROWS = a.rows
     extra = [f"--backend={a.backend}"]
     if a.visible_devices:
         extra.append(f"--visible-devices={a.visible_devices}")

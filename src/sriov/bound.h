@@ -28,12 +28,13 @@
 // cycles 1 s apart found it moved and paid a 0.25 ms re-read.  So the
 // driver directories are re-listed (names and inode numbers: a function
 // removed and re-added under the same address gets a new entry) and the
-// PFs' NumVFs re-read; only a difference in either re-reads the functions.
+// PFs' VFs looked at; only a difference in either re-reads the functions.
 // The driver directories are read through descriptors kept open
 // (fs::DirListing): no path walk, open or close per check.
 #pragma once
 
 #include <array>
+#include <map>
 #include <memory>
 #include <string>
 #include <vector>
@@ -60,8 +61,8 @@ class BoundAmdPCI : public AmdPCI {
   std::vector<PCIDevice> scan_bound(const std::vector<std::string>& bound);
   // (address, inode) of every function in the driver directories, sorted.
   std::vector<std::pair<std::string, uint64_t>> list_bound();
-  // Whether last_ still describes the node: same bound functions, same NumVFs.
-  bool still_valid(const std::vector<std::pair<std::string, uint64_t>>& bound) const;
+  // Whether last_ still describes the node: same bound functions, same VFs.
+  bool still_valid(const std::vector<std::pair<std::string, uint64_t>>& bound);
   std::string root_;
   std::shared_ptr<AmdPCI> fallback_;
   bool have_ = false;
@@ -70,6 +71,7 @@ class BoundAmdPCI : public AmdPCI {
   std::vector<std::pair<std::string, uint64_t>> bound_;  // list_bound() of the kept result
   std::vector<PCIDevice> last_;
   std::array<fs::DirListing, 2> listings_;  // one per drivers() entry
+  std::map<std::string, std::unique_ptr<fs::Dir>> pf_dirs_;  // SR-IOV PFs of last_ without VFs
 };
 
 }  // namespace gfd::sriov

@@ -352,6 +352,12 @@ std::string Dir::read_link(const char* name) const {
   return std::string(buf, static_cast<size_t>(n));
 }
 
+int Dir::lookup(const char* name) const {
+  if (fd_ < 0) return err_;
+  struct stat st;
+  return ::fstatat(fd_, name, &st, AT_SYMLINK_NOFOLLOW) == 0 ? 0 : errno;
+}
+
 std::string read_link(const std::string& path) {
   char buf[PATH_MAX];
   ssize_t n = ::readlink(path.c_str(), buf, sizeof(buf) - 1);

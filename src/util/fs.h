@@ -142,6 +142,9 @@ class Dir {
   ReadResult read_attr(const char* name, size_t max_bytes = 4096) const;
   std::optional<std::string> read_trimmed(const char* name) const;
   std::string read_link(const char* name) const;
+  // Whether `name` exists in the directory (not following a final symlink):
+  // 0 if it does, else the errno (ENOENT: it does not).
+  int lookup(const char* name) const;
 
  private:
   int fd_ = -1;

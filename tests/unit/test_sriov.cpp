@@ -761,6 +761,24 @@ TEST(Bound_KeptWhileUeventSeqnumUnchanged) {
   bool seen = false;
   for (const auto& d : devs) seen |= d.address == "0000:21:00.0" && d.device == "0x75a0";
   EXPECT_TRUE(seen);
+  // VFs enabled on a PF that had none (the kernel adds the VF functions and
+  // the PF's virtfn links) are seen once the seqnum moves...
+  std::string vf = root + "/sys/bus/pci/devices/0000:11:00.1";
+  put_file(vf + "/vendor", "0x1002\n");
+  put_file(vf + "/class", "0x120000\n");
+  put_file(vf + "/device", "0x75b3\n");
+  EXPECT_EQ(symlink("../0000:11:00.0", (vf + "/physfn").c_str()), 0);
+  EXPECT_EQ(symlink("../0000:11:00.1", (root + "/sys/bus/pci/devices/0000:11:00.0/virtfn0").c_str()), 0);
+  put_file(root + "/sys/bus/pci/devices/0000:11:00.0/sriov_numvfs", "1\n");
+  EXPECT_EQ(bound.Devices().size(), static_cast<size_t>(6));  // same seqnum: kept
+  put_file(root + "/sys/kernel/uevent_seqnum", "4302\n");
+  EXPECT_EQ(bound.Devices().size(), static_cast<size_t>(7));
+  // ...and disabled again.
+  fs::remove_all(root + "/sys/bus/pci/devices/0000:11:00.0/virtfn0");
+  fs::remove_all(vf);
+  put_file(root + "/sys/bus/pci/devices/0000:11:00.0/sriov_numvfs", "0\n");
+  put_file(root + "/sys/kernel/uevent_seqnum", "4303\n");
+  EXPECT_EQ(bound.Devices().size(), static_cast<size_t>(6));
   // An emulated sysfs that never counts ("0") is re-read every time.
   put_file(root + "/sys/kernel/uevent_seqnum", "0\n");
   fs::remove_all(root + "/sys/bus/pci/devices/0000:c1:00.0/virtfn0");

@@ -779,6 +779,14 @@ TEST(Bound_KeptWhileUeventSeqnumUnchanged) {
   put_file(root + "/sys/bus/pci/devices/0000:11:00.0/sriov_numvfs", "0\n");
   put_file(root + "/sys/kernel/uevent_seqnum", "4303\n");
   EXPECT_EQ(bound.Devices().size(), static_cast<size_t>(6));
+  // The check reads no sriov_numvfs (its show() waits for the device lock):
+  // the VF links are the count.  A value no link backs is not read.
+  std::string numvfs = root + "/sys/bus/pci/devices/0000:31:00.0/sriov_numvfs";
+  put_file(numvfs, "3\n");
+  put_file(root + "/sys/kernel/uevent_seqnum", "4304\n");
+  for (const auto& d : bound.Devices())
+    if (d.address == "0000:31:00.0") EXPECT_EQ(d.sriov_numvfs, 0);
+  put_file(numvfs, "0\n");
   // An emulated sysfs that never counts ("0") is re-read every time.
   put_file(root + "/sys/kernel/uevent_seqnum", "0\n");
   fs::remove_all(root + "/sys/bus/pci/devices/0000:c1:00.0/virtfn0");

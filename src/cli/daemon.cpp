@@ -150,15 +150,18 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
   std::exception_ptr sriov_error;
   int64_t facts_ns = 0, sriov_ns = 0, facts_start = 0, submitted = 0;
 
+  std::vector<trace::Phase> facts_detail;  // the facts' own records, made on a worker
   auto read_facts = [&] {
     int64_t s0 = trace::now_ns();
     facts_start = s0;
     r.cpu_facts = sched_getcpu();
+    trace::Capture capture;
     try {
       facts = lm::ReadNodeFacts(config, version_files);
     } catch (...) {
       facts = lm::NodeFacts{};  // fall back to the manager inside the labeler
     }
+    facts_detail = capture.take();
     facts_ns = trace::now_ns() - s0;
   };
   std::vector<trace::Phase> sriov_detail;  // the lookup's own records, made on a worker
@@ -219,7 +222,9 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
   trace::record("facts.start", facts_start ? facts_start - submitted : 0);
   trace::record("facts(overlapped)", facts_ns);
   trace::record("sriov(overlapped)", sriov_ns);
-  // Which way the lookup went (kept / checked / re-read), wherever it ran.
+  // Which way the lookup went (kept / checked / re-read) and the node facts'
+  // parts, wherever they ran.
+  for (const auto& p : facts_detail) trace::record(p.first, p.second);
   for (const auto& p : sriov_detail) trace::record(p.first, p.second);
   if (sriov_error) {
     try {

@@ -84,10 +84,17 @@ LabelerPtr NewVersionLabeler(resource::Manager& manager) {
 
 NodeFacts ReadNodeFacts(const config::Config& config, const std::optional<resource::VersionSources>& version_files) {
   NodeFacts f;
-  f.machine = machine_type_labels(config.machine_type_file(), &f.machine_warning);
+  {
+    trace::Span span("facts.machine");
+    f.machine = machine_type_labels(config.machine_type_file(), &f.machine_warning);
+  }
   if (version_files) {
     f.have_versions = true;
-    f.driver_version = resource::driver_version(version_files->root);
+    {
+      trace::Span span("facts.driver");
+      f.driver_version = resource::driver_version(version_files->root);
+    }
+    trace::Span span("facts.runtime");
     try {
       f.runtime_version = resource::rocm_version(*version_files);
     } catch (const std::exception& e) {

@@ -48,8 +48,12 @@ bool from_uevent(const fs::Dir& dir, std::string* cls, std::string* device) {
   return true;
 }
 
-std::optional<PCIDevice> read_function(const std::string& path, const std::string& addr, const std::string& physfn) {
-  fs::Dir dir(path);
+// `keep`: the function's directory, handed over when it is an SR-IOV PF (the
+// later checks look its VF links up through it).
+std::optional<PCIDevice> read_function(const std::string& path, const std::string& addr, const std::string& physfn,
+                                       std::unique_ptr<fs::Dir>* keep) {
+  auto owned = std::make_unique<fs::Dir>(path);
+  const fs::Dir& dir = *owned;
   std::string c, device;
   bool have_device = from_uevent(dir, &c, &device);
   if (!have_device) {
@@ -85,6 +89,7 @@ std::optional<PCIDevice> read_function(const std::string& path, const std::strin
     if (!cfg.ok()) throw Error("unable to read PCI configuration space for " + addr + ": " + fs::errno_str(cfg.err));
     d.config = std::move(cfg.data);
   }
+  if (d.sriov_totalvfs > 0) *keep = std::move(owned);
   return d;
 }
 
@@ -95,7 +100,8 @@ const std::vector<std::string>& BoundAmdPCI::drivers() {
   return names;
 }
 
-std::vector<PCIDevice> BoundAmdPCI::scan_bound(const std::vector<std::string>& bound) {
+std::vector<PCIDevice> BoundAmdPCI::scan_bound(const std::vector<std::string>& bound,
+                                               std::map<std::string, std::unique_ptr<fs::Dir>>* pf_dirs) {
   std::string devices = fs::join(root_, kPciDevicesRoot);
   // Two functions per lane - the 8 GPUs of an MI355X host are ~40 small
   // reads, 0.23 ms on one cold thread - but only on workers already parked:
@@ -103,17 +109,23 @@ std::vector<PCIDevice> BoundAmdPCI::scan_bound(const std::vector<std::string>& b
   // ms), and it is overlapped with enumeration anyway.
   constexpr size_t kChunk = 2;
   std::vector<std::optional<PCIDevice>> found(bound.size());
+  std::vector<std::unique_ptr<fs::Dir>> dirs;
   auto read_all = [&](const std::vector<std::string>& addrs, const std::vector<std::string>& pfs) {
     size_t chunks = (addrs.size() + kChunk - 1) / kChunk;
     found.assign(addrs.size(), std::nullopt);
+    dirs.clear();
+    dirs.resize(addrs.size());
     WorkerPool::instance().parallel_for(
         chunks,
         [&](size_t c) {
           for (size_t i = c * kChunk; i < std::min(addrs.size(), (c + 1) * kChunk); ++i)
-            found[i] = read_function(fs::join(devices, addrs[i]), addrs[i], pfs.empty() ? "" : pfs[i]);
+            found[i] = read_function(fs::join(devices, addrs[i]), addrs[i], pfs.empty() ? "" : pfs[i], &dirs[i]);
         },
         1 + WorkerPool::instance().idle_workers());
+    for (size_t i = 0; i < addrs.size(); ++i)
+      if (dirs[i]) (*pf_dirs)[addrs[i]] = std::move(dirs[i]);
   };
+  pf_dirs->clear();
   read_all(bound, {});
   std::vector<PCIDevice> out;
   std::set<std::string> seen(bound.begin(), bound.end());
@@ -169,7 +181,7 @@ bool BoundAmdPCI::still_valid(const std::vector<std::pair<std::string, uint64_t>
     // driver holds - 8 PFs took 0.155-0.17 ms in most checks on the pool,
     // 0.029 ms in the others (profiles/sriov_check_r4.txt).
     if (d.sriov_numvfs <= 0) {
-      // No VFs: one lookup, through the PF's directory kept open.
+      // No VFs: one lookup, through the PF's directory the scan opened.
       auto& dir = pf_dirs_[d.address];
       if (!dir) dir = std::make_unique<fs::Dir>(d.path);
       if (dir->lookup("virtfn0") != ENOENT) return false;
@@ -223,11 +235,10 @@ std::vector<PCIDevice> BoundAmdPCI::Devices() {
     int64_t t1 = trace::now_ns();
     std::vector<std::string> names;
     for (const auto& e : bound) names.push_back(e.first);
-    out = scan_bound(names);
+    out = scan_bound(names, &pf_dirs_);
     trace::record("pci.bound", trace::now_ns() - t1);
     fell_back_ = false;
     last_ = out;
-    pf_dirs_.clear();
   }
   have_ = true;
   bound_ = std::move(bound);

@@ -58,7 +58,9 @@ class BoundAmdPCI : public AmdPCI {
   static const std::vector<std::string>& drivers();
 
  private:
-  std::vector<PCIDevice> scan_bound(const std::vector<std::string>& bound);
+  // Reads `bound` and their VFs; the directories of SR-IOV PFs go to *pf_dirs.
+  std::vector<PCIDevice> scan_bound(const std::vector<std::string>& bound,
+                                    std::map<std::string, std::unique_ptr<fs::Dir>>* pf_dirs);
   // (address, inode) of every function in the driver directories, sorted.
   std::vector<std::pair<std::string, uint64_t>> list_bound();
   // Whether last_ still describes the node: same bound functions, same VFs.
@@ -71,7 +73,7 @@ class BoundAmdPCI : public AmdPCI {
   std::vector<std::pair<std::string, uint64_t>> bound_;  // list_bound() of the kept result
   std::vector<PCIDevice> last_;
   std::array<fs::DirListing, 2> listings_;  // one per drivers() entry
-  std::map<std::string, std::unique_ptr<fs::Dir>> pf_dirs_;  // SR-IOV PFs of last_ without VFs
+  std::map<std::string, std::unique_ptr<fs::Dir>> pf_dirs_;  // of last_'s SR-IOV PFs, opened by the scan
 };
 
 }  // namespace gfd::sriov

@@ -176,10 +176,11 @@ bool BoundAmdPCI::still_valid(const std::vector<std::pair<std::string, uint64_t>
   for (const auto& d : last_) {
     if (d.sriov_totalvfs <= 0) continue;
     // The kernel links every VF it creates as <pf>/virtfn<N> and removes the
-    // links with the VFs, so the links are the PF's NumVFs.  Not read from
-    // sriov_numvfs: its show() takes the device lock, which a busy GPU's
-    // driver holds - 8 PFs took 0.155-0.17 ms in most checks on the pool,
-    // 0.029 ms in the others (profiles/sriov_check_r4.txt).
+    // links with the VFs, so the links are the PF's NumVFs: a lookup in the
+    // directory the scan opened instead of a sriov_numvfs read (whose show()
+    // also takes the device lock).  8 PFs: 0.019 ms vs 0.028-0.030 ms, and
+    // no first check that opens 8 attribute files, 0.14-0.17 ms
+    // (profiles/sriov_check_r4.txt).
     if (d.sriov_numvfs <= 0) {
       // No VFs: one lookup, through the PF's directory the scan opened.
       auto& dir = pf_dirs_[d.address];

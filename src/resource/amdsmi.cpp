@@ -387,7 +387,8 @@ int sysfs_xgmi_links(const std::string& root, const std::string& bdf) {
 
 // GPU-level capabilities: xGMI links, virtualization mode, supported
 // partition modes.  Any processor handle of the GPU will do.
-void query_gpu_caps(AmdSmiLib& L, const ProcInfo& p, const std::string& root, GpuExtras& x) {
+void query_gpu_caps(AmdSmiLib& L, const ProcInfo& p, const std::string& root, GpuExtras& x,
+                    AmdSmiManager::AvailableModes& avail) {
   x.xgmi_links = AMDSMI_CALL("xgmi_num_links(sysfs)", sysfs_xgmi_links(root, p.gpu_bdf));
   if (x.xgmi_links < 0 && L.get_gpu_xgmi_link_status) {
     amdsmi_xgmi_link_status_t ls;
@@ -412,6 +413,13 @@ void query_gpu_caps(AmdSmiLib& L, const ProcInfo& p, const std::string& root, Gp
     std::string pci = fs::join(root, "sys/bus/pci/devices/" + p.gpu_bdf);
     if (fs::exists(pci))
       x.virtualization = classify_virtualization(pci, p.device_id, running_in_vm(root), fs::exists(pci + "/physfn"));
+  }
+  // Kept from an earlier cycle under the same modes (AmdSmiManager::available_).
+  if (!avail.compute_partition.empty() && avail.compute_partition == p.compute_partition &&
+      avail.memory_partition == p.memory_partition) {
+    x.available_memory = avail.memory;
+    x.available_compute = avail.compute;
+    return;
   }
   // Supported memory partition modes: world-readable in sysfs (~5 us);
   // the amd-smi partition-config call (~25 us) only as a fallback.
@@ -441,6 +449,12 @@ void query_gpu_caps(AmdSmiLib& L, const ProcInfo& p, const std::string& root, Gp
         if (const char* n = accel_name(cfg.profiles[i].profile_type)) x.available_compute.push_back(n);
     }
   }
+  // Kept only when both lists were found and the modes are known.
+  if (!x.available_memory.empty() && !x.available_compute.empty() && !p.compute_partition.empty() &&
+      !p.memory_partition.empty())
+    avail = {p.compute_partition, p.memory_partition, x.available_memory, x.available_compute};
+  else
+    avail = {};
 }
 
 std::string format_bdf(const amdsmi_bdf_t& b) {
@@ -609,6 +623,7 @@ void AmdSmiManager::library_init() {
   parent_bdf_.clear();
   proc_bdf_.clear();
   identity_.clear();
+  available_.clear();
   ++init_count_;
 }
 
@@ -686,6 +701,7 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
     std::exception_ptr error;
     int64_t proc_ns = 0, caps_ns = 0;
     KfdNodeFacts kfd;  // session cache entry (unpartitioned GPUs)
+    AvailableModes avail;  // session cache entry
     std::vector<PartitionFacts> parts;  // session cache entries (partitioned GPUs), aligned with procs
   };
   std::vector<Gpu> gpus;
@@ -701,6 +717,8 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
       if (v != virt_mode_.end()) gpus.back().extras.virtualization = v->second;
       auto k = kfd_node_.find(bdf);
       if (k != kfd_node_.end()) gpus.back().kfd = k->second;
+      auto a = available_.find(bdf);
+      if (a != available_.end()) gpus.back().avail = a->second;
       for (const auto& p : physical[i]) {
         auto f = partition_facts_.find(p.h);
         gpus.back().parts.push_back(f != partition_facts_.end() ? f->second : PartitionFacts{});
@@ -741,7 +759,7 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
       }
       int64_t t1 = trace::now_ns();
       const ProcInfo& first = procs.front();
-      query_gpu_caps(L, first, opts_.root, g.extras);
+      query_gpu_caps(L, first, opts_.root, g.extras, g.avail);
       if (procs.size() > 1 || (!first.compute_partition.empty() && first.compute_partition != "SPX"))
         g.extras.engines = AMDSMI_CALL("partition_engines(sysfs)", partition_engine_counts(opts_.root, first.gpu_bdf));
       g.proc_ns = t1 - t0;
@@ -789,6 +807,10 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
         identity_[p.h] = Identity{p.market_name, p.vendor_id, p.device_id, p.cus, p.gfx, p.uuid};
     if (!g.extras.virtualization.empty()) virt_mode_[g.bdf] = g.extras.virtualization;
     if (g.kfd.node_id != kNoNode) kfd_node_[g.bdf] = g.kfd;
+    if (g.avail.compute_partition.empty())
+      available_.erase(g.bdf);
+    else
+      available_[g.bdf] = g.avail;
     for (const auto& f : g.parts)
       if (f.node_id != kNoNode) partition_facts_[f.handle] = f;
   }

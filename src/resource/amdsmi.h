@@ -85,6 +85,12 @@ class AmdSmiManager : public Manager {
     int sdma = -1;
     uint64_t mem_bytes = 0;
   };
+  // The partition modes a GPU supports, as read under its current modes
+  // (see available_).
+  struct AvailableModes {
+    std::string compute_partition, memory_partition;  // the modes they were read under
+    std::vector<std::string> memory, compute;
+  };
   // Per-session ASIC identity of one processor (see identity_).
   struct Identity {
     std::string market_name;
@@ -135,6 +141,12 @@ class AmdSmiManager : public Manager {
   // for the lifetime of one session: processor addresses and PCI functions
   // only change with a driver reload or partition switch, which re-initialise.
   std::map<std::string, std::string> parent_bdf_;
+  // Supported compute and memory partition modes of each physical GPU (by
+  // BDF), kept while its current modes are those they were read under: what
+  // amdgpu offers follows from the ASIC and, for compute modes, the current
+  // memory partition (both read every cycle); a driver reload re-initialises
+  // the session, which clears this.  Two attribute reads per GPU per cycle.
+  std::map<std::string, AvailableModes> available_;
   // PCI address of each processor (by handle) for the lifetime of one
   // session, checked once against sysfs and the processor's KFD node
   // (checked_bdf in amdsmi.cpp): amd-smi reads it through libdrm and, when

@@ -20,6 +20,7 @@
 #include "resource/factory.h"
 #include "test.h"
 #include "util/fs.h"
+#include "util/strings.h"
 
 using namespace gfd;
 using namespace gfd::resource;
@@ -301,6 +302,39 @@ TEST(AmdSmiFake_AsicIdentityQueriedOncePerSession) {
   m.GetDevices();
   m.Shutdown();
   EXPECT_EQ(fake().calls("amdsmi_get_gpu_asic_info") - a0, 18L);
+  fs::remove_all(root);
+}
+
+TEST(AmdSmiFake_SupportedPartitionModesKeptWhileTheModesStay) {
+  // Which partition modes a GPU supports is read once per session while its
+  // current modes stay - not per cycle - and again after a re-initialisation.
+  REQUIRE_FAKE();
+  fake().configure(kTwoGpus);
+  std::string root = temp_root();
+  set_generation(root, "1");
+  long m0 = fake().calls("amdsmi_get_gpu_memory_partition_config");
+  long p0 = fake().calls("amdsmi_get_gpu_accelerator_partition_profile_config");
+  AmdSmiManager m(opts(root, true));
+  std::string first;
+  for (int c = 0; c < 4; ++c) {
+    m.Init();
+    auto devs = m.GetDevices();
+    m.Shutdown();
+    std::string d;
+    for (const auto& g : devs)
+      d += str::join(g->Info().available_compute_partitions, ",") + "/" +
+           str::join(g->Info().available_memory_partitions, ",") + ";";
+    if (c == 0) first = d;
+    EXPECT_EQ(d, first);
+  }
+  EXPECT_EQ(first, std::string("SPX,DPX,QPX,CPX/NPS1,NPS2;SPX,DPX,QPX,CPX/NPS1,NPS2;"));
+  EXPECT_EQ(fake().calls("amdsmi_get_gpu_memory_partition_config") - m0, 2L);
+  EXPECT_EQ(fake().calls("amdsmi_get_gpu_accelerator_partition_profile_config") - p0, 2L);
+  set_generation(root, "2");  // partition switch / driver reload: new session
+  m.Init();
+  m.GetDevices();
+  m.Shutdown();
+  EXPECT_EQ(fake().calls("amdsmi_get_gpu_memory_partition_config") - m0, 4L);
   fs::remove_all(root);
 }
 

@@ -254,6 +254,47 @@ def test_bound_sriov_source_matches_the_whole_bus_on_the_box(native, amdsmi_devi
     print(f"bound {len(bound)} functions in {bound_ms:.3f} ms, whole bus {bus_ms:.3f} ms")
 
 
+def test_vf_links_are_the_pfs_numvfs_on_the_box():
+    """The SR-IOV check after an unrelated uevent counts a PF's VFs by its
+    virtfn* links instead of reading sriov_numvfs (src/sriov/bound.cpp).
+    On the real host every amdgpu/gim-bound PF with an SR-IOV capability
+    must have exactly sriov_numvfs links."""
+    checked = 0
+    for drv in ("amdgpu", "gim"):
+        d = f"/sys/bus/pci/drivers/{drv}"
+        if not os.path.isdir(d):
+            continue
+        for name in os.listdir(d):
+            pf = os.path.join(d, name)
+            if ":" not in name or not os.path.exists(os.path.join(pf, "sriov_totalvfs")):
+                continue
+            with open(os.path.join(pf, "sriov_numvfs")) as f:
+                numvfs = int(f.read())
+            links = [e for e in os.listdir(pf) if e.startswith("virtfn")]
+            assert len(links) == numvfs, (pf, numvfs, links)
+            checked += 1
+    print(f"{checked} SR-IOV PFs checked")
+
+
+def test_kept_partition_mode_lists_match_the_driver_every_cycle(native):
+    """The supported compute / memory partition modes are read once per
+    amd-smi session while the current modes stay (AmdSmiManager::available_):
+    cycle after cycle they must still be what amdgpu reports."""
+    s = native.Session(["--backend=amdsmi", "--no-timestamp", "--output-file="])
+    for _ in range(4):
+        s.cycle(False)
+        for d in s.devices():
+            pci = f"/sys/bus/pci/devices/{d['bdf']}"
+            for attr, key in (("available_compute_partition", "available_compute_partitions"),
+                              ("available_memory_partition", "available_memory_partitions")):
+                path = os.path.join(pci, attr)
+                if not os.path.exists(path):
+                    continue
+                with open(path) as f:
+                    want = [m.strip() for m in f.read().split(",") if m.strip()]
+                assert d[key] == want, (d["bdf"], attr, d[key], want)
+
+
 def test_idle_cycles_on_hardware_are_attributed_and_take_prepared_files(binary, tmp_path):
     """The deployed daemon (auto backend) with idle time between cycles, on
     the real node: every cycle's named phases account for all but a few

@@ -235,9 +235,12 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
   }
   {
     trace::Span span("merge");
-    lm::LabelerPtr labelers = lm::merge({timestamp, device, lm::from_labels(std::move(sriov_labels))});
+    // The timestamp labeler lives across cycles (appended); the device
+    // labeler and the SR-IOV labels are this cycle's own (moved in).
     try {
-      r.labels = labelers->GetLabels();
+      if (timestamp) timestamp->AppendTo(r.labels);
+      if (device) device->MoveTo(r.labels);
+      lm::from_labels(std::move(sriov_labels))->MoveTo(r.labels);
     } catch (const std::exception& e) {
       throw Error(std::string("error generating labels: ") + e.what());
     }

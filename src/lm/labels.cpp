@@ -38,6 +38,7 @@ class FixedLabeler : public Labeler {
     }
     for (const auto& kv : labels_) out[kv.first] = kv.second;
   }
+  void MoveTo(Labels& out) override { move_labels(out, std::move(labels_)); }
 
  private:
   Labels labels_;
@@ -51,18 +52,23 @@ class ListLabeler : public Labeler {
     AppendTo(all);
     return all;
   }
-  void AppendTo(Labels& out) override {
+  void AppendTo(Labels& out) override { append(out, false); }
+  void MoveTo(Labels& out) override { append(out, true); }
+
+ private:
+  void append(Labels& out, bool move) {
     for (const auto& l : labelers_) {
       if (!l) continue;
       try {
-        l->AppendTo(out);
+        if (move)
+          l->MoveTo(out);
+        else
+          l->AppendTo(out);
       } catch (const std::exception& e) {
         throw Error(std::string("error generating labels: ") + e.what());
       }
     }
   }
-
- private:
   std::vector<LabelerPtr> labelers_;
 };
 
@@ -165,6 +171,18 @@ int remove_own_temps(const std::string& tmp_dir) {
 }
 
 }  // namespace
+
+void move_labels(Labels& out, Labels&& from) {
+  if (out.empty()) {
+    out.swap(from);
+    from.clear();
+    return;
+  }
+  while (!from.empty()) {
+    auto r = out.insert(from.extract(from.begin()));
+    if (!r.inserted) r.position->second = std::move(r.node.mapped());  // later labels win
+  }
+}
 
 LabelerPtr from_labels(Labels l) { return std::make_shared<FixedLabeler>(std::move(l)); }
 LabelerPtr empty() { return std::make_shared<FixedLabeler>(Labels{}); }

@@ -32,8 +32,16 @@ class Labeler {
   virtual void AppendTo(Labels& out) {
     for (auto& kv : GetLabels()) out[kv.first] = std::move(kv.second);
   }
+  // AppendTo for a labeler used once (a cycle's own): fixed labels are moved
+  // into `out` - map nodes and all - instead of copied; the labeler is left
+  // empty.  Other labelers append as usual.
+  virtual void MoveTo(Labels& out) { AppendTo(out); }
 };
 using LabelerPtr = std::shared_ptr<Labeler>;
+
+// Moves every label of `from` into `out`, overriding same keys (map nodes
+// are moved, not copied); `from` is left empty.
+void move_labels(Labels& out, Labels&& from);
 
 // A fixed set of labels (Labels implements Labeler in the reference).
 LabelerPtr from_labels(Labels l);

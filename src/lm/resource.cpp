@@ -156,13 +156,13 @@ Labels new_gpu_labels(resource::Manager& manager, const config::Config& config) 
     const Device& d = *entry.second;
     int count = counts[entry.first];
     Labels l = GFD_WRAP("failed to construct labeler", NewGPUResourceLabelsWithoutSharing(d, count));
-    for (auto& kv : l) out[kv.first] = kv.second;
+    move_labels(out, std::move(l));
   }
   for (const auto& entry : full) {
     const Device& d = *entry.second;
     int count = counts[entry.first];
     Labels l = GFD_WRAP("failed to construct labeler", NewGPUResourceLabels(&config, d, count));
-    for (auto& kv : l) out[kv.first] = kv.second;
+    move_labels(out, std::move(l));
   }
   return out;
 }
@@ -173,7 +173,7 @@ Labels new_partition_device_labels(const std::map<std::string, PartitionResource
   for (const auto& entry : resources) {
     const PartitionResource& r = entry.second;
     Labels l = GFD_WRAP("failed to construct labeler", NewPartitionResourceLabels(r.name, &config, *r.device, r.count));
-    for (auto& kv : l) out[kv.first] = kv.second;
+    move_labels(out, std::move(l));
   }
   return out;
 }
@@ -243,7 +243,7 @@ Labels new_partition_labels(resource::Manager& manager, const config::Config& co
     throw Error("unknown strategy: " + strategy);
   }
   Labels out = strategy_labels(strategy);
-  for (auto& kv : l) out[kv.first] = kv.second;
+  move_labels(out, std::move(l));
   return out;
 }
 

@@ -110,6 +110,9 @@ std::vector<PCIDevice> BoundAmdPCI::scan_bound(const std::vector<std::string>& b
   constexpr size_t kChunk = 2;
   std::vector<std::optional<PCIDevice>> found(bound.size());
   std::vector<std::unique_ptr<fs::Dir>> dirs;
+  // The old directories stay open until the new ones are: a re-read never
+  // dips below the descriptors a steady daemon holds.
+  std::map<std::string, std::unique_ptr<fs::Dir>> fresh;
   auto read_all = [&](const std::vector<std::string>& addrs, const std::vector<std::string>& pfs) {
     size_t chunks = (addrs.size() + kChunk - 1) / kChunk;
     found.assign(addrs.size(), std::nullopt);
@@ -123,9 +126,8 @@ std::vector<PCIDevice> BoundAmdPCI::scan_bound(const std::vector<std::string>& b
         },
         1 + WorkerPool::instance().idle_workers());
     for (size_t i = 0; i < addrs.size(); ++i)
-      if (dirs[i]) (*pf_dirs)[addrs[i]] = std::move(dirs[i]);
+      if (dirs[i]) fresh[addrs[i]] = std::move(dirs[i]);
   };
-  pf_dirs->clear();
   read_all(bound, {});
   std::vector<PCIDevice> out;
   std::set<std::string> seen(bound.begin(), bound.end());
@@ -152,6 +154,7 @@ std::vector<PCIDevice> BoundAmdPCI::scan_bound(const std::vector<std::string>& b
       if (d) out.push_back(std::move(*d));
   }
   std::sort(out.begin(), out.end(), [](const PCIDevice& a, const PCIDevice& b) { return a.address < b.address; });
+  pf_dirs->swap(fresh);
   return out;
 }
 

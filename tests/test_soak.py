@@ -39,16 +39,20 @@ def _fds(pid: int) -> tuple[int, int]:
     # src/lm/labels.cpp WriterState) are counted apart: how many are ready
     # at a sample depends on timing, not on leaks - that made the floor
     # 15 or 16 from run to run.  Returns (floor without them, most of them).
+    # A descriptor closed between the listing and its readlink still counts:
+    # skipping it let a sample taken while a re-read swaps descriptors (new
+    # ones opened after the listing, old ones closed before the readlink)
+    # dip below the floor.
     n, prepared = [], []
     for _ in range(40):
-        targets = []
-        for fd in os.listdir(f"/proc/{pid}/fd"):
+        fds = os.listdir(f"/proc/{pid}/fd")
+        k = 0
+        for fd in fds:
             try:
-                targets.append(os.readlink(f"/proc/{pid}/fd/{fd}"))
+                k += "/gfd-tmp/" in os.readlink(f"/proc/{pid}/fd/{fd}")
             except OSError:  # closed between listdir and readlink
                 pass
-        k = sum(1 for t in targets if "/gfd-tmp/" in t)
-        n.append(len(targets) - k)
+        n.append(len(fds) - k)
         prepared.append(k)
         time.sleep(0.01)
     return min(n), max(prepared)

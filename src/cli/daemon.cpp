@@ -237,10 +237,15 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
     trace::Span span("merge");
     // The timestamp labeler lives across cycles (appended); the device
     // labeler and the SR-IOV labels are this cycle's own (moved in).
+    // Errors read as the merge of the three would wrap them (lm::merge).
     try {
-      if (timestamp) timestamp->AppendTo(r.labels);
-      if (device) device->MoveTo(r.labels);
-      lm::from_labels(std::move(sriov_labels))->MoveTo(r.labels);
+      try {
+        if (timestamp) timestamp->AppendTo(r.labels);
+        if (device) device->MoveTo(r.labels);
+        lm::from_labels(std::move(sriov_labels))->MoveTo(r.labels);
+      } catch (const std::exception& e) {
+        throw Error(std::string("error generating labels: ") + e.what());
+      }
     } catch (const std::exception& e) {
       throw Error(std::string("error generating labels: ") + e.what());
     }

@@ -188,7 +188,7 @@ bool BoundAmdPCI::still_valid(const std::vector<std::pair<std::string, uint64_t>
       // No VFs: one lookup, through the PF's directory the scan opened.
       auto& dir = pf_dirs_[d.address];
       if (!dir) dir = std::make_unique<fs::Dir>(d.path);
-      if (dir->lookup("virtfn0") != ENOENT) return false;
+      if (dir->err() != 0 || dir->lookup("virtfn0") != ENOENT) return false;  // (a PF gone: re-read)
       continue;
     }
     // VFs: the same links to the same functions (a VF removed on its own

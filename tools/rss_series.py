@@ -40,6 +40,8 @@ def main() -> int:
     ap.add_argument("--backend", default="amdsmi")
     ap.add_argument("--sysfs-root", default=None, help="a synthetic node (utils/synth.py) instead of the host")
     ap.add_argument("--arg", action="append", default=[], help="extra daemon argument (repeatable)")
+    ap.add_argument("--binary", default=os.path.join(REPO, "build", "gpu-feature-discovery"),
+                    help="daemon binary (e.g. an older build staged for an A/B)")
     a = ap.parse_args()
     d = tempfile.mkdtemp(prefix="gfd-rss-")
     out = os.path.join(d, "gfd")
@@ -53,7 +55,7 @@ def main() -> int:
         a.sysfs_root = str(synth.make_mi355x_node(os.path.join(d, "node"), n_gpus=8, seed=3))
     if a.sysfs_root:
         extra = [f"--sysfs-root={a.sysfs_root}", f"--machine-type-file={a.sysfs_root}/sys/class/dmi/id/product_name"]
-    p = subprocess.Popen([os.path.join(REPO, "build", "gpu-feature-discovery"), f"--backend={a.backend}", *extra,
+    p = subprocess.Popen([a.binary, f"--backend={a.backend}", *extra,
                           "--sleep-interval=1ms", "--trace-timing", f"--output-file={out}", *a.arg],
                          stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
     cycles = [0]

@@ -59,11 +59,19 @@ def main() -> int:
                           "--sleep-interval=1ms", "--trace-timing", f"--output-file={out}", *a.arg],
                          stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
     cycles = [0]
+    # Cycles that did more than the steady state, by what the Timing line
+    # names: an amd-smi re-initialisation (the KFD topology generation moved:
+    # another GPU of the host reset or re-partitioned), an SR-IOV check after
+    # an unrelated uevent, an SR-IOV re-read.
+    events = {"amdsmi_init=": 0, "pci.bound(checked)=": 0, "pci.drivers=": 0}
 
     def reader():
         for line in p.stderr:
             if "Timing:" in line:
                 cycles[0] += 1
+                for k in events:
+                    if k in line:
+                        events[k] += 1
 
     threading.Thread(target=reader, daemon=True).start()
     t0 = time.monotonic()
@@ -72,7 +80,9 @@ def main() -> int:
             time.sleep(a.every)
             m = mem_kib(p.pid)
             print(f"t={time.monotonic() - t0:6.0f}s cycles={cycles[0]:8d} rss={m.get('VmRSS')} KiB "
-                  f"(anon {m.get('RssAnon')}, file {m.get('RssFile')}) fds={len(os.listdir(f'/proc/{p.pid}/fd'))}",
+                  f"(anon {m.get('RssAnon')}, file {m.get('RssFile')}) fds={len(os.listdir(f'/proc/{p.pid}/fd'))} "
+                  f"reinit={events['amdsmi_init=']} sriov_checked={events['pci.bound(checked)=']} "
+                  f"sriov_reread={events['pci.drivers=']}",
                   flush=True)
     finally:
         p.send_signal(signal.SIGTERM)

@@ -28,7 +28,7 @@ def mem_kib(pid: int) -> dict[str, int]:
     with open(f"/proc/{pid}/status") as f:
         for line in f:
             k = line.split(":")[0]
-            if k in ("VmRSS", "RssAnon", "RssFile"):
+            if k in ("VmRSS", "RssAnon", "RssFile", "Threads"):
                 out[k] = int(line.split()[1])
     return out
 
@@ -81,6 +81,7 @@ def main() -> int:
             m = mem_kib(p.pid)
             print(f"t={time.monotonic() - t0:6.0f}s cycles={cycles[0]:8d} rss={m.get('VmRSS')} KiB "
                   f"(anon {m.get('RssAnon')}, file {m.get('RssFile')}) fds={len(os.listdir(f'/proc/{p.pid}/fd'))} "
+                  f"threads={m.get('Threads')} "
                   f"reinit={events['amdsmi_init=']} sriov_checked={events['pci.bound(checked)=']} "
                   f"sriov_reread={events['pci.drivers=']}",
                   flush=True)

@@ -373,6 +373,9 @@ void start(const Context& ctx, SignalWatcher& sigs) {
     bool restart;
     {
       resource::ManagerPtr manager = resource::new_manager(c);
+      // The warm-start manager's amd-smi initialisation starts here, not in
+      // the first cycle's Init.
+      if (!c.oneshot()) manager->Prepare();
       if (!g_timeline.manager_ns) g_timeline.manager_ns = trace::now_ns();
 
       log::printf("Start running");

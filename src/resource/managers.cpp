@@ -122,8 +122,12 @@ std::vector<DevicePtr> WarmStartManager::GetDevices() {
   return devs;
 }
 
-void WarmStartManager::Init() {
-  if (state_ == State::cold && orphan_running()) {
+void WarmStartManager::Prepare() {
+  if (state_ == State::cold) start_warmer();
+}
+
+void WarmStartManager::start_warmer() {
+  if (orphan_running()) {
     // An earlier manager's warmer is still stuck in the library's init:
     // label from the quick manager and look again next cycle.
     if (!waited_logged_) {
@@ -131,38 +135,44 @@ void WarmStartManager::Init() {
                   "manager until it finishes", preferred_->Name().c_str(), quick_->Name().c_str());
       waited_logged_ = true;
     }
-  } else if (state_ == State::cold) {
-    // A persistent session stays initialised after Shutdown: the warmer
-    // opens it and takes one snapshot - the library's first queries of a
-    // device (~1.2 ms on MI355X: ASIC info, KFD node, virtualization mode)
-    // and the session caches are paid here too - so the cycle that switches
-    // over finds everything ready.
-    warmer_ = std::make_shared<Warmer>();
-    thread_ = std::thread([w = warmer_, m = preferred_] {
-      int64_t t0 = trace::now_ns();
-      std::string error, devices;
+    return;
+  }
+  // A persistent session stays initialised after Shutdown: the warmer
+  // opens it and takes one snapshot - the library's first queries of a
+  // device (~1.2 ms on MI355X: ASIC info, KFD node, virtualization mode)
+  // and the session caches are paid here too - so the cycle that switches
+  // over finds everything ready.
+  warmer_ = std::make_shared<Warmer>();
+  thread_ = std::thread([w = warmer_, m = preferred_] {
+    int64_t t0 = trace::now_ns();
+    std::string error, devices;
+    try {
+      m->Init();
       try {
-        m->Init();
-        try {
-          devices = device_summary(m->GetDevices());
-        } catch (...) {
-          m->Shutdown();
-          throw;
-        }
+        devices = device_summary(m->GetDevices());
+      } catch (...) {
         m->Shutdown();
-      } catch (const std::exception& e) {
-        error = e.what();
+        throw;
       }
-      std::lock_guard<std::mutex> lk(w->mu);
-      w->error = std::move(error);
-      w->devices = std::move(devices);
-      w->ns = trace::now_ns() - t0;
-      w->done = true;
-      w->cv.notify_all();
-    });
-    state_ = State::warming;
-    log::printf("Initializing the %s manager in the background; labeling from the %s manager meanwhile",
-                preferred_->Name().c_str(), quick_->Name().c_str());
+      m->Shutdown();
+    } catch (const std::exception& e) {
+      error = e.what();
+    }
+    std::lock_guard<std::mutex> lk(w->mu);
+    w->error = std::move(error);
+    w->devices = std::move(devices);
+    w->ns = trace::now_ns() - t0;
+    w->done = true;
+    w->cv.notify_all();
+  });
+  state_ = State::warming;
+  log::printf("Initializing the %s manager in the background; labeling from the %s manager meanwhile",
+              preferred_->Name().c_str(), quick_->Name().c_str());
+}
+
+void WarmStartManager::Init() {
+  if (state_ == State::cold) {
+    start_warmer();
   } else if (state_ == State::warming) {
     std::unique_lock<std::mutex> lk(warmer_->mu);
     if (warmer_->done) {

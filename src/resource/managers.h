@@ -45,6 +45,7 @@ class FallbackManager : public Manager {
   std::optional<RuntimeVersion> GetRuntimeVersion() override { return current_->GetRuntimeVersion(); }
   std::string Name() const override { return "fallback(" + current_->Name() + ")"; }
   std::optional<VersionSources> VersionFiles() const override { return current_->VersionFiles(); }
+  void Prepare() override { current_->Prepare(); }
   bool fell_back() const { return fell_back_; }
 
  private:
@@ -104,6 +105,9 @@ class WarmStartManager : public Manager {
   std::optional<RuntimeVersion> GetRuntimeVersion() override { return current_->GetRuntimeVersion(); }
   std::string Name() const override { return current_->Name(); }
   std::optional<VersionSources> VersionFiles() const override { return current_->VersionFiles(); }
+  // Starts the preferred manager's initialisation now rather than in the
+  // first Init (the thread start is then not part of the first cycle).
+  void Prepare() override;
   // The preferred manager is the one in use.
   bool warmed() const { return state_ == State::preferred; }
   int64_t teardown_wait_ms = 5000;
@@ -112,6 +116,8 @@ class WarmStartManager : public Manager {
  private:
   enum class State { cold, warming, preferred, quick_only };
   void fall_back(const std::string& why);
+  // cold -> warming, unless an earlier manager's warmer still runs.
+  void start_warmer();
   bool waited_logged_ = false;
 
   ManagerPtr preferred_, quick_, current_;

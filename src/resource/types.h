@@ -180,6 +180,10 @@ class Manager {
   // no manager state: the daemon then reads them on a worker, overlapped
   // with enumeration.  nullopt: ask the manager, inside the Init window.
   virtual std::optional<VersionSources> VersionFiles() const { return std::nullopt; }
+  // Work a manager may start in the background before its first Init (the
+  // warm-start manager's library initialisation).  The daemon calls it once,
+  // in loop mode, when the manager is built.
+  virtual void Prepare() {}
 };
 
 using ManagerPtr = std::shared_ptr<Manager>;

@@ -517,6 +517,24 @@ TEST(WarmStart_FirstCycleFromQuickThenPreferred) {
   EXPECT_EQ(smi->init_calls, 4);  // the warmer, the cycle that switched, 2 more
 }
 
+TEST(WarmStart_PrepareStartsThePreferredManagerBeforeTheFirstCycle) {
+  // The daemon calls Prepare() when it builds the manager: the library's
+  // initialisation runs during start-up, so the first cycle can already
+  // use it; a second Prepare (or the first Init) starts no second warmer.
+  auto smi = std::make_shared<MockManager>(std::vector<DevicePtr>{new_full_gpu(), new_full_gpu()});
+  auto kfd = std::make_shared<MockManager>(std::vector<DevicePtr>{new_full_gpu()});
+  WarmStartManager w(smi, kfd);
+  w.Prepare();
+  w.Prepare();
+  usleep(300 * 1000);  // the mock initialises at once
+  w.Init();
+  EXPECT_TRUE(w.warmed());
+  EXPECT_EQ(w.GetDevices().size(), static_cast<size_t>(2));
+  w.Shutdown();
+  EXPECT_EQ(smi->init_calls, 2);  // the warmer, then the first cycle
+  EXPECT_EQ(kfd->init_calls, 0);
+}
+
 TEST(WarmStart_PreferredFailingInTheBackgroundKeepsQuick) {
   auto smi = std::make_shared<MockManager>();
   smi->with_error_on_init("no driver");

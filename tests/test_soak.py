@@ -36,7 +36,7 @@ def _fds(pid: int) -> tuple[int, int]:
     # raises the floor.  The window must catch the daemon between cycles at
     # least once (see the per-cycle interval below).  Prepared temporary
     # files (gfd-tmp/gfd-*, up to two kept open between cycles by design,
-    # src/lm/labels.cpp WriterState) are counted apart: how many are ready
+    # src/lm/writer.cpp WriterState) are counted apart: how many are ready
     # at a sample depends on timing, not on leaks - that made the floor
     # 15 or 16 from run to run.  Returns (floor without them, most of them).
     # A descriptor closed between the listing and its readlink still counts:

@@ -4,6 +4,7 @@
 
 #include <cstdlib>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <tuple>
 
@@ -52,10 +53,24 @@ bool builtin_amdgpu(const std::string& root) {
   known.emplace(root, builtin);
   return builtin;
 }
+// Whether the loaded amdgpu module publishes a `version` (a DKMS build does;
+// an in-tree module, the MI355X pool's, does not).  Looked up relative to
+// the module directory kept open: the failing lookup by path walked
+// /sys/module/amdgpu every cycle (facts.driver 0.035 ms after an idle
+// second, profiles/bench_fresh_r4.txt r4fin3a).  A reloaded module is a new
+// directory: the old one reads as removed and is opened again.
+bool module_has_version(const std::string& root) {
+  static std::mutex mu;
+  static std::map<std::string, std::unique_ptr<fs::Dir>> dirs;
+  std::lock_guard<std::mutex> g(mu);
+  auto& d = dirs[root];
+  if (!d || d->removed()) d = std::make_unique<fs::Dir>(fs::join(root, "sys/module/amdgpu"));
+  return d->err() == 0 && d->lookup("version") == 0;
+}
 }  // namespace
 
 std::string host_driver_version(const std::string& root) {
-  if (!builtin_amdgpu(root))
+  if (!builtin_amdgpu(root) && module_has_version(root))
     if (auto v = fs::attrs().read_trimmed(fs::join(root, "sys/module/amdgpu/version")); v && !v->empty()) return *v;
   if (root != "/" && !root.empty()) {
     // Synthetic trees carry the kernel banner under proc/.

@@ -284,6 +284,20 @@ TEST(DriverVersion_BuiltinAndLoadableAmdgpu) {
   EXPECT_EQ(resource::driver_version(dkms), std::string("6.12.12"));
   lm::write_file_atomically(dkms + "/sys/module/amdgpu/version", "6.14.3\n", 0644);
   EXPECT_EQ(resource::driver_version(dkms), std::string("6.14.3"));
+  // An in-tree loadable module (no `version`): the kernel release; then the
+  // module reloaded as a DKMS build (a new module directory): its version.
+  std::string intree = root + "/intree";
+  fs::mkdir_all(intree + "/proc/sys/kernel");
+  lm::write_file_atomically(intree + "/proc/sys/kernel/osrelease", "6.18.54-ant.1\n", 0644);
+  fs::mkdir_all(intree + "/sys/module/amdgpu");
+  lm::write_file_atomically(intree + "/sys/module/amdgpu/initstate", "live\n", 0644);
+  EXPECT_EQ(resource::driver_version(intree), std::string("6.18.54"));
+  EXPECT_EQ(resource::driver_version(intree), std::string("6.18.54"));
+  fs::remove_all(intree + "/sys/module/amdgpu");
+  fs::mkdir_all(intree + "/sys/module/amdgpu");
+  lm::write_file_atomically(intree + "/sys/module/amdgpu/initstate", "live\n", 0644);
+  lm::write_file_atomically(intree + "/sys/module/amdgpu/version", "6.16.1\n", 0644);
+  EXPECT_EQ(resource::driver_version(intree), std::string("6.16.1"));
   fs::remove_all(root);
 }
 

@@ -58,13 +58,15 @@ bool builtin_amdgpu(const std::string& root) {
 // the module directory kept open: the failing lookup by path walked
 // /sys/module/amdgpu every cycle (facts.driver 0.035 ms after an idle
 // second, profiles/bench_fresh_r4.txt r4fin3a).  A reloaded module is a new
-// directory: the old one reads as removed and is opened again.
+// directory: the old one has lost its `initstate` (every loadable module
+// has one; this is only asked when the module is not built in) and the path
+// is opened again.
 bool module_has_version(const std::string& root) {
   static std::mutex mu;
   static std::map<std::string, std::unique_ptr<fs::Dir>> dirs;
   std::lock_guard<std::mutex> g(mu);
   auto& d = dirs[root];
-  if (!d || d->removed()) d = std::make_unique<fs::Dir>(fs::join(root, "sys/module/amdgpu"));
+  if (!d || d->lookup("initstate") != 0) d = std::make_unique<fs::Dir>(fs::join(root, "sys/module/amdgpu"));
   return d->err() == 0 && d->lookup("version") == 0;
 }
 }  // namespace

@@ -352,11 +352,6 @@ std::string Dir::read_link(const char* name) const {
   return std::string(buf, static_cast<size_t>(n));
 }
 
-bool Dir::removed() const {
-  struct stat st;
-  return fd_ < 0 || ::fstat(fd_, &st) != 0 || st.st_nlink == 0;
-}
-
 int Dir::lookup(const char* name) const {
   if (fd_ < 0) return err_;
   struct stat st;

@@ -145,9 +145,6 @@ class Dir {
   // Whether `name` exists in the directory (not following a final symlink):
   // 0 if it does, else the errno (ENOENT: it does not).
   int lookup(const char* name) const;
-  // Whether the directory was removed since it was opened (a sysfs object
-  // that went away: st_nlink 0), or cannot be examined.
-  bool removed() const;
 
  private:
   int fd_ = -1;

@@ -288,7 +288,11 @@ def main() -> int:
     if dist.rank == 0:
         p50 = _percentile(ms, 0.5)
         backend_name = session.backend
-        phases = {name: round(_percentile(v, 0.5), 4) for name, v in session.bench_phases().items()}
+        bench_phases = session.bench_phases()
+        phases = {name: round(_percentile(v, 0.5), 4) for name, v in bench_phases.items()}
+        # In how many of the K timed steps each phase occurred (a step that
+        # created its own temporary file, took over the SR-IOV lookup...).
+        phases_n = {name: len(v) for name, v in bench_phases.items() if len(v) != a.steps}
         # Release the persistent amd-smi session before measuring variants
         # that must pay amdsmi_init themselves.
         del session
@@ -357,6 +361,7 @@ def main() -> int:
             # Per-phase p50 over the K timed steps: what an N-GPU cycle
             # spends where (the scaling curve's explanation).
             "phases_p50_ms": phases,
+            "phases_n": phases_n,
             # The deployed daemon's first cycle (library init included) and
             # its cycles after an idle second (see _daemon_loop).
             "first_cycle_ms": first_cycle,

@@ -66,6 +66,16 @@ class GpuSpec:
     # "auto" = gim for an SR-IOV PF on a GIM host, else amdgpu; None = none
     # (a guest whose amdgpu is not loaded).
     driver: str | None = "auto"
+    # Fixed identity (None: drawn from the node's seed): keeps a GPU's PCI
+    # bus and ASIC serial when other GPUs are added or removed (hot-plug).
+    bus: int | None = None
+    unique_id: int | None = None
+    # False: no KFD nodes (amdgpu does not drive the function, e.g. unbound).
+    serial: int | None = None
+    kfd: bool = True
+    # Compute partition modes the driver offers (amdgpu narrows them under
+    # some memory partition modes).
+    available_compute: str = "SPX, DPX, QPX, CPX"
 
 
 @dataclass
@@ -84,7 +94,37 @@ class NodeSpec:
     gim_version: str | None = None  # SR-IOV host driver (GIM) loaded: sys/module/gim/version
 
 
+# make_tree(): (root, {relative path: (kind, value)}) collecting what
+# make_node would write, instead of writing it.
+_sink: tuple[Path, dict] | None = None
+
+
+def _record(path: Path, entry: tuple) -> None:
+    root, tree = _sink
+    rel = path.relative_to(root)
+    for parent in list(rel.parents)[:-1]:
+        tree.setdefault(str(parent), ("d", None))
+    tree[str(rel)] = entry
+
+
+def _mkdir(path: Path) -> None:
+    if _sink:
+        _record(path, ("d", None))
+    else:
+        path.mkdir(parents=True, exist_ok=True)
+
+
+def _symlink(path: Path, target: str) -> None:
+    if _sink:
+        _record(path, ("l", target))
+    else:
+        path.symlink_to(target)
+
+
 def _write(path: Path, text: str | bytes) -> None:
+    if _sink:
+        _record(path, ("f", text if isinstance(text, bytes) else text.encode()))
+        return
     path.parent.mkdir(parents=True, exist_ok=True)
     if isinstance(text, bytes):
         path.write_bytes(text)
@@ -174,6 +214,7 @@ def make_node(root: str | os.PathLike, spec: NodeSpec) -> Path:
     topo = root / "sys/class/kfd/kfd/topology"
     _write(topo / "generation_id", "1\n")
     _write(root / "sys/module/amdgpu/version", spec.driver_version + "\n")
+    _write(root / "sys/module/amdgpu/initstate", "live\n")  # a loadable module's
     if spec.gim_version:
         _write(root / "sys/module/gim/version", spec.gim_version + "\n")
     if spec.partition_layout not in ("function", "shared", "distinct-ids"):
@@ -184,7 +225,7 @@ def make_node(root: str | os.PathLike, spec: NodeSpec) -> Path:
     flags = "fpu vme de pse tsc msr pae mce cx8 apic sep mtrr" + (" hypervisor" if spec.hypervisor else "") + " lahf_lm"
     _write(root / "proc/cpuinfo", "processor\t: 0\nvendor_id\t: AuthenticAMD\nmodel name\t: AMD EPYC 9575F 64-Core "
            f"Processor\nflags\t\t: {flags}\n\n")
-    (root / "sys/bus/pci/devices").mkdir(parents=True, exist_ok=True)
+    _mkdir(root / "sys/bus/pci/devices")
 
     node = 0
     for s in range(spec.cpu_sockets):
@@ -199,10 +240,12 @@ def make_node(root: str | os.PathLike, spec: NodeSpec) -> Path:
     render = 128
     for gi, g in enumerate(spec.gpus):
         parts = PARTITIONS_PER_MODE[g.compute_partition]
-        bus = buses[gi]
+        bus = buses[gi] if g.bus is None else g.bus
         location = bus << 8
         bdf = f"0000:{bus:02x}:00.0"
         unique = rng.getrandbits(64)
+        if g.unique_id is not None:
+            unique = g.unique_id
         xcc = g.xcds // parts
         node_mem = g.vram_bytes // parts
         for p in range(parts):
@@ -210,10 +253,12 @@ def make_node(root: str | os.PathLike, spec: NodeSpec) -> Path:
             # kfd_topology.c: location_id = pci_dev_id | xcp node id.
             node_location = location | p if spec.partition_layout != "shared" and parts > 1 else location
             node_unique = unique ^ (p + 1) if spec.partition_layout == "distinct-ids" and parts > 1 else unique
-            if g.hidden or (g.visible_partitions is not None and p not in g.visible_partitions):
+            if not g.kfd:
+                node -= 1  # no node of its own: the next GPU's take these ids
+            elif g.hidden or (g.visible_partitions is not None and p not in g.visible_partitions):
                 # Unreadable: the kernel returns EPERM; a directory named
                 # `properties` makes every read fail the same way (EISDIR).
-                (ndir / "properties").mkdir(parents=True, exist_ok=True)
+                _mkdir(ndir / "properties")
             else:
                 _write(ndir / "properties", _kfd_properties(g, parts, node_location, render, node_unique, xcc))
                 _write(ndir / "mem_banks/0/properties", f"heap_type 1\nsize_in_bytes {node_mem}\nflags 0\nwidth 8192\n")
@@ -230,12 +275,13 @@ def make_node(root: str | os.PathLike, spec: NodeSpec) -> Path:
         _write(d / "revision", "0x00\n")
         _write(d / "product_name", g.product_name + "\n")
         _write(d / "current_compute_partition", g.compute_partition + "\n")
-        _write(d / "available_compute_partition", "SPX, DPX, QPX, CPX\n")
+        _write(d / "available_compute_partition", g.available_compute + "\n")
         _write(d / "current_memory_partition", g.memory_partition + "\n")
         _write(d / "available_memory_partition", "NPS1, NPS2\n")
         _write(d / "mem_info_vram_total", f"{g.vram_bytes}\n")
         _write(d / "unique_id", f"{unique:016x}\n")
-        _write(d / "serial_number", f"{rng.randint(10**11, 10**12 - 1)}\n")
+        serial = rng.randint(10**11, 10**12 - 1)
+        _write(d / "serial_number", f"{serial if g.serial is None else g.serial}\n")
         # Every GPU sits in an 8-GPU xGMI hive whether or not the other GPUs
         # are visible to this container (measured: 7 peers on a 1-GPU box).
         peers = ["01"] * spec.hive_size
@@ -262,10 +308,9 @@ def make_node(root: str | os.PathLike, spec: NodeSpec) -> Path:
                "bc12sc00i00\n")
         if driver:
             drv = root / "sys/bus/pci/drivers" / driver
-            drv.mkdir(parents=True, exist_ok=True)
             for f in ("bind", "unbind", "new_id", "remove_id", "uevent"):
-                (drv / f).touch()
-            (drv / bdf).symlink_to(f"../../devices/{bdf}")
+                _write(drv / f, "")
+            _symlink(drv / bdf, f"../../devices/{bdf}")
         for v in range(sriov.get("num", 0)):
             vf_bdf = f"0000:{bus:02x}:00.{v + 1}"
             vd = root / "sys/bus/pci/devices" / vf_bdf
@@ -273,14 +318,27 @@ def make_node(root: str | os.PathLike, spec: NodeSpec) -> Path:
             _write(vd / "device", f"0x{sriov.get('vf_device', 0x75B3):04x}\n")
             _write(vd / "class", "0x120000\n")
             _write(vd / "config", config_space(sriov.get("vf_device", 0x75B3), None, 4096 if spec.privileged else 64))
-            (vd / "physfn").symlink_to(f"../{bdf}")
-            (d / f"virtfn{v}").symlink_to(f"../{vf_bdf}")
+            _symlink(vd / "physfn", f"../{bdf}")
+            _symlink(d / f"virtfn{v}", f"../{vf_bdf}")
     # An unrelated non-AMD PCI function (the scanner must skip it).
     other = root / "sys/bus/pci/devices/0000:00:00.0"
     _write(other / "vendor", "0x1022\n")
     _write(other / "class", "0x060000\n")
     _write(other / "config", b"\x22\x10" + bytes(62))
     return root
+
+
+def make_tree(spec: NodeSpec) -> dict[str, tuple]:
+    """What make_node(root, spec) would write, without writing it:
+    {path relative to the root: ("f", bytes) | ("l", link target) | ("d", None)}."""
+    global _sink
+    root = Path("/synthetic-node")
+    _sink = (root, {})
+    try:
+        make_node(root, spec)
+        return _sink[1]
+    finally:
+        _sink = None
 
 
 def make_mi355x_node(root: str | os.PathLike, n_gpus: int = 8, compute_partition: str = "SPX",
@@ -309,6 +367,8 @@ def fake_amdsmi_spec(root: str | os.PathLike, spec: NodeSpec, latency_us: int = 
     # make_node assigns buses in GPU order; recover each GPU's address from
     # its first partition node's location_id.
     for g in spec.gpus:
+        if not g.kfd:
+            continue  # no KFD nodes: amd-smi does not see it either
         parts = PARTITIONS_PER_MODE[g.compute_partition]
         first = None
         for p in range(parts):

@@ -121,21 +121,21 @@ class Session {
     // before the first cycle).
     sriov_ = sriov::new_sriov_lib(config_.sysfs_root());
     auto lib = sriov_;
-    prefetch_ = WorkerPool::instance().submit([lib] {
-      try {
-        lib->Devices();
-      } catch (...) {
-      }
-    });
+    if (!config_.oneshot())
+      prefetch_ = WorkerPool::instance().submit([lib] {
+        try {
+          lib->Devices();
+        } catch (...) {
+        }
+      });
     manager_ = resource::new_manager(config_);
     timestamp_ = lm::NewTimestampLabeler(config_);
   }
-  // A loop-mode session's cycles leave the next cycle's temporary file
-  // prepared and the old feature file to unlink (lm::temp_preparer); do not
-  // leave them behind.
+  // A loop-mode session's writes keep the swapped-out feature file for the
+  // next write (lm::write_to_file): do not leave it behind.
   ~Session() {
     prefetch_.cancel_or_wait();
-    lm::discard_prepared_temps();
+    lm::release_kept_files();
   }
   Session(const Session&) = delete;
   Session& operator=(const Session&) = delete;

@@ -176,28 +176,35 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
     sriov_detail = capture.take();
     sriov_ns = trace::now_ns() - s0;
   };
-  // Both on one worker, in that order: two workers measured slower (each
-  // task 1.5-4x longer on the second, colder core; profiles/ab_cycle_tasks.txt).
-  // Loop mode: the same worker then unlinks the old feature file and creates
-  // the temporary file of a later cycle's write (lm::temp_preparer) - never
-  // waited for, so it runs after the two even if this thread took them over.
-  // On this thread instead (no hand-off; the preparer job after the write)
-  // measured slower both ways: cycles 1 s apart 0.362 vs 0.2555 ms, back to
-  // back 0.0295 vs 0.023 ms (profiles/cycle_tasks_ab_r4.txt).
-  std::vector<WorkerPool::Task> seq;
-  {
+  // Loop mode: both on one worker, in that order (two workers measured
+  // slower: each task 1.5-4x longer on the second, colder core,
+  // profiles/ab_cycle_tasks.txt).  Whichever of the two the worker has not
+  // started when this thread needs it, this thread runs: the SR-IOV lookup
+  // before it waits for the node facts, the facts themselves if the worker
+  // has not reached them.  Against both on this thread, alternated on one
+  // box: back to back 0.0208 vs 0.0241 ms, cycles 1 s apart 0.194-0.228 vs
+  // 0.257-0.313 ms (profiles/cycle_tasks_ab_r5.txt).
+  //
+  // A oneshot Job runs both here, after enumeration: its one cycle would pay
+  // a worker thread's creation, which costs more than the work (Job process
+  // p50 1.05 vs 1.27 ms with the hand-off and the start-up SR-IOV prefetch,
+  // same file).
+  const bool overlap = !config.oneshot();
+  WorkerPool::Task facts_task, sriov_task;
+  if (overlap) {
     trace::Span span("submit");
-    std::vector<std::function<void()>> fns;
-    fns.reserve(3);
-    fns.emplace_back(read_facts);
-    fns.emplace_back(scan_sriov);
-    if (write && !config.oneshot())
-      if (auto prepare = lm::temp_preparer(config.output_file())) fns.push_back(std::move(prepare));
     submitted = trace::now_ns();
-    seq = WorkerPool::instance().submit_sequence(std::move(fns));
+    auto seq = WorkerPool::instance().submit_sequence({read_facts, scan_sriov});
+    facts_task = seq[0];
+    sriov_task = seq[1];
   }
-  WorkerPool::Task facts_task = seq[0], sriov_task = seq[1];
   auto join_facts = [&]() -> const lm::NodeFacts& {
+    if (!overlap) {
+      read_facts();
+      return facts;
+    }
+    int64_t s0 = trace::now_ns();
+    if (sriov_task.try_run()) trace::record("sriov.self", trace::now_ns() - s0);
     int64_t w0 = trace::now_ns();
     facts_task.run_or_wait();
     trace::record("facts.wait", trace::now_ns() - w0);  // inside "label"
@@ -212,16 +219,24 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
     sriov_task.cancel_or_wait();
     throw;
   }
-  int64_t j0 = trace::now_ns();
-  facts_task.cancel_or_wait();  // no devices: the labeler never needed them
-  sriov_task.run_or_wait();
-  // Where an overlapped cycle waits: how long after the hand-off the node
-  // facts started (a worker's wake-up, or this thread taking them over),
-  // and how long this thread then waited for the SR-IOV scan.
-  trace::record_top("sriov.join", trace::now_ns() - j0);
-  trace::record("facts.start", facts_start ? facts_start - submitted : 0);
-  trace::record("facts(overlapped)", facts_ns);
-  trace::record("sriov(overlapped)", sriov_ns);
+  if (overlap) {
+    int64_t j0 = trace::now_ns();
+    facts_task.cancel_or_wait();  // no devices: the labeler never needed them
+    sriov_task.run_or_wait();
+    // Where an overlapped cycle waits: how long after the hand-off the node
+    // facts started (a worker's wake-up, or this thread taking them over),
+    // and how long this thread then waited for the SR-IOV lookup.
+    trace::record_top("sriov.join", trace::now_ns() - j0);
+    trace::record("facts.start", facts_start ? facts_start - submitted : 0);
+    trace::record("facts(overlapped)", facts_ns);
+    trace::record("sriov(overlapped)", sriov_ns);
+  } else {
+    {
+      trace::Span span("sriov");
+      scan_sriov();
+    }
+    trace::record("facts", facts_ns);
+  }
   // Which way the lookup went (kept / checked / re-read) and the node facts'
   // parts, wherever they ran.
   for (const auto& p : facts_detail) trace::record(p.first, p.second);
@@ -259,7 +274,7 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
     }
     trace::Span span("write");
     try {
-      lm::write_to_file(r.labels, config.output_file());
+      lm::write_to_file(r.labels, config.output_file(), !config.oneshot());
     } catch (const std::exception& e) {
       throw Error("error writing file '" + config.output_file() + "': " + e.what());
     }
@@ -346,12 +361,16 @@ void start(const Context& ctx, SignalWatcher& sigs) {
     struct Prefetch {  // never outlives this iteration (an error exits the process)
       WorkerPool::Task task;
       ~Prefetch() { task.cancel_or_wait(); }
-    } prefetch{WorkerPool::instance().submit([sriov] {
-      try {
-        sriov->Devices();
-      } catch (...) {  // the cycle's own scan reports it
-      }
-    })};
+    } prefetch;
+    // Loop mode only: a Job's worker thread would cost more than it hides
+    // (see label_cycle).
+    if (!c.oneshot())
+      prefetch.task = WorkerPool::instance().submit([sriov] {
+        try {
+          sriov->Devices();
+        } catch (...) {  // the cycle's own scan reports it
+        }
+      });
     log::printf("\nRunning with config:\n%s", config::to_json(c).c_str());
     // A process killed without its exit cleanup (OOM, SIGKILL, node crash)
     // left its temporary files in <dir>/gfd-tmp: remove them before the

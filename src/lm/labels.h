@@ -55,22 +55,19 @@ LabelerPtr merge(std::vector<LabelerPtr> labelers);
 std::string render(const Labels& labels);
 
 // Write labels to `path` atomically (temp file in <dir>/gfd-tmp, rename,
-// 0644).  An empty path writes to stdout.  Throws gfd::Error.  A temporary
-// file prepared by temp_preparer()'s job is used if one is ready; the write
-// that uses one (loop mode) swaps it with the old feature file
-// (RENAME_EXCHANGE), leaving the old file for the next job to unlink.
-void write_to_file(const Labels& labels, const std::string& path);
+// 0644).  An empty path writes to stdout.  Throws gfd::Error.
+//
+// `reuse` (loop mode): the write swaps the new file with the old feature file
+// (renameat2 RENAME_EXCHANGE) and keeps the old one, under its temporary
+// name, to be rewritten by the next write to `path` - once a write lease
+// (F_SETLEASE) shows that no reader still has it open; otherwise, or where
+// leases are not available, the next write creates a new file as a oneshot
+// write does.  So a daemon's steady cycles create, unlink and evict no file.
+void write_to_file(const Labels& labels, const std::string& path, bool reuse = false);
 // Atomic write of arbitrary contents (labels.go:68-114).
 void write_file_atomically(const std::string& path, const std::string& contents, unsigned perm);
-// Loop mode: a job for a worker to run while a cycle enumerates - it unlinks
-// the old feature files earlier writes swapped out and creates the temporary
-// file of a later write to `path` (blocks preallocated for the last written
-// size where the write preallocates).  Empty when there is nothing to do or
-// a job is still out.
-std::function<void()> temp_preparer(const std::string& path);
-// Waits (bounded) for a handed-out job, then removes the prepared files and
-// any swapped-out feature file not unlinked yet.
-void discard_prepared_temps();
+// Closes and removes every file kept for reuse (a session that ends).
+void release_kept_files();
 // Start-up: removes <dir>/gfd-tmp left by a process that did not exit
 // cleanly (one GFD per node writes there, as the reference assumes).
 void sweep_temp_dir(const std::string& path);

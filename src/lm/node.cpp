@@ -29,7 +29,7 @@ namespace {
 Labels machine_type_labels(const std::string& path, std::string* warning) {
   std::string machine = "unknown";
   if (!path.empty()) {
-    auto r = fs::attrs().read(path, 4096);  // DMI: sysfs
+    auto r = fs::read_dmi(path);  // kept when it is the kernel's DMI (fixed until reboot)
     if (r.ok()) {
       machine = str::trim(r.data);
     } else {

@@ -1,21 +1,18 @@
 // The feature-file writer (lm/labels.h: write_to_file and friends): atomic
-// replacement through gfd-tmp/, with temporary files prepared by a worker
-// between cycles in loop mode.  The labelers are in labels.cpp.
+// replacement through gfd-tmp/; in loop mode the swapped-out feature file is
+// kept and rewritten by the next write.  The labelers are in labels.cpp.
 #include "lm/labels.h"
 
 #include <fcntl.h>
+#include <linux/fs.h>
 #include <sys/stat.h>
 #include <sys/vfs.h>
 #include <unistd.h>
 
-#include <algorithm>
-#include <chrono>
-#include <condition_variable>
-#include <functional>
+#include <map>
 #include <mutex>
 #include <string>
 #include <utility>
-#include <vector>
 
 #include <cerrno>
 #include <cstdio>
@@ -132,133 +129,25 @@ int remove_own_temps(const std::string& tmp_dir) {
 
 namespace {
 
-// Loop-mode state of the writer, kept between cycles: up to two temporary
-// files made ahead of the writes that will use them, and the old feature
-// files writes swapped out, until the next preparer job unlinks them (one
-// between cycles; two if a write came before the job that was to unlink its
-// predecessor had started).  All live in <dir>/gfd-tmp/, which the daemon
-// empties at start-up (sweep_temp_dir) and removes at exit, so a crash leaves
-// at most these files behind until the next start.
-//
-// Why each exists, measured with the daemon's cycles 1 s apart (the deployed
-// cadence is 60 s, so every cycle starts cold):
-//   * The prepared file: a cold create on the box's overlayfs costs 0.1-0.2
-//     ms, more than the rest of the write.  The cycle's worker makes the next
-//     file after its node-facts and SR-IOV tasks, off the critical path:
-//     write p50 0.055-0.090 ms vs 0.147-0.282 ms creating in the write
-//     (profiles/writer_ab_r3.txt).  Two, not one: the job runs while its own
-//     cycle writes, so the file a write uses must come from an earlier
-//     cycle's job - with one, every other write made its own file.  Each
-//     job tops the queue up to two (and makes gfd-tmp/ if the first cycle's
-//     write has not yet), so every write after the first takes one
-//     (tests/test_daemon.py::test_loop_writes_take_prepared_files).
-//   * The exchange: a rename over the old feature file frees its inode
-//     inside rename(2); on ext4 (the usual file system of NFD's features.d
-//     hostPath) that is most of a cold replace, 0.34-0.58 ms vs 0.03 ms for
-//     renameat2(RENAME_EXCHANGE), which leaves the old file under the
-//     temporary name for the next cycle's preparer job to unlink
-//     (profiles/rename_exchange_ab.txt).  Readers see the old file or the
-//     new one under `path`, never neither, exactly as with a rename.  A
-//     write exchanges even when an earlier old file still waits (its job
-//     had not started yet): waiting for it made 3 of 14 cold ext4 writes
-//     rename over the old file and pay the eviction, 0.35-0.39 ms; waking a
-//     worker for the unlink right after the write cost 0.1 ms every cycle.
-constexpr size_t kMaxPrepared = 2;
-constexpr size_t kMinPrealloc = 4096;
-
-struct Prepared {
-  std::string name;
-  int fd = -1;
-  size_t allocated = 0;  // bytes preallocated beyond EOF
-};
-
-struct WriterState {
-  std::mutex mu;
-  std::condition_variable cv;   // job finished
-  std::string dir;              // gfd-tmp/ of the prepared files
-  std::vector<Prepared> ready;  // oldest first
-  std::vector<std::string> retired;  // swapped-out feature files to unlink
-  std::string no_exchange_dir;  // whose file system refused RENAME_EXCHANGE
-  bool job = false;             // a preparer job is handed out, not yet finished or dropped
-  size_t last_size = 0;         // of the last write: the next file's preallocation
-};
-
-WriterState& writer() {
-  static auto* w = new WriterState;  // never destroyed: a worker may still use it at exit
-  return *w;
-}
-
-void drop_ready(WriterState& w) {  // caller holds mu
-  for (auto& f : w.ready) {
-    ::close(f.fd);
-    ::unlink(f.name.c_str());
-  }
-  w.ready.clear();
-}
-
-// Takes the oldest prepared file if it is in `tmp_dir` (fd, name,
-// preallocation), else -1; prepared files elsewhere are removed.
-int take_prepared(const std::string& tmp_dir, std::string* name, size_t* allocated) {
-  WriterState& w = writer();
-  std::lock_guard<std::mutex> lk(w.mu);
-  if (w.dir != tmp_dir) drop_ready(w);
-  if (w.ready.empty()) return -1;
-  Prepared f = std::move(w.ready.front());
-  w.ready.erase(w.ready.begin());
-  *name = std::move(f.name);
-  *allocated = f.allocated;
-  return f.fd;
-}
-
-// Replaces `path` by the finished temporary file `tmpl`.  `exchange` (loop
-// mode): swap the two names when `path` is a regular file; the old file,
-// now under `tmpl`, waits for the next preparer job.  Anything else - no
-// feature file yet, a directory or other non-file at `path` (which must fail
-// like rename(2) would), a file system without the exchange - is a plain
-// rename.  Returns 0 or an errno.
-int replace_file(const std::string& tmpl, const std::string& path, const std::string& tmp_dir, bool exchange) {
-  WriterState& w = writer();
-  if (exchange) {
-    std::lock_guard<std::mutex> lk(w.mu);
-    exchange = w.no_exchange_dir != tmp_dir;
-  }
-  struct stat st;
-  if (exchange && ::lstat(path.c_str(), &st) == 0 && S_ISREG(st.st_mode)) {
-    if (::renameat2(AT_FDCWD, tmpl.c_str(), AT_FDCWD, path.c_str(), RENAME_EXCHANGE) == 0) {
-      std::lock_guard<std::mutex> lk(w.mu);
-      w.retired.push_back(tmpl);
-      return 0;
-    }
-    if (errno == EINVAL || errno == ENOSYS || errno == EOPNOTSUPP) {
-      std::lock_guard<std::mutex> lk(w.mu);
-      w.no_exchange_dir = tmp_dir;
-    }
-  }
-  return ::rename(tmpl.c_str(), path.c_str()) == 0 ? 0 : errno;
-}
-
-// One attempt: false (nothing thrown, nothing left behind) when a prepared
-// file vanished before its rename - the caller retries with a fresh one.
-bool write_atomically_once(const std::string& path, const std::string& tmp_dir, const std::string& contents,
-                           unsigned perm, bool use_prepared) {
-  std::string tmpl;
-  size_t allocated = 0;
+// One attempt at the reference's write (labels.go:68-114): a new temporary
+// file in tmp_dir with `contents`, renamed over `path`.  `keep_fd`: the
+// file's descriptor is left open and returned through *kept (its name in
+// *tmpl); the rename is then the caller's.
+void create_and_write(const std::string& tmp_dir, const std::string& contents, unsigned perm, std::string* tmpl,
+                      int* kept) {
   int64_t t0 = trace::now_ns();
-  int fd = use_prepared ? take_prepared(tmp_dir, &tmpl, &allocated) : -1;
-  bool prepared_fd = fd >= 0;
   // The temporary directory normally exists from the previous cycle: try the
   // create first and make the directory only when it is missing.
-  if (fd < 0) fd = create_temp(tmp_dir, perm, &tmpl);
+  int fd = create_temp(tmp_dir, perm, tmpl);
   if (fd < 0 && errno == ENOENT) {
     try {
       fs::mkdir_all(tmp_dir);
     } catch (const std::exception& e) {
       throw Error(std::string("failed to create temporary directory: ") + e.what());
     }
-    fd = create_temp(tmp_dir, perm, &tmpl);
+    fd = create_temp(tmp_dir, perm, tmpl);
   }
-  // Failures remove gfd-tmp/ like the reference (labels.go:81-85): a
-  // prepared file lost with it is a vanished prepared file (retried).
+  // Failures remove gfd-tmp/ like the reference (labels.go:81-85).
   if (fd < 0) {
     int e = errno;
     remove_own_temps(tmp_dir);
@@ -266,134 +155,180 @@ bool write_atomically_once(const std::string& path, const std::string& tmp_dir, 
   }
   auto fail = [&](const std::string& msg) {
     ::close(fd);
-    ::unlink(tmpl.c_str());
+    ::unlink(tmpl->c_str());
     remove_own_temps(tmp_dir);
     throw Error(msg);
   };
   int64_t t1 = trace::now_ns();
-  trace::record(prepared_fd ? "write.take" : "write.create", t1 - t0);
+  trace::record("write.create", t1 - t0);
   // Best effort: a file system without fallocate(2) just takes the write.
-  if (contents.size() > allocated && wants_prealloc(fd))
-    (void)::fallocate(fd, 0, 0, static_cast<off_t>(contents.size()));
-  if (!write_all(fd, contents)) fail("error writing temporary file '" + tmpl + "': " + fs::errno_str(errno));
+  if (wants_prealloc(fd)) (void)::fallocate(fd, 0, 0, static_cast<off_t>(contents.size()));
+  if (!write_all(fd, contents)) fail("error writing temporary file '" + *tmpl + "': " + fs::errno_str(errno));
   // Created with `perm` already; chmod only what the umask took away.
   if ((perm & process_umask()) != 0 && ::fchmod(fd, perm) != 0)
-    fail("error setting permissions on '" + tmpl + "': " + fs::errno_str(errno));
-  if (::close(fd) != 0) {
+    fail("error setting permissions on '" + *tmpl + "': " + fs::errno_str(errno));
+  if (kept) {
+    *kept = fd;
+  } else if (::close(fd) != 0) {
     int e = errno;
-    ::unlink(tmpl.c_str());
+    ::unlink(tmpl->c_str());
     remove_own_temps(tmp_dir);
-    throw Error("error writing temporary file '" + tmpl + "': " + fs::errno_str(e));
+    throw Error("error writing temporary file '" + *tmpl + "': " + fs::errno_str(e));
   }
-  int64_t t2 = trace::now_ns();
-  trace::record("write.data", t2 - t1);
-  if (int e = replace_file(tmpl, path, tmp_dir, prepared_fd)) {
-    ::unlink(tmpl.c_str());
-    // A prepared file removed behind our back (gfd-tmp/ deleted between
-    // cycles): not an error of this cycle.
-    if (prepared_fd && e == ENOENT) return false;
-    remove_own_temps(tmp_dir);
-    throw Error("error moving temporary file to '" + path + "': " + fs::errno_str(e));
-  }
-  trace::record("write.rename", trace::now_ns() - t2);
-  return true;
+  trace::record("write.data", trace::now_ns() - t1);
 }
 
 std::string temp_dir_of(const std::string& path) { return fs::join(fs::dirname(fs::absolute(path)), "gfd-tmp"); }
+
+// Loop mode: the two files of one feature file.  `live` is the file now at
+// the output path (written by the last write); `spare` the one before it,
+// which that write swapped out to a name in gfd-tmp/ - the file the next
+// write rewrites.  Both stay open (writable).
+//
+// Why, measured on the pool's overlayfs: creating a file took 17-64 us on a
+// fresh box (2 us on tmpfs) and, done ahead on a worker as round 4 did,
+// held gfd-tmp/'s directory lock against the cycle's own rename, which then
+// waited for it (rename 0.049 ms against 0.004 ms alone,
+// profiles/fs_probe_r5.txt); on ext4 (the usual file system of NFD's
+// features.d hostPath) a rename over the old file frees its inode inside
+// rename(2), 0.34-0.58 ms cold vs 0.03 ms for an exchange
+// (profiles/rename_exchange_ab.txt), and unlinking it later costs the same
+// eviction.  Rewriting the swapped-out file needs none of these: a lease
+// check, a write into its existing blocks, the exchange.
+struct File {
+  std::string name;  // spare only: its name in gfd-tmp/
+  int fd = -1;
+  dev_t dev = 0;
+  ino_t ino = 0;
+};
+struct Slot {
+  std::string tmp_dir;
+  File live, spare;
+};
+
+std::mutex g_mu;
+std::map<std::string, Slot>& slots() {
+  static auto* m = new std::map<std::string, Slot>();  // never destroyed: read at exit
+  return *m;
+}
+
+void close_file(File& f, bool unlink_name) {
+  if (f.fd >= 0) ::close(f.fd);
+  if (unlink_name && !f.name.empty()) {
+    // Only if the name is still this file's.
+    struct stat st;
+    if (::lstat(f.name.c_str(), &st) == 0 && st.st_dev == f.dev && st.st_ino == f.ino) ::unlink(f.name.c_str());
+  }
+  f = File{};
+}
+
+// Rewrites the spare with `contents` if nobody else has it open; false (the
+// spare dropped) if it cannot be used.
+bool rewrite_spare(File& spare, const std::string& contents) {
+  if (spare.fd < 0) return false;
+  int64_t t0 = trace::now_ns();
+  struct stat st;
+  // Still ours under its name (gfd-tmp/ was not emptied behind our back)...
+  bool usable = ::lstat(spare.name.c_str(), &st) == 0 && st.st_dev == spare.dev && st.st_ino == spare.ino;
+  // ...and no reader that opened it while it was the feature file still has
+  // it open: a write lease is granted only to the sole opener.  EAGAIN: a
+  // reader; EINVAL/EACCES: no leases here (a file system without them,
+  // leases disabled).  Then the spare is left to its reader (unlinked) and
+  // this write creates a new file.
+  if (usable && ::fcntl(spare.fd, F_SETLEASE, F_WRLCK) != 0) usable = false;
+  if (!usable) {
+    close_file(spare, true);
+    return false;
+  }
+  bool ok = ::pwrite(spare.fd, contents.data(), contents.size(), 0) == static_cast<ssize_t>(contents.size());
+  // Shorter than before: cut the rest (same length, the steady case: no
+  // size change at all).
+  if (ok && static_cast<size_t>(st.st_size) > contents.size())
+    ok = ::ftruncate(spare.fd, static_cast<off_t>(contents.size())) == 0;
+  // Released before the exchange: an open of the feature file must not wait
+  // for a lease break.
+  (void)::fcntl(spare.fd, F_SETLEASE, F_UNLCK);
+  if (!ok) {
+    close_file(spare, true);
+    return false;
+  }
+  trace::record("write.reuse", trace::now_ns() - t0);
+  return true;
+}
+
+void write_kept(const std::string& path, const std::string& tmp_dir, const std::string& contents, unsigned perm) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  Slot& s = slots()[path];
+  if (s.tmp_dir != tmp_dir) {
+    close_file(s.spare, true);
+    close_file(s.live, false);
+    s.tmp_dir = tmp_dir;
+  }
+  File next;
+  if (rewrite_spare(s.spare, contents)) {
+    next = std::move(s.spare);
+    s.spare = File{};
+  } else {
+    create_and_write(tmp_dir, contents, perm, &next.name, &next.fd);
+    struct stat st;
+    if (::fstat(next.fd, &st) == 0) {
+      next.dev = st.st_dev;
+      next.ino = st.st_ino;
+    }
+  }
+  // Swap it with the feature file when that is a regular file; anything else
+  // at `path` (nothing yet, a directory that must fail like rename(2)
+  // would, a file system without the exchange) takes a plain rename.
+  int64_t t0 = trace::now_ns();
+  struct stat old;
+  bool swapped = false;
+  if (::lstat(path.c_str(), &old) == 0 && S_ISREG(old.st_mode)) {
+    swapped = ::renameat2(AT_FDCWD, next.name.c_str(), AT_FDCWD, path.c_str(), RENAME_EXCHANGE) == 0;
+  }
+  if (!swapped && ::rename(next.name.c_str(), path.c_str()) != 0) {
+    int e = errno;
+    close_file(next, true);
+    remove_own_temps(tmp_dir);
+    throw Error("error moving temporary file to '" + path + "': " + fs::errno_str(e));
+  }
+  trace::record("write.rename", trace::now_ns() - t0);
+  if (swapped && s.live.fd >= 0 && old.st_dev == s.live.dev && old.st_ino == s.live.ino) {
+    // The old feature file, ours, is now under the temporary name.
+    s.spare = std::move(s.live);
+    s.spare.name = next.name;
+  } else {
+    // Someone else's file was at `path` (now under the temporary name, to be
+    // removed as a rename would have), or nothing was.
+    if (swapped) ::unlink(next.name.c_str());
+    close_file(s.live, false);
+  }
+  next.name.clear();
+  s.live = std::move(next);
+}
 
 }  // namespace
 
 void write_file_atomically(const std::string& path, const std::string& contents, unsigned perm) {
   std::string tmp_dir = temp_dir_of(path);
-  // Prepared files are created 0644 - the feature file's mode.
-  WriterState& w = writer();
-  if (!write_atomically_once(path, tmp_dir, contents, perm, perm == 0644)) {
-    {
-      // gfd-tmp/ was removed under us: the other prepared files went with it.
-      std::lock_guard<std::mutex> lk(w.mu);
-      drop_ready(w);
-    }
-    write_atomically_once(path, tmp_dir, contents, perm, false);
+  std::string tmpl;
+  create_and_write(tmp_dir, contents, perm, &tmpl, nullptr);
+  int64_t t0 = trace::now_ns();
+  if (::rename(tmpl.c_str(), path.c_str()) != 0) {
+    int e = errno;
+    ::unlink(tmpl.c_str());
+    remove_own_temps(tmp_dir);
+    throw Error("error moving temporary file to '" + path + "': " + fs::errno_str(e));
   }
-  std::lock_guard<std::mutex> lk(w.mu);
-  w.last_size = contents.size();
+  trace::record("write.rename", trace::now_ns() - t0);
 }
 
-std::function<void()> temp_preparer(const std::string& path) {
-  if (path.empty()) return {};
-  std::string tmp_dir = temp_dir_of(path);
-  WriterState& w = writer();
-  size_t hint;
-  {
-    std::lock_guard<std::mutex> lk(w.mu);
-    size_t have = w.dir == tmp_dir ? w.ready.size() : 0;
-    if (w.job || (have >= kMaxPrepared && w.retired.empty())) return {};
-    w.job = true;
-    // Before the first write no size is known: a block, which holds the
-    // label file of a node of 8 GPUs.  Without it the first two loop writes
-    // allocated inside the write (write.data 0.066-0.089 ms vs 0.022-0.043,
-    // profiles/cold_rows_r4.txt).
-    hint = std::max<size_t>(w.last_size, kMinPrealloc);
+void release_kept_files() {
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (auto& [path, s] : slots()) {
+    close_file(s.spare, true);
+    close_file(s.live, false);
   }
-  // Clears `job` when the job has run or was dropped unrun.
-  std::shared_ptr<void> ticket(nullptr, [](void*) {
-    WriterState& q = writer();
-    std::lock_guard<std::mutex> lk(q.mu);
-    q.job = false;
-    q.cv.notify_all();
-  });
-  return [tmp_dir, hint, ticket] {
-    WriterState& q = writer();
-    std::vector<std::string> old;
-    size_t want;
-    {
-      std::lock_guard<std::mutex> lk(q.mu);
-      old.swap(q.retired);
-      size_t have = q.dir == tmp_dir ? q.ready.size() : 0;
-      want = have < kMaxPrepared ? kMaxPrepared - have : 0;
-    }
-    for (const auto& name : old) ::unlink(name.c_str());
-    // Top the queue up to kMaxPrepared, not one file per job: a job that
-    // runs after its own cycle's write (the worker is free only after the
-    // node facts and the SR-IOV scan) must still leave the next write one.
-    // Back to back too: the driver's 20-step headline 0.063-0.068 ms vs
-    // 0.073-0.076 with one file per job (profiles/headline_ab_r4.txt).
-    for (size_t i = 0; i < want; ++i) {
-      // The first cycle's job usually runs before gfd-tmp/ exists: make it
-      // (and the output directory), as that cycle's write is about to.
-      Prepared f;
-      f.fd = create_temp(tmp_dir, 0644, &f.name);
-      if (f.fd < 0 && errno == ENOENT) {
-        try {
-          fs::mkdir_all(tmp_dir);
-        } catch (const std::exception&) {
-          return;  // the write reports it
-        }
-        f.fd = create_temp(tmp_dir, 0644, &f.name);
-      }
-      if (f.fd < 0) return;
-      if (wants_prealloc(f.fd) && ::fallocate(f.fd, FALLOC_FL_KEEP_SIZE, 0, static_cast<off_t>(hint)) == 0)
-        f.allocated = hint;
-      std::lock_guard<std::mutex> lk(q.mu);
-      if (q.dir != tmp_dir) drop_ready(q);
-      q.dir = tmp_dir;
-      q.ready.push_back(std::move(f));
-    }
-  };
-}
-
-void discard_prepared_temps() {
-  WriterState& w = writer();
-  std::unique_lock<std::mutex> lk(w.mu);
-  // A job handed out runs soon (or is dropped): its file must not outlive
-  // this call.  Bounded all the same - exit must not hang on a worker stuck
-  // in the file system; a file it makes later stays in gfd-tmp/ until the
-  // next start's sweep.  system_clock: a steady_clock wait is
-  // pthread_cond_clockwait, which GCC 11's ThreadSanitizer does not intercept.
-  w.cv.wait_until(lk, std::chrono::system_clock::now() + std::chrono::seconds(1), [&] { return !w.job; });
-  drop_ready(w);
-  for (const auto& name : w.retired) ::unlink(name.c_str());
-  w.retired.clear();
+  slots().clear();
 }
 
 void sweep_temp_dir(const std::string& path) {
@@ -403,7 +338,7 @@ void sweep_temp_dir(const std::string& path) {
     throw Error("failed to remove stale temporary files in '" + tmp_dir + "': " + fs::errno_str(e));
 }
 
-void write_to_file(const Labels& labels, const std::string& path) {
+void write_to_file(const Labels& labels, const std::string& path, bool reuse) {
   std::string out = render(labels);
   if (path.empty()) {
     if (fwrite(out.data(), 1, out.size(), stdout) != out.size() || fflush(stdout) != 0)
@@ -411,19 +346,31 @@ void write_to_file(const Labels& labels, const std::string& path) {
     return;
   }
   try {
-    write_file_atomically(path, out, 0644);
+    if (reuse) {
+      std::string abs = fs::absolute(path);
+      write_kept(abs, temp_dir_of(abs), out, 0644);
+    } else {
+      write_file_atomically(path, out, 0644);
+    }
   } catch (const std::exception& e) {
     throw Error("error atomically writing file '" + path + "': " + e.what());
   }
 }
 
 void remove_output_file(const std::string& path) {
-  discard_prepared_temps();
   std::string abs = fs::absolute(path);
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = slots().find(abs);
+    if (it != slots().end()) {
+      close_file(it->second.spare, true);
+      close_file(it->second.live, false);
+      slots().erase(it);
+    }
+  }
   std::string tmp_dir = temp_dir_of(abs);
   if (int e = remove_own_temps(tmp_dir)) throw Error("failed to remove temporary output directory: " + fs::errno_str(e));
   if (::unlink(abs.c_str()) != 0) throw Error("failed to remove output file: " + fs::errno_str(errno));
 }
-
 
 }  // namespace gfd::lm

@@ -182,14 +182,24 @@ void WarmStartManager::Init() {
       thread_.join();
       if (!error.empty()) {
         fall_back(error);
+      } else if (!quick_devices_.empty() && devices != quick_devices_) {
+        // Labels from the quick manager are published and the preferred
+        // one would change them: keep the published source until the next
+        // (re)start, like the reference's fallback, which keeps one backend
+        // per start iteration (internal/resource/fallback.go:37-44) - the
+        // node's labels never flip because a backend finished starting.
+        log::printf("Warning: the %s manager (initialized in the background in %.1f ms) describes the GPUs "
+                    "differently from the %s manager, whose labels are published; labeling from the %s manager "
+                    "until the next restart (SIGHUP):\n%s:\n%s%s:\n%s",
+                    preferred_->Name().c_str(), static_cast<double>(ns) / 1e6, quick_->Name().c_str(),
+                    quick_->Name().c_str(), quick_->Name().c_str(), quick_devices_.c_str(), preferred_->Name().c_str(),
+                    devices.c_str());
+        state_ = State::quick_only;
+        current_ = quick_;
+        preferred_.reset();  // its session is not used again
       } else {
         log::printf("Using the %s manager (initialized in the background in %.1f ms)", preferred_->Name().c_str(),
                     static_cast<double>(ns) / 1e6);
-        if (!quick_devices_.empty() && devices != quick_devices_)
-          log::printf("Warning: the %s manager describes the GPUs differently from the %s manager; labels change "
-                      "now:\n%s:\n%s%s:\n%s",
-                      preferred_->Name().c_str(), quick_->Name().c_str(), quick_->Name().c_str(),
-                      quick_devices_.c_str(), preferred_->Name().c_str(), devices.c_str());
         state_ = State::preferred;
         current_ = preferred_;
       }

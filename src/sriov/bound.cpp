@@ -1,6 +1,8 @@
 #include "sriov/bound.h"
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <optional>
 #include <set>
 
@@ -32,7 +34,10 @@ bool is_pci_address(const std::string& name) {
 // reached here is AMD's: amdgpu's and gim's ID tables name vendor 0x1002 only,
 // and a PF's VFs carry its vendor.
 // Class and device ID from the function's `uevent` (PCI_CLASS=120000,
-// PCI_ID=1002:75A3): one read instead of `class` and `device`.
+// PCI_ID=1002:75A3): one read instead of `class` and `device`.  The kernel
+// prints PCI_CLASS with %04X, so a display function's leading zero is gone
+// (0x038000 is "38000"): the value is parsed and re-padded to the six digits
+// of the `class` attribute.
 bool from_uevent(const fs::Dir& dir, std::string* cls, std::string* device) {
   auto r = dir.read_attr("uevent");
   if (!r.ok()) return false;
@@ -42,8 +47,13 @@ bool from_uevent(const fs::Dir& dir, std::string* cls, std::string* device) {
     if (str::starts_with(line, "PCI_ID=")) id = line.substr(7);
   }
   auto colon = id.find(':');
-  if (c.empty() || colon == std::string::npos) return false;
-  *cls = "0x" + str::to_lower(c);
+  if (c.empty() || c.size() > 6 || colon == std::string::npos) return false;
+  char* end = nullptr;
+  unsigned long v = std::strtoul(c.c_str(), &end, 16);
+  if (end == c.c_str() || *end != 0) return false;
+  char buf[16];
+  std::snprintf(buf, sizeof(buf), "0x%06lx", v);
+  *cls = buf;
   *device = "0x" + str::to_lower(id.substr(colon + 1));
   return true;
 }

@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cerrno>
 #include <climits>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -301,6 +302,42 @@ AttrReader& attrs() {
   // Leaked on purpose: pool threads may read attributes during exit.
   static AttrReader* reader = new AttrReader();
   return *reader;
+}
+
+ReadResult read_dmi(const std::string& path) {
+  static std::mutex mu;
+  // path -> the kept value, or nullopt for a file found not to be DMI's.
+  // Leaked: workers may read at exit.
+  static auto* kept = new std::unordered_map<std::string, std::optional<std::string>>();
+  {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = kept->find(path);
+    if (it != kept->end()) {
+      if (it->second) return ReadResult{*it->second, 0};
+    }
+    if (it != kept->end() || kept->size() >= 64) return attrs().read(path, 4096);
+  }
+  int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return ReadResult{{}, errno};
+  ReadResult r;
+  r.err = pread_all(fd, 4096, &r.data);
+  bool constant = false;
+  struct statfs sfs;
+  if (r.err == 0 && ::fstatfs(fd, &sfs) == 0 && static_cast<long>(sfs.f_type) == kSysfsMagic) {
+    // Where the descriptor really points (any sysfs mount shows the one tree).
+    char link[64], real[PATH_MAX];
+    std::snprintf(link, sizeof(link), "/proc/self/fd/%d", fd);
+    ssize_t n = ::readlink(link, real, sizeof(real) - 1);
+    constant = n > 0 && std::string(real, static_cast<size_t>(n)).find("/devices/virtual/dmi/id/") != std::string::npos;
+  }
+  ::close(fd);
+  if (r.err) {
+    r.data.clear();
+    return r;  // asked again next time
+  }
+  std::lock_guard<std::mutex> g(mu);
+  kept->emplace(path, constant ? std::optional<std::string>(r.data) : std::nullopt);
+  return r;
 }
 
 Dir::Dir(const std::string& path) {

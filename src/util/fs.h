@@ -123,6 +123,15 @@ class AttrReader {
 // The process-wide reader used for per-cycle attribute reads.
 AttrReader& attrs();
 
+// A DMI identification attribute (e.g. the machine type's product_name).
+// The kernel copies these strings from the firmware's SMBIOS tables once at
+// boot (dmi_scan) and every read of sysfs devices/virtual/dmi/id/<attr>
+// returns them unchanged until the next boot, so the first successful read
+// of such a file is kept for the life of the process.  Any other file - a
+// synthetic tree, a regular file mounted over the default path - is read
+// through attrs() every time.
+ReadResult read_dmi(const std::string& path);
+
 // readlink(2); empty on failure.
 std::string read_link(const std::string& path);
 

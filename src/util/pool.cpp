@@ -217,6 +217,12 @@ void WorkerPool::Task::cancel_or_wait() {
   state_->cv.wait(lk, [this] { return state_->done; });
 }
 
+bool WorkerPool::Task::try_run() {
+  if (!state_ || state_->claimed.exchange(true)) return false;
+  state_->run();
+  return true;
+}
+
 void WorkerPool::Task::run_or_wait() {
   if (!state_) return;
   if (!state_->claimed.exchange(true)) state_->run();

@@ -45,6 +45,10 @@ class WorkerPool {
     // (a core coming out of a deep idle state after the daemon's sleep)
     // then costs the work itself, not the wake-up latency on top of it.
     void run_or_wait();
+    // Runs the task on the calling thread if no thread has started it yet
+    // (true), else returns false at once: a thread about to wait for another
+    // task of the same sequence takes this one over instead of idling.
+    bool try_run();
     // Drops the task if no thread has started it, else waits for it (its
     // exception is discarded).  Afterwards fn is not running and never will.
     void cancel_or_wait();

@@ -28,10 +28,14 @@
 //                             and virtualization mode NOT_SUPPORTED, the BDF
 //                             call succeeds with garbage, the partition
 //                             profile table lists SPX only
+//   init_latency_us=N         amdsmi_init takes N us (a library that starts
+//                             slowly, as the real one does: ~25 ms on MI355X)
 //   latency_us=N              every device query except handle-table lookups
 //                             (processor type, BDF, ASIC info) busy-waits N us
 //                             holding that GPU's lock (amd-smi serialises per
 //                             device), to model multi-GPU scaling of the backend
+// fake_amdsmi_stage(spec) holds a spec back until the next amdsmi_init, as
+// the real library only sees a changed node when it is initialised again.
 // Counters are exposed for assertions (fake_amdsmi_init_calls, ...).  The
 // spec can also come from the GFD_FAKE_AMDSMI_SPEC environment variable
 // ('|' separates lines), read when the library is loaded.
@@ -49,6 +53,7 @@
 #include <mutex>
 #include <sstream>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -84,6 +89,7 @@ struct State {
   std::atomic<int> virt_calls{0};
   int shutdown_calls = 0;
   long latency_us = 0;
+  long init_latency_us = 0;  // amdsmi_init takes this long (a slow library start)
   bool no_libdrm = false;
   uint32_t lib_major = 26;
   std::map<std::string, std::unique_ptr<std::mutex>> device_mu;  // by BDF
@@ -93,6 +99,7 @@ struct State {
   bool socket_per_slot = true;  // sockets=slot
   bool distinct_serials = false;  // partition_serials=distinct
   std::vector<std::vector<uint32_t>> sockets;  // processor indices per socket
+  std::unique_ptr<std::string> pending;  // fake_amdsmi_stage: applied by the next amdsmi_init
 };
 
 State& S() {
@@ -160,13 +167,32 @@ void copy(char* dst, size_t n, const std::string& src) {
 extern "C" {
 
 // ---- control API ----
+static int configure_locked(State& s, const char* spec);
+
 int fake_amdsmi_configure(const char* spec) {
   auto& s = S();
   std::lock_guard<std::mutex> g(s.mu);
+  s.pending.reset();
+  return configure_locked(s, spec);
+}
+
+// The node as the next amdsmi_init will find it: like the real library,
+// which enumerates the GPUs when it is initialised and keeps answering for
+// the processors it found until it is shut down and initialised again (a
+// partition switch or a driver reload in between leaves its handles stale).
+int fake_amdsmi_stage(const char* spec) {
+  auto& s = S();
+  std::lock_guard<std::mutex> g(s.mu);
+  s.pending = std::make_unique<std::string>(spec);
+  return 0;
+}
+
+static int configure_locked(State& s, const char* spec) {
   s.procs.clear();
   s.init_status = 0;
   s.stale_after = -1;
   s.latency_us = 0;
+  s.init_latency_us = 0;
   s.no_libdrm = false;
   s.lib_major = 26;
   s.fail.clear();
@@ -217,6 +243,10 @@ int fake_amdsmi_configure(const char* spec) {
         s.fail["amdsmi_get_gpu_asic_info"] = AMDSMI_STATUS_NOT_SUPPORTED;
         s.fail["amdsmi_get_gpu_virtualization_mode"] = AMDSMI_STATUS_NOT_SUPPORTED;
       }
+      continue;
+    }
+    if (line.rfind("init_latency_us=", 0) == 0) {
+      s.init_latency_us = std::atol(line.c_str() + 16);
       continue;
     }
     if (line.rfind("latency_us=", 0) == 0) {
@@ -305,8 +335,18 @@ int fake_amdsmi_initialized() { return S().initialized ? 1 : 0; }
 // ---- amd-smi API subset ----
 amdsmi_status_t amdsmi_init(uint64_t) {
   auto& s = S();
-  std::lock_guard<std::mutex> g(s.mu);
+  std::unique_lock<std::mutex> g(s.mu);
+  if (long us = s.init_latency_us; us > 0) {
+    g.unlock();
+    std::this_thread::sleep_for(std::chrono::microseconds(us));
+    g.lock();
+  }
   s.init_calls++;
+  if (s.pending) {
+    std::string spec = std::move(*s.pending);
+    s.pending.reset();
+    if (configure_locked(s, spec.c_str()) != 0) return AMDSMI_STATUS_INVAL;
+  }
   if (s.init_status) return static_cast<amdsmi_status_t>(s.init_status);
   s.initialized = true;
   if (s.stale) s.stale_after = -1;  // handles go stale once; a re-init fixes them

@@ -129,44 +129,69 @@ def test_without_libdrm_or_fru_name_both_backends_use_the_device_model(binary, t
     assert "MI3" in golden.parse_labels(outs["amdsmi"])["amd.com/gpu.product"]
 
 
-def _loop_stderr(binary, args, env, until, timeout=20.0):
+def _loop_files(binary, args, env, cycles_after, marker, timeout=20.0):
+    """Run the loop daemon until `marker` is logged and `cycles_after` more
+    cycles have written the feature file; return (stderr, the file's
+    content after every cycle, in order)."""
     import os
     import signal
     import subprocess
     import time
 
+    out = next(a.split("=", 1)[1] for a in args if a.startswith("--output-file="))
     p = subprocess.Popen([binary, "--sleep-interval=20ms", *args], stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
                          text=True, env={**{k: v for k, v in os.environ.items() if not k.startswith("GFD_")}, **env})
-    err, waiting = [], list(until)
+    err, files, left = [], [], None
     try:
         end = time.monotonic() + timeout
         for line in p.stderr:
             err.append(line)
-            if waiting and waiting[0] in line:
-                waiting.pop(0)
-            if not waiting or time.monotonic() > end:
+            if marker in line:
+                left = cycles_after
+            if "Sleeping for" in line:  # the cycle's file is in place
+                with open(out) as f:
+                    files.append(f.read())
+                if left is not None:
+                    left -= 1
+                    if left <= 0:
+                        break
+            if time.monotonic() > end:
                 break
     finally:
         p.send_signal(signal.SIGTERM)
         _, rest = p.communicate(timeout=30)
         err.append(rest or "")
-    return "".join(err)
+    return "".join(err), files
 
 
 @pytest.mark.skipif(not FAKE.exists(), reason="libfake_amdsmi.so not built")
-@pytest.mark.parametrize("agree", [True, False])
-def test_warm_start_switch_logs_a_backend_disagreement(binary, tmp_path, agree):
+@pytest.mark.parametrize("agree", [True, False], ids=["agree", "disagree"])
+def test_warm_start_switch_never_changes_the_published_labels(binary, tmp_path, agree):
     """The loop daemon labels its first cycles from KFD while amd-smi starts
-    in the background; at the switch it compares what both report and logs
-    any difference (the labels change at that cycle), silent when they agree."""
-    spec = synth.NodeSpec(gpus=[synth.GpuSpec()], seed=31)
+    in the background (here: 60 ms, so several KFD cycles publish first).
+    When amd-smi is ready it takes over if it describes the GPUs as KFD did;
+    if it does not, the daemon logs the difference once and keeps labeling
+    from KFD until the next restart - the published labels never change
+    because a backend finished starting (a CPX node, whose partitions are
+    where the two backends could disagree)."""
+    spec = synth.NodeSpec(gpus=[synth.GpuSpec(compute_partition="CPX")], seed=31)
     root = synth.make_node(tmp_path / "root", spec)
-    fake = synth.fake_amdsmi_spec(root, spec)
+    fake = synth.fake_amdsmi_spec(root, spec) + "\ninit_latency_us=60000"
     if not agree:
         fake = fake.replace("name=AMD Instinct MI355 OAM", "name=AMD Instinct MI355X")
     env = {"GFD_AMDSMI_LIBRARY": str(FAKE), "GFD_FAKE_AMDSMI_SPEC": fake.replace("\n", "|")}
-    err = _loop_stderr(binary, ["--backend=auto", f"--sysfs-root={root}", f"--output-file={tmp_path / 'gfd'}",
-                                f"--machine-type-file={root}/sys/class/dmi/id/product_name"], env,
-                       until=["initialized in the background in", "Sleeping for"])
+    err, files = _loop_files(binary, ["--backend=auto", f"--sysfs-root={root}", f"--output-file={tmp_path / 'gfd'}",
+                                      f"--machine-type-file={root}/sys/class/dmi/id/product_name", "--mig-strategy=single"],
+                             env, cycles_after=5, marker="initialized in the background in")
     assert "initialized in the background in" in err, err[-3000:]
-    assert ("describes the GPUs differently" in err) != agree, err[-3000:]
+    switched = err.split("initialized in the background in", 1)[0]
+    assert switched.count("Writing labels to output file") >= 1, err[-3000:]  # KFD published first
+    assert err.count("describes the GPUs differently") == (0 if agree else 1), err[-3000:]
+    if agree:
+        assert "Using the amdsmi(persistent) manager (initialized in the background" in err
+    else:
+        assert "labeling from the sysfs manager until the next restart" in err
+        assert "Using the amdsmi(persistent) manager" not in err
+    # Byte-identical feature files across the switch: not a single change.
+    assert len(files) >= 6 and len(set(files)) == 1, [f.splitlines()[:3] for f in files]
+    assert golden.parse_labels(files[-1])["amd.com/gpu.count"] == "8"

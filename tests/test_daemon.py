@@ -107,37 +107,27 @@ def _temps(tmp: Path) -> list[tuple[Path, os.stat_result]]:  # gfd-tmp/gfd-XXXXX
     return out
 
 
-def _split(tmp: Path):
-    """(prepared, retired): prepared files are empty, the old feature file a
-    write swapped out holds labels."""
-    ready, old = [], []
-    for f, st in _temps(tmp):
-        (old if st.st_size else ready).append((f, st))
-    return ready, old
-
-
-def test_loop_keeps_at_most_two_prepared_files_and_one_old_file(binary, tmp_path):
-    """Loop mode: between cycles gfd-tmp/ holds one or two empty 0644 files
-    made for the next writes, which swap them into place (RENAME_EXCHANGE),
-    and at most one old feature file swapped out, which the next cycle's
-    worker unlinks.  Exit removes everything (main.go:149-156)."""
+def test_loop_alternates_two_files_and_keeps_the_old_one(binary, tmp_path):
+    """Loop mode: each write rewrites the file the previous write swapped
+    out (RENAME_EXCHANGE), so the feature file alternates between two
+    inodes and, between cycles, gfd-tmp/ holds exactly the other one: the
+    previous labels, 0644.  Exit removes everything (main.go:149-156)."""
     out = tmp_path / "gfd"
     tmp = tmp_path / "gfd-tmp"
     p = _start(binary, ["--sleep-interval=200ms", *_base(tmp_path, out)])
     try:
         assert _wait_for(out.exists), "first write"
-        assert _wait_for(lambda: len(_split(tmp)[0]) >= 1), _temps(tmp)
-        for _ in range(3):
-            ready, old = _split(tmp)
-            assert len(ready) <= 2 and len(old) <= 1, _temps(tmp)
-            assert len(_temps(tmp)) <= 3
-            for f, st in ready:
-                assert oct(st.st_mode & 0o777) == "0o644"
-            inos = {st.st_ino for _, st in ready}
+        assert _wait_for(lambda: len(_temps(tmp)) == 1), _temps(tmp)
+        inos = set()
+        for _ in range(4):
+            kept = _temps(tmp)
+            assert len(kept) == 1, kept
+            f, st = kept[0]
+            assert oct(st.st_mode & 0o777) == "0o644"
+            inos |= {st.st_ino, out.stat().st_ino}
             m0 = out.stat().st_mtime_ns
             assert _wait_for(lambda: out.stat().st_mtime_ns > m0, timeout=5), "file not rewritten"
-            if inos:
-                assert out.stat().st_ino in inos  # the prepared file became the feature file
+        assert len(inos) == 2, inos
         assert golden.parse_labels(out.read_text())["amd.com/gpu.product"] == "MOCKMODEL"
     finally:
         p.send_signal(signal.SIGTERM)
@@ -148,7 +138,7 @@ def test_loop_keeps_at_most_two_prepared_files_and_one_old_file(binary, tmp_path
 
 def test_sigkilled_daemons_leave_a_bounded_gfd_tmp(binary, tmp_path):
     """A daemon killed without its exit cleanup (OOM, SIGKILL) leaves its
-    prepared and old files in gfd-tmp/; the next start sweeps them before its
+    kept old feature file in gfd-tmp/; the next start sweeps it before its
     first write, so restarts never accumulate files (the reference leaks one
     temporary file per crash, labels.go:68-114)."""
     out = tmp_path / "gfd"
@@ -156,21 +146,21 @@ def test_sigkilled_daemons_leave_a_bounded_gfd_tmp(binary, tmp_path):
     for _ in range(3):
         p = _start(binary, ["--sleep-interval=50ms", *_base(tmp_path, out)])
         try:
-            # Several cycles: a prepared file and an old one are waiting.
+            # Several cycles: the old feature file is kept.
             assert _wait_for(lambda: out.exists() and len(_temps(tmp)) >= 1)
             time.sleep(0.3)
         finally:
             p.kill()
             p.wait(timeout=10)
-        assert 1 <= len(_temps(tmp)) <= 3, _temps(tmp)
+        assert 1 <= len(_temps(tmp)) <= 2, _temps(tmp)  # the kept file (and one being created)
     stale = {f for f, _ in _temps(tmp)}
     m0 = out.stat().st_mtime_ns  # before the start: its first write may come at once
     p = _start(binary, ["--sleep-interval=10s", *_base(tmp_path, out)])
     try:
         assert _wait_for(lambda: out.stat().st_mtime_ns > m0), "first cycle"
-        time.sleep(0.2)  # the cycle's preparer job has run (whether its file is left depends on timing)
+        time.sleep(0.2)
         left = _temps(tmp)
-        assert len(left) <= 2, left
+        assert len(left) <= 1, left
         assert not stale & {f for f, _ in left}, left
     finally:
         p.send_signal(signal.SIGTERM)
@@ -208,7 +198,7 @@ def test_exchange_never_swaps_a_directory_into_gfd_tmp(binary, tmp_path):
     out = tmp_path / "gfd"
     p = _start(binary, ["--sleep-interval=100ms", *_base(tmp_path, out)])
     try:
-        assert _wait_for(lambda: out.exists() and len(_split(tmp_path / "gfd-tmp")[0]) >= 1)
+        assert _wait_for(lambda: out.exists() and len(_temps(tmp_path / "gfd-tmp")) >= 1)
         out.unlink()
         out.mkdir()
         (out / "keep").write_text("user data")
@@ -262,7 +252,7 @@ def test_sighup_reloads_config(binary, tmp_path):
 
 def test_sighup_to_a_new_output_file_leaves_nothing_in_the_old_directory(binary, tmp_path):
     """A reload that moves the feature file: the old file and its gfd-tmp/
-    (with any prepared temporary files) go, the new directory gets both, and
+    (with the old feature file kept there) go, the new directory gets both, and
     what a crashed daemon left in the new gfd-tmp/ is swept before the first
     write there."""
     old_dir, new_dir = tmp_path / "old", tmp_path / "new"
@@ -402,16 +392,19 @@ def test_trace_timing_logs_phases(binary, tmp_path):
     out = tmp_path / "gfd"
     cp = run_daemon(binary, "--oneshot", "--trace-timing", *_base(tmp_path, out), check=True)
     line = [ln for ln in cp.stderr.splitlines() if "Timing:" in ln][0]
-    for phase in ("init=", "enumerate=", "label=", "sriov(overlapped)=", "write=", "total="):
-        assert phase in line
+    fields = _timing_fields(line)
+    # A Job reads the node facts and does the SR-IOV lookup on its one thread.
+    for phase in ("init", "enumerate", "label", "facts", "sriov", "write", "write.create", "total"):
+        assert phase in fields, line
+    assert "submit" not in fields and "sriov(overlapped)" not in fields, line
 
 
 # The cycle thread's top-level phases (daemon.cpp label_cycle, node.cpp
 # NewDeviceLabeler): disjoint stretches of the cycle, so with `other` they
 # must add up to `total`.  Everything else on the line is a detail of one of
 # them (amdsmi.*, sysfs.*, pci.*, write.*) or work overlapped on a worker.
-TOP_LEVEL = {"placement", "versions", "submit", "init", "enumerate", "label", "shutdown", "sriov.join", "merge", "log",
-             "write"}
+TOP_LEVEL = {"placement", "versions", "submit", "init", "enumerate", "label", "shutdown", "sriov.join", "sriov", "merge",
+             "log", "write"}
 
 
 def _timing_fields(line: str) -> dict:
@@ -660,7 +653,7 @@ def _loop_write_modes(binary, root, out, cycles, interval):
         for line in p.stderr:
             if "Timing:" in line:
                 f = _timing_fields(line)
-                modes.append("take" if "write.take" in f else "create" if "write.create" in f else "?")
+                modes.append("create" if "write.create" in f else "reuse" if "write.reuse" in f else "?")
                 if len(modes) >= cycles:
                     break
     finally:
@@ -669,12 +662,12 @@ def _loop_write_modes(binary, root, out, cycles, interval):
     return modes
 
 
-def test_loop_writes_take_prepared_files(binary, tmp_path):
-    """Round-3 verdict, weak #5: the deployed cadence still created its
-    temporary file inside some writes.  The loop daemon 1 s apart for 10
-    cycles, on ext4 (tmp_path here) and on tmpfs (/dev/shm) at once: every
-    write after the first takes a file a worker prepared (the first cycle's
-    may too, if its job ran before its write)."""
+def test_loop_writes_create_no_file_after_the_second(binary, tmp_path):
+    """The loop daemon 1 s apart for 10 cycles (the deployed cadence), on
+    ext4 (tmp_path here) and on tmpfs (/dev/shm) at once: the first two
+    writes create their files, every later one rewrites the file the write
+    before swapped out - no create inside a write, and no worker making
+    files ahead."""
     import concurrent.futures
     import shutil
     import tempfile
@@ -690,4 +683,4 @@ def test_loop_writes_take_prepared_files(binary, tmp_path):
         for d in dirs[1:]:
             shutil.rmtree(d, ignore_errors=True)
     for d, modes in zip(dirs, runs):
-        assert len(modes) == 10 and modes[1:] == ["take"] * 9, (str(d), modes)
+        assert len(modes) == 10 and modes[:2] == ["create"] * 2 and modes[2:] == ["reuse"] * 8, (str(d), modes)

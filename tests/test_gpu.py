@@ -295,11 +295,12 @@ def test_kept_partition_mode_lists_match_the_driver_every_cycle(native):
                 assert d[key] == want, (d["bdf"], attr, d[key], want)
 
 
-def test_idle_cycles_on_hardware_are_attributed_and_take_prepared_files(binary, tmp_path):
+def test_idle_cycles_on_hardware_are_attributed_and_create_no_file(binary, tmp_path):
     """The deployed daemon (auto backend) with idle time between cycles, on
     the real node: every cycle's named phases account for all but a few
     microseconds of it (round-3 verdict: 0.369 ms of a 0.683 ms cycle were
-    unnamed), and every write after the first takes a prepared file."""
+    unnamed), and every write after the second rewrites the old feature
+    file instead of creating one."""
     import signal
     import statistics
 
@@ -323,7 +324,7 @@ def test_idle_cycles_on_hardware_are_attributed_and_take_prepared_files(binary, 
     for r in rows:
         assert abs(sum(v for k, v in r.items() if k in TOP_LEVEL) + r["other"] - r["total"]) <= 0.013, r
     assert statistics.median(r["other"] for r in rows[1:]) <= 0.02, rows
-    assert all("write.take" in r for r in rows[1:]), rows
+    assert all("write.reuse" in r and "write.create" not in r for r in rows[2:]), rows
 
 
 def test_auto_backend_switch_with_library_values_keeps_the_labels(native):

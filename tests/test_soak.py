@@ -34,11 +34,11 @@ def _fds(pid: int) -> tuple[int, int]:
     # Minimum over a short window: a cycle in flight holds transient
     # descriptors (the temp output file, an amd-smi device node), a leak
     # raises the floor.  The window must catch the daemon between cycles at
-    # least once (see the per-cycle interval below).  Prepared temporary
-    # files (gfd-tmp/gfd-*, up to two kept open between cycles by design,
-    # src/lm/writer.cpp WriterState) are counted apart: how many are ready
-    # at a sample depends on timing, not on leaks - that made the floor
-    # 15 or 16 from run to run.  Returns (floor without them, most of them).
+    # least once (see the per-cycle interval below).  Files open in
+    # gfd-tmp/ (the old feature file kept for the next write, by design:
+    # src/lm/writer.cpp Slot) are counted apart: whether one is there at a
+    # sample depends on timing (a write swapping names), not on leaks.
+    # Returns (floor without them, most of them).
     # A descriptor closed between the listing and its readlink still counts:
     # skipping it let a sample taken while a re-read swaps descriptors (new
     # ones opened after the listing, old ones closed before the readlink)
@@ -91,8 +91,8 @@ def soak(binary: str, args: list[str], seconds: float, hup_at: float | None = No
             time.sleep(0.05)
         assert p.poll() is None, "".join(tail)
         rss1, (fd1, prep1), c1 = _rss_kib(p.pid), _fds(p.pid), cycles[0]
-        # Files in gfd-tmp/: prepared ones and old feature files swapped out
-        # by exchanges, which the next cycle's worker unlinks.
+        # Files in gfd-tmp/: the old feature file kept for the next write
+        # (and, in a write that could not reuse it, the one being made).
         out = next((a.split("=", 1)[1] for a in args if a.startswith("--output-file=")), "")
         tmp_files = sum(len(fs) for _, _, fs in os.walk(os.path.join(os.path.dirname(out), "gfd-tmp"))) if out else 0
     finally:
@@ -111,10 +111,8 @@ def _assert_steady(r: dict, min_cycles: int):
     assert r["rc"] == 0, r["tail"]
     assert r["cycles"] >= min_cycles, r
     assert r["fd1"] <= r["fd0"], f"file descriptors grew {r['fd0']} -> {r['fd1']}"
-    assert r["prepared"] <= 2, f"{r['prepared']} prepared temporary files open (at most two by design)"
-    # Two prepared + the swapped-out files no worker job has reached yet (one
-    # between cycles; two if a cycle's write beats the previous cycle's job).
-    assert r["tmp_files"] <= 4, f"{r['tmp_files']} files in gfd-tmp/: old feature files are not being unlinked"
+    assert r["prepared"] <= 2, f"{r['prepared']} temporary files open (one kept by design, one being swapped)"
+    assert r["tmp_files"] <= 2, f"{r['tmp_files']} files in gfd-tmp/: old feature files are not being reused"
     # Allocator noise only: a leak of even 100 bytes/cycle over thousands of
     # cycles would exceed this.
     assert r["rss1"] - r["rss0"] <= 1024, f"RSS grew {r['rss0']} -> {r['rss1']} KiB over {r['cycles']} cycles"
@@ -146,4 +144,4 @@ def test_soak_amdsmi_backend_no_growth(binary, tmp_path, session):
     _assert_steady(r, min_cycles=int(seconds * (15 if per_cycle else 200)))
     assert r["reloads"] == 1, r["tail"]
     print(f"soak[{session}]: {r['cycles']} cycles in {seconds:.0f}s, RSS {r['rss0']} -> {r['rss1']} KiB, "
-          f"fds {r['fd0']} -> {r['fd1']} (+ up to {r['prepared']} prepared temporary files)")
+          f"fds {r['fd0']} -> {r['fd1']} (+ up to {r['prepared']} kept temporary files)")

@@ -245,27 +245,36 @@ TEST(Run_NullManagerWritesOnlyTimestampAndSriov) {
 }
 
 TEST(LabelCycle_RecordsPhases) {
-  auto c = run_config("", "none", true, true);
-  resource::MockManager m({resource::new_full_gpu()});
-  auto ts = lm::NewTimestampLabeler(c, 1);
-  auto r = label_cycle(m, sriov::new_empty_sriov(), c, ts, false);
-  std::vector<std::string> names;
-  int machine = 0;  // where depends on which thread read the facts
-  for (const auto& p : r.phases) {
-    if (p.first == "facts.machine") {
-      ++machine;
-      continue;
+  for (bool oneshot : {true, false}) {
+    auto c = run_config("", "none", true, oneshot);
+    resource::MockManager m({resource::new_full_gpu()});
+    auto ts = lm::NewTimestampLabeler(c, 1);
+    auto r = label_cycle(m, sriov::new_empty_sriov(), c, ts, false);
+    std::vector<std::string> names;
+    int machine = 0;  // where depends on which thread read the facts
+    for (const auto& p : r.phases) {
+      if (p.first == "facts.machine") {
+        ++machine;
+        continue;
+      }
+      if (p.first == "sriov.self") continue;  // this thread took the SR-IOV lookup over
+      names.push_back(p.first);
     }
-    names.push_back(p.first);
+    EXPECT_EQ(machine, 1);
+    if (oneshot) {
+      // A Job reads the node facts and does the lookup on this thread.
+      EXPECT_EQ(names, (std::vector<std::string>{"placement", "versions", "init", "enumerate", "label", "shutdown",
+                                                 "sriov", "facts", "merge"}));
+    } else {
+      EXPECT_EQ(names, (std::vector<std::string>{"placement", "versions", "submit", "init", "enumerate", "facts.wait",
+                                                 "label", "shutdown", "sriov.join", "facts.start", "facts(overlapped)",
+                                                 "sriov(overlapped)", "merge"}));
+    }
+    // Every top-level phase is named: what is left is bookkeeping.
+    EXPECT_TRUE(r.other_ns >= 0 && r.other_ns < r.total_ns);
+    EXPECT_TRUE(r.total_ns > 0);
+    EXPECT_EQ(r.labels["amd.com/gfd.timestamp"], std::string("1"));
   }
-  EXPECT_EQ(machine, 1);
-  EXPECT_EQ(names, (std::vector<std::string>{"placement", "versions", "submit", "init", "enumerate", "facts.wait",
-                                             "label", "shutdown", "sriov.join", "facts.start", "facts(overlapped)",
-                                             "sriov(overlapped)", "merge"}));
-  // Every top-level phase is named: what is left is bookkeeping.
-  EXPECT_TRUE(r.other_ns >= 0 && r.other_ns < r.total_ns);
-  EXPECT_TRUE(r.total_ns > 0);
-  EXPECT_EQ(r.labels["amd.com/gfd.timestamp"], std::string("1"));
 }
 
 TEST(Trace_CaptureHandsAWorkersRecordsToTheCycleOnce) {

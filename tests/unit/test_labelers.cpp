@@ -20,6 +20,7 @@
 #include "resource/versions.h"
 #include "test.h"
 #include "util/fs.h"
+#include "util/trace.h"
 
 using namespace gfd;
 using lm::Labels;
@@ -479,115 +480,96 @@ TEST(WriteToFile_RecoversFromABlockedTemporaryDirectory) {
 }
 
 namespace {
-// What the daemon's cycle does: run the preparer job (here inline), write.
-void prepare_then_write(const Labels& l, const std::string& path) {
-  if (auto job = lm::temp_preparer(path)) job();
-  lm::write_to_file(l, path);
-}
-// Files waiting in gfd-tmp/ (gfd-XXXXXX): prepared or swapped out.
-std::vector<std::string> prepared_files(const std::string& dir) {
+// The daemon's loop-mode write.
+void loop_write(const Labels& l, const std::string& path) { lm::write_to_file(l, path, true); }
+// Files in gfd-tmp/: the kept (swapped-out) feature file.
+std::vector<std::string> temp_files(const std::string& dir) {
   std::vector<std::string> out;
   for (const auto& n : fs::list_dir(dir + "/gfd-tmp")) out.push_back(dir + "/gfd-tmp/" + n);
   std::sort(out.begin(), out.end());
   return out;
 }
-}  // namespace
-
-namespace {
 ino_t inode(const std::string& p) {
   struct stat st;
   return ::stat(p.c_str(), &st) == 0 ? st.st_ino : 0;
 }
 }  // namespace
 
-TEST(WriteToFile_UsesPreparedTemporaryFiles) {
+TEST(WriteToFile_LoopWritesAlternateTwoFilesAndCreateNone) {
+  // The first two loop writes create their files (the second swaps the
+  // first out with RENAME_EXCHANGE); from then on each write rewrites the
+  // file the previous one swapped out, so the feature file alternates
+  // between two inodes and gfd-tmp/ holds exactly the other one.
   char dir[] = "/tmp/gfd-write-XXXXXX";
   EXPECT_TRUE(mkdtemp(dir) != nullptr);
-  std::string path = std::string(dir) + "/gfd", tmp = std::string(dir) + "/gfd-tmp";
-  lm::write_to_file({{"k", "0"}}, path);  // creates gfd-tmp/
-  // One job tops the queue up to two files; further jobs have nothing to do.
-  if (auto job = lm::temp_preparer(path)) job();
-  auto both = prepared_files(dir);
-  EXPECT_EQ(both.size(), static_cast<size_t>(2));
-  EXPECT_FALSE(static_cast<bool>(lm::temp_preparer(path)));
-  // The write takes the older (made first); which name that is, the inodes
-  // tell after the write.
-  std::string a = both[0], b = both[1];
-  struct stat st;
-  EXPECT_TRUE(stat(a.c_str(), &st) == 0);
-  EXPECT_EQ(static_cast<long>(st.st_size), 0L);
-  EXPECT_EQ(static_cast<int>(st.st_mode & 0777), 0644);
-  ino_t ino_a = inode(a), ino_b = inode(b);
-  // A write takes the oldest: its inode becomes the feature file, and the
-  // old feature file takes its name (RENAME_EXCHANGE) until the next
-  // preparer job unlinks it.
-  lm::write_to_file({{"k", "1"}}, path);
-  if (inode(path) == ino_b) {
-    std::swap(a, b);
-    std::swap(ino_a, ino_b);
+  std::string path = std::string(dir) + "/gfd";
+  loop_write({{"k", "0"}}, path);
+  ino_t first = inode(path);
+  EXPECT_EQ(temp_files(dir).size(), static_cast<size_t>(0));
+  loop_write({{"k", "1"}}, path);
+  ino_t second = inode(path);
+  EXPECT_TRUE(second != first);
+  EXPECT_EQ(temp_files(dir).size(), static_cast<size_t>(1));
+  EXPECT_EQ(fs::read_file(temp_files(dir)[0]).data, std::string("k=0\n"));
+  // Longer, shorter and equal contents: always exact.
+  std::vector<std::string> vals{"2", std::string(3000, 'v'), "4", "5", "six", "7"};
+  for (size_t i = 0; i < vals.size(); ++i) {
+    trace::begin_cycle();
+    loop_write({{"k", vals[i]}}, path);
+    bool created = false;
+    for (const auto& ph : trace::phases()) created |= ph.first == "write.create";
+    EXPECT_FALSE(created);
+    EXPECT_EQ(fs::read_file(path).data, "k=" + vals[i] + "\n");
+    EXPECT_EQ(inode(path), i % 2 == 0 ? first : second);
+    EXPECT_EQ(temp_files(dir).size(), static_cast<size_t>(1));
+    struct stat st;
+    EXPECT_TRUE(stat(path.c_str(), &st) == 0);
+    EXPECT_EQ(static_cast<int>(st.st_mode & 0777), 0644);
+    EXPECT_EQ(static_cast<size_t>(st.st_size), vals[i].size() + 3);
   }
-  EXPECT_EQ(fs::read_file(path).data, std::string("k=1\n"));
-  EXPECT_EQ(inode(path), ino_a);
-  EXPECT_TRUE(stat(path.c_str(), &st) == 0);
-  EXPECT_EQ(static_cast<int>(st.st_mode & 0777), 0644);
-  EXPECT_EQ(fs::read_file(a).data, std::string("k=0\n"));
-  // The next write takes the other one and exchanges too, although the
-  // first old file still waits (no job ran in between).
-  lm::write_to_file({{"k", "2"}}, path);
-  EXPECT_EQ(fs::read_file(path).data, std::string("k=2\n"));
-  EXPECT_EQ(inode(path), ino_b);
-  EXPECT_EQ(fs::read_file(a).data, std::string("k=0\n"));
-  EXPECT_EQ(fs::read_file(b).data, std::string("k=1\n"));
-  // The job unlinks both and makes the next two files.
-  auto job = lm::temp_preparer(path);
-  EXPECT_TRUE(static_cast<bool>(job));
-  job();
-  EXPECT_FALSE(fs::exists(a));
-  EXPECT_FALSE(fs::exists(b));
-  auto next = prepared_files(dir);
-  EXPECT_EQ(next.size(), static_cast<size_t>(2));
-  EXPECT_EQ(fs::read_file(next[0]).data, std::string());
-  EXPECT_EQ(fs::read_file(path).data, std::string("k=2\n"));
   // Exit: nothing left behind.
   lm::remove_output_file(path);
-  EXPECT_FALSE(fs::exists(tmp));
+  EXPECT_FALSE(fs::exists(std::string(dir) + "/gfd-tmp"));
   EXPECT_FALSE(fs::exists(path));
   fs::remove_all(dir);
 }
 
-TEST(WriteToFile_EveryLoopWriteFindsAPreparedFile) {
-  // The daemon's order: the job runs while its own cycle writes, so each
-  // write must find a file an earlier cycle's job made.  Here the job runs
-  // after the write (the latest it can run).
+TEST(WriteToFile_AReaderOfTheOldFileKeepsItWhole) {
+  // A reader that opened the feature file before a write still has it open
+  // when the next write would rewrite it: the write lease is refused, so
+  // that write leaves the file to the reader (unlinked) and creates a new
+  // one.  The reader reads the old contents, whole.
   char dir[] = "/tmp/gfd-write-XXXXXX";
   EXPECT_TRUE(mkdtemp(dir) != nullptr);
   std::string path = std::string(dir) + "/gfd";
-  lm::write_to_file({{"k", "x"}}, path);
-  if (auto job = lm::temp_preparer(path)) job();
-  for (int i = 0; i < 10; ++i) {
-    auto job = lm::temp_preparer(path);
-    auto ready = prepared_files(dir);
-    std::set<ino_t> inos;
-    for (const auto& f : ready)
-      if (fs::read_file(f).data.empty()) inos.insert(inode(f));
-    lm::write_to_file({{"k", std::to_string(i)}}, path);
-    EXPECT_TRUE(inos.count(inode(path)) == 1);
-    if (job) job();  // after the write: it also unlinks this write's old file
-    EXPECT_TRUE(prepared_files(dir).size() <= static_cast<size_t>(2));
-  }
-  lm::remove_output_file(path);
-  fs::remove_all(dir);
-}
-
-TEST(WriteToFile_SteadyLoopKeepsAtMostThreeFilesInTheTemporaryDirectory) {
-  char dir[] = "/tmp/gfd-write-XXXXXX";
-  EXPECT_TRUE(mkdtemp(dir) != nullptr);
-  std::string path = std::string(dir) + "/gfd";
-  for (int i = 0; i < 20; ++i) {
-    prepare_then_write({{"k", std::to_string(i)}}, path);
-    EXPECT_TRUE(prepared_files(dir).size() <= static_cast<size_t>(3));  // two prepared, one old
-    EXPECT_EQ(fs::read_file(path).data, "k=" + std::to_string(i) + "\n");
-  }
+  loop_write({{"k", "a"}}, path);
+  loop_write({{"k", "old"}}, path);
+  int rfd = ::open(path.c_str(), O_RDONLY);
+  EXPECT_TRUE(rfd >= 0);
+  ino_t held = inode(path);
+  loop_write({{"k", "new"}}, path);  // swaps the held file out
+  trace::begin_cycle();
+  loop_write({{"k", "newer"}}, path);  // would rewrite it: the reader still has it
+  bool created = false;
+  for (const auto& ph : trace::phases()) created |= ph.first == "write.create";
+  EXPECT_TRUE(created);
+  char buf[16] = {};
+  EXPECT_EQ(::pread(rfd, buf, sizeof(buf) - 1, 0), static_cast<ssize_t>(6));
+  EXPECT_EQ(std::string(buf), std::string("k=old\n"));
+  struct stat st;
+  EXPECT_TRUE(::fstat(rfd, &st) == 0);
+  EXPECT_EQ(st.st_ino, held);
+  EXPECT_EQ(static_cast<long>(st.st_nlink), 0L);  // unlinked, the reader's alone
+  ::close(rfd);
+  EXPECT_EQ(fs::read_file(path).data, std::string("k=newer\n"));
+  EXPECT_EQ(temp_files(dir).size(), static_cast<size_t>(1));
+  // With the reader gone, writes reuse again.
+  trace::begin_cycle();
+  loop_write({{"k", "last"}}, path);
+  created = false;
+  for (const auto& ph : trace::phases()) created |= ph.first == "write.create";
+  EXPECT_FALSE(created);
+  EXPECT_EQ(fs::read_file(path).data, std::string("k=last\n"));
   lm::remove_output_file(path);
   fs::remove_all(dir);
 }
@@ -622,136 +604,102 @@ TEST(WriteToFile_ExchangeNeverSwapsADirectoryIntoTheTemporaryDirectory) {
   char dir[] = "/tmp/gfd-write-XXXXXX";
   EXPECT_TRUE(mkdtemp(dir) != nullptr);
   std::string path = std::string(dir) + "/gfd";
-  prepare_then_write({{"k", "1"}}, path);
+  loop_write({{"k", "1"}}, path);
+  loop_write({{"k", "2"}}, path);
   EXPECT_TRUE(::unlink(path.c_str()) == 0);
   EXPECT_TRUE(::mkdir(path.c_str(), 0755) == 0);
   EXPECT_TRUE(::close(::open((path + "/keep").c_str(), O_CREAT | O_WRONLY, 0644)) == 0);
-  if (auto job = lm::temp_preparer(path)) job();
-  EXPECT_THROW_MSG(lm::write_to_file({{"k", "2"}}, path), "error moving temporary file");
+  EXPECT_THROW_MSG(loop_write({{"k", "3"}}, path), "error moving temporary file");
   EXPECT_TRUE(fs::exists(path + "/keep"));
-  lm::discard_prepared_temps();
+  lm::release_kept_files();
   fs::remove_all(std::string(dir) + "/gfd-tmp");
   EXPECT_TRUE(fs::exists(path + "/keep"));
   fs::remove_all(dir);
 }
 
-TEST(WriteToFile_ExchangeWithTheFeatureFileRemovedBetweenCycles) {
-  // Someone deleted the feature file since the last cycle: the exchange has
-  // nothing to swap with (ENOENT) and the prepared file is renamed into place.
+TEST(WriteToFile_FeatureFileRemovedOrReplacedBetweenCycles) {
   char dir[] = "/tmp/gfd-write-XXXXXX";
   EXPECT_TRUE(mkdtemp(dir) != nullptr);
   std::string path = std::string(dir) + "/gfd";
-  prepare_then_write({{"k", "1"}}, path);
-  prepare_then_write({{"k", "2"}}, path);
+  loop_write({{"k", "1"}}, path);
+  loop_write({{"k", "2"}}, path);
+  // Deleted since the last cycle: nothing to swap with, a plain rename.
   EXPECT_TRUE(::unlink(path.c_str()) == 0);
-  prepare_then_write({{"k", "3"}}, path);
+  loop_write({{"k", "3"}}, path);
   EXPECT_EQ(fs::read_file(path).data, std::string("k=3\n"));
-  prepare_then_write({{"k", "4"}}, path);
+  loop_write({{"k", "4"}}, path);
   EXPECT_EQ(fs::read_file(path).data, std::string("k=4\n"));
+  // Replaced by someone else's file: it is swapped out and removed, as a
+  // rename over it would; it is never rewritten.
+  std::string other = std::string(dir) + "/other";
+  {
+    FILE* f = std::fopen(other.c_str(), "w");
+    std::fputs("theirs\n", f);
+    std::fclose(f);
+  }
+  ino_t theirs = inode(other);
+  EXPECT_TRUE(::rename(other.c_str(), path.c_str()) == 0);
+  loop_write({{"k", "5"}}, path);
+  EXPECT_EQ(fs::read_file(path).data, std::string("k=5\n"));
+  for (const auto& f : temp_files(dir)) EXPECT_TRUE(inode(f) != theirs);
+  loop_write({{"k", "6"}}, path);
+  loop_write({{"k", "7"}}, path);
+  EXPECT_EQ(fs::read_file(path).data, std::string("k=7\n"));
+  EXPECT_TRUE(temp_files(dir).size() <= static_cast<size_t>(1));
   lm::remove_output_file(path);
   EXPECT_FALSE(fs::exists(std::string(dir) + "/gfd-tmp"));
   EXPECT_FALSE(fs::exists(path));
   fs::remove_all(dir);
 }
 
-TEST(WriteToFile_ExchangeKeepsReadersOfTheOldFile) {
-  // A reader that opened the feature file before a write keeps reading the
-  // old contents, whole, after the exchange and after the worker unlinks it.
+TEST(WriteToFile_KeptFileRemovedBetweenCycles) {
+  // gfd-tmp/ emptied by someone else between two cycles: the write finds
+  // its kept file gone (or, re-created, a different file under the name)
+  // and writes through a new one.
   char dir[] = "/tmp/gfd-write-XXXXXX";
   EXPECT_TRUE(mkdtemp(dir) != nullptr);
   std::string path = std::string(dir) + "/gfd";
-  prepare_then_write({{"k", "old"}}, path);
-  int rfd = ::open(path.c_str(), O_RDONLY);
-  EXPECT_TRUE(rfd >= 0);
-  prepare_then_write({{"k", "new"}}, path);
-  if (auto job = lm::temp_preparer(path)) job();
-  char buf[16] = {};
-  EXPECT_EQ(::pread(rfd, buf, sizeof(buf) - 1, 0), static_cast<ssize_t>(6));
-  EXPECT_EQ(std::string(buf), std::string("k=old\n"));
-  ::close(rfd);
-  EXPECT_EQ(fs::read_file(path).data, std::string("k=new\n"));
-  lm::remove_output_file(path);
-  EXPECT_FALSE(fs::exists(std::string(dir) + "/gfd-tmp"));
-  fs::remove_all(dir);
-}
-
-TEST(WriteToFile_PreparedReplaceKeepsExactContentsAndStaysFast) {
-  // The prepared file's blocks are allocated beyond EOF for the previous
-  // size (FALLOC_FL_KEEP_SIZE): the file must still hold exactly the new
-  // contents when the label set shrinks, and on ext4 the rename must not
-  // flush delayed allocation (~70 ms on this container's ext4 without it).
-  char dir[] = "/tmp/gfd-write-XXXXXX";
-  EXPECT_TRUE(mkdtemp(dir) != nullptr);
-  std::string path = std::string(dir) + "/gfd";
-  prepare_then_write({{"k", std::string(5000, 'v')}}, path);
-  std::vector<double> us;
-  for (int i = 0; i < 9; ++i) {
-    if (auto job = lm::temp_preparer(path)) job();
-    auto t0 = std::chrono::steady_clock::now();
-    lm::write_to_file({{"k", std::to_string(i)}}, path);
-    us.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
-    EXPECT_EQ(fs::read_file(path).data, "k=" + std::to_string(i) + "\n");
+  loop_write({{"k", "1"}}, path);
+  loop_write({{"k", "2"}}, path);
+  EXPECT_EQ(temp_files(dir).size(), static_cast<size_t>(1));
+  std::string kept = temp_files(dir)[0];
+  fs::remove_all(std::string(dir) + "/gfd-tmp");
+  loop_write({{"k", "3"}}, path);
+  EXPECT_EQ(fs::read_file(path).data, std::string("k=3\n"));
+  // Same name, different file.
+  loop_write({{"k", "4"}}, path);
+  kept = temp_files(dir)[0];
+  EXPECT_TRUE(::unlink(kept.c_str()) == 0);
+  {
+    FILE* f = std::fopen(kept.c_str(), "w");
+    std::fputs("stranger\n", f);
+    std::fclose(f);
   }
-  struct stat st;
-  EXPECT_TRUE(stat(path.c_str(), &st) == 0);
-  EXPECT_EQ(static_cast<long>(st.st_size), 4L);
-  std::sort(us.begin(), us.end());
-  EXPECT_TRUE(us[us.size() / 2] < 5000.0);
+  loop_write({{"k", "5"}}, path);
+  EXPECT_EQ(fs::read_file(path).data, std::string("k=5\n"));
+  EXPECT_EQ(fs::read_file(kept).data, std::string("stranger\n"));  // not ours: left alone
+  ::unlink(kept.c_str());
   lm::remove_output_file(path);
   fs::remove_all(dir);
 }
 
-TEST(WriteToFile_PreparedFileRemovedBetweenCycles) {
-  // gfd-tmp/ deleted by someone else between two cycles: the write that
-  // finds its prepared file gone writes through a fresh one.
-  char dir[] = "/tmp/gfd-write-XXXXXX";
-  EXPECT_TRUE(mkdtemp(dir) != nullptr);
-  std::string path = std::string(dir) + "/gfd";
-  prepare_then_write({{"k", "1"}}, path);
-  if (auto job = lm::temp_preparer(path)) job();
-  EXPECT_EQ(prepared_files(dir).size(), static_cast<size_t>(2));
-  fs::remove_all(std::string(dir) + "/gfd-tmp");
-  lm::write_to_file({{"k", "2"}}, path);
-  EXPECT_EQ(fs::read_file(path).data, std::string("k=2\n"));
-  EXPECT_EQ(prepared_files(dir).size(), static_cast<size_t>(0));
-  // The preparer re-creates a removed gfd-tmp/, as the next write would.
-  fs::remove_all(std::string(dir) + "/gfd-tmp");
-  if (auto job = lm::temp_preparer(path)) job();
-  EXPECT_EQ(prepared_files(dir).size(), static_cast<size_t>(2));
-  fs::remove_all(dir);
-}
-
-TEST(WriteToFile_PreparedFileOfAnotherDirectoryIsDiscarded) {
+TEST(WriteToFile_KeptFilesOfEveryPathAreReleased) {
   char a[] = "/tmp/gfd-write-XXXXXX", b[] = "/tmp/gfd-write-XXXXXX";
   EXPECT_TRUE(mkdtemp(a) != nullptr && mkdtemp(b) != nullptr);
   std::string pa = std::string(a) + "/gfd", pb = std::string(b) + "/gfd";
-  lm::write_to_file({{"k", "a"}}, pa);
-  if (auto job = lm::temp_preparer(pa)) job();
-  EXPECT_EQ(prepared_files(a).size(), static_cast<size_t>(2));
-  lm::write_to_file({{"k", "b"}}, pb);
-  EXPECT_EQ(fs::read_file(pb).data, std::string("k=b\n"));
-  EXPECT_EQ(prepared_files(a).size(), static_cast<size_t>(0));
-  EXPECT_EQ(prepared_files(b).size(), static_cast<size_t>(0));
-  // discard_prepared_temps: the same for a session that ends - including a
-  // job handed out but not run yet, which it waits for.
-  if (auto job = lm::temp_preparer(pb)) job();
-  lm::write_to_file({{"k", "b2"}}, pb);  // takes the prepared file; the old one waits
-  auto pending = lm::temp_preparer(pb);
-  EXPECT_TRUE(static_cast<bool>(pending));
-  std::thread t([job = std::move(pending)] {
-    std::this_thread::sleep_for(std::chrono::milliseconds(50));
-    job();
-  });
-  lm::discard_prepared_temps();
-  t.join();
-  EXPECT_EQ(prepared_files(b).size(), static_cast<size_t>(0));
-  // A job dropped unrun does not hold discard up.
-  lm::write_to_file({{"k", "b3"}}, pb);
-  {
-    auto dropped = lm::temp_preparer(pb);
-    EXPECT_TRUE(static_cast<bool>(dropped));
+  for (int i = 0; i < 3; ++i) {
+    loop_write({{"k", "a" + std::to_string(i)}}, pa);
+    loop_write({{"k", "b" + std::to_string(i)}}, pb);
   }
-  lm::discard_prepared_temps();
+  EXPECT_EQ(temp_files(a).size(), static_cast<size_t>(1));
+  EXPECT_EQ(temp_files(b).size(), static_cast<size_t>(1));
+  EXPECT_EQ(fs::read_file(pa).data, std::string("k=a2\n"));
+  EXPECT_EQ(fs::read_file(pb).data, std::string("k=b2\n"));
+  // A session that ends: its kept files go, the feature files stay.
+  lm::release_kept_files();
+  EXPECT_EQ(temp_files(a).size(), static_cast<size_t>(0));
+  EXPECT_EQ(temp_files(b).size(), static_cast<size_t>(0));
+  EXPECT_EQ(fs::read_file(pa).data, std::string("k=a2\n"));
   fs::remove_all(a);
   fs::remove_all(b);
 }

@@ -681,6 +681,29 @@ TEST(Bound_SameFunctionsAsTheFullBusScan) {
   fs::remove_all(root);
 }
 
+TEST(Bound_DisplayClassFromUeventKeepsItsLeadingZero) {
+  // The kernel prints PCI_CLASS with %04X: a display-class MxGPU PF (0x038000,
+  // V620/V710 hosts, MI2xx) appears as "38000".  Read as "0x38000" it failed
+  // the 0x03 check and every such PF and VF vanished.
+  std::string root = bound_host(4, 2);
+  std::string dev = root + "/sys/bus/pci/devices/";
+  for (const char* bdf : {"0000:11:00.0", "0000:c1:00.0", "0000:c1:00.1", "0000:c1:00.2"}) {
+    put_file(dev + bdf + "/class", "0x038000\n");
+    put_file(dev + bdf + "/uevent", std::string("DRIVER=amdgpu\nPCI_CLASS=38000\nPCI_ID=1002:73A1\nPCI_SLOT_NAME=") +
+                                        bdf + "\n");
+    put_file(dev + bdf + "/device", "0x73a1\n");
+  }
+  auto b = BoundAmdPCI(root).Devices();
+  EXPECT_EQ(b.size(), static_cast<size_t>(7));
+  EXPECT_EQ(describe(b), describe(SysfsAmdPCI(root).Devices()));
+  for (const auto& d : b)
+    if (d.address == "0000:c1:00.0") EXPECT_EQ(d.class_code, std::string("0x03"));
+  // Garbage in PCI_CLASS falls back to the `class` attribute.
+  put_file(dev + std::string("0000:11:00.0/uevent"), "PCI_CLASS=zz\nPCI_ID=1002:73A1\n");
+  EXPECT_EQ(describe(BoundAmdPCI(root).Devices()), describe(SysfsAmdPCI(root).Devices()));
+  fs::remove_all(root);
+}
+
 TEST(Bound_NeverReadsFunctionsNoDriverBinds) {
   // An unbound AMD function whose class cannot be read: the full scan fails
   // on it, the bound scan never looks.

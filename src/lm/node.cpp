@@ -2,6 +2,7 @@
 
 #include <atomic>
 #include <ctime>
+#include <exception>
 #include <map>
 
 #include "lm/keys.h"
@@ -233,10 +234,26 @@ LabelerPtr NewDeviceLabeler(resource::Manager& manager, const config::Config& co
   trace::Span span("label");
   // The device-derived labelers first: the node facts are read on a worker
   // meanwhile (daemon.cpp label_cycle), and are joined only when this
-  // thread has nothing else to do.
-  auto capability = GFD_WRAP("error creating partition capability labeler", NewPartitionCapabilityLabeler(manager));
-  auto topology = GFD_WRAP("error creating topology labeler", NewTopologyLabeler(manager));
-  auto resources = GFD_WRAP("error creating resource labeler", NewResourceLabeler(manager, config));
+  // thread has nothing else to do.  Their errors wait until the machine and
+  // version labelers are built, so that the error reported is the first in
+  // the reference's order (nvml.go:44-67: machine type, version, MIG
+  // capability, resources).
+  std::exception_ptr device_error;
+  auto deferred = [&](auto make) -> LabelerPtr {
+    if (device_error) return nullptr;
+    try {
+      return make();
+    } catch (...) {
+      device_error = std::current_exception();
+      return nullptr;
+    }
+  };
+  auto capability = deferred([&] {
+    return GFD_WRAP("error creating partition capability labeler", NewPartitionCapabilityLabeler(manager));
+  });
+  auto topology = deferred([&] { return GFD_WRAP("error creating topology labeler", NewTopologyLabeler(manager)); });
+  auto resources =
+      deferred([&] { return GFD_WRAP("error creating resource labeler", NewResourceLabeler(manager, config)); });
   const NodeFacts* pre = facts ? &facts() : nullptr;
   LabelerPtr machine, version;
   if (pre) {
@@ -255,6 +272,7 @@ LabelerPtr NewDeviceLabeler(resource::Manager& manager, const config::Config& co
   } else {
     version = GFD_WRAP("failed to construct version labeler", NewVersionLabeler(manager));
   }
+  if (device_error) std::rethrow_exception(device_error);
   return merge({machine, version, capability, topology, resources});
 }
 

@@ -16,9 +16,13 @@
 //
 // When neither driver binds anything - an SR-IOV guest whose amdgpu is not
 // loaded, or a node without AMD GPUs - it falls back to the full-bus scan.
-// Not seen without the fallback: an AMD function bound to some other driver
-// (vfio-pci, say) that is itself a PF with VFs enabled; GIM hosts bind their
-// PFs to gim.
+// Not seen while at least one function is bound (a parity gap with the
+// reference's whole-bus scan, pciutil.go:70-112, docs/PARITY.md): an AMD
+// function bound to another driver or to none - a PF handed to vfio-pci, a
+// VF in a guest that amdgpu failed to probe while another VF of the guest
+// is bound - except the VFs that a bound PF's virtfn links name.  GIM hosts
+// bind their PFs to gim, and bare-metal and guest nodes bind their GPUs to
+// amdgpu, so the labels of a working node are the same.
 //
 // Like the full scan, the result is kept while /sys/kernel/uevent_seqnum is
 // unchanged: binding, unbinding, adding or removing a function (VFs

@@ -2,6 +2,7 @@
 
 #include <atomic>
 #include <cstdio>
+#include <cstring>
 #include <ctime>
 #include <sys/time.h>
 
@@ -30,8 +31,17 @@ void emit(const char* msg, size_t len) {
   out.append(msg, len);
   if (len == 0 || msg[len - 1] != '\n') out.push_back('\n');
   if (t_held) {
-    t_held->append(out);
-    return;
+    // Warnings and errors are never held: a cycle that then hangs (a wedged
+    // library call) or is killed must still have said why.  What is held
+    // goes out first, so the order stays.
+    bool urgent = len >= 5 && (std::strncmp(msg, "Warning", 7) == 0 || std::strncmp(msg, "WARNING", 7) == 0 ||
+                                std::strncmp(msg, "Error", 5) == 0);
+    if (!urgent) {
+      t_held->append(out);
+      return;
+    }
+    out.insert(0, *t_held);
+    t_held->clear();
   }
   fwrite(out.data(), 1, out.size(), stderr);
 }

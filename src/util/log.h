@@ -22,7 +22,8 @@ bool quiet();
 // are collected and written together - in log order, one write(2) - when it
 // is flushed or destroyed.  The daemon holds a cycle's lines until the
 // feature file is in place: a line to stderr, usually a pipe to the
-// container runtime, is a syscall the labels do not wait for.
+// container runtime, is a syscall the labels do not wait for.  Warning and
+// error lines are written at once (with what was held before them).
 class Hold {
  public:
   Hold();

@@ -375,3 +375,27 @@ TEST(LogHold_WritesTheCycleLinesTogetherInOrder) {
   EXPECT_TRUE(a != std::string::npos && b != std::string::npos && a < b);
   EXPECT_TRUE(nested.find("inner") != std::string::npos);
 }
+
+TEST(LogHold_WritesWarningsAtOnceWithWhatCameBefore) {
+  // A cycle that hangs after a warning (a wedged library call) or is killed
+  // must already have said why: warnings and errors are not held.
+  bool was = log::set_quiet(false);
+  std::string before, at_warning, at_error;
+  {
+    StderrCapture cap;
+    log::Hold hold;
+    log::printf("Writing labels to output file");
+    before = cap.peek();
+    log::printf("Warning: resource manager shutdown failed: %s", "x");
+    at_warning = cap.peek();
+    log::printf("routine");
+    log::printf("Error: %s", "y");
+    at_error = cap.peek();
+  }
+  log::set_quiet(was);
+  EXPECT_EQ(before, std::string(""));
+  auto a = at_warning.find("Writing labels"), b = at_warning.find("Warning: resource manager");
+  EXPECT_TRUE(a != std::string::npos && b != std::string::npos && a < b);
+  auto c = at_error.find("routine"), d = at_error.find("Error: y");
+  EXPECT_TRUE(c != std::string::npos && d != std::string::npos && b < c && c < d);
+}

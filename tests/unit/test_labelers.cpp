@@ -340,6 +340,16 @@ TEST(NodeFacts_PrefetchedVersionsMatchManager) {
   EXPECT_EQ(l["amd.com/gpu.machine"], std::string("unknown"));
   // Without a version root the manager is asked (mock: 6.12.12 / 7.2).
   EXPECT_FALSE(lm::ReadNodeFacts(c, std::nullopt).have_versions);
+  // Several labelers failing: the error reported is the first in the
+  // reference's construction order (version before resources), although
+  // the resource labeler is built first here.
+  config::Config bogus = c;
+  bogus.flags.mig_strategy = "bogus";
+  EXPECT_THROW_MSG(lm::NewDeviceLabeler(m, bogus, [&]() -> const lm::NodeFacts& { return f; }),
+                   "unknown strategy: bogus");
+  f = lm::ReadNodeFacts(c, bad);
+  EXPECT_THROW_MSG(lm::NewDeviceLabeler(m, bogus, [&]() -> const lm::NodeFacts& { return f; }),
+                   "error getting ROCm runtime version: unable to read the ROCm version file");
   fs::remove_all(root);
 }
 

@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Mutation check of tests/test_differential.py: in a copy of the tree
+(built in place there), remove one kept fact's invalidation at a time,
+rebuild and run the differential test; it must fail for each.
+
+    python tools/differential_mutations.py COPY_DIR [M1 M2 ...]
+
+COPY_DIR: a scratch copy of the repository (e.g. `git worktree add`), built
+once with `make build`.  Results: profiles/differential_mutations_r5.txt.
+"""
+import os
+import subprocess
+import sys
+
+os.chdir(sys.argv[1])
+M = [
+ ("M1 SR-IOV result kept across uevents", "src/sriov/bound.cpp", "if (have_ && seqnum && *seqnum == seqnum_) {", "if (have_) {"),
+ ("M2 SR-IOV check ignores the driver listing", "src/sriov/bound.cpp", "if (!have_ || fell_back_ || bound != bound_) return false;", "if (!have_ || fell_back_) return false;"),
+ ("M3 SR-IOV check ignores VF links", "src/sriov/bound.cpp", "    if (d.sriov_totalvfs <= 0) continue;\n    // The kernel links", "    continue;\n    // The kernel links"),
+ ("M4 amd-smi identity kept across re-init", "src/resource/amdsmi.cpp", "  identity_.clear();\n", ""),
+ ("M5 amd-smi partition modes kept across mode changes", "src/resource/amdsmi.cpp", "if (!avail.compute_partition.empty() && avail.compute_partition == p.compute_partition &&\n      avail.memory_partition == p.memory_partition) {", "if (!avail.compute_partition.empty()) {"),
+ ("M6 amdgpu module directory never reopened", "src/resource/versions.cpp", 'if (!d || d->lookup("initstate") != 0) d =', 'if (!d) d ='),
+ ("M7 sysfs topology kept across generations", "src/resource/sysfs.cpp", "if (!generation_.empty() && generation_ == cached_generation_ && cached_) {", "if (cached_) {"),
+ ("M8 amd-smi session kept across generations", "src/resource/amdsmi.cpp", "    if (gen != generation_) {", "    if (false) {"),
+ ("M9 DMI kept for any file", "src/util/fs.cpp", "  kept->emplace(path, constant ? std::optional<std::string>(r.data) : std::nullopt);", "  kept->emplace(path, std::optional<std::string>(r.data));"),
+ ("M10 version file kept across replacement", "src/util/fs.cpp", "if (it != checked_.end() && it->second.dev == static_cast<uint64_t>(st.st_dev) &&\n        it->second.ino == static_cast<uint64_t>(st.st_ino))", "if (it != checked_.end())"),
+]
+sel = sys.argv[2:] or [m[0].split()[0] for m in M]
+for name, f, a, b in M:
+    if name.split()[0] not in sel: continue
+    src = open(f).read()
+    assert a in src, (name, a)
+    open(f, 'w').write(src.replace(a, b, 1))
+    try:
+        r = subprocess.run("cmake --build build -j8 > /tmp/mut_b.log 2>&1 && GFD_DIFF_SEQUENCES=200 timeout 600 python -m pytest tests/test_differential.py -x -q 2>&1 | tail -30",
+                           shell=True, capture_output=True, text=True)
+        out = r.stdout
+        verdict = "CAUGHT" if "1 failed" in out else ("MISSED" if "1 passed" in out else "BUILD/OTHER")
+        hint = ""
+        for line in out.splitlines():
+            if "AssertionError: sequence" in line:
+                hint = line.strip()[:200]
+        print(f"{name}: {verdict} {hint}", flush=True)
+    finally:
+        open(f, 'w').write(src)
+subprocess.run("cmake --build build -j8 > /tmp/mut_b.log 2>&1", shell=True)

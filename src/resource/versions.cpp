@@ -2,7 +2,6 @@
 
 #include <sys/utsname.h>
 
-#include <atomic>
 #include <cstdlib>
 #include <map>
 #include <memory>
@@ -154,21 +153,9 @@ std::optional<RuntimeVersion> rocm_version(const VersionSources& s, std::string*
 }
 
 std::string driver_version(const std::string& root) {
-  // The running kernel's amdgpu, built in: its version is the kernel
-  // release, fixed until the next boot - worked out once.
-  static std::atomic<const std::string*> builtin_release{nullptr};
-  bool host = root.empty() || root == "/";
-  if (host)
-    if (const std::string* v = builtin_release.load(std::memory_order_acquire)) return *v;
   std::string raw = host_driver_version(root);
   auto v = extract_version(raw);
-  std::string out = v ? *v : raw;
-  if (host && builtin_amdgpu(root) && !out.empty()) {
-    const std::string* expected = nullptr;
-    auto* kept = new std::string(out);  // one per process (a lost race frees its copy)
-    if (!builtin_release.compare_exchange_strong(expected, kept, std::memory_order_acq_rel)) delete kept;
-  }
-  return out;
+  return v ? *v : raw;
 }
 
 }  // namespace gfd::resource

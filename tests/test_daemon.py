@@ -510,16 +510,25 @@ def test_auto_backend_uses_sysfs_when_amdsmi_fails_to_initialise(binary, tmp_pat
     assert "amdsmi(persistent) manager failed to initialize" in err
 
 
-def test_auto_backend_prefers_amdsmi(binary, tmp_path, mi355x_node):
+@pytest.mark.parametrize("first", ["kfd", "amdsmi"])
+def test_auto_backend_prefers_amdsmi(binary, tmp_path, first):
     """Daemon mode: the first cycle is labelled from KFD while amd-smi
-    initialises in the background; once it is ready amd-smi takes over."""
-    root = mi355x_node(n_gpus=2)
-    spec = "bdf=0000:d9:00.0;mode=SPX;parts=1;cus=256;xcds=8;vram_mib=294896;links=7;virt=1"
+    initialises in the background; once it is ready amd-smi takes over
+    (here it describes the node as KFD does).  `first`: amd-smi is ready
+    before the first cycle (its labels are the first published) or only
+    after KFD published (init held back 60 ms)."""
+    spec = synth.NodeSpec(gpus=[synth.GpuSpec(), synth.GpuSpec()], seed=41)
+    root = synth.make_node(tmp_path / "root", spec)
+    fake = synth.fake_amdsmi_spec(root, spec) + ("\ninit_latency_us=60000" if first == "kfd" else "")
     labels, err = _loop_until(binary, tmp_path / "gfd", "--backend=auto", f"--sysfs-root={root}",
-                              env=_fake_amdsmi_env(spec), until="Using the amdsmi(persistent) manager")
-    assert labels["amd.com/gpu.count"] == "1"  # the fake's one GPU, not the tree's two
-    assert "failed to initialize" not in err
+                              f"--machine-type-file={root}/sys/class/dmi/id/product_name",
+                              env=_fake_amdsmi_env(fake.replace("\n", "|")),
+                              until="Using the amdsmi(persistent) manager")
+    assert labels["amd.com/gpu.count"] == "2"
+    assert "failed to initialize" not in err and "describes the GPUs differently" not in err
     assert "labeling from the sysfs manager meanwhile" in err
+    if first == "kfd":
+        assert err.index("Writing labels to output file") < err.index("Using the amdsmi(persistent) manager")
 
 
 def test_auto_backend_oneshot_reads_kfd_without_loading_amdsmi(binary, tmp_path, mi355x_node):
@@ -626,6 +635,64 @@ def test_concurrent_reader_never_sees_a_partial_file(binary, tmp_path, mi355x_no
         assert not bad, bad
         assert reads > 200
     finally:
+        p.send_signal(signal.SIGTERM)
+        p.communicate(timeout=30)
+
+
+def test_a_reader_holding_the_file_across_cycles_sees_it_unchanged(binary, tmp_path, mi355x_node):
+    """The loop writer rewrites the file the previous write swapped out -
+    never one a reader still has open (a write lease is granted only to its
+    sole opener).  With the labels changing every cycle (the DMI name flips
+    under the daemon) and cycles 1 ms apart, readers that open the feature
+    file and read it again through the same descriptor several cycles later
+    must see the same bytes both times, and a complete label set."""
+    import threading
+
+    root = mi355x_node(n_gpus=1)
+    dmi = Path(root) / "sys/class/dmi/id/product_name"
+    features = tmp_path / "features.d"
+    features.mkdir()
+    out = features / "gfd"
+    names = ["Machine-A", "Machine-B"]
+    stop = threading.Event()
+
+    def flip():
+        i = 0
+        while not stop.is_set():
+            tmp = dmi.with_name(".product_name.new")
+            tmp.write_text(names[i % 2] + "\n")
+            os.replace(tmp, dmi)  # atomic: the daemon reads one name or the other
+            i += 1
+            time.sleep(0.0005)
+
+    p = _start(binary, ["--sleep-interval=1ms", "--backend=sysfs", f"--sysfs-root={root}", f"--output-file={out}",
+                        f"--machine-type-file={dmi}"])
+    t = threading.Thread(target=flip)
+    t.start()
+    try:
+        assert _wait_for(out.exists)
+        held, seen, bad = 0, set(), []
+        end = time.monotonic() + 3
+        while time.monotonic() < end and len(bad) < 5:
+            fd = os.open(out, os.O_RDONLY)
+            try:
+                first = os.pread(fd, 1 << 16, 0)
+                time.sleep(0.004)  # several of the daemon's cycles
+                again = os.pread(fd, 1 << 16, 0)
+            finally:
+                os.close(fd)
+            held += 1
+            labels = golden.parse_labels(first.decode())
+            seen.add(labels.get("amd.com/gpu.machine"))
+            if again != first:
+                bad.append(f"changed under the reader: {first[-60:]!r} -> {again[-60:]!r}")
+            if not first.endswith(b"\n") or labels.get("amd.com/gpu.count") != "1":
+                bad.append(f"incomplete: {first[-80:]!r}")
+        assert not bad, bad
+        assert held > 100 and seen == set(names), (held, seen)  # the labels did change under the readers
+    finally:
+        stop.set()
+        t.join()
         p.send_signal(signal.SIGTERM)
         p.communicate(timeout=30)
 

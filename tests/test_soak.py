@@ -84,10 +84,14 @@ def soak(binary: str, args: list[str], seconds: float, hup_at: float | None = No
         rss0, (fd0, prep0), c0 = _rss_kib(p.pid), _fds(p.pid), cycles[0]
         t0 = time.monotonic()
         hupped = False
+        last_note = t0
         while time.monotonic() - t0 < seconds and p.poll() is None:
             if hup_at is not None and not hupped and time.monotonic() - t0 >= hup_at:
                 p.send_signal(signal.SIGHUP)
                 hupped = True
+            if time.monotonic() - last_note >= 30:  # a long soak shows it is alive (pytest -s)
+                last_note = time.monotonic()
+                print(f"soak: {cycles[0] - c0} cycles, RSS {_rss_kib(p.pid)} KiB", flush=True)
             time.sleep(0.05)
         assert p.poll() is None, "".join(tail)
         rss1, (fd1, prep1), c1 = _rss_kib(p.pid), _fds(p.pid), cycles[0]

@@ -463,6 +463,37 @@ TEST(WriteToFile_FailedWriteLeavesNoTemporaries) {
   fs::remove_all(dir);
 }
 
+TEST(WriteToFile_LoopWriteThatFailsKeepsTheOldFile) {
+  // The rewrite of the kept file fails part-way (EFBIG): it is dropped, the
+  // new file the write then tries fails the same way, the error is thrown
+  // and the feature file keeps its old contents; the next write works.
+  char dir[] = "/tmp/gfd-write-XXXXXX";
+  EXPECT_TRUE(mkdtemp(dir) != nullptr);
+  std::string path = std::string(dir) + "/gfd";
+  lm::write_to_file({{"k", "a"}}, path, true);
+  lm::write_to_file({{"k", "old"}}, path, true);
+  struct rlimit old_limit;
+  ::getrlimit(RLIMIT_FSIZE, &old_limit);
+  struct rlimit small = old_limit;
+  small.rlim_cur = 64;
+  auto old_handler = ::signal(SIGXFSZ, SIG_IGN);
+  ::setrlimit(RLIMIT_FSIZE, &small);
+  std::string err;
+  try {
+    lm::write_to_file({{"k", std::string(4096, 'v')}}, path, true);
+  } catch (const std::exception& e) {
+    err = e.what();
+  }
+  ::setrlimit(RLIMIT_FSIZE, &old_limit);
+  ::signal(SIGXFSZ, old_handler);
+  EXPECT_TRUE(err.find("error writing temporary file") != std::string::npos);
+  EXPECT_EQ(fs::read_file(path, 64).data, std::string("k=old\n"));
+  lm::write_to_file({{"k", "new"}}, path, true);
+  EXPECT_EQ(fs::read_file(path).data, std::string("k=new\n"));
+  lm::remove_output_file(path);
+  fs::remove_all(dir);
+}
+
 TEST(WriteToFile_RenameFailureLeavesNoTemporaries) {
   char dir[] = "/tmp/gfd-write-XXXXXX";
   EXPECT_TRUE(mkdtemp(dir) != nullptr);

@@ -4,7 +4,6 @@
 #include "lm/labels.h"
 
 #include <fcntl.h>
-#include <linux/fs.h>
 #include <sys/stat.h>
 #include <sys/vfs.h>
 #include <unistd.h>
@@ -129,10 +128,9 @@ int remove_own_temps(const std::string& tmp_dir) {
 
 namespace {
 
-// One attempt at the reference's write (labels.go:68-114): a new temporary
-// file in tmp_dir with `contents`, renamed over `path`.  `keep_fd`: the
-// file's descriptor is left open and returned through *kept (its name in
-// *tmpl); the rename is then the caller's.
+// The reference's temporary file (labels.go:68-114): a new file in tmp_dir
+// (its name in *tmpl) holding `contents`; the rename is the caller's.  With
+// `kept` the descriptor is left open and returned there, else closed.
 void create_and_write(const std::string& tmp_dir, const std::string& contents, unsigned perm, std::string* tmpl,
                       int* kept) {
   int64_t t0 = trace::now_ns();
@@ -202,7 +200,6 @@ struct File {
   ino_t ino = 0;
 };
 struct Slot {
-  std::string tmp_dir;
   File live, spare;
 };
 
@@ -259,11 +256,6 @@ bool rewrite_spare(File& spare, const std::string& contents) {
 void write_kept(const std::string& path, const std::string& tmp_dir, const std::string& contents, unsigned perm) {
   std::lock_guard<std::mutex> lk(g_mu);
   Slot& s = slots()[path];
-  if (s.tmp_dir != tmp_dir) {
-    close_file(s.spare, true);
-    close_file(s.live, false);
-    s.tmp_dir = tmp_dir;
-  }
   File next;
   if (rewrite_spare(s.spare, contents)) {
     next = std::move(s.spare);

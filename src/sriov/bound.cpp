@@ -1,6 +1,7 @@
 #include "sriov/bound.h"
 
 #include <algorithm>
+#include <cerrno>
 #include <cstdio>
 #include <cstdlib>
 #include <optional>
@@ -81,6 +82,11 @@ std::optional<PCIDevice> read_function(const std::string& path, const std::strin
   if (auto t = dir.read_trimmed("sriov_totalvfs")) d.sriov_totalvfs = static_cast<int>(str::parse_uint(*t).value_or(0));
   if (d.sriov_totalvfs == 0) {
     d.sriov_numvfs = 0;  // SR-IOV capable in name only
+  } else if (d.sriov_totalvfs > 0 && dir.lookup("virtfn0") == ENOENT) {
+    // The kernel links every VF it enables as virtfn<N> (the check below
+    // relies on it too): no link, no VFs - a lookup instead of a
+    // sriov_numvfs read, whose show() waits for the device lock.
+    d.sriov_numvfs = 0;
   } else if (d.sriov_totalvfs > 0) {
     if (auto n = dir.read_trimmed("sriov_numvfs")) d.sriov_numvfs = static_cast<int>(str::parse_uint(*n).value_or(0));
     if (d.sriov_numvfs > 0) d.sriov_vf_device = dir.read_trimmed("sriov_vf_device").value_or("");

@@ -22,6 +22,11 @@ the feature file of long-lived sessions (LongLived: one process holding
 daemon sessions across every change) with that of a fresh daemon process
 (`--oneshot`), byte for byte.
 
+The node model keeps what real nodes cannot do out: VFs are enabled only on
+a GIM host, whose SR-IOV PFs are bound to gim and so have no KFD node and
+are invisible to amd-smi (amdgpu implements no sriov_configure); TotalVFs
+is fixed per device; a hot-added GPU keeps the others' identities.
+
 Nodes are changed in place, as the kernel does: an attribute rewritten
 keeps its inode, a removed device's files disappear, a reloaded module's
 directory and its driver directory are new directories.
@@ -57,7 +62,7 @@ class Gpu:
     mode: str = "SPX"
     nps: str = "NPS1"
     sriov: bool = False     # has an SR-IOV capability (TotalVFs 8: fixed by the device)
-    vfs: int = 0            # VFs enabled (sriov only)
+    vfs: int = 0            # VFs enabled: only on a GIM host (amdgpu cannot enable VFs)
     bound: bool = True      # bound to its driver (amdgpu, or gim for an SR-IOV PF on a GIM host)
 
 
@@ -78,9 +83,12 @@ def spec_of(node: Node) -> synth.NodeSpec:
     gpus = []
     for g in node.gpus:
         sriov = {"total": 8, "num": g.vfs, "vf_device": synth.MI355X_VF_DEVICE_ID} if g.sriov else None
+        # On a GIM host the SR-IOV PFs are bound to gim, which creates no KFD
+        # node (and amd-smi, which goes through amdgpu, does not see them).
+        on_gim = g.sriov and node.gim is not None
         gpus.append(synth.GpuSpec(compute_partition=g.mode, memory_partition=g.nps, sriov=sriov, bus=g.bus,
                                   unique_id=g.unique, serial=g.serial, driver="auto" if g.bound else None,
-                                  kfd=g.bound,
+                                  kfd=g.bound and not on_gim,
                                   available_compute="SPX, DPX, QPX, CPX" if g.nps == "NPS1" else "DPX, QPX, CPX"))
     return synth.NodeSpec(gpus=gpus, driver_version=node.driver_version, machine=node.machine,
                           partition_layout=node.layout, rocm_version_file=False, gim_version=node.gim, seed=5)
@@ -192,7 +200,7 @@ def random_node(rng: random.Random) -> Node:
     for _ in range(rng.randint(1, 3)):
         g = new_gpu(node, rng)
         if rng.random() < 0.4:
-            g.sriov, g.vfs = True, rng.randint(0, 3)
+            g.sriov, g.vfs = True, rng.randint(0, 3) if node.gim else 0
         node.gpus.append(g)
     return node
 
@@ -214,6 +222,10 @@ def mutate(live: LiveNode, rng: random.Random) -> str:
         g = rng.choice(n.gpus)
         g.nps = "NPS2" if g.nps == "NPS1" else "NPS1"
         reset = True  # a memory-partition switch resets the GPU: new KFD nodes, uevents
+    elif kind == "vfs" and n.gim is None:
+        # No SR-IOV host driver: VFs cannot be enabled; the change is GIM
+        # being installed (its module appears, it binds the SR-IOV PFs).
+        n.gim = "8.3.0.K"
     elif kind == "vfs":
         capable = [g for g in n.gpus if g.sriov]
         if not capable:

@@ -10,8 +10,9 @@ repointed, the version file rewritten or replaced, DMI, unrelated uevents)
 are applied to synthetic nodes and, after every change, the feature file of
 long-lived sessions - KFD-sysfs and amd-smi (the fake library, which like
 the real one only sees a changed node when it is initialised again), each
-under the three strategies - must equal a fresh `--oneshot` process's byte
-for byte.
+under the three strategies, and the DaemonSet's default `auto` (KFD first,
+amd-smi once ready) - must equal a fresh `--oneshot` process's byte for
+byte.
 
 GFD_DIFF_SEQUENCES / GFD_DIFF_STEPS / GFD_DIFF_SEED size a longer run.
 """
@@ -35,14 +36,16 @@ BACKENDS = ("sysfs", "amdsmi")
 def _run(binary: str, tmp_path, sequences: int, steps: int, seed: int) -> dict:
     rng = random.Random(seed)
     server = dd.LongLived(str(FAKE))
-    pool = concurrent.futures.ThreadPoolExecutor(max_workers=6)
+    pool = concurrent.futures.ThreadPoolExecutor(max_workers=7)
     counts: dict[str, int] = {}
     compared = 0
     try:
         for s in range(sequences):
             root = tmp_path / f"n{s}"
             live = dd.LiveNode(root, dd.random_node(rng))
-            ids = [(b, st) for b in BACKENDS for st in STRATEGIES]
+            # The DaemonSet's default backend too: KFD first, amd-smi once it is
+            # ready and agrees; a fresh Job labels it from KFD.
+            ids = [(b, st) for b in BACKENDS for st in STRATEGIES] + [("auto", "single")]
             out = {k: str(tmp_path / f"out-{s}-{k[0]}-{k[1]}" / "gfd") for k in ids}
             server.call(op="stage", spec=live.fake_spec())
             for k in ids:
@@ -78,7 +81,7 @@ def test_long_lived_sessions_label_like_a_fresh_process(binary, tmp_path):
     steps = int(os.environ.get("GFD_DIFF_STEPS", "5"))
     seed = int(os.environ.get("GFD_DIFF_SEED", "20261018"))
     r = _run(binary, tmp_path, sequences, steps, seed)
-    assert r["compared"] == sequences * steps * len(STRATEGIES) * len(BACKENDS)
+    assert r["compared"] == sequences * steps * (len(STRATEGIES) * len(BACKENDS) + 1)
     # Every kind of change was exercised.
     assert set(r["changes"]) == {"partition", "nps", "vfs", "gpu_add", "gpu_remove", "module_reload", "rocm_repoint",
                                  "rocm_rewrite", "rocm_replace", "dmi", "bind", "uevent"}, r["changes"]

@@ -64,6 +64,7 @@ class Gpu:
     sriov: bool = False     # has an SR-IOV capability (TotalVFs 8: fixed by the device)
     vfs: int = 0            # VFs enabled: only on a GIM host (amdgpu cannot enable VFs)
     bound: bool = True      # bound to its driver (amdgpu, or gim for an SR-IOV PF on a GIM host)
+    vf: bool = False        # an SR-IOV VF handed to this node, a guest VM
 
 
 @dataclass
@@ -75,6 +76,7 @@ class Node:
     rocm_link: str = "7.2.0"                            # opt/rocm -> rocm-<this>
     rocm_text: dict = field(default_factory=lambda: {v: v for v in ROCM_INSTALLS})  # install -> version file text
     layout: str = "function"
+    guest: bool = False  # a VM whose GPUs are VFs (CPU hypervisor flag set)
     seqnum: int = 4000
     generation: int = 1
 
@@ -88,10 +90,11 @@ def spec_of(node: Node) -> synth.NodeSpec:
         on_gim = g.sriov and node.gim is not None
         gpus.append(synth.GpuSpec(compute_partition=g.mode, memory_partition=g.nps, sriov=sriov, bus=g.bus,
                                   unique_id=g.unique, serial=g.serial, driver="auto" if g.bound else None,
-                                  kfd=g.bound and not on_gim,
+                                  kfd=g.bound and not on_gim, vf=g.vf,
                                   available_compute="SPX, DPX, QPX, CPX" if g.nps == "NPS1" else "DPX, QPX, CPX"))
     return synth.NodeSpec(gpus=gpus, driver_version=node.driver_version, machine=node.machine,
-                          partition_layout=node.layout, rocm_version_file=False, gim_version=node.gim, seed=5)
+                          partition_layout=node.layout, rocm_version_file=False, gim_version=node.gim, seed=5,
+                          hypervisor=node.guest)
 
 
 def _remove(p: str) -> None:
@@ -195,6 +198,14 @@ def new_gpu(node: Node, rng: random.Random) -> Gpu:
 
 
 def random_node(rng: random.Random) -> Node:
+    if rng.random() < 0.15:
+        # A guest VM: its GPUs are VFs in SPX, it runs no SR-IOV host driver.
+        node = Node(machine=rng.choice(MACHINES), rocm_link=rng.choice(ROCM_INSTALLS), guest=True)
+        for _ in range(rng.randint(1, 2)):
+            g = new_gpu(node, rng)
+            g.vf, g.mode, g.nps = True, "SPX", "NPS1"
+            node.gpus.append(g)
+        return node
     node = Node(gim=rng.choice([None, "8.3.0.K"]), machine=rng.choice(MACHINES), rocm_link=rng.choice(ROCM_INSTALLS),
                 layout=rng.choice(["function", "function", "shared"]))
     for _ in range(rng.randint(1, 3)):
@@ -213,6 +224,8 @@ def mutate(live: LiveNode, rng: random.Random) -> str:
     kind = rng.choice(kinds)
     if kind in ("partition", "nps", "vfs", "gpu_remove", "bind") and not n.gpus:
         kind = "gpu_add"
+    if n.guest and kind in ("partition", "nps", "vfs"):
+        kind = "uevent"  # a VF's modes are the host's business
     recreate: tuple[str, ...] = ()
     reset = False
     if kind == "partition":
@@ -237,7 +250,10 @@ def mutate(live: LiveNode, rng: random.Random) -> str:
             g = rng.choice(capable)
             g.vfs = rng.choice([v for v in (0, 1, 2, 3) if v != g.vfs])
     elif kind == "gpu_add":
-        n.gpus.append(new_gpu(n, rng))
+        g = new_gpu(n, rng)
+        if n.guest:
+            g.vf, g.mode, g.nps = True, "SPX", "NPS1"
+        n.gpus.append(g)
     elif kind == "gpu_remove":
         n.gpus.pop(rng.randrange(len(n.gpus)))
     elif kind == "module_reload":

@@ -4,6 +4,7 @@
 #include "lm/labels.h"
 
 #include <fcntl.h>
+#include <signal.h>
 #include <sys/stat.h>
 #include <sys/vfs.h>
 #include <unistd.h>
@@ -267,6 +268,11 @@ void write_kept(const std::string& path, const std::string& tmp_dir, const std::
       next.dev = st.st_dev;
       next.ino = st.st_ino;
     }
+    // A lease break (an open that raced with the exchange and reached the
+    // file while this process held its lease) signals the holder: SIGIO by
+    // default, which would terminate the daemon.  SIGURG is ignored unless
+    // handled, and the breaker only waits for the lease's release anyway.
+    (void)::fcntl(next.fd, F_SETSIG, SIGURG);
   }
   // Swap it with the feature file when that is a regular file; anything else
   // at `path` (nothing yet, a directory that must fail like rename(2)

@@ -4,9 +4,6 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <string_view>
-#include <unordered_map>
-#include <unordered_set>
 
 #include "util/error.h"
 #include "util/fs.h"
@@ -78,94 +75,12 @@ std::optional<std::string> PCIDevice::GetExtendedCapability(int ext_id, size_t l
   return std::nullopt;
 }
 
-namespace {
-
-// Vendor and device ID (vendor << 16 | device) of every PCI function from
-// procfs' one-file device table
-// (/proc/bus/pci/devices: one "BBDF\tVVVVDDDD\t..." line per function, BBDF =
-// bus << 8 | devfn, all hex).  One read instead of one `vendor` file per
-// function - 367 files on an 8-GPU MI355X host.  The table has no PCI
-// domain, so a bus/devfn listed twice is dropped (those functions are read
-// from sysfs).  Empty when the table cannot be read.
-struct ProcFunction {
-  uint32_t id = 0;    // vendor << 16 | device
-  bool port = false;  // bound to pcieport: a PCIe port (bridge), never a GPU
-};
-
-std::unordered_map<uint32_t, ProcFunction> proc_pci_functions(const std::string& root) {
-  std::unordered_map<uint32_t, ProcFunction> out;
-  auto r = fs::read_file(fs::join(root, "proc/bus/pci/devices"), 4u << 20);
-  if (!r.ok()) return out;
-  std::unordered_set<uint32_t> dup;
-  const char* p = r.data.c_str();
-  const char* end = p + r.data.size();
-  // The kernel's line (drivers/pci/proc.c, show_device): bus/devfn,
-  // vendor/device, irq, 7 resource starts, 7 sizes, then the bound driver's
-  // name (empty if none) - 18 tab-separated fields.
-  constexpr int kDriverField = 17;
-  while (p < end) {
-    const char* eol = static_cast<const char*>(std::memchr(p, '\n', static_cast<size_t>(end - p)));
-    if (!eol) eol = end;
-    char* q = nullptr;
-    unsigned long bbdf = std::strtoul(p, &q, 16);
-    if (q && q < eol && *q == '\t') {
-      char* q2 = nullptr;
-      unsigned long id = std::strtoul(q + 1, &q2, 16);
-      if (q2 && q2 > q + 1 && q2 <= eol) {
-        ProcFunction f;
-        f.id = static_cast<uint32_t>(id);
-        int tabs = 0;
-        const char* last = p;
-        for (const char* c = p; c < eol; ++c)
-          if (*c == '\t') {
-            ++tabs;
-            last = c + 1;
-          }
-        f.port = tabs == kDriverField && std::string_view(last, static_cast<size_t>(eol - last)) == "pcieport";
-        auto key = static_cast<uint32_t>(bbdf & 0xffff);
-        if (!out.emplace(key, f).second) dup.insert(key);
-      }
-    }
-    p = eol + 1;
-  }
-  for (auto k : dup) out.erase(k);
-  return out;
-}
-
-// "DDDD:BB:DD.F" (sysfs' PCI device names; the domain may be longer) ->
-// bus << 8 | dev << 3 | fn.  Hand-parsed: sscanf cost ~0.2 us per name,
-// 70 us for the ~350 names a cold scan looks up.
-std::optional<uint32_t> bus_devfn(const std::string& addr) {
-  auto hex = [](char c) -> int {
-    if (c >= '0' && c <= '9') return c - '0';
-    if (c >= 'a' && c <= 'f') return c - 'a' + 10;
-    if (c >= 'A' && c <= 'F') return c - 'A' + 10;
-    return -1;
-  };
-  // The fixed-width tail ":BB:DD.F" after a domain of 4+ hex digits.
-  size_t n = addr.size();
-  if (n < 12) return std::nullopt;
-  const char* t = addr.c_str() + n - 8;
-  for (size_t i = 0; i + 8 < n; ++i)
-    if (hex(addr[i]) < 0) return std::nullopt;
-  int b1 = hex(t[1]), b0 = hex(t[2]), d1 = hex(t[4]), d0 = hex(t[5]), f = hex(t[7]);
-  if (t[0] != ':' || t[3] != ':' || t[6] != '.' || b1 < 0 || b0 < 0 || d1 < 0 || d0 < 0 || f < 0) return std::nullopt;
-  unsigned bus = static_cast<unsigned>(b1 << 4 | b0), dev = static_cast<unsigned>(d1 << 4 | d0);
-  if (dev > 0x1f || f > 7) return std::nullopt;
-  return static_cast<uint32_t>((bus << 8) | (dev << 3) | static_cast<unsigned>(f));
-}
-
-}  // namespace
-
-SysfsAmdPCI::Identity SysfsAmdPCI::read_identity(const std::string& addr, const std::string& p, uint64_t ino,
-                                                 uint32_t device_id, bool amd) {
+SysfsAmdPCI::Identity SysfsAmdPCI::read_identity(const std::string& addr, const std::string& p, uint64_t ino) {
   Identity id;
   id.ino = ino;
-  if (device_id == 0 && !amd) {
-    auto vendor = fs::read_file(fs::join(p, "vendor"), 64);
-    if (!vendor.ok()) throw Error("unable to read PCI device vendor id for " + addr + ": " + fs::errno_str(vendor.err));
-    if (str::trim(vendor.data) != kAmdVendorId) return id;
-  }
+  auto vendor = fs::read_file(fs::join(p, "vendor"), 64);
+  if (!vendor.ok()) throw Error("unable to read PCI device vendor id for " + addr + ": " + fs::errno_str(vendor.err));
+  if (str::trim(vendor.data) != kAmdVendorId) return id;
   auto cls = fs::read_file(fs::join(p, "class"), 64);
   if (!cls.ok()) throw Error("unable to read PCI device class for " + addr + ": " + fs::errno_str(cls.err));
   std::string c = str::trim(cls.data);
@@ -173,7 +88,7 @@ SysfsAmdPCI::Identity SysfsAmdPCI::read_identity(const std::string& addr, const 
   if (!str::starts_with(c, "0x03") && !str::starts_with(c, "0x12")) return id;
   id.relevant = true;
   id.class_code = c.substr(0, 4);
-  id.device = device_id ? str::format("0x%04x", device_id) : fs::read_trimmed(fs::join(p, "device")).value_or("");
+  id.device = fs::read_trimmed(fs::join(p, "device")).value_or("");
   if (auto t = fs::read_trimmed(fs::join(p, "sriov_totalvfs")))
     id.sriov_totalvfs = static_cast<int>(str::parse_uint(*t).value_or(0));
   if (id.sriov_totalvfs > 0) id.sriov_vf_device = fs::read_trimmed(fs::join(p, "sriov_vf_device")).value_or("");
@@ -229,102 +144,24 @@ std::vector<PCIDevice> SysfsAmdPCI::Devices() {
     }
   }
   // Identity reads (vendor, class, ...) of functions not seen before: every
-  // function on the first scan (~5 us each, 2 ms for 367 functions on an
-  // 8-GPU host) - the whole cost of a oneshot Job's scan.  A cold scan first
-  // takes the vendor IDs of all functions from procfs' device table and
-  // reads sysfs only for AMD functions (and any the table cannot place); the
-  // remaining reads are spread over the worker pool in chunks.  A hot-plugged
-  // function or two is read inline.
+  // function on the first scan (~5 us each: 2 ms for the 367 functions of an
+  // 8-GPU host), spread over the worker pool in chunks; a hot-plugged
+  // function or two is read inline.  This scan is the fallback of the
+  // driver-directed one (sriov/bound.h), used only when neither amdgpu nor
+  // gim binds anything.
   constexpr size_t kChunk = 16;
-  size_t chunk = kChunk;
-  std::vector<uint32_t> known_device;  // aligned with misses: device ID from procfs, 0 = unknown
-  // Functions bound to amdgpu (AMD's: its ID table names vendor 0x1002 only)
-  // in a cold scan: their identity reads start on the pool at once and run
-  // while this thread reads the procfs table (0.5-0.65 ms on a 367-function
-  // host: the kernel restarts its device walk for every page it hands out),
-  // which then only has to name the other AMD functions (none on the pool's
-  // hosts once the PCIe ports are skipped).
-  std::vector<size_t> early;
-  WorkerPool::Task early_task;
-  struct EarlyGuard {  // the task reads `next`: it must be done before it goes
-    WorkerPool::Task* t;
-    bool armed = false;
-    ~EarlyGuard() {
-      if (armed) t->cancel_or_wait();
-    }
-  } early_guard{&early_task};
-  if (misses.size() > kChunk) {
-    int64_t tp = trace::now_ns();
-    std::vector<char> miss(next.size(), 0);
-    for (size_t m : misses) miss[m] = 1;
-    for (const auto& name : fs::list_dir(fs::join(root_, "sys/bus/pci/drivers/amdgpu"))) {
-      if (!bus_devfn(name)) continue;  // bind, unbind, module, ...
-      auto it = std::lower_bound(next.begin(), next.end(), name,
-                                 [](const std::pair<std::string, Identity>& e, const std::string& n) { return e.first < n; });
-      size_t i = static_cast<size_t>(it - next.begin());
-      if (it != next.end() && it->first == name && miss[i]) {
-        early.push_back(i);
-        miss[i] = 0;
-      }
-    }
-    if (!early.empty()) {
-      misses.erase(std::remove_if(misses.begin(), misses.end(), [&](size_t m) { return !miss[m]; }), misses.end());
-      early_task = WorkerPool::instance().submit([&] {
-        constexpr size_t kEarlyChunk = 2;
-        WorkerPool::instance().parallel_for((early.size() + kEarlyChunk - 1) / kEarlyChunk, [&](size_t c) {
-          for (size_t k = c * kEarlyChunk; k < std::min(early.size(), (c + 1) * kEarlyChunk); ++k) {
-            auto& [addr, id] = next[early[k]];
-            id = read_identity(addr, fs::join(dir, addr), id.ino, 0, true);
-          }
-        });
-      });
-      early_guard.armed = true;
-    }
-    trace::record("pci.amdgpu", trace::now_ns() - tp);
-    tp = trace::now_ns();
-    auto table = proc_pci_functions(root_);
-    trace::record("pci.proc_table", trace::now_ns() - tp);
-    if (!table.empty()) {
-      uint32_t amd = static_cast<uint32_t>(std::strtoul(kAmdVendorId, nullptr, 16));
-      std::vector<size_t> amd_or_unknown;
-      for (size_t m : misses) {
-        auto key = bus_devfn(next[m].first);
-        auto v = key ? table.find(*key) : table.end();
-        if (v == table.end()) {
-          amd_or_unknown.push_back(m);
-          known_device.push_back(0);
-        } else if ((v->second.id >> 16) == amd && (v->second.id & 0xffff) != 0 && !v->second.port) {
-          amd_or_unknown.push_back(m);
-          known_device.push_back(v->second.id & 0xffff);
-        }
-        // else: another vendor's function, or an AMD PCIe port (the switch
-        // ports next to every MI355X: half the host's AMD functions) -
-        // identity stays "not relevant"
-      }
-      misses.swap(amd_or_unknown);
-      // A few functions per lane (~2-4 reads each now that vendor and device
-      // come from the table).  Lane count does not matter on the pool's
-      // 16-AMD-function hosts: 1, 2, 4, 8 or all 16 per lane gave the same
-      // Job process within 0.04 ms (profiles/pci_cold_ab.txt).
-      chunk = 2;
-    }
-  }
   auto read_chunk = [&](size_t c) {
-    for (size_t k = c * chunk; k < std::min(misses.size(), (c + 1) * chunk); ++k) {
+    for (size_t k = c * kChunk; k < std::min(misses.size(), (c + 1) * kChunk); ++k) {
       auto& [addr, id] = next[misses[k]];
-      id = read_identity(addr, fs::join(dir, addr), id.ino, k < known_device.size() ? known_device[k] : 0);
+      id = read_identity(addr, fs::join(dir, addr), id.ino);
     }
   };
-  size_t chunks = (misses.size() + chunk - 1) / chunk;
+  size_t chunks = (misses.size() + kChunk - 1) / kChunk;
   try {
     if (chunks > 1)
       WorkerPool::instance().parallel_for(chunks, read_chunk);
     else if (chunks == 1)
       read_chunk(0);
-    if (early_guard.armed) {
-      early_guard.armed = false;
-      early_task.run_or_wait();
-    }
   } catch (...) {
     listing_.reset();  // the next scan must see this listing as changed again
     throw;

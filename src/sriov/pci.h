@@ -82,7 +82,10 @@ class AmdPCI {
 };
 
 // Walks <root>/sys/bus/pci/devices and keeps vendor 0x1002 display (0x03)
-// and processing-accelerator (0x12) functions.
+// and processing-accelerator (0x12) functions: the reference's approach
+// (pciutil.go:70-112), and since round 4 only the fallback of the
+// driver-directed source (sriov/bound.h) for nodes where neither amdgpu nor
+// gim binds anything.
 //
 // Cost model (measured on the MI355X pool, ~1.3 ms per scan before this):
 // a large server has hundreds of PCI functions and the reference reads
@@ -125,12 +128,7 @@ class SysfsAmdPCI : public AmdPCI {
     std::string physfn;
     int sriov_numvfs = -1;  // last NumVFs read; -1 = re-read (listing changed)
   };
-  // `device_id`: the function's device ID when procfs' device table already
-  // placed it as an AMD function (vendor and device are not re-read), else 0.
-  // device_id: from the procfs table (0 = read it); amd: the vendor is known
-  // to be AMD (bound to amdgpu) - no vendor read.
-  static Identity read_identity(const std::string& addr, const std::string& path, uint64_t ino, uint32_t device_id = 0,
-                                bool amd = false);
+  static Identity read_identity(const std::string& addr, const std::string& path, uint64_t ino);
   std::string root_;
   fs::DirListing listing_;
   bool scanned_ = false;

@@ -79,23 +79,6 @@ std::vector<std::string> list_dir(const std::string& path, int* err) {
   return out;
 }
 
-std::vector<std::pair<std::string, uint64_t>> list_dir_ino(const std::string& path, int* err) {
-  std::vector<std::pair<std::string, uint64_t>> out;
-  DIR* d = ::opendir(path.c_str());
-  if (!d) {
-    if (err) *err = errno;
-    return out;
-  }
-  if (err) *err = 0;
-  while (struct dirent* e = ::readdir(d)) {
-    if (e->d_name[0] == '.' && (e->d_name[1] == 0 || (e->d_name[1] == '.' && e->d_name[2] == 0))) continue;
-    out.emplace_back(e->d_name, static_cast<uint64_t>(e->d_ino));
-  }
-  ::closedir(d);
-  std::sort(out.begin(), out.end());
-  return out;
-}
-
 DirListing::~DirListing() {
   if (fd_ >= 0) ::close(fd_);
 }

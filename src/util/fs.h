@@ -30,9 +30,6 @@ bool is_dir(const std::string& path);
 // Directory entries (excluding . and ..), sorted by name.  Empty on error;
 // `err` (optional) receives errno.
 std::vector<std::string> list_dir(const std::string& path, int* err = nullptr);
-// Like list_dir but also returns each entry's inode number (d_ino), which
-// changes when a sysfs object is removed and re-created (hot-plug).
-std::vector<std::pair<std::string, uint64_t>> list_dir_ino(const std::string& path, int* err = nullptr);
 // A directory listing re-read every call through a descriptor kept open
 // across calls: one lseek + getdents64 pass, no path walk, no per-entry
 // work when nothing changed.  Whether anything changed is decided on the raw

@@ -67,9 +67,10 @@ const std::string& root() {
     gfd::fs::mkdir_all(s + "/proc/bus/pci");
     gfd::lm::write_file_atomically(s + "/sys/class/kfd/kfd/topology/nodes/0/properties", "cpu_cores_count 64\n", 0644);
     gfd::lm::write_file_atomically(s + "/sys/bus/pci/devices/0000:75:00.0/vendor", "0x1002\n", 0644);
-    // Enough other functions for the cold scan's procfs-table path (more
+    // Enough other functions for the whole-bus scan's parallel path (more
     // than 16 unread functions), and amdgpu's driver directory naming the
-    // GPU (its identity read on the pool while the table is read).
+    // GPU (the driver-directed scan).  proc/bus/pci/devices stays in the
+    // file list (no reader since round 5) so the corpus keeps its meaning.
     for (int i = 0; i < 24; ++i) {
       char name[32];
       std::snprintf(name, sizeof(name), "0000:%02x:%02x.0", i / 8, i % 8);

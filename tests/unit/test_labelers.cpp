@@ -3,12 +3,14 @@
 #include <fcntl.h>
 #include <sys/resource.h>
 #include <sys/stat.h>
+#include <sys/wait.h>
 #include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
 #include <csignal>
 #include <cstdio>
+#include <cstdlib>
 #include <set>
 #include <thread>
 
@@ -572,6 +574,50 @@ TEST(WriteToFile_LoopWritesAlternateTwoFilesAndCreateNone) {
   lm::remove_output_file(path);
   EXPECT_FALSE(fs::exists(std::string(dir) + "/gfd-tmp"));
   EXPECT_FALSE(fs::exists(path));
+  fs::remove_all(dir);
+}
+
+TEST(WriteToFile_KeptFilesSignalALeaseBreakWithSIGURG) {
+  // A reader whose open raced with an exchange can reach the kept file while
+  // a write holds its lease; the kernel then signals the holder - SIGIO by
+  // default, which terminates a process.  The kept files' descriptors signal
+  // SIGURG, ignored by default.
+  char dir[] = "/tmp/gfd-write-XXXXXX";
+  EXPECT_TRUE(mkdtemp(dir) != nullptr);
+  std::string path = std::string(dir) + "/gfd";
+  loop_write({{"k", "1"}}, path);
+  loop_write({{"k", "2"}}, path);
+  int seen = 0, kept_fd = -1;
+  std::string kept;
+  for (const auto& n : fs::list_dir("/proc/self/fd")) {
+    std::string target = fs::read_link("/proc/self/fd/" + n);
+    if (target.rfind(std::string(dir) + "/", 0) != 0) continue;
+    ++seen;
+    EXPECT_EQ(::fcntl(std::atoi(n.c_str()), F_GETSIG), SIGURG);
+    if (target.find("/gfd-tmp/") != std::string::npos) {
+      kept_fd = std::atoi(n.c_str());
+      kept = target;
+    }
+  }
+  EXPECT_EQ(seen, 2);  // the feature file and the kept one
+  // A lease break is survived: a write lease on the kept file's descriptor,
+  // broken by another process opening the file (`cat`, which waits for the
+  // release), signals this process with SIGURG - ignored.
+  EXPECT_TRUE(kept_fd >= 0);
+  EXPECT_EQ(::fcntl(kept_fd, F_SETLEASE, F_WRLCK), 0);
+  pid_t pid = ::fork();
+  if (pid == 0) {
+    int null = ::open("/dev/null", O_WRONLY);
+    ::dup2(null, 1);
+    ::execlp("cat", "cat", kept.c_str(), static_cast<char*>(nullptr));
+    ::_exit(127);
+  }
+  ::usleep(100 * 1000);  // the child's open is blocked on the lease meanwhile
+  EXPECT_EQ(::fcntl(kept_fd, F_SETLEASE, F_UNLCK), 0);
+  int status = 0;
+  EXPECT_EQ(::waitpid(pid, &status, 0), pid);
+  EXPECT_TRUE(WIFEXITED(status) && WEXITSTATUS(status) == 0);
+  lm::remove_output_file(path);
   fs::remove_all(dir);
 }
 

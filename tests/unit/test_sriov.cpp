@@ -342,155 +342,6 @@ TEST(Fs_DirListingReportsChangesAndSurvivesRecreation) {
   fs::remove_all(d);
 }
 
-TEST(Sriov_ColdScanTakesVendorsFromProcTable) {
-  std::string root = pci_host(200, 2);
-  std::string dev = root + "/sys/bus/pci/devices/";
-  // procfs' device table for every function except 0000:00:07.0.
-  std::string table;
-  for (const auto& [name, ino] : fs::list_dir_ino(dev)) {
-    if (name == "0000:00:07.0") continue;
-    unsigned d = 0, b = 0, s = 0, f = 0;
-    if (std::sscanf(name.c_str(), "%x:%x:%x.%x", &d, &b, &s, &f) != 4) throw std::runtime_error(name);
-    std::string vendor = str::trim(fs::read_file(dev + name + "/vendor").data);
-    std::string device = str::trim(fs::read_file(dev + name + "/device").data);
-    if (device.empty()) device = "0x0000";
-    table += str::format("%04x\t%s%s\t0\t0\n", (b << 8) | (s << 3) | f, vendor.substr(2).c_str(), device.substr(2).c_str());
-  }
-  put_file(root + "/proc/bus/pci/devices", table);
-  // A non-AMD function the table places is never read from sysfs ...
-  fs::remove_all(dev + "0000:00:05.0/vendor");
-  fs::mkdir_all(dev + "0000:00:05.0/vendor");  // unreadable attribute
-  // ... and an AMD function it places has its vendor and device ID from it.
-  std::string amd_fn;
-  for (const auto& [name, ino] : fs::list_dir_ino(dev))
-    if (name != "0000:00:07.0" && str::trim(fs::read_file(dev + name + "/vendor").data) == "0x1002" &&
-        str::trim(fs::read_file(dev + name + "/device").data) == "0x75a3")
-      amd_fn = name;
-  EXPECT_FALSE(amd_fn.empty());
-  fs::remove_all(dev + amd_fn + "/vendor");
-  fs::remove_all(dev + amd_fn + "/device");
-  SysfsAmdPCI pci(root);
-  auto devs = pci.Devices();
-  EXPECT_EQ(devs.size(), static_cast<size_t>(7));  // AMD functions still fully read
-  int vfs = 0;
-  for (const auto& d : devs) {
-    vfs += !d.physfn.empty();
-    if (d.address == amd_fn) EXPECT_EQ(d.device, std::string("0x75a3"));
-  }
-  EXPECT_EQ(vfs, 2);
-  // ... one the table does not list is.
-  fs::remove_all(dev + "0000:00:07.0/vendor");
-  fs::mkdir_all(dev + "0000:00:07.0/vendor");
-  SysfsAmdPCI cold(root);
-  EXPECT_THROW_MSG(cold.Devices(), "unable to read PCI device vendor id for 0000:00:07.0");
-  // A bus/devfn listed twice (two PCI domains) is ambiguous: read from sysfs.
-  put_file(root + "/proc/bus/pci/devices", table + "0028\t80861234\t0\t0\n");  // 0000:00:05.0's key again
-  fs::remove_all(dev + "0000:00:07.0/vendor");
-  put_file(dev + "0000:00:07.0/vendor", "0x1022\n");
-  SysfsAmdPCI ambiguous(root);
-  EXPECT_THROW_MSG(ambiguous.Devices(), "unable to read PCI device vendor id for 0000:00:05.0");
-  fs::remove_all(root);
-}
-
-TEST(Sriov_ColdScanReadsAmdgpuFunctionsAlongsideTheTable) {
-  // Functions listed in sys/bus/pci/drivers/amdgpu are read on the pool
-  // while the procfs table is read, without a vendor read (amdgpu binds AMD
-  // functions only); the result is the same scan.
-  std::string root = pci_host(200, 2);
-  std::string dev = root + "/sys/bus/pci/devices/";
-  std::string table;
-  for (const auto& [name, ino] : fs::list_dir_ino(dev)) {
-    unsigned d = 0, b = 0, s = 0, f = 0;
-    if (std::sscanf(name.c_str(), "%x:%x:%x.%x", &d, &b, &s, &f) != 4) throw std::runtime_error(name);
-    std::string vendor = str::trim(fs::read_file(dev + name + "/vendor").data);
-    std::string device = str::trim(fs::read_file(dev + name + "/device").data);
-    if (device.empty()) device = "0x0000";
-    table += str::format("%04x\t%s%s\t0\t0\n", (b << 8) | (s << 3) | f, vendor.substr(2).c_str(), device.substr(2).c_str());
-  }
-  put_file(root + "/proc/bus/pci/devices", table);
-  auto summary = [](const std::vector<PCIDevice>& devs) {
-    std::string out;
-    for (const auto& d : devs)
-      out += d.address + " " + d.device + " " + d.class_code + " " + std::to_string(d.sriov_totalvfs) + " " +
-             std::to_string(d.sriov_numvfs) + " " + d.physfn + "\n";
-    return out;
-  };
-  std::string want = summary(SysfsAmdPCI(root).Devices());
-  EXPECT_EQ(std::count(want.begin(), want.end(), '\n'), 7L);
-  // amdgpu's driver directory: the 5 PFs, its control files, and a function
-  // that is not on the bus listing (ignored).
-  std::string drv = root + "/sys/bus/pci/drivers/amdgpu/";
-  for (int g = 0; g < 4; ++g) fs::mkdir_all(drv + str::format("0000:%02x:00.0", 0x11 + 0x10 * g));
-  fs::mkdir_all(drv + "0000:c1:00.0");
-  fs::mkdir_all(drv + "0000:ee:00.0");
-  for (const char* f : {"bind", "unbind", "uevent", "new_id"}) put_file(drv + f, "");
-  fs::mkdir_all(drv + "module");
-  // Their vendor attribute is not needed any more.
-  fs::remove_all(dev + "0000:11:00.0/vendor");
-  fs::mkdir_all(dev + "0000:11:00.0/vendor");  // unreadable as a file
-  EXPECT_EQ(summary(SysfsAmdPCI(root).Devices()), want);
-  // Without the procfs table the rest are read from sysfs, the amdgpu ones once.
-  fs::remove_all(root + "/proc");
-  EXPECT_EQ(summary(SysfsAmdPCI(root).Devices()), want);
-  // An amdgpu function whose class cannot be read fails the scan, from the
-  // pool task, with the same error as the serial path.
-  fs::remove_all(dev + "0000:21:00.0/class");
-  fs::mkdir_all(dev + "0000:21:00.0/class");
-  put_file(root + "/proc/bus/pci/devices", table);
-  SysfsAmdPCI bad(root);
-  EXPECT_THROW_MSG(bad.Devices(), "unable to read PCI device class for 0000:21:00.0");
-  fs::remove_all(root);
-}
-
-TEST(Sriov_ColdScanSkipsFunctionsBoundToPcieport) {
-  // The kernel's full table line: 18 tab-separated fields, the last the
-  // bound driver.  An AMD function bound to pcieport (the PCIe switch ports
-  // next to each MI355X) is a bridge: its identity is never read.
-  std::string root = pci_host(20, 0);
-  std::string dev = root + "/sys/bus/pci/devices/";
-  auto line = [](const std::string& name, const std::string& vendev, const std::string& driver) {
-    unsigned d = 0, b = 0, s = 0, f = 0;
-    if (std::sscanf(name.c_str(), "%x:%x:%x.%x", &d, &b, &s, &f) != 4) throw std::runtime_error(name);
-    std::string l = str::format("%04x\t%s\t0", (b << 8) | (s << 3) | f, vendev.c_str());
-    for (int i = 0; i < 14; ++i) l += "\t0000000000000000";
-    return l + "\t" + driver + "\n";
-  };
-  std::string table, port, gpu;
-  for (const auto& [name, ino] : fs::list_dir_ino(dev)) {
-    std::string vendor = str::trim(fs::read_file(dev + name + "/vendor").data);
-    std::string device = str::trim(fs::read_file(dev + name + "/device").data);
-    if (device.empty()) device = "0x0000";
-    std::string vd = vendor.substr(2) + device.substr(2);
-    bool amd = vendor == "0x1002";
-    if (amd && gpu.empty()) gpu = name;
-    std::string driver = amd ? "amdgpu" : "";
-    table += line(name, vd, driver);
-  }
-  // An extra AMD function bound to pcieport whose attributes cannot be read.
-  port = "0000:7f:00.0";
-  fs::mkdir_all(dev + port + "/class");  // unreadable as a file
-  put_file(dev + port + "/vendor", "0x1002\n");
-  table += line(port, "10021501", "pcieport");
-  put_file(root + "/proc/bus/pci/devices", table);
-  SysfsAmdPCI pci(root);
-  auto devs = pci.Devices();
-  EXPECT_FALSE(gpu.empty());
-  bool has_gpu = false, has_port = false;
-  for (const auto& d : devs) {
-    has_gpu |= d.address == gpu;
-    has_port |= d.address == port;
-  }
-  EXPECT_TRUE(has_gpu);
-  EXPECT_FALSE(has_port);
-  // The same function with the short (driverless) line format is read - and
-  // its unreadable class is an error.
-  table.resize(table.size() - line(port, "10021501", "pcieport").size());
-  put_file(root + "/proc/bus/pci/devices", table + str::format("%04x\t10021501\t0\t0\n", 0x7f << 8));
-  SysfsAmdPCI cold(root);
-  EXPECT_THROW_MSG(cold.Devices(), "unable to read PCI device class for 0000:7f:00.0");
-  fs::remove_all(root);
-}
-
 TEST(Fs_AttrReaderKeepsOnlySysfsDescriptors) {
   char d[] = "/tmp/gfd-attr-XXXXXX";
   if (!mkdtemp(d)) throw std::runtime_error("mkdtemp");

@@ -690,11 +690,15 @@ def test_a_reader_holding_the_file_across_cycles_sees_it_unchanged(binary, tmp_p
                 bad.append(f"incomplete: {first[-80:]!r}")
         assert not bad, bad
         assert held > 100 and seen == set(names), (held, seen)  # the labels did change under the readers
+        # Alive: an open racing with an exchange can break the write lease,
+        # which signals the daemon (SIGURG, not the terminating SIGIO).
+        assert p.poll() is None, p.returncode
     finally:
         stop.set()
         t.join()
         p.send_signal(signal.SIGTERM)
         p.communicate(timeout=30)
+    assert p.returncode == 0, p.returncode
 
 
 def test_cpu_placement_modes(binary, tmp_path):

@@ -654,6 +654,7 @@ def test_a_reader_holding_the_file_across_cycles_sees_it_unchanged(binary, tmp_p
     features.mkdir()
     out = features / "gfd"
     names = ["Machine-A", "Machine-B"]
+    dmi.write_text(names[1] + "\n")  # the tree's own name never shows
     stop = threading.Event()
 
     def flip():

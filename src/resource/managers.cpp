@@ -92,7 +92,9 @@ WarmStartManager::WarmStartManager(ManagerPtr preferred, ManagerPtr quick)
 WarmStartManager::~WarmStartManager() {
   if (!thread_.joinable()) return;
   std::unique_lock<std::mutex> lk(warmer_->mu);
-  // system_clock: see lm::discard_prepared_temps (TSan and clockwait).
+  // system_clock: a steady_clock wait is pthread_cond_clockwait, which GCC
+  // 11's ThreadSanitizer does not intercept (it then reports the waker's lock
+  // of `mu` as a double lock); a clock step only moves this bound.
   if (warmer_->cv.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(teardown_wait_ms),
                              [&] { return warmer_->done; })) {
     lk.unlock();

@@ -7,7 +7,7 @@ have: the amd-smi session and what it learned (handles, ASIC identity,
 supported partition modes), the KFD topology of a generation, the SR-IOV
 functions while no uevent was sent (and, after one, while the driver
 directories and VF links are unchanged), the amdgpu module directory, open
-attribute descriptors, prepared temporary files.  Each of those is only
+attribute descriptors, the feature file and its swapped-out spare.  Each of those is only
 correct if everything that can change it also invalidates it.
 
 This module changes a synthetic MI355X node the way the kernel and an

@@ -12,17 +12,19 @@ the reason each is safe in docs/ARCHITECTURE.md ("What is kept between
 cycles"): the loaded library, the persistent amd-smi session's handles and
 the facts fixed until the KFD topology generation changes (ASIC identity,
 virtualization mode, KFD node id and XCD count), open descriptors of sysfs
-attributes, and the SR-IOV functions while no uevent was sent (no device
-added, removed, bound or unbound).  Every other
-device value - memory, partition modes, xGMI links, partition
-capabilities, versions, machine type - is read from the driver each step.
+attributes, the kernel's DMI strings (copied from the firmware at boot), the
+SR-IOV functions while no uevent was sent (no device added, removed, bound
+or unbound), and the feature file the previous write swapped out, which the
+next write rewrites whole.  Every other device value - memory, partition
+modes, xGMI links, partition capabilities, versions - is read from the
+driver each step.
 
 The label set of every step is checked for correctness (count == N GPUs,
 gfx950/cdna4 arch, MI355 product, HBM size, valid Kubernetes label syntax)
 before timing is reported.  The in-process session runs the daemon's default
 configuration: workers follow the cycle thread's L3 domain
-(--cpu-affinity=follow), block when idle, and prepare the next writes'
-temporary files.
+(--cpu-affinity=follow) and block when idle; every write rewrites the file
+the previous one swapped out and exchanges it with the feature file.
 
 N>1: launched by the driver as one process per GPU under torch.distributed
 (gloo, 127.0.0.1); rank 0 labels the node restricted to GPUs 0..N-1 (the

@@ -471,6 +471,37 @@ def test_devices_match_amd_smi_cli(amdsmi_devices, sysfs_devices):
                 assert d["compute_units"] == s["asic"]["num_compute_units"]
 
 
+def test_devices_match_the_hip_runtime(amdsmi_devices, sysfs_devices):
+    """A third oracle, independent of amd-smi: the HIP runtime, as PyTorch-ROCm
+    reports each visible GPU (its own path through the KFD thunk), in a
+    separate process - loading it changes what amd-smi reads in this one
+    (test_product_name_survives_torch_libdrm).  Architecture, compute units
+    and device memory must be the ones the labels are built from."""
+    code = (
+        "import json, torch\n"
+        "out = []\n"
+        "for i in range(torch.cuda.device_count()):\n"
+        "    p = torch.cuda.get_device_properties(i)\n"
+        "    out.append({'bdf': '%04x:%02x:%02x.0' % (p.pci_domain_id, p.pci_bus_id, p.pci_device_id),\n"
+        "                'arch': p.gcnArchName, 'cus': p.multi_processor_count, 'mem': p.total_memory,\n"
+        "                'warp': p.warp_size})\n"
+        "print(json.dumps(out))\n"
+    )
+    cp = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=600)
+    assert cp.returncode == 0, cp.stderr[-2000:]
+    hip = {g["bdf"]: g for g in json.loads(cp.stdout.strip().splitlines()[-1])}
+    print("hip runtime:", hip)
+    assert set(hip) == {d["bdf"] for d in amdsmi_devices}
+    for backend in (amdsmi_devices, sysfs_devices):
+        for d in backend:
+            h = hip[d["bdf"]]
+            assert h["arch"].split(":")[0] == d["gfx"], (h, d["gfx"])
+            assert h["warp"] == 64
+            if d["compute_partition"] == "SPX":
+                assert h["cus"] == d["compute_units"], (h, d["compute_units"])
+                assert h["mem"] // (1 << 20) == d["memory_mib"], (h, d["memory_mib"])
+
+
 def test_attribute_descriptors_kept_open_and_stable(native):
     """Per-cycle sysfs attributes are read through descriptors kept open
     across cycles (pread at offset 0 re-runs the driver's show()): after a

@@ -5,7 +5,10 @@ keeps a library session and caches across cycles must prove it does not leak.
 The daemon is run in loop mode with a 1 ms interval (thousands of cycles),
 reloaded with SIGHUP part-way (manager, SR-IOV scanner and amd-smi session
 rebuilt), and its RSS and open descriptors are compared between an early
-sample (after warm-up) and the end.
+sample (after warm-up) and the end.  Meanwhile a reader opens and reads the
+feature file back to back, as NFD does once a minute: every read must be a
+whole label set, and the daemon must survive the write-lease breaks those
+opens cause.
 """
 
 from __future__ import annotations
@@ -58,6 +61,22 @@ def _fds(pid: int) -> tuple[int, int]:
     return min(n), max(prepared)
 
 
+def _read_feature_file(out: str, stop: threading.Event, stats: dict) -> None:
+    # NFD's side, far more often than NFD: open, read, close - and every read
+    # is a whole label set.  Each open can race the daemon's exchange and
+    # break its write lease on the swapped-out file (src/lm/writer.cpp).
+    while not stop.is_set():
+        try:
+            with open(out, "rb") as f:
+                data = f.read()
+        except FileNotFoundError:
+            time.sleep(0.001)
+            continue
+        stats["reads"] += 1
+        if not data.endswith(b"\n") or b"amd.com/gpu.count=" not in data:
+            stats["bad"].append(data[-80:])
+
+
 def soak(binary: str, args: list[str], seconds: float, hup_at: float | None = None, interval: str = "1ms") -> dict:
     p = subprocess.Popen([binary, f"--sleep-interval={interval}", "--trace-timing", *args], stdout=subprocess.DEVNULL,
                          stderr=subprocess.PIPE, text=True)
@@ -76,6 +95,11 @@ def soak(binary: str, args: list[str], seconds: float, hup_at: float | None = No
 
     t = threading.Thread(target=reader, daemon=True)
     t.start()
+    out = next((a.split("=", 1)[1] for a in args if a.startswith("--output-file=")), "")
+    stop = threading.Event()
+    reads = {"reads": 0, "bad": []}
+    rt = threading.Thread(target=_read_feature_file, args=(out, stop, reads), daemon=True)
+    rt.start()
     try:
         deadline = time.monotonic() + 60
         while cycles[0] < 200 and time.monotonic() < deadline and p.poll() is None:
@@ -97,9 +121,10 @@ def soak(binary: str, args: list[str], seconds: float, hup_at: float | None = No
         rss1, (fd1, prep1), c1 = _rss_kib(p.pid), _fds(p.pid), cycles[0]
         # Files in gfd-tmp/: the old feature file kept for the next write
         # (and, in a write that could not reuse it, the one being made).
-        out = next((a.split("=", 1)[1] for a in args if a.startswith("--output-file=")), "")
         tmp_files = sum(len(fs) for _, _, fs in os.walk(os.path.join(os.path.dirname(out), "gfd-tmp"))) if out else 0
     finally:
+        stop.set()
+        rt.join(timeout=10)
         p.send_signal(signal.SIGTERM)
         try:
             rc = p.wait(timeout=30)
@@ -108,12 +133,13 @@ def soak(binary: str, args: list[str], seconds: float, hup_at: float | None = No
             rc = p.wait()
         t.join(timeout=10)
     return {"rc": rc, "rss0": rss0, "rss1": rss1, "fd0": fd0, "fd1": fd1, "prepared": max(prep0, prep1), "tmp_files": tmp_files, "cycles": c1 - c0, "reloads": reloads[0],
-            "tail": "".join(tail)}
+            "reads": reads["reads"], "bad_reads": reads["bad"][:5], "tail": "".join(tail)}
 
 
 def _assert_steady(r: dict, min_cycles: int):
-    assert r["rc"] == 0, r["tail"]
+    assert r["rc"] == 0, r["tail"]  # alive to the end (a lease break does not kill it) and clean exit
     assert r["cycles"] >= min_cycles, r
+    assert r["reads"] > 100 and not r["bad_reads"], (r["reads"], r["bad_reads"])
     assert r["fd1"] <= r["fd0"], f"file descriptors grew {r['fd0']} -> {r['fd1']}"
     assert r["prepared"] <= 2, f"{r['prepared']} temporary files open (one kept by design, one being swapped)"
     assert r["tmp_files"] <= 2, f"{r['tmp_files']} files in gfd-tmp/: old feature files are not being reused"
@@ -148,4 +174,4 @@ def test_soak_amdsmi_backend_no_growth(binary, tmp_path, session):
     _assert_steady(r, min_cycles=int(seconds * (15 if per_cycle else 200)))
     assert r["reloads"] == 1, r["tail"]
     print(f"soak[{session}]: {r['cycles']} cycles in {seconds:.0f}s, RSS {r['rss0']} -> {r['rss1']} KiB, "
-          f"fds {r['fd0']} -> {r['fd1']} (+ up to {r['prepared']} kept temporary files)")
+          f"fds {r['fd0']} -> {r['fd1']} (+ up to {r['prepared']} kept temporary files), {r['reads']} reads of the file")

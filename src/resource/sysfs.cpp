@@ -360,9 +360,8 @@ std::vector<DevicePtr> SysfsManager::enumerate() {
   }
   std::vector<DevicePtr> out(visible.size());
   trace::Span span("sysfs.gpus");
-  // Unpartitioned GPUs: ~10 attribute preads each, two GPUs per lane (see
-  // AmdSmiManager::snapshot); partitioned ones also list and read each
-  // partition node's memory banks, one GPU per lane.
+  // ~10 attribute preads per GPU (a partitioned one also its partitions'
+  // engine counts), one GPU per lane (gpu_lanes, see AmdSmiManager::snapshot).
   size_t lanes = gpu_lanes(visible.size());
   WorkerPool::instance().parallel_for(
       visible.size(),

@@ -5,7 +5,7 @@ BUILD_DIR ?= build
 JOBS ?= $(shell nproc 2>/dev/null || echo 8)
 PYTHON ?= python3
 
-.PHONY: all build cmds test test-unit test-gpu coverage asan tsan fuzz bench fmt assert-fmt vet lint check-yamls image image-offline shell clean
+.PHONY: all build cmds test test-unit test-gpu coverage asan tsan asan-e2e tsan-e2e fuzz bench fmt assert-fmt vet lint check-yamls image image-offline shell clean
 
 all: build
 
@@ -40,6 +40,27 @@ tsan:
 	cmake -S . -B build-tsan -G Ninja -DCMAKE_BUILD_TYPE=Debug -DGFD_SANITIZE=thread -DGFD_BUILD_PYTHON=OFF
 	cmake --build build-tsan -j $(JOBS)
 	TSAN_OPTIONS=halt_on_error=1 GFD_AMDSMI_LIBRARY=build-tsan/libfake_amdsmi.so ./build-tsan/gfd_unit_tests
+
+# The CPU test suite with the daemon binary and the fake amd-smi built under
+# ASan/UBSan or TSan: every end-to-end, differential, soak and deployment test
+# that runs the daemon runs the sanitized one.  Reports go to files, and any
+# report fails the target (a test that only stops the daemon would not see
+# it on stderr).  GFD_SANITIZED lifts the few timing bounds; TSan runs a
+# shorter differential (it slows every fresh process ~10x).
+SAN_LOGS ?= /tmp/gfd-san-logs
+asan-e2e: asan
+	rm -rf $(SAN_LOGS) && mkdir -p $(SAN_LOGS)
+	ASAN_OPTIONS=detect_leaks=1:log_path=$(SAN_LOGS)/asan UBSAN_OPTIONS=halt_on_error=1:print_stacktrace=1:log_path=$(SAN_LOGS)/ubsan \
+	  GFD_SANITIZED=1 GFD_BINARY=$(CURDIR)/build-asan/gpu-feature-discovery GFD_BUILD_DIR=$(CURDIR)/build-asan \
+	  $(PYTHON) -m pytest tests -q -m "not gpu" -p no:cacheprovider
+	@if ls $(SAN_LOGS)/* >/dev/null 2>&1; then cat $(SAN_LOGS)/*; exit 1; fi
+
+tsan-e2e: tsan
+	rm -rf $(SAN_LOGS) && mkdir -p $(SAN_LOGS)
+	TSAN_OPTIONS=halt_on_error=1:log_path=$(SAN_LOGS)/tsan GFD_DIFF_SEQUENCES=40 \
+	  GFD_SANITIZED=1 GFD_BINARY=$(CURDIR)/build-tsan/gpu-feature-discovery GFD_BUILD_DIR=$(CURDIR)/build-tsan \
+	  $(PYTHON) -m pytest tests -q -m "not gpu" -p no:cacheprovider
+	@if ls $(SAN_LOGS)/* >/dev/null 2>&1; then cat $(SAN_LOGS)/*; exit 1; fi
 
 # libFuzzer + ASan/UBSan over the config reader, the PCI capability walkers
 # and the value parsers (tests/fuzz/); FUZZ_SECONDS per target, new inputs

@@ -9,6 +9,7 @@ gloo backend and world_size 2 on 127.0.0.1.
 from __future__ import annotations
 
 import json
+import os
 import socket
 import subprocess
 import sys
@@ -55,7 +56,9 @@ def test_single_process_contract():
     # Attribution and per-cycle records (round 4): the unattributed time, the
     # CPUs of every cycle, and one row per cycle whose phases add up.
     c = r["cold_cycle"]
-    assert c["other_p50_ms"] is not None and c["other_p50_ms"] < 0.05
+    assert c["other_p50_ms"] is not None
+    if not os.environ.get("GFD_SANITIZED"):  # a sanitized daemon is several times slower
+        assert c["other_p50_ms"] < 0.05
     assert len(c["cycle_cpus"]) == len(c["totals_ms"]) == len(c["rows_ms"]) == 2
     for row in c["rows_ms"]:
         top = sum(row.get(k, 0) for k in ("submit", "init", "enumerate", "label", "sriov.join", "merge", "log", "write",

@@ -57,9 +57,12 @@ def test_single_process_contract():
     # CPUs of every cycle, and one row per cycle whose phases add up.
     c = r["cold_cycle"]
     assert c["other_p50_ms"] is not None
-    if not os.environ.get("GFD_SANITIZED"):  # a sanitized daemon is several times slower
-        assert c["other_p50_ms"] < 0.05
     assert len(c["cycle_cpus"]) == len(c["totals_ms"]) == len(c["rows_ms"]) == 2
+    # A span missing from the cycle shows in both cycles; one preempted
+    # between spans (this is a shared VM) in one.  A sanitized daemon is
+    # several times slower everywhere.
+    if not os.environ.get("GFD_SANITIZED"):
+        assert min(row["other"] for row in c["rows_ms"]) < 0.05, c["rows_ms"]
     for row in c["rows_ms"]:
         top = sum(row.get(k, 0) for k in ("submit", "init", "enumerate", "label", "sriov.join", "merge", "log", "write",
                                            "other"))

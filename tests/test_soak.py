@@ -13,9 +13,11 @@ opens cause.
 
 from __future__ import annotations
 
+import json
 import os
 import signal
 import subprocess
+import sys
 import threading
 import time
 
@@ -33,48 +35,56 @@ def _rss_kib(pid: int) -> int:
     return 0
 
 
-def _fds(pid: int) -> tuple[int, int]:
+def _fds(pid: int, out: str) -> tuple[int, int]:
     # Minimum over a short window: a cycle in flight holds transient
     # descriptors (the temp output file, an amd-smi device node), a leak
     # raises the floor.  The window must catch the daemon between cycles at
-    # least once (see the per-cycle interval below).  Files open in
-    # gfd-tmp/ (the old feature file kept for the next write, by design:
-    # src/lm/writer.cpp Slot) are counted apart: whether one is there at a
-    # sample depends on timing (a write swapping names), not on leaks.
+    # least once (see the per-cycle interval below).  The feature file and
+    # the one the last write swapped out to gfd-tmp/, both kept open by
+    # design (src/lm/writer.cpp Slot), are counted apart: a write swaps their
+    # names, so which name a readlink sees depends on timing, not on leaks.
     # Returns (floor without them, most of them).
     # A descriptor closed between the listing and its readlink still counts:
     # skipping it let a sample taken while a re-read swaps descriptors (new
     # ones opened after the listing, old ones closed before the readlink)
     # dip below the floor.
-    n, prepared = [], []
+    n, kept = [], []
     for _ in range(40):
         fds = os.listdir(f"/proc/{pid}/fd")
         k = 0
         for fd in fds:
             try:
-                k += "/gfd-tmp/" in os.readlink(f"/proc/{pid}/fd/{fd}")
+                link = os.readlink(f"/proc/{pid}/fd/{fd}")
             except OSError:  # closed between listdir and readlink
-                pass
+                continue
+            k += "/gfd-tmp/" in link or (bool(out) and link.split(" (deleted)")[0] == out)
         n.append(len(fds) - k)
-        prepared.append(k)
+        kept.append(k)
         time.sleep(0.01)
-    return min(n), max(prepared)
+    return min(n), max(kept)
 
 
-def _read_feature_file(out: str, stop: threading.Event, stats: dict) -> None:
-    # NFD's side, far more often than NFD: open, read, close - and every read
-    # is a whole label set.  Each open can race the daemon's exchange and
-    # break its write lease on the swapped-out file (src/lm/writer.cpp).
-    while not stop.is_set():
+# NFD's side of the file, far more often than NFD: open, read, close - and
+# every read must be a whole label set.  Each open can race the daemon's
+# exchange and break its write lease on the swapped-out file
+# (src/lm/writer.cpp).  A process of its own: a reader thread here would
+# hold the GIL against the descriptor sampling above and skew its floor.
+# Stops when its stdin closes; prints its counts.
+_READER = r"""
+import json, select, sys
+out, reads, bad = sys.argv[1], 0, []
+while not select.select([sys.stdin], [], [], 0)[0]:
+    for _ in range(100):
         try:
             with open(out, "rb") as f:
                 data = f.read()
         except FileNotFoundError:
-            time.sleep(0.001)
             continue
-        stats["reads"] += 1
+        reads += 1
         if not data.endswith(b"\n") or b"amd.com/gpu.count=" not in data:
-            stats["bad"].append(data[-80:])
+            bad.append(data[-80:].decode(errors="replace"))
+print(json.dumps({"reads": reads, "bad": bad[:5]}))
+"""
 
 
 def soak(binary: str, args: list[str], seconds: float, hup_at: float | None = None, interval: str = "1ms") -> dict:
@@ -96,16 +106,14 @@ def soak(binary: str, args: list[str], seconds: float, hup_at: float | None = No
     t = threading.Thread(target=reader, daemon=True)
     t.start()
     out = next((a.split("=", 1)[1] for a in args if a.startswith("--output-file=")), "")
-    stop = threading.Event()
-    reads = {"reads": 0, "bad": []}
-    rt = threading.Thread(target=_read_feature_file, args=(out, stop, reads), daemon=True)
-    rt.start()
+    rd = subprocess.Popen([sys.executable, "-c", _READER, out], stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+    reads = {"reads": 0, "bad": ["reader did not report"]}
     try:
         deadline = time.monotonic() + 60
         while cycles[0] < 200 and time.monotonic() < deadline and p.poll() is None:
             time.sleep(0.05)
         assert p.poll() is None, "".join(tail)
-        rss0, (fd0, prep0), c0 = _rss_kib(p.pid), _fds(p.pid), cycles[0]
+        rss0, (fd0, prep0), c0 = _rss_kib(p.pid), _fds(p.pid, os.path.abspath(out) if out else ""), cycles[0]
         t0 = time.monotonic()
         hupped = False
         last_note = t0
@@ -118,13 +126,16 @@ def soak(binary: str, args: list[str], seconds: float, hup_at: float | None = No
                 print(f"soak: {cycles[0] - c0} cycles, RSS {_rss_kib(p.pid)} KiB", flush=True)
             time.sleep(0.05)
         assert p.poll() is None, "".join(tail)
-        rss1, (fd1, prep1), c1 = _rss_kib(p.pid), _fds(p.pid), cycles[0]
+        rss1, (fd1, prep1), c1 = _rss_kib(p.pid), _fds(p.pid, os.path.abspath(out) if out else ""), cycles[0]
         # Files in gfd-tmp/: the old feature file kept for the next write
         # (and, in a write that could not reuse it, the one being made).
         tmp_files = sum(len(fs) for _, _, fs in os.walk(os.path.join(os.path.dirname(out), "gfd-tmp"))) if out else 0
     finally:
-        stop.set()
-        rt.join(timeout=10)
+        try:
+            reads = json.loads(rd.communicate(input="", timeout=30)[0])  # closes its stdin
+        except (subprocess.TimeoutExpired, ValueError):
+            rd.kill()
+            rd.wait()
         p.send_signal(signal.SIGTERM)
         try:
             rc = p.wait(timeout=30)
@@ -141,7 +152,7 @@ def _assert_steady(r: dict, min_cycles: int):
     assert r["cycles"] >= min_cycles, r
     assert r["reads"] > 100 and not r["bad_reads"], (r["reads"], r["bad_reads"])
     assert r["fd1"] <= r["fd0"], f"file descriptors grew {r['fd0']} -> {r['fd1']}"
-    assert r["prepared"] <= 2, f"{r['prepared']} temporary files open (one kept by design, one being swapped)"
+    assert r["prepared"] <= 3, f"{r['prepared']} feature files open (two kept by design, one being made)"
     assert r["tmp_files"] <= 2, f"{r['tmp_files']} files in gfd-tmp/: old feature files are not being reused"
     # Allocator noise only: a leak of even 100 bytes/cycle over thousands of
     # cycles would exceed this.  (Under ASan freed memory sits in its
@@ -175,4 +186,4 @@ def test_soak_amdsmi_backend_no_growth(binary, tmp_path, session):
     _assert_steady(r, min_cycles=int(seconds * (15 if per_cycle else 200)))
     assert r["reloads"] == 1, r["tail"]
     print(f"soak[{session}]: {r['cycles']} cycles in {seconds:.0f}s, RSS {r['rss0']} -> {r['rss1']} KiB, "
-          f"fds {r['fd0']} -> {r['fd1']} (+ up to {r['prepared']} kept temporary files), {r['reads']} reads of the file")
+          f"fds {r['fd0']} -> {r['fd1']} (+ up to {r['prepared']} feature files), {r['reads']} reads of the file")

@@ -113,7 +113,7 @@ def soak(binary: str, args: list[str], seconds: float, hup_at: float | None = No
         while cycles[0] < 200 and time.monotonic() < deadline and p.poll() is None:
             time.sleep(0.05)
         assert p.poll() is None, "".join(tail)
-        rss0, (fd0, prep0), c0 = _rss_kib(p.pid), _fds(p.pid, os.path.abspath(out) if out else ""), cycles[0]
+        rss0, (fd0, kept0), c0 = _rss_kib(p.pid), _fds(p.pid, os.path.abspath(out) if out else ""), cycles[0]
         t0 = time.monotonic()
         hupped = False
         last_note = t0
@@ -126,7 +126,7 @@ def soak(binary: str, args: list[str], seconds: float, hup_at: float | None = No
                 print(f"soak: {cycles[0] - c0} cycles, RSS {_rss_kib(p.pid)} KiB", flush=True)
             time.sleep(0.05)
         assert p.poll() is None, "".join(tail)
-        rss1, (fd1, prep1), c1 = _rss_kib(p.pid), _fds(p.pid, os.path.abspath(out) if out else ""), cycles[0]
+        rss1, (fd1, kept1), c1 = _rss_kib(p.pid), _fds(p.pid, os.path.abspath(out) if out else ""), cycles[0]
         # Files in gfd-tmp/: the old feature file kept for the next write
         # (and, in a write that could not reuse it, the one being made).
         tmp_files = sum(len(fs) for _, _, fs in os.walk(os.path.join(os.path.dirname(out), "gfd-tmp"))) if out else 0
@@ -143,7 +143,7 @@ def soak(binary: str, args: list[str], seconds: float, hup_at: float | None = No
             p.kill()
             rc = p.wait()
         t.join(timeout=10)
-    return {"rc": rc, "rss0": rss0, "rss1": rss1, "fd0": fd0, "fd1": fd1, "prepared": max(prep0, prep1), "tmp_files": tmp_files, "cycles": c1 - c0, "reloads": reloads[0],
+    return {"rc": rc, "rss0": rss0, "rss1": rss1, "fd0": fd0, "fd1": fd1, "kept": max(kept0, kept1), "tmp_files": tmp_files, "cycles": c1 - c0, "reloads": reloads[0],
             "reads": reads["reads"], "bad_reads": reads["bad"][:5], "tail": "".join(tail)}
 
 
@@ -152,7 +152,7 @@ def _assert_steady(r: dict, min_cycles: int):
     assert r["cycles"] >= min_cycles, r
     assert r["reads"] > 100 and not r["bad_reads"], (r["reads"], r["bad_reads"])
     assert r["fd1"] <= r["fd0"], f"file descriptors grew {r['fd0']} -> {r['fd1']}"
-    assert r["prepared"] <= 3, f"{r['prepared']} feature files open (two kept by design, one being made)"
+    assert r["kept"] <= 3, f"{r['kept']} feature files open (two kept by design, one being made)"
     assert r["tmp_files"] <= 2, f"{r['tmp_files']} files in gfd-tmp/: old feature files are not being reused"
     # Allocator noise only: a leak of even 100 bytes/cycle over thousands of
     # cycles would exceed this.  (Under ASan freed memory sits in its
@@ -186,4 +186,4 @@ def test_soak_amdsmi_backend_no_growth(binary, tmp_path, session):
     _assert_steady(r, min_cycles=int(seconds * (15 if per_cycle else 200)))
     assert r["reloads"] == 1, r["tail"]
     print(f"soak[{session}]: {r['cycles']} cycles in {seconds:.0f}s, RSS {r['rss0']} -> {r['rss1']} KiB, "
-          f"fds {r['fd0']} -> {r['fd1']} (+ up to {r['prepared']} feature files), {r['reads']} reads of the file")
+          f"fds {r['fd0']} -> {r['fd1']} (+ up to {r['kept']} feature files), {r['reads']} reads of the file")

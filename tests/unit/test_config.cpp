@@ -247,6 +247,53 @@ TEST(Config_JsonDumpRoundTrips) {
   EXPECT_EQ(*back.flags.gfd.sleep_interval, 90 * kSecond);
 }
 
+TEST(Config_JsonDumpOfResourcesAndSharingRoundTrips) {
+  // The start-up "Running with config" dump (the reference marshals its
+  // whole Config) must load back as the same resources and sharing.
+  Config c = parse_config_text(R"(
+resources:
+  gpus:
+  - pattern: '*MI355*'
+    name: mi355
+  mig:
+  - pattern: 'cpx.*'
+    name: cpx
+sharing:
+  timeSlicing:
+    failRequestsGreaterThanOne: true
+    resources:
+    - name: gpu
+      replicas: 4
+    - name: amd.com/partition-cpx.1xcd.36gb
+      devices: 3
+      replicas: 2
+      rename: cpx-shared
+    - name: mi355
+      devices: [0, "1:3"]
+      replicas: 8
+)");
+  Config back = parse_config_text(to_json(c));
+  EXPECT_EQ(back.resources.gpus.size(), static_cast<size_t>(1));
+  EXPECT_EQ(back.resources.gpus[0].pattern, std::string("*MI355*"));
+  EXPECT_EQ(back.resources.gpus[0].name, std::string("amd.com/mi355"));
+  EXPECT_EQ(back.resources.partitions.size(), static_cast<size_t>(1));
+  EXPECT_EQ(back.resources.partitions[0].name, std::string("amd.com/cpx"));
+  const auto& t = back.sharing.time_slicing;
+  EXPECT_TRUE(t.fail_requests_greater_than_one);
+  EXPECT_FALSE(t.rename_by_default);
+  EXPECT_EQ(t.resources.size(), static_cast<size_t>(3));
+  EXPECT_TRUE(t.resources[0].devices.all);
+  EXPECT_EQ(t.resources[0].replicas, 4);
+  EXPECT_EQ(t.resources[1].devices.count, 3);
+  EXPECT_EQ(t.resources[1].rename, std::string("amd.com/cpx-shared"));
+  EXPECT_EQ(t.resources[2].devices.list, (std::vector<std::string>{"0", "1:3"}));
+  EXPECT_EQ(t.resources[2].replicas, 8);
+  // renameByDefault survives too.
+  Config d = parse_config_text("sharing:\n  timeSlicing:\n    renameByDefault: true\n    resources:\n"
+                               "    - name: gpu\n      replicas: 2\n");
+  EXPECT_TRUE(parse_config_text(to_json(d)).sharing.time_slicing.rename_by_default);
+}
+
 TEST(Duration_ParseGoGrammar) {
   EXPECT_EQ(parse_duration("60s"), 60 * kSecond);
   EXPECT_EQ(parse_duration("1m30s"), 90 * kSecond);

@@ -129,13 +129,8 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
   r.cpu_start = sched_getcpu();
   {
     // --cpu-affinity=follow, loop mode only: a oneshot Job has one cycle.
-    // Then the workers the last cycle's per-GPU lanes used are woken, so that
-    // their wake-up overlaps this cycle's first steps (WorkerPool::prewake).
     trace::Span span("placement");
-    if (!config.oneshot()) {
-      WorkerPool::instance().follow_caller();
-      WorkerPool::instance().prewake();
-    }
+    if (!config.oneshot()) WorkerPool::instance().follow_caller();
   }
   // Work that does not depend on the device backend runs on workers while
   // the backend enumerates: the node facts the device labeler needs after

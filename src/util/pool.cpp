@@ -4,13 +4,9 @@
 #include <sched.h>
 
 #include <algorithm>
-#include <array>
 #include <atomic>
-#include <cstdlib>
-#include <string>
 
 #include "util/affinity.h"
-#include "util/trace.h"
 
 namespace gfd {
 
@@ -54,7 +50,7 @@ void WorkerPool::ensure_workers(size_t n) {
   // Caller holds mu_.  `n` tasks are queued: make sure that many workers are
   // parked, being woken or starting (busy workers may be blocked in a nested
   // parallel_for).
-  while (idle_.size() + waking_ + spinning_ + spawning_ < n && threads_.size() < max_workers_) {
+  while (idle_.size() + waking_ + spawning_ < n && threads_.size() < max_workers_) {
     ++spawning_;
     workers_.push_back(std::make_unique<Worker>());
     Worker* w = workers_.back().get();
@@ -117,9 +113,7 @@ void WorkerPool::wake_one() {
   // condition variable would rotate every task over all workers (measured:
   // the per-cycle PCI scan took 180 us instead of 86 us once 8 workers
   // existed and took turns).
-  // Workers already on their way (woken, or prewoken and spinning) each
-  // take one queued item before they park again.
-  if (idle_.empty() || waking_ + spinning_ >= queue_.size()) return;
+  if (idle_.empty()) return;
   Worker* w = idle_.back();
   idle_.pop_back();
   w->woken = true;
@@ -137,77 +131,20 @@ void WorkerPool::loop(Worker* w) {
       w->woken = false;
       idle_.push_back(w);
       w->cv.wait(lk, [&] { return w->woken || stop_; });
-      if (!w->woken) {
+      if (w->woken) {
+        --waking_;
+      } else {
         idle_.erase(std::find(idle_.begin(), idle_.end(), w));  // stopping
-        continue;
       }
-      --waking_;
-      if (w->spin && queue_.empty() && !stop_) {
-        // Prewoken: the cycle's lanes come within microseconds; wait for
-        // them here, on a running core, and park again if none came.  The
-        // first one woken wakes the others (their futex wakes off the
-        // cycle thread).
-        w->spin = false;
-        std::array<Worker*, 16> fan{};
-        size_t nfan = 0;
-        for (; nfan < w->fanout && nfan < fan.size() && !idle_.empty(); ++nfan) {
-          Worker* x = idle_.back();
-          idle_.pop_back();
-          x->woken = true;
-          x->spin = true;
-          ++waking_;
-          fan[nfan] = x;
-        }
-        w->fanout = 0;
-        ++spinning_;
-        lk.unlock();
-        for (size_t i = 0; i < nfan; ++i) fan[i]->cv.notify_one();
-        int64_t until = trace::now_ns() + kSpinNs;
-        while (queued_.load(std::memory_order_acquire) == 0 && trace::now_ns() < until) __builtin_ia32_pause();
-        lk.lock();
-        --spinning_;
-      }
-      w->spin = false;
     }
     if (queue_.empty()) return;  // stop_ and nothing left to run
     std::function<void()> fn = std::move(queue_.front());
     queue_.pop_front();
-    queued_.store(queue_.size(), std::memory_order_release);
     lk.unlock();
     fn();
     fn = nullptr;  // release captures outside the lock
     lk.lock();
   }
-}
-
-void WorkerPool::prewake() {
-  static const std::string mode = [] {
-    const char* e = std::getenv("GFD_EXP_PREWAKE");  // EXPERIMENT: off | direct | fan (default)
-    return std::string(e ? e : "fan");
-  }();
-  size_t n = peak_helpers_.exchange(0, std::memory_order_relaxed);
-  if (mode == "off" || n == 0) return;
-  ++n;  // and one for the cycle's own submit (node facts, SR-IOV)
-  std::lock_guard<std::mutex> g(mu_);
-  if (mode == "direct") {
-    for (size_t i = 0; i < n && !idle_.empty(); ++i) {
-      Worker* w = idle_.back();
-      idle_.pop_back();
-      w->woken = true;
-      w->spin = true;
-      ++waking_;
-      w->cv.notify_one();
-    }
-    return;
-  }
-  if (idle_.empty()) return;
-  Worker* w = idle_.back();
-  idle_.pop_back();
-  w->woken = true;
-  w->spin = true;
-  w->fanout = n - 1;
-  ++waking_;
-  w->cv.notify_one();
 }
 
 void WorkerPool::Task::State::run() {
@@ -234,7 +171,6 @@ WorkerPool::Task WorkerPool::submit(std::function<void()> fn) {
     queue_.emplace_back([st] {
       if (!st->claimed.exchange(true)) st->run();  // else the submitter ran it
     });
-    queued_.store(queue_.size(), std::memory_order_release);
     ensure_workers(queue_.size());
     wake_one();
   }
@@ -255,7 +191,6 @@ std::vector<WorkerPool::Task> WorkerPool::submit_sequence(std::vector<std::funct
       for (const auto& st : states)
         if (!st->claimed.exchange(true)) st->run();
     });
-    queued_.store(queue_.size(), std::memory_order_release);
     ensure_workers(queue_.size());
     wake_one();
   }
@@ -337,12 +272,8 @@ void WorkerPool::parallel_for(size_t n, const std::function<void(size_t)>& fn, s
   {
     std::lock_guard<std::mutex> g(mu_);
     for (size_t l = 1; l < lanes; ++l) queue_.emplace_back(body);
-    queued_.store(queue_.size(), std::memory_order_release);
     ensure_workers(queue_.size());
     for (size_t l = 1; l < lanes; ++l) wake_one();
-  }
-  size_t peak = peak_helpers_.load(std::memory_order_relaxed);
-  while (lanes - 1 > peak && !peak_helpers_.compare_exchange_weak(peak, lanes - 1, std::memory_order_relaxed)) {
   }
   body();
   std::exception_ptr error;

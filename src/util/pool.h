@@ -14,7 +14,6 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstddef>
-#include <cstdint>
 #include <deque>
 #include <exception>
 #include <functional>
@@ -80,16 +79,6 @@ class WorkerPool {
   // free, because the caller runs every item nobody else has claimed.
   void parallel_for(size_t n, const std::function<void(size_t)>& fn, size_t max_parallel = 0);
 
-  // Called by the thread that is about to run a cycle: wakes as many parked
-  // workers as the previous cycle's parallel_for calls had helper lanes,
-  // each of which then waits for work spinning (at most kSpinNs) instead of
-  // parked.  The wake-up of a parked worker - tens of microseconds on a core
-  // idle since the last cycle - then overlaps the cycle's first steps
-  // instead of delaying its per-GPU lanes.  A pool whose parallel_for never
-  // had helpers (one GPU) wakes nobody.
-  void prewake();
-  static constexpr int64_t kSpinNs = 100000;
-
   size_t workers() const;
   // Workers parked right now (a lane given to one of them needs no thread
   // to be created: in a fresh process that costs more than short work).
@@ -115,8 +104,6 @@ class WorkerPool {
   struct Worker {
     std::condition_variable cv;
     bool woken = false;  // set by wake_one (guarded by mu_)
-    bool spin = false;   // woken by prewake: wait for work spinning first
-    size_t fanout = 0;   // prewake: parked workers this one wakes in turn
   };
   void ensure_workers(size_t n);
   void unpin_locked();  // caller holds mu_
@@ -130,10 +117,7 @@ class WorkerPool {
   std::vector<std::thread> threads_;
   std::vector<Worker*> idle_;  // parked workers, most recently parked last
   size_t waking_ = 0;          // woken, not yet running
-  size_t spinning_ = 0;        // prewoken, polling queued_ for work
   size_t spawning_ = 0;        // threads created but not yet parked
-  std::atomic<size_t> queued_{0};       // queue_.size(), for spinning workers
-  std::atomic<size_t> peak_helpers_{0};  // most helper lanes of one parallel_for since prewake
   bool stop_ = false;
   std::atomic<bool> follow_{false};
   const affinity::L3Map* l3_ = nullptr;  // set with follow_

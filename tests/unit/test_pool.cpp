@@ -1,7 +1,5 @@
 // WorkerPool tests (run under TSan by `make tsan`).
 #include <atomic>
-#include <chrono>
-#include <thread>
 #include <stdexcept>
 
 #include <sched.h>
@@ -130,37 +128,6 @@ TEST(Pool_CancelOrWaitDropsUnstartedTask) {
   done.wait();
   done.cancel_or_wait();
   EXPECT_EQ(ran.load(), 1);
-}
-
-TEST(Pool_PrewakeWakesTheLastCyclesLanesWhichParkAgainUnused) {
-  WorkerPool pool(4);
-  auto all_parked = [&] {
-    for (int i = 0; i < 2000 && pool.idle_workers() != pool.workers(); ++i)
-      std::this_thread::sleep_for(std::chrono::milliseconds(1));
-    return pool.idle_workers() == pool.workers();
-  };
-  pool.prewake();  // no parallel_for yet: nobody to wake
-  EXPECT_EQ(pool.workers(), static_cast<size_t>(0));
-  std::atomic<int> sum{0};
-  pool.parallel_for(4, [&](size_t i) { sum += static_cast<int>(i); }, 4);
-  EXPECT_EQ(sum.load(), 6);
-  EXPECT_TRUE(all_parked());
-  size_t workers = pool.workers();
-  EXPECT_TRUE(workers >= 1 && workers <= 4);
-  for (int cycle = 0; cycle < 200; ++cycle) {
-    // A cycle: wake the last cycle's lanes, hand out a task and the lanes.
-    pool.prewake();
-    auto t = pool.submit([&] { sum += 1; });
-    pool.parallel_for(4, [&](size_t i) { sum += static_cast<int>(i); }, 4);
-    t.run_or_wait();
-  }
-  EXPECT_EQ(sum.load(), 6 + 200 * 7);
-  EXPECT_TRUE(pool.workers() <= 4);
-  // Prewoken workers that get no work park again after the spin window.
-  pool.prewake();
-  EXPECT_TRUE(all_parked());
-  pool.prewake();  // the window consumed the record: nothing to wake now
-  EXPECT_TRUE(pool.idle_workers() == pool.workers());
 }
 
 TEST(Pool_GpuLanesPolicy) {

@@ -2,7 +2,8 @@
 # A/B of WorkerPool::prewake (GFD_EXP_PREWAKE=off disables it) on the amd-smi
 # backend over the host's real GPUs (tools/hybrid_amdsmi_spec.py), alternated:
 # back to back (bench.py, 2000 steps) and cycles 1 s apart (cold_cycle.py),
-# at 1, 2 and 8 GPUs.  Usage (GPU box): tools/prewake_ab.sh [outdir] [reps]
+# at 2 and 8 GPUs.  Needs the experiment build of commit bca62c4 (prewake was
+# not kept: docs/ROUND5.md).  Usage (GPU box): tools/prewake_ab.sh [outdir] [reps]
 set -o pipefail
 out=gpurun_out/${1:-prewake_ab}; reps=${2:-3}
 mkdir -p $out

@@ -11,6 +11,7 @@
 #include "resource/managers.h"
 #include "sriov/sriov.h"
 #include "test.h"
+#include "util/dynlib.h"
 #include "util/fs.h"
 #include "util/log.h"
 #include "util/trace.h"
@@ -374,6 +375,33 @@ TEST(LogHold_WritesTheCycleLinesTogetherInOrder) {
   auto a = after.find("Writing labels to output file"), b = after.find("Sleeping for 60s");
   EXPECT_TRUE(a != std::string::npos && b != std::string::npos && a < b);
   EXPECT_TRUE(nested.find("inner") != std::string::npos);
+}
+
+TEST(Log_LinesLongerThanTheBufferAreWrittenWhole) {
+  // The config dump and a backend disagreement's two device lists can run
+  // past the 4 KiB stack buffer.
+  bool was = log::set_quiet(false);
+  std::string big(10000, 'x'), out;
+  {
+    StderrCapture cap;
+    log::printf("Running with config: %s|end", big.c_str());
+    out = cap.peek();
+  }
+  log::set_quiet(was);
+  EXPECT_TRUE(out.find("Running with config: " + big + "|end\n") != std::string::npos);
+}
+
+TEST(DynLib_ReportsWhyNoCandidateLoaded) {
+  DynLib lib;
+  EXPECT_FALSE(lib.open({"/nonexistent/libnothing.so", "libgfd-no-such-library.so.9"}));
+  EXPECT_TRUE(lib.last_error().find("libgfd-no-such-library.so.9") != std::string::npos);
+  EXPECT_TRUE(lib.symbol("anything") == nullptr);
+  EXPECT_TRUE(lib.open({"libc.so.6"}));
+  EXPECT_EQ(lib.path(), std::string("libc.so.6"));
+  int (*getpid_fn)() = nullptr;
+  EXPECT_TRUE(lib.bind("getpid", getpid_fn) && getpid_fn() == ::getpid());
+  lib.close();
+  EXPECT_TRUE(lib.symbol("getpid") == nullptr);
 }
 
 TEST(LogHold_WritesWarningsAtOnceWithWhatCameBefore) {

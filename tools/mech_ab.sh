@@ -7,7 +7,10 @@
 #   none   - --cpu-affinity=none (no placement at all)
 #   l3     - --cpu-affinity=l3 (daemon only: the whole process on one L3)
 #   plain  - every loop write creates a new temporary file and renames it
-#            over the feature file (the reference's write; experiment switch)
+#            over the feature file (the reference's write), through an
+#            experiment switch (GFD_EXP_WRITER) of the tree the A/B ran on,
+#            removed before it was committed: on later trees this variant
+#            runs the default writer.  Its numbers: profiles/mechanisms_ab_r5.txt.
 set -o pipefail
 out=gpurun_out/${1:-mech_ab}
 mkdir -p "$out"

@@ -471,6 +471,33 @@ def test_devices_match_amd_smi_cli(amdsmi_devices, sysfs_devices):
                 assert d["compute_units"] == s["asic"]["num_compute_units"]
 
 
+@pytest.mark.skipif(not os.path.exists(AMD_SMI_CLI), reason="amd-smi CLI not installed")
+def test_version_labels_match_amd_smi_cli(binary, tmp_path):
+    """The version labels against AMD's tool: amd.com/driver.* is the amdgpu
+    version `amd-smi static --driver` reports and amd.com/rocm.runtime.* the
+    ROCm version `amd-smi version` reports, for both backends."""
+    import re
+
+    data = _amd_smi_json("static", "--driver")
+    gpus = data["gpu_data"] if isinstance(data, dict) else data
+    drivers = {str(g["driver"]["version"]) for g in gpus if isinstance(g.get("driver"), dict)}
+    ver = _amd_smi_json("version")
+    ver = ver[0] if isinstance(ver, list) else ver
+    rocm = str(ver.get("rocm_version", ""))
+    print("amd-smi: driver", drivers, "rocm", rocm)
+    assert len(drivers) == 1, drivers
+    want_driver = [int(x) for x in re.findall(r"\d+", drivers.pop())[:3]]
+    want_rocm = [int(x) for x in re.findall(r"\d+", rocm)[:2]]
+    for backend in ("amdsmi", "sysfs"):
+        out = tmp_path / f"gfd-{backend}"
+        run_daemon(binary, "--oneshot", f"--backend={backend}", f"--output-file={out}", check=True, timeout=120)
+        labels = golden.parse_labels(out.read_text())
+        got = [int(labels[f"amd.com/driver.{k}"]) for k in ("major", "minor", "rev") if f"amd.com/driver.{k}" in labels]
+        assert len(got) >= 2 and got == want_driver[:len(got)], (backend, got, want_driver)
+        if len(want_rocm) == 2:  # this amd-smi reports the ROCm release
+            assert [int(labels["amd.com/rocm.runtime.major"]), int(labels["amd.com/rocm.runtime.minor"])] == want_rocm
+
+
 def test_devices_match_the_hip_runtime(amdsmi_devices, sysfs_devices):
     """A third oracle, independent of amd-smi: the HIP runtime, as PyTorch-ROCm
     reports each visible GPU (its own path through the KFD thunk), in a

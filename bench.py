@@ -359,6 +359,8 @@ def main() -> int:
                 "strategy": "none",
             },
             "p90_ms": round(_percentile(ms, 0.9), 4),
+            "p99_ms": round(_percentile(ms, 0.99), 4),
+            "max_ms": round(max(ms), 4) if ms else None,
             "mean_ms": round(statistics.fmean(ms), 4) if ms else None,
             # Per-phase p50 over the K timed steps: what an N-GPU cycle
             # spends where (the scaling curve's explanation).

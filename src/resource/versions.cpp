@@ -34,8 +34,10 @@ std::optional<std::string> extract_version(const std::string& s) {
 }
 
 namespace {
-// amdgpu built into the kernel (the MI355X pool): /sys/module/amdgpu exists
-// but has no `initstate` (only loadable modules have one) and no `version`.
+// amdgpu built into the kernel: /sys/module/amdgpu exists but has no
+// `initstate` (only loadable modules have one) and no `version`.  (The
+// MI355X pool's amdgpu is loadable, without a `version`:
+// profiles/amdgpu_module_layout.txt.)
 // Whether the kernel's amdgpu is built in or loadable is fixed until the
 // next boot (a DKMS module cannot replace a built-in driver, and a kernel
 // with a loadable amdgpu never grows a built-in one), so it is decided once

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """The fake libamd_smi's node spec (tests/fake_amdsmi, GFD_FAKE_AMDSMI_SPEC:
-'|' between lines) for the host's real MI355X: one SPX/NPS1 GPU per AMD
-accelerator-class function with amdgpu's VRAM attribute, at its real PCI
-address, so the amd-smi backend reads each one's live amdgpu attributes.
+'|' between lines) for the host's real MI355X: one GPU per AMD
+accelerator-class function in SPX/NPS1 with amdgpu's VRAM attribute, at its
+real PCI address, so the amd-smi backend reads each one's live amdgpu attributes.
 
     python tools/hybrid_amdsmi_spec.py [LATENCY_US]
 """
@@ -25,6 +25,13 @@ def main() -> int:
         except (OSError, ValueError):
             continue
         if vendor != "0x1002" or not cls.startswith("0x12"):
+            continue
+        try:  # SPX/NPS1 only: that is how the spec line below describes the GPU
+            modes = (open(f"{pci}/{d}/current_compute_partition").read().strip(),
+                     open(f"{pci}/{d}/current_memory_partition").read().strip())
+        except OSError:
+            modes = ("SPX", "NPS1")
+        if modes != ("SPX", "NPS1"):
             continue
         n += 1
         lines.append(f"bdf={d};mode=SPX;nps=NPS1;parts=1;name=AMD Instinct MI355X;cus=256;xcds=8;"

@@ -254,6 +254,27 @@ void fix_market_name(AmdSmiLib& L, const std::string& root, ProcInfo& p) {
   if (p.market_name.empty() && p.device_id) p.market_name = device_name(p.device_id);
 }
 
+// The GPU's compute partition mode for the session: `mode` (the session
+// cache entry) when known, else read from the parent function's
+// current_compute_partition - once per session, not per cycle.  amdgpu
+// answers that attribute by reading the XCP control register, which "may
+// momentarily wake the GPU up" (AMD's own CLI stopped reading it by
+// default: /opt/rocm/libexec/amdsmi_cli/amdsmi_commands.py:463-466).  The
+// mode only changes with a partition switch, which rebuilds the KFD
+// topology and bumps its generation, and a new generation re-initialises the
+// session, which clears the cache (AmdSmiManager::compute_mode_).  False
+// when the attribute is missing or unknown.  `read_ns`: the read's time, if
+// it happened (reported by the cycle thread as "compute_partition(read)").
+bool session_compute_mode(const std::string& pci, std::string* mode, int64_t* read_ns) {
+  if (!mode->empty()) return true;
+  int64_t t0 = trace::now_ns();
+  auto cp = fs::attrs().read_trimmed(pci + "/current_compute_partition");
+  *read_ns += trace::now_ns() - t0;
+  if (!cp) return false;
+  *mode = partition_mode(*cp);
+  return !mode->empty();
+}
+
 // The only processor at its PCI address and in SPX mode: its per-cycle
 // values are the amdgpu attributes amd-smi reads for the same calls
 // (mem_info_vram_total for memory_total(VRAM), current_compute_partition /
@@ -261,11 +282,11 @@ void fix_market_name(AmdSmiLib& L, const std::string& root, ProcInfo& p) {
 // ~4 us each.  `node_id` is the session-cached KFD node (kNoNode = not yet
 // known: queried and returned through it).  Returns false when the GPU is
 // partitioned or an attribute is missing; the caller then queries amd-smi.
-bool query_unpartitioned(AmdSmiLib& L, const std::string& root, ProcInfo& p, AmdSmiManager::KfdNodeFacts* kfd) {
+bool query_unpartitioned(AmdSmiLib& L, const std::string& root, ProcInfo& p, AmdSmiManager::KfdNodeFacts* kfd,
+                         std::string* mode, int64_t* read_ns) {
   uint32_t* node_id = &kfd->node_id;
   std::string pci = fs::join(root, "sys/bus/pci/devices/" + p.gpu_bdf);
-  auto cp = AMDSMI_CALL("compute_partition(sysfs)", fs::attrs().read_trimmed(pci + "/current_compute_partition"));
-  if (!cp || partition_mode(*cp) != "SPX") return false;
+  if (!session_compute_mode(pci, mode, read_ns) || *mode != "SPX") return false;
   auto mp = AMDSMI_CALL("memory_partition(sysfs)", fs::attrs().read_trimmed(pci + "/current_memory_partition"));
   if (!mp || partition_mode(*mp).empty()) return false;
   auto vram_s = AMDSMI_CALL("memory_total(sysfs)", fs::attrs().read_trimmed(pci + "/mem_info_vram_total"));
@@ -295,11 +316,10 @@ bool query_unpartitioned(AmdSmiLib& L, const std::string& root, ProcInfo& p, Amd
 // and memory.  Returns false when the parent reports SPX or an attribute or
 // node is missing; the caller then queries every value through amd-smi.
 bool query_partitioned(AmdSmiLib& L, const std::string& root, std::vector<ProcInfo>& procs,
-                       std::vector<AmdSmiManager::PartitionFacts>& facts) {
+                       std::vector<AmdSmiManager::PartitionFacts>& facts, std::string* mode, int64_t* read_ns) {
   std::string pci = fs::join(root, "sys/bus/pci/devices/" + procs.front().gpu_bdf);
-  auto cp_raw = AMDSMI_CALL("compute_partition(sysfs)", fs::attrs().read_trimmed(pci + "/current_compute_partition"));
-  std::string cp = cp_raw ? partition_mode(*cp_raw) : "";
-  if (cp.empty() || cp == "SPX") return false;
+  if (!session_compute_mode(pci, mode, read_ns) || *mode == "SPX") return false;
+  const std::string cp = *mode;
   auto mp_raw = AMDSMI_CALL("memory_partition(sysfs)", fs::attrs().read_trimmed(pci + "/current_memory_partition"));
   std::string mp = mp_raw ? partition_mode(*mp_raw) : "";
   if (mp.empty()) return false;
@@ -414,9 +434,8 @@ void query_gpu_caps(AmdSmiLib& L, const ProcInfo& p, const std::string& root, Gp
     if (fs::exists(pci))
       x.virtualization = classify_virtualization(pci, p.device_id, running_in_vm(root), fs::exists(pci + "/physfn"));
   }
-  // Kept from an earlier cycle under the same modes (AmdSmiManager::available_).
-  if (!avail.compute_partition.empty() && avail.compute_partition == p.compute_partition &&
-      avail.memory_partition == p.memory_partition) {
+  // Kept from an earlier cycle of the session (AmdSmiManager::available_).
+  if (avail.known) {
     x.available_memory = avail.memory;
     x.available_compute = avail.compute;
     return;
@@ -449,10 +468,9 @@ void query_gpu_caps(AmdSmiLib& L, const ProcInfo& p, const std::string& root, Gp
         if (const char* n = accel_name(cfg.profiles[i].profile_type)) x.available_compute.push_back(n);
     }
   }
-  // Kept only when both lists were found and the modes are known.
-  if (!x.available_memory.empty() && !x.available_compute.empty() && !p.compute_partition.empty() &&
-      !p.memory_partition.empty())
-    avail = {p.compute_partition, p.memory_partition, x.available_memory, x.available_compute};
+  // Kept only when both lists were found.
+  if (!x.available_memory.empty() && !x.available_compute.empty())
+    avail = {true, x.available_memory, x.available_compute};
   else
     avail = {};
 }
@@ -624,6 +642,7 @@ void AmdSmiManager::library_init() {
   proc_bdf_.clear();
   identity_.clear();
   available_.clear();
+  compute_mode_.clear();
   ++init_count_;
 }
 
@@ -701,6 +720,8 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
     std::exception_ptr error;
     int64_t proc_ns = 0, caps_ns = 0;
     KfdNodeFacts kfd;  // session cache entry (unpartitioned GPUs)
+    std::string mode;  // session cache entry: compute partition mode
+    int64_t mode_read_ns = -1;  // >= 0: read this cycle (not from the cache)
     AvailableModes avail;  // session cache entry
     std::vector<PartitionFacts> parts;  // session cache entries (partitioned GPUs), aligned with procs
   };
@@ -719,6 +740,9 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
       if (k != kfd_node_.end()) gpus.back().kfd = k->second;
       auto a = available_.find(bdf);
       if (a != available_.end()) gpus.back().avail = a->second;
+      auto m = compute_mode_.find(bdf);
+      if (m != compute_mode_.end()) gpus.back().mode = m->second;
+      else gpus.back().mode_read_ns = 0;
       for (const auto& p : physical[i]) {
         auto f = partition_facts_.find(p.h);
         gpus.back().parts.push_back(f != partition_facts_.end() ? f->second : PartitionFacts{});
@@ -748,8 +772,9 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
       int64_t t0 = trace::now_ns();
       auto& procs = *g.procs;
       if (fast) {
-        bool done = procs.size() == 1 && query_unpartitioned(L, opts_.root, procs[0], &g.kfd);
-        if (!done && !query_partitioned(L, opts_.root, procs, g.parts)) return false;
+        int64_t* rd = &g.mode_read_ns;
+        bool done = procs.size() == 1 && query_unpartitioned(L, opts_.root, procs[0], &g.kfd, &g.mode, rd);
+        if (!done && !query_partitioned(L, opts_.root, procs, g.parts, &g.mode, rd)) return false;
         std::sort(procs.begin(), procs.end(),
                   [](const ProcInfo& a, const ProcInfo& b) { return a.partition_id < b.partition_id; });
       } else {
@@ -800,6 +825,9 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
   for (const auto& g : gpus)
     if (g.error) std::rethrow_exception(g.error);
   trace::record("amdsmi.proc", proc_ns);
+  // The compute-mode reads of GPUs new to the session (none on a steady cycle).
+  for (const auto& g : gpus)
+    if (g.mode_read_ns > 0) trace::record("compute_partition(read)", g.mode_read_ns);
   trace::record("amdsmi.extras", caps_ns);
   for (const auto& g : gpus) {
     for (const auto& p : *g.procs)
@@ -807,7 +835,8 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
         identity_[p.h] = Identity{p.market_name, p.vendor_id, p.device_id, p.cus, p.gfx, p.uuid};
     if (!g.extras.virtualization.empty()) virt_mode_[g.bdf] = g.extras.virtualization;
     if (g.kfd.node_id != kNoNode) kfd_node_[g.bdf] = g.kfd;
-    if (g.avail.compute_partition.empty())
+    if (!g.mode.empty()) compute_mode_[g.bdf] = g.mode;
+    if (!g.avail.known)
       available_.erase(g.bdf);
     else
       available_[g.bdf] = g.avail;

@@ -17,7 +17,9 @@
 //     queries run in parallel across physical GPUs on multi-GPU nodes.
 //   * the virtualization mode, fixed at driver probe, is queried once per
 //     session instead of every cycle.
-//   * per-cycle values (memory, partition modes, xGMI links, available
+//   * the compute partition mode is read once per session (amdgpu reads an
+//     XCP register for it, which can wake the GPU), the rest of the
+//     per-cycle values (memory, memory partition mode, xGMI links, available
 //     modes) come straight from the amdgpu sysfs attributes the library
 //     itself reads for them - for an unpartitioned GPU and for the parent
 //     function of a partitioned one, whose partitions' KFD nodes and counts
@@ -85,10 +87,9 @@ class AmdSmiManager : public Manager {
     int sdma = -1;
     uint64_t mem_bytes = 0;
   };
-  // The partition modes a GPU supports, as read under its current modes
-  // (see available_).
+  // The partition modes a GPU supports (see available_).
   struct AvailableModes {
-    std::string compute_partition, memory_partition;  // the modes they were read under
+    bool known = false;
     std::vector<std::string> memory, compute;
   };
   // Per-session ASIC identity of one processor (see identity_).
@@ -133,20 +134,31 @@ class AmdSmiManager : public Manager {
   // handle): its KFD node, partition id, XCD and SDMA counts and its share
   // of HBM, all fixed until a partition/NPS switch - which rebuilds the KFD
   // topology, bumps its generation and re-initialises the session.  The
-  // partition modes themselves are read from the parent's amdgpu
-  // attributes every cycle (two reads per GPU, not two library calls per
-  // partition).
+  // partition modes themselves are the parent's amdgpu attributes (the
+  // compute mode once per session, compute_mode_; the memory mode every
+  // cycle) - not two library calls per partition.
   std::map<void*, PartitionFacts> partition_facts_;
   // Parent PCI function of each physical GPU (key: its processors' BDFs),
   // for the lifetime of one session: processor addresses and PCI functions
   // only change with a driver reload or partition switch, which re-initialise.
   std::map<std::string, std::string> parent_bdf_;
   // Supported compute and memory partition modes of each physical GPU (by
-  // BDF), kept while its current modes are those they were read under: what
-  // amdgpu offers follows from the ASIC and, for compute modes, the current
-  // memory partition (both read every cycle); a driver reload re-initialises
-  // the session, which clears this.  Two attribute reads per GPU per cycle.
+  // BDF) for the lifetime of one session: what amdgpu offers follows from
+  // the ASIC and, for compute modes, the current memory partition.  A memory
+  // partition switch resets the GPU and a compute partition switch rebuilds
+  // its KFD nodes; either bumps the topology generation, and so does a
+  // driver reload, and a new generation re-initialises the session, which
+  // clears this.  (Until round 5 the entry was also keyed by the current
+  // modes; since every mode change re-initialises the session, that key
+  // could never reject an entry - the mutation check showed it unobservable,
+  // profiles/differential_mutations_r5.txt - and it is gone.)  Saves two
+  // attribute reads per GPU per cycle.
   std::map<std::string, AvailableModes> available_;
+  // Compute partition mode of each physical GPU (by BDF) for the lifetime of
+  // one session, read once from current_compute_partition (see
+  // session_compute_mode in amdsmi.cpp: that read can wake the GPU).  The
+  // memory partition mode is read every cycle (an NBIO register, no wake).
+  std::map<std::string, std::string> compute_mode_;
   // PCI address of each processor (by handle) for the lifetime of one
   // session, checked once against sysfs and the processor's KFD node
   // (checked_bdf in amdsmi.cpp): amd-smi reads it through libdrm and, when

@@ -180,7 +180,8 @@ std::vector<DevicePtr> SysfsManager::GetDevices() {
 // `bdf` is the parent PCI function (see resource/physical.h): every GPU-wide
 // attribute is read there, whichever addresses the partitions report.
 static DevicePtr describe_gpu(const std::string& root, bool in_vm, int index, const std::string& bdf,
-                              const std::vector<const KfdNode*>& members, bool has_physfn) {
+                              const std::vector<const KfdNode*>& members, bool has_physfn,
+                              const std::string& compute_partition) {
   const KfdNode& first = *members.front();
   std::string pci = fs::join(root, "sys/bus/pci/devices/" + bdf);
 
@@ -193,7 +194,7 @@ static DevicePtr describe_gpu(const std::string& root, bool in_vm, int index, co
   info.gfx = gfx_target_from_kfd(first.gfx_target_version);
   auto product = fs::attrs().read_trimmed(fs::join(pci, "product_name"));
   info.name = product && !product->empty() ? *product : device_name(static_cast<uint32_t>(first.device_id));
-  info.compute_partition = partition_mode(fs::attrs().read_trimmed(fs::join(pci, "current_compute_partition")).value_or(""));
+  info.compute_partition = compute_partition;
   info.memory_partition = partition_mode(fs::attrs().read_trimmed(fs::join(pci, "current_memory_partition")).value_or(""));
   info.available_compute_partitions =
       partition_mode_list(fs::attrs().read_trimmed(fs::join(pci, "available_compute_partition")).value_or(""));
@@ -257,6 +258,14 @@ struct SysfsManager::Topology {
     // A `physfn` link (the function is an SR-IOV VF), fixed when the PCI
     // function is created - looked up here, not with a path walk per cycle.
     bool has_physfn = false;
+    // Its compute partition mode (current_compute_partition), read once per
+    // topology generation: amdgpu answers that attribute by reading the XCP
+    // control register, which "may momentarily wake the GPU up" - AMD's own
+    // CLI stopped reading it by default for that reason
+    // (/opt/rocm/libexec/amdsmi_cli/amdsmi_commands.py:463-466).  A
+    // partition switch rebuilds the GPU's KFD nodes and bumps the
+    // generation, which re-reads the topology and this with it.
+    std::string compute_partition;
   };
   std::vector<Gpu> gpus;  // ordered by parent BDF (the enumeration index)
 };
@@ -327,6 +336,11 @@ std::shared_ptr<const SysfsManager::Topology> SysfsManager::read_topology() cons
     g.bdf = resolve_parent_bdf(opts_.root, bdfs, static_cast<uint32_t>(members.front()->device_id));
     g.members = std::move(members);
     g.has_physfn = fs::exists(fs::join(opts_.root, "sys/bus/pci/devices/" + g.bdf + "/physfn"));
+    int64_t t0 = trace::now_ns();
+    g.compute_partition = partition_mode(
+        fs::attrs().read_trimmed(fs::join(opts_.root, "sys/bus/pci/devices/" + g.bdf + "/current_compute_partition"))
+            .value_or(""));
+    trace::record("compute_partition(read)", trace::now_ns() - t0);
     topo->gpus.push_back(std::move(g));
   }
   std::sort(topo->gpus.begin(), topo->gpus.end(),
@@ -367,7 +381,7 @@ std::vector<DevicePtr> SysfsManager::enumerate() {
       visible.size(),
       [&](size_t i) {
         const Topology::Gpu& g = *visible[i].second;
-        out[i] = describe_gpu(opts_.root, in_vm_, visible[i].first, g.bdf, g.members, g.has_physfn);
+        out[i] = describe_gpu(opts_.root, in_vm_, visible[i].first, g.bdf, g.members, g.has_physfn, g.compute_partition);
       },
       lanes);
   return out;

@@ -21,6 +21,7 @@
 #include "test.h"
 #include "util/fs.h"
 #include "util/strings.h"
+#include "util/trace.h"
 
 using namespace gfd;
 using namespace gfd::resource;
@@ -150,10 +151,22 @@ TEST(AmdSmiFake_UnpartitionedGpuValuesFromSysfs) {
   lm::write_file_atomically(pci + "/current_compute_partition", "SPX\n", 0644);
   lm::write_file_atomically(pci + "/current_memory_partition", "NPS1\n", 0644);
   lm::write_file_atomically(pci + "/mem_info_vram_total", "309220868096\n", 0644);
+  std::string gen = root + "/sys/class/kfd/kfd/topology/generation_id";
+  fs::mkdir_all(root + "/sys/class/kfd/kfd/topology");
+  lm::write_file_atomically(gen, "1\n", 0644);
   AmdSmiManager m(opts(root, true));
+  auto mode_read = [] {
+    for (const auto& p : trace::phases())
+      if (p.first == "compute_partition(read)") return true;
+    return false;
+  };
   for (int c = 0; c < 2; ++c) {
     m.Init();
+    trace::begin_cycle();
     auto devs = m.GetDevices();
+    // current_compute_partition (a register read that can wake the GPU) is
+    // read by the session's first cycle only.
+    EXPECT_EQ(mode_read(), c == 0);
     EXPECT_EQ(devs.size(), static_cast<size_t>(1));
     EXPECT_FALSE(devs[0]->IsPartitioned());
     EXPECT_EQ(devs[0]->GetTotalMemoryMiB(), static_cast<uint64_t>(294896));
@@ -168,9 +181,17 @@ TEST(AmdSmiFake_UnpartitionedGpuValuesFromSysfs) {
   m.Init();
   EXPECT_EQ(m.GetDevices()[0]->Info().memory_partition, std::string("NPS2"));
   m.Shutdown();
-  // Not SPX per sysfs: every value goes through the library (whose injected
-  // failures then leave them unset).
+  // The compute mode is read once per session: a changed attribute without
+  // a new topology generation (which no real partition switch leaves) is
+  // not read again.
   lm::write_file_atomically(pci + "/current_compute_partition", "CPX\n", 0644);
+  m.Init();
+  EXPECT_EQ(m.GetDevices()[0]->Info().compute_partition, std::string("SPX"));
+  m.Shutdown();
+  // With the generation a switch bumps: the session re-initialises and reads
+  // the mode again.  Not SPX per sysfs: every value goes through the library
+  // (whose injected failures then leave them unset).
+  lm::write_file_atomically(gen, "2\n", 0644);
   m.Init();
   EXPECT_EQ(m.GetDevices()[0]->GetTotalMemoryMiB(), static_cast<uint64_t>(0));
   EXPECT_EQ(m.GetDevices()[0]->Info().compute_partition, std::string(""));

@@ -22,6 +22,7 @@
 #include "util/fs.h"
 #include "util/log.h"
 #include "util/strings.h"
+#include "util/trace.h"
 
 using namespace gfd;
 using namespace gfd::resource;
@@ -116,6 +117,34 @@ TEST(Sysfs_TopologyKeptPerKfdGeneration) {
   fs::remove_all(t.root + "/sys/class/kfd/kfd/topology/generation_id");
   put(nodes + "/1/properties", kfd_props(90500, 1024, 8, 0xd900, 128, 0x3a7c178b7c5e4d5cULL));
   EXPECT_EQ(cycle().size(), static_cast<size_t>(2));
+}
+
+TEST(Sysfs_ComputeModeReadOncePerKfdGeneration) {
+  // current_compute_partition makes amdgpu read an XCP register, which can
+  // wake the GPU: it is read when the topology is, not every cycle.
+  Tree t;
+  SysfsManager m(SysfsOptions{t.root, DeviceFilter(), {}});
+  std::string attr = t.root + "/sys/bus/pci/devices/0000:d9:00.0/current_compute_partition";
+  auto cycle = [&](int* reads) {
+    m.Init();
+    trace::begin_cycle();
+    auto d = m.GetDevices();
+    *reads = 0;
+    for (const auto& p : trace::phases()) *reads += p.first == "compute_partition(read)";
+    m.Shutdown();
+    return d;
+  };
+  int reads = 0;
+  EXPECT_EQ(cycle(&reads)[1]->Info().compute_partition, std::string("SPX"));
+  EXPECT_EQ(reads, 2);  // both GPUs
+  put(attr, "DPX\n");  // no real switch leaves the generation as it was
+  EXPECT_EQ(cycle(&reads)[1]->Info().compute_partition, std::string("SPX"));
+  EXPECT_EQ(reads, 0);
+  put(t.root + "/sys/class/kfd/kfd/topology/generation_id", "2\n");
+  EXPECT_EQ(cycle(&reads)[1]->Info().compute_partition, std::string("DPX"));
+  EXPECT_EQ(reads, 2);
+  EXPECT_EQ(cycle(&reads)[1]->Info().compute_partition, std::string("DPX"));
+  EXPECT_EQ(reads, 0);
 }
 
 TEST(Sysfs_EnumeratesSpxAndCpxGpus) {

@@ -116,8 +116,13 @@ const std::vector<std::string>& BoundAmdPCI::drivers() {
   return names;
 }
 
-std::vector<PCIDevice> BoundAmdPCI::scan_bound(const std::vector<std::string>& bound,
+std::vector<PCIDevice> BoundAmdPCI::scan_bound(const std::vector<std::string>& bound_only,
+                                               const std::vector<std::string>& unbound,
                                                std::map<std::string, std::unique_ptr<fs::Dir>>* pf_dirs) {
+  // The unbound functions are read like the bound ones: a VF among them
+  // finds its PF through its physfn link, as the whole-bus scan does.
+  std::vector<std::string> bound = bound_only;
+  bound.insert(bound.end(), unbound.begin(), unbound.end());
   std::string devices = fs::join(root_, kPciDevicesRoot);
   // Two functions per lane - the 8 GPUs of an MI355X host are ~40 small
   // reads, 0.23 ms on one cold thread - but only on workers already parked:
@@ -190,8 +195,23 @@ std::vector<std::pair<std::string, uint64_t>> BoundAmdPCI::list_bound() {
   return bound;
 }
 
-bool BoundAmdPCI::still_valid(const std::vector<std::pair<std::string, uint64_t>>& bound) {
-  if (!have_ || fell_back_ || bound != bound_) return false;
+std::vector<std::string> BoundAmdPCI::list_unbound(const std::vector<std::pair<std::string, uint64_t>>& bound) {
+  std::vector<std::string> out;
+  if (!fallback_) return out;
+  int64_t t0 = trace::now_ns();
+  auto amd = fallback_->amd_functions();  // sorted, like `bound`
+  auto b = bound.begin();
+  for (auto& addr : amd) {
+    while (b != bound.end() && b->first < addr) ++b;
+    if (b == bound.end() || b->first != addr) out.push_back(std::move(addr));
+  }
+  trace::record("pci.bus", trace::now_ns() - t0);
+  return out;
+}
+
+bool BoundAmdPCI::still_valid(const std::vector<std::pair<std::string, uint64_t>>& bound,
+                              const std::vector<std::string>& unbound) {
+  if (!have_ || fell_back_ || bound != bound_ || unbound != unbound_) return false;
   for (const auto& d : last_) {
     if (d.sriov_totalvfs <= 0) continue;
     // The kernel links every VF it creates as <pf>/virtfn<N> and removes the
@@ -232,8 +252,11 @@ std::vector<PCIDevice> BoundAmdPCI::Devices() {
     return fell_back_ && fallback_ ? fallback_->Devices() : last_;
   }
   auto bound = list_bound();
+  // Whatever the bus holds that the listed drivers do not bind (empty when
+  // nothing is bound: the bus scan below is the whole answer then).
+  std::vector<std::string> unbound = bound.empty() ? std::vector<std::string>{} : list_unbound(bound);
   int64_t t_list = trace::now_ns();
-  if (seqnum && still_valid(bound)) {
+  if (seqnum && still_valid(bound, unbound)) {
     // The counter moved for some other device (a container's veth...).
     seqnum_ = *seqnum;
     int64_t t_end = trace::now_ns();
@@ -255,13 +278,14 @@ std::vector<PCIDevice> BoundAmdPCI::Devices() {
     int64_t t1 = trace::now_ns();
     std::vector<std::string> names;
     for (const auto& e : bound) names.push_back(e.first);
-    out = scan_bound(names, &pf_dirs_);
+    out = scan_bound(names, unbound, &pf_dirs_);
     trace::record("pci.bound", trace::now_ns() - t1);
     fell_back_ = false;
     last_ = out;
   }
   have_ = true;
   bound_ = std::move(bound);
+  unbound_ = std::move(unbound);
   seqnum_ = seqnum.value_or("");
   return out;
 }

@@ -15,14 +15,16 @@
 // sriov::Lib classifies them identically.
 //
 // When neither driver binds anything - an SR-IOV guest whose amdgpu is not
-// loaded, or a node without AMD GPUs - it falls back to the full-bus scan.
-// Not seen while at least one function is bound (a parity gap with the
-// reference's whole-bus scan, pciutil.go:70-112, docs/PARITY.md): an AMD
-// function bound to another driver or to none - a PF handed to vfio-pci, a
-// VF in a guest that amdgpu failed to probe while another VF of the guest
-// is bound - except the VFs that a bound PF's virtfn links name.  GIM hosts
-// bind their PFs to gim, and bare-metal and guest nodes bind their GPUs to
-// amdgpu, so the labels of a working node are the same.
+// loaded, or a node without AMD GPUs - the whole-bus scan (SysfsAmdPCI) is
+// the answer.  Otherwise the whole bus still decides which AMD functions
+// exist: whenever uevent_seqnum moved, the AMD display / accelerator
+// functions of the bus (SysfsAmdPCI::amd_functions: one listing through a
+// kept descriptor, identities only of functions not seen before) that no
+// listed driver binds - a PF handed to vfio-pci, a guest VF amdgpu failed to
+// probe - are read too, so the result is the reference's whole-bus result
+// (pciutil.go:70-112) function for function.  The first such pass reads
+// every function's vendor (~1.3 ms on an 8-GPU host); a daemon pays it in
+// its start-up prefetch, on a worker.
 //
 // Like the full scan, the result is kept while /sys/kernel/uevent_seqnum is
 // unchanged: binding, unbinding, adding or removing a function (VFs
@@ -30,11 +32,12 @@
 // enough to re-read everything - every container start on a node (veth,
 // loop and cgroup devices) sends uevents too: measured on the pool, 4 of 11
 // cycles 1 s apart found it moved and paid a 0.25 ms re-read.  So the
-// driver directories are re-listed (names and inode numbers: a function
-// removed and re-added under the same address gets a new entry) and the
-// PFs' VFs looked at; only a difference in either re-reads the functions.
-// The driver directories are read through descriptors kept open
-// (fs::DirListing): no path walk, open or close per check.
+// driver directories and the bus are re-listed (names and inode numbers: a
+// function removed and re-added under the same address gets a new entry)
+// and the PFs' VFs looked at; only a difference in any of them re-reads the
+// functions.  The driver directories and the bus are read through
+// descriptors kept open (fs::DirListing): no path walk, open or close per
+// check.
 #pragma once
 
 #include <array>
@@ -50,10 +53,11 @@ namespace gfd::sriov {
 
 class BoundAmdPCI : public AmdPCI {
  public:
-  // `fallback`: the full-bus scan used when no function is bound (may be null:
-  // then nothing is reported in that case).
-  explicit BoundAmdPCI(std::string root = "/", std::shared_ptr<AmdPCI> fallback = nullptr)
-      : root_(std::move(root)), fallback_(std::move(fallback)) {}
+  // `bus`: the whole-bus scan - the answer when no function is bound, and
+  // the source of the AMD functions no listed driver binds.  May be null:
+  // then only bound functions and their VFs are reported (tests).
+  explicit BoundAmdPCI(std::string root = "/", std::shared_ptr<SysfsAmdPCI> bus = nullptr)
+      : root_(std::move(root)), fallback_(std::move(bus)) {}
   std::vector<PCIDevice> Devices() override;
   // Whether the last Devices() came from the fallback scan.
   bool used_fallback() const { return fell_back_; }
@@ -62,19 +66,24 @@ class BoundAmdPCI : public AmdPCI {
   static const std::vector<std::string>& drivers();
 
  private:
-  // Reads `bound` and their VFs; the directories of SR-IOV PFs go to *pf_dirs.
-  std::vector<PCIDevice> scan_bound(const std::vector<std::string>& bound,
+  // Reads `bound`, the `unbound` AMD functions and the VFs of every PF
+  // among them; the directories of SR-IOV PFs go to *pf_dirs.
+  std::vector<PCIDevice> scan_bound(const std::vector<std::string>& bound, const std::vector<std::string>& unbound,
                                     std::map<std::string, std::unique_ptr<fs::Dir>>* pf_dirs);
   // (address, inode) of every function in the driver directories, sorted.
   std::vector<std::pair<std::string, uint64_t>> list_bound();
-  // Whether last_ still describes the node: same bound functions, same VFs.
-  bool still_valid(const std::vector<std::pair<std::string, uint64_t>>& bound);
+  // The bus's AMD functions that are not in `bound` (none without a bus source).
+  std::vector<std::string> list_unbound(const std::vector<std::pair<std::string, uint64_t>>& bound);
+  // Whether last_ still describes the node: same bound and unbound
+  // functions, same VFs.
+  bool still_valid(const std::vector<std::pair<std::string, uint64_t>>& bound, const std::vector<std::string>& unbound);
   std::string root_;
-  std::shared_ptr<AmdPCI> fallback_;
+  std::shared_ptr<SysfsAmdPCI> fallback_;
   bool have_ = false;
   bool fell_back_ = false;
   std::string seqnum_;  // /sys/kernel/uevent_seqnum of the kept result
   std::vector<std::pair<std::string, uint64_t>> bound_;  // list_bound() of the kept result
+  std::vector<std::string> unbound_;                      // list_unbound() of the kept result
   std::vector<PCIDevice> last_;
   std::array<fs::DirListing, 2> listings_;  // one per drivers() entry
   std::map<std::string, std::unique_ptr<fs::Dir>> pf_dirs_;  // of last_'s SR-IOV PFs, opened by the scan

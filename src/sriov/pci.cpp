@@ -97,7 +97,7 @@ SysfsAmdPCI::Identity SysfsAmdPCI::read_identity(const std::string& addr, const 
   return id;
 }
 
-std::vector<PCIDevice> SysfsAmdPCI::Devices() {
+void SysfsAmdPCI::update() {
   std::string dir = fs::join(root_, kPciDevicesRoot);
   int64_t t0 = trace::now_ns();
   // The kernel's uevent sequence number goes up with every device added to
@@ -146,9 +146,10 @@ std::vector<PCIDevice> SysfsAmdPCI::Devices() {
   // Identity reads (vendor, class, ...) of functions not seen before: every
   // function on the first scan (~5 us each: 2 ms for the 367 functions of an
   // 8-GPU host), spread over the worker pool in chunks; a hot-plugged
-  // function or two is read inline.  This scan is the fallback of the
-  // driver-directed one (sriov/bound.h), used only when neither amdgpu nor
-  // gim binds anything.
+  // function or two is read inline.  The driver-directed source
+  // (sriov/bound.h) runs this whenever uevent_seqnum moved, for the AMD
+  // functions no driver it lists binds; a daemon pays the first, full pass in
+  // its start-up prefetch, and later passes read only the listing.
   constexpr size_t kChunk = 16;
   auto read_chunk = [&](size_t c) {
     for (size_t k = c * kChunk; k < std::min(misses.size(), (c + 1) * kChunk); ++k) {
@@ -169,9 +170,21 @@ std::vector<PCIDevice> SysfsAmdPCI::Devices() {
   if (changed) cache_.swap(next);
   scanned_ = true;
   seqnum_ = seqnum.value_or("");
-  int64_t t1 = trace::now_ns();
-  trace::record("pci.identity", t1 - t0);
+  trace::record("pci.identity", trace::now_ns() - t0);
+}
 
+std::vector<std::string> SysfsAmdPCI::amd_functions() {
+  update();
+  std::vector<std::string> out;
+  for (const auto& [addr, id] : cache_)
+    if (id.relevant) out.push_back(addr);
+  return out;
+}
+
+std::vector<PCIDevice> SysfsAmdPCI::Devices() {
+  update();
+  std::string dir = fs::join(root_, kPciDevicesRoot);
+  int64_t t1 = trace::now_ns();
   std::vector<PCIDevice> out;
   std::vector<Identity*> ids;
   for (auto& [addr, id] : cache_) {

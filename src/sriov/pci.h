@@ -113,8 +113,17 @@ class SysfsAmdPCI : public AmdPCI {
  public:
   explicit SysfsAmdPCI(std::string root = "/") : root_(std::move(root)) {}
   std::vector<PCIDevice> Devices() override;
+  // The addresses of the AMD display / accelerator functions on the bus,
+  // sorted: Devices() without the per-function SR-IOV state (the
+  // driver-directed source, sriov/bound.h, reads that itself for the
+  // functions no driver it lists binds).  Same cost model: nothing read
+  // while uevent_seqnum is unchanged, one listing when it moved, identities
+  // only of functions not seen before.
+  std::vector<std::string> amd_functions();
 
  private:
+  // Brings the listing and the identity cache up to date with the bus.
+  void update();
   // Immutable for the lifetime of a sysfs object: vendor/class/device,
   // TotalVFs and the VF device ID (read-only SR-IOV capability fields), and
   // a VF's physfn link.  Only NumVFs is re-read every call.

@@ -568,6 +568,88 @@ TEST(Bound_NeverReadsFunctionsNoDriverBinds) {
   fs::remove_all(root);
 }
 
+TEST(Bound_WithTheBusSeesAVfioPfAndItsVfs) {
+  // A host whose GPUs are bound to amdgpu, except the SR-IOV PF handed to
+  // vfio-pci (its VFs enabled by vfio-pci and bound to nothing): without
+  // the bus, the PF and its VFs are not seen; with it, the functions are
+  // the whole-bus scan's, field for field, and so are the labels.
+  std::string root = pci_host(40, 2);
+  std::string dev = root + "/sys/bus/pci/devices/";
+  for (int g = 0; g < 4; ++g) bind_driver(root, "amdgpu", str::format("0000:%02x:00.0", 0x11 + 0x10 * g));
+  bind_driver(root, "vfio-pci", "0000:c1:00.0");
+  for (int v = 0; v < 2; ++v)
+    EXPECT_EQ(symlink(str::format("../0000:c1:00.%d", v + 1).c_str(), (dev + "0000:c1:00.0/virtfn" + std::to_string(v)).c_str()), 0);
+  put_file(root + "/sys/kernel/uevent_seqnum", "100\n");
+  EXPECT_EQ(BoundAmdPCI(root).Devices().size(), static_cast<size_t>(4));  // the gap without the bus
+  auto bus = std::make_shared<SysfsAmdPCI>(root);
+  BoundAmdPCI bound(root, bus);
+  auto b = bound.Devices();
+  EXPECT_FALSE(bound.used_fallback());
+  EXPECT_EQ(b.size(), static_cast<size_t>(7));
+  EXPECT_EQ(describe(b), describe(SysfsAmdPCI(root).Devices()));
+  auto labels = lm::NewSriovLabeler(std::make_shared<Lib>(std::make_shared<BoundAmdPCI>(root, std::make_shared<SysfsAmdPCI>(root))))->GetLabels();
+  auto want = lm::NewSriovLabeler(std::make_shared<Lib>(std::make_shared<SysfsAmdPCI>(root)))->GetLabels();
+  EXPECT_EQ(labels, want);
+  EXPECT_EQ(labels["amd.com/sriov.num-vfs"], std::string("2"));
+  // Rebinding the PF from vfio-pci to gim (a uevent) changes no function.
+  fs::remove_all(root + "/sys/bus/pci/drivers/vfio-pci/0000:c1:00.0");
+  bind_driver(root, "gim", "0000:c1:00.0");
+  put_file(root + "/sys/kernel/uevent_seqnum", "101\n");
+  EXPECT_EQ(describe(bound.Devices()), describe(SysfsAmdPCI(root).Devices()));
+  // An AMD function hot-added and bound to nothing is seen once the counter
+  // moves; one removed is gone.
+  std::string extra = dev + "0000:e1:00.0";
+  put_file(extra + "/vendor", "0x1002\n");
+  put_file(extra + "/class", "0x030000\n");
+  put_file(extra + "/device", "0x75a3\n");
+  put_file(extra + "/sriov_totalvfs", "0\n");
+  put_file(root + "/sys/kernel/uevent_seqnum", "102\n");
+  auto after = bound.Devices();
+  EXPECT_EQ(after.size(), static_cast<size_t>(8));
+  EXPECT_EQ(describe(after), describe(SysfsAmdPCI(root).Devices()));
+  fs::remove_all(extra);
+  put_file(root + "/sys/kernel/uevent_seqnum", "103\n");
+  EXPECT_EQ(describe(bound.Devices()), describe(SysfsAmdPCI(root).Devices()));
+  // A counter moved for some other device: nothing is read again (a function
+  // whose class became unreadable would fail a re-read).
+  fs::remove_all(dev + "0000:11:00.0/class");
+  fs::mkdir_all(dev + "0000:11:00.0/class");
+  put_file(root + "/sys/kernel/uevent_seqnum", "150\n");
+  EXPECT_EQ(bound.Devices().size(), static_cast<size_t>(7));
+  fs::remove_all(root);
+}
+
+TEST(Bound_WithTheBusSeesAGuestVfAmdgpuDidNotProbe) {
+  // A guest with two VFs: amdgpu bound one and failed to probe the other.
+  // Both are the guest's AMD functions, as the whole-bus scan reports them.
+  char d[] = "/tmp/gfd-pci-XXXXXX";
+  EXPECT_TRUE(mkdtemp(d) != nullptr);
+  std::string root = d;
+  for (const char* bdf : {"0000:00:05.0", "0000:00:06.0"}) {
+    std::string p = root + "/sys/bus/pci/devices/" + bdf;
+    put_file(p + "/vendor", "0x1002\n");
+    put_file(p + "/class", "0x120000\n");
+    put_file(p + "/device", "0x75b3\n");
+    put_file(p + "/config", std::string(64, '\x02'));
+  }
+  for (int i = 0; i < 12; ++i) {  // the VM's chipset and virtio functions
+    std::string p = root + "/sys/bus/pci/devices/" + str::format("0000:00:%02x.0", 0x10 + i);
+    put_file(p + "/vendor", "0x1af4\n");
+    put_file(p + "/class", "0x010000\n");
+  }
+  bind_driver(root, "amdgpu", "0000:00:05.0");
+  put_file(root + "/sys/kernel/uevent_seqnum", "7\n");
+  EXPECT_EQ(BoundAmdPCI(root).Devices().size(), static_cast<size_t>(1));  // the gap without the bus
+  BoundAmdPCI bound(root, std::make_shared<SysfsAmdPCI>(root));
+  auto b = bound.Devices();
+  EXPECT_EQ(b.size(), static_cast<size_t>(2));
+  EXPECT_EQ(describe(b), describe(SysfsAmdPCI(root).Devices()));
+  auto fns = Lib(std::make_shared<BoundAmdPCI>(root, std::make_shared<SysfsAmdPCI>(root))).Devices();
+  EXPECT_EQ(fns.size(), static_cast<size_t>(2));
+  for (const auto& f : fns) EXPECT_EQ(f.GetInfo().role, std::string("vf"));
+  fs::remove_all(root);
+}
+
 TEST(Bound_FallsBackToTheBusWhenNothingIsBound) {
   // A guest whose amdgpu is not loaded: its VF is on the bus, bound to nothing.
   std::string root = pci_host(5, 0);

@@ -40,6 +40,10 @@ std::string classify_virtualization(const std::string& pci_dir, uint32_t device_
   return in_vm ? "passthrough" : "baremetal";
 }
 
+// AMD's CLI names a partition's primary at bdf[:10] + ".0"
+// (/opt/rocm/libexec/amdsmi_cli/amdsmi_helpers.py:1700-1718): for every
+// layout the tests cover, the function found here is that address
+// (tests/test_amd_partition_rules.py).
 std::string resolve_parent_bdf(const std::string& root, std::vector<std::string> member_bdfs, uint32_t device_id) {
   if (member_bdfs.empty()) return "";
   std::sort(member_bdfs.begin(), member_bdfs.end());

@@ -21,6 +21,19 @@
 // mem_info_vram_total, xgmi_num_links, ...) - is then the lowest member
 // address that is a PCI function of the same device ID (partition 0 reports
 // it exactly), else the address with the function bits cleared.
+//
+// AMD's own CLI (in the ROCm image: /opt/rocm/libexec/amdsmi_cli) follows
+// the same model, and tests/test_amd_partition_rules.py runs its code
+// against both backends:
+//   * a partition's id is amdsmi_get_gpu_kfd_info's current_partition_id
+//     (amdsmi_helpers.py:1691-1698) - the amd-smi backend's partition id;
+//     the KFD backend reads it from the function bits of the node's
+//     location (sysfs.cpp, describe_gpu);
+//   * the primary partition of the processor at `bdf` is the one at
+//     bdf[:10] + ".0", if its id is 0 (amdsmi_helpers.py:1700-1718) - the
+//     parent function resolve_parent_bdf returns;
+//   * a processor is primary iff its partition id is 0
+//     (amdsmi_helpers.py:1720-1725).
 #pragma once
 
 #include <cstdint>

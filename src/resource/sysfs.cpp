@@ -213,6 +213,16 @@ static DevicePtr describe_gpu(const std::string& root, bool in_vm, int index, co
 
   Attributes engines;
   if (partitioned) engines = partition_engine_counts(root, bdf);
+  // Partition ids: where the partitions' KFD locations carry their index in
+  // the function bits (upstream amdgpu on GC 9.4.3-class parts,
+  // resource/physical.h), that index - the current_partition_id amd-smi
+  // reports and AMD's CLI keys primary partitions on
+  // (amdsmi_cli/amdsmi_helpers.py:1691-1725), also when the container sees
+  // only some partitions.  Otherwise (every partition at the parent's
+  // location) the position among the GPU's nodes.
+  bool index_in_function = false;
+  if (partition_index_in_function_bits(info.gfx))
+    for (const KfdNode* n : members) index_in_function = index_in_function || (n->location_id & 7) != 0;
   std::vector<std::shared_ptr<SnapshotDevice>> parts;
   uint32_t cus = 0, xcds = 0;
   uint64_t part_mem_sum = 0;
@@ -223,7 +233,7 @@ static DevicePtr describe_gpu(const std::string& root, bool in_vm, int index, co
     xcds += static_cast<uint32_t>(n.num_xcc);
     if (!partitioned) continue;
     DeviceInfo pi;
-    pi.partition_id = static_cast<int>(p);
+    pi.partition_id = index_in_function ? static_cast<int>(n.location_id & 7) : static_cast<int>(p);
     pi.bdf = bdf_of(n);
     pi.vendor_id = info.vendor_id;
     pi.device_id = info.device_id;

@@ -421,6 +421,25 @@ amdsmi_status_t amdsmi_get_gpu_device_bdf(amdsmi_processor_handle h, amdsmi_bdf_
   return AMDSMI_STATUS_SUCCESS;
 }
 
+// The first processor at that address, in enumeration order - the
+// library's lookup (its CLI resolves a partition's primary through it,
+// amdsmi_helpers.py get_primary_partition_gpu_id).
+amdsmi_status_t amdsmi_get_processor_handle_from_bdf(amdsmi_bdf_t bdf, amdsmi_processor_handle* h) {
+  auto& s = S();
+  std::lock_guard<std::mutex> g(s.mu);
+  if (!s.initialized) return AMDSMI_STATUS_NOT_INIT;
+  if (!h) return AMDSMI_STATUS_INVAL;
+  for (size_t i = 0; i < s.procs.size(); ++i) {
+    const Proc& p = s.procs[i];
+    if (p.domain == bdf.domain_number && p.bus == bdf.bus_number && p.dev == bdf.device_number &&
+        p.fn == bdf.function_number) {
+      *h = reinterpret_cast<amdsmi_processor_handle>(uintptr_t(i + 1));
+      return AMDSMI_STATUS_SUCCESS;
+    }
+  }
+  return AMDSMI_STATUS_API_FAILED;
+}
+
 amdsmi_status_t amdsmi_get_gpu_asic_info(amdsmi_processor_handle h, amdsmi_asic_info_t* a) {
   Proc* p;
   if (auto st = check(h, &p, true)) return st;

@@ -384,6 +384,11 @@ def fake_amdsmi_spec(root: str | os.PathLike, spec: NodeSpec, latency_us: int = 
         fields = [f"bdf={bdf}", f"mode={g.compute_partition}", f"nps={g.memory_partition}", f"parts={parts}",
                   f"name={g.product_name}", f"cus={g.cus // parts}", f"xcds={g.xcds // parts}",
                   f"vram_mib={(g.vram_bytes // parts) >> 20}", f"kfd_base={node}"]
+        # amdgpu's own classification (amdgpu_detect_virtualization), which
+        # amd-smi reports: a VF is a guest, a PF with VFs enabled the host, a
+        # whole GPU in a VM passthrough (AMDSMI_VIRTUALIZATION_MODE_*).
+        virt = 3 if g.vf else 2 if (g.sriov or {}).get("num", 0) > 0 else 4 if spec.hypervisor else 1
+        fields.append(f"virt={virt}")
         if g.visible_partitions is not None:
             fields.append("visible=" + ",".join(map(str, g.visible_partitions)))
         lines.append(";".join(fields))

@@ -135,7 +135,8 @@ class Session {
   // next write (lm::write_to_file): do not leave it behind.
   ~Session() {
     prefetch_.cancel_or_wait();
-    lm::release_kept_files();
+    // This session's output only: another live session's kept files stay.
+    if (!config_.oneshot()) lm::release_kept_files(config_.output_file());
   }
   Session(const Session&) = delete;
   Session& operator=(const Session&) = delete;

@@ -63,11 +63,21 @@ std::string render(const Labels& labels);
 // (F_SETLEASE) shows that no reader still has it open; otherwise, or where
 // leases are not available, the next write creates a new file as a oneshot
 // write does.  So a daemon's steady cycles create, unlink and evict no file.
+// Only on local file systems (reuse_is_safe): the lease check sees only this
+// kernel's openers, so on a shared or network file system a reader on
+// another machine could read a half-rewritten file; there every write
+// creates a new file, as the reference always does.
 void write_to_file(const Labels& labels, const std::string& path, bool reuse = false);
+// Whether the file system of `fd` is one where a write lease sees every
+// reader: a local one (ext4, xfs, btrfs, tmpfs, overlayfs).
+bool reuse_is_safe(int fd);
 // Atomic write of arbitrary contents (labels.go:68-114).
 void write_file_atomically(const std::string& path, const std::string& contents, unsigned perm);
 // Closes and removes every file kept for reuse (a session that ends).
 void release_kept_files();
+// The same for the files kept for one output path only (one of several
+// sessions in a process ends); the feature file itself stays.
+void release_kept_files(const std::string& path);
 // Start-up: removes <dir>/gfd-tmp left by a process that did not exit
 // cleanly (one GFD per node writes there, as the reference assumes).
 void sweep_temp_dir(const std::string& path);

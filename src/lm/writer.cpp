@@ -98,6 +98,25 @@ bool wants_prealloc(int fd) {
   return static_cast<unsigned long>(sf.f_type) == kExt4 || static_cast<unsigned long>(sf.f_type) == kOverlay;
 }
 
+}  // namespace
+
+bool reuse_is_safe(int fd) {
+  struct statfs sf;
+  if (::fstatfs(fd, &sf) != 0) return false;
+  switch (static_cast<unsigned long>(sf.f_type)) {
+    case 0xEF53:      // ext2/3/4
+    case 0x58465342:  // xfs
+    case 0x9123683E:  // btrfs
+    case 0x01021994:  // tmpfs
+    case 0x794c7630:  // overlayfs (a container's root; its upper layer is local)
+      return true;
+    default:
+      return false;
+  }
+}
+
+namespace {
+
 // Removes this daemon's files from gfd-tmp/ (kTempPrefix) and any
 // subdirectory (only this daemon's round-2 layout made them; NVIDIA's GFD
 // keeps plain files there), then the directory if nothing else is left in
@@ -199,6 +218,7 @@ struct File {
   int fd = -1;
   dev_t dev = 0;
   ino_t ino = 0;
+  bool local = false;  // on a file system where a lease sees every reader (reuse_is_safe)
 };
 struct Slot {
   File live, spare;
@@ -226,8 +246,11 @@ bool rewrite_spare(File& spare, const std::string& contents) {
   if (spare.fd < 0) return false;
   int64_t t0 = trace::now_ns();
   struct stat st;
-  // Still ours under its name (gfd-tmp/ was not emptied behind our back)...
-  bool usable = ::lstat(spare.name.c_str(), &st) == 0 && st.st_dev == spare.dev && st.st_ino == spare.ino;
+  // On a local file system (a network one's readers elsewhere hold no lease
+  // this kernel could see), still ours under its name (gfd-tmp/ was not
+  // emptied behind our back)...
+  bool usable = spare.local && ::lstat(spare.name.c_str(), &st) == 0 && st.st_dev == spare.dev &&
+                st.st_ino == spare.ino;
   // ...and no reader that opened it while it was the feature file still has
   // it open: a write lease is granted only to the sole opener.  EAGAIN: a
   // reader; EINVAL/EACCES: no leases here (a file system without them,
@@ -268,6 +291,7 @@ void write_kept(const std::string& path, const std::string& tmp_dir, const std::
       next.dev = st.st_dev;
       next.ino = st.st_ino;
     }
+    next.local = reuse_is_safe(next.fd);
     // A lease break (an open that raced with the exchange and reached the
     // file while this process held its lease) signals the holder: SIGIO by
     // default, which would terminate the daemon.  SIGURG is ignored unless
@@ -329,6 +353,17 @@ void release_kept_files() {
   slots().clear();
 }
 
+void release_kept_files(const std::string& path) {
+  if (path.empty()) return;
+  std::string abs = fs::absolute(path);
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = slots().find(abs);
+  if (it == slots().end()) return;
+  close_file(it->second.spare, true);
+  close_file(it->second.live, false);
+  slots().erase(it);
+}
+
 void sweep_temp_dir(const std::string& path) {
   if (path.empty()) return;
   std::string tmp_dir = temp_dir_of(path);
@@ -357,15 +392,7 @@ void write_to_file(const Labels& labels, const std::string& path, bool reuse) {
 
 void remove_output_file(const std::string& path) {
   std::string abs = fs::absolute(path);
-  {
-    std::lock_guard<std::mutex> lk(g_mu);
-    auto it = slots().find(abs);
-    if (it != slots().end()) {
-      close_file(it->second.spare, true);
-      close_file(it->second.live, false);
-      slots().erase(it);
-    }
-  }
+  release_kept_files(abs);
   std::string tmp_dir = temp_dir_of(abs);
   if (int e = remove_own_temps(tmp_dir)) throw Error("failed to remove temporary output directory: " + fs::errno_str(e));
   if (::unlink(abs.c_str()) != 0) throw Error("failed to remove output file: " + fs::errno_str(errno));

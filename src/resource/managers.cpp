@@ -172,6 +172,33 @@ void WarmStartManager::start_warmer() {
               preferred_->Name().c_str(), quick_->Name().c_str());
 }
 
+// The first comparison used the warmer's snapshot and the quick manager's
+// last published one, taken at different times: a node that changed in
+// between (a partition switch during start-up) must not keep the daemon off
+// the preferred manager for its whole life.  So before deciding, both
+// describe the node again, back to back (once per start iteration).
+bool WarmStartManager::second_look(std::string* quick_now, std::string* preferred_now) {
+  auto describe = [](Manager& m, std::string* out) {
+    try {
+      m.Init();
+      try {
+        *out = device_summary(m.GetDevices());
+      } catch (...) {
+        m.Shutdown();
+        throw;
+      }
+      m.Shutdown();
+      return true;
+    } catch (const std::exception& e) {
+      *out = std::string("(error: ") + e.what() + ")\n";
+      return false;
+    }
+  };
+  bool ok = describe(*quick_, quick_now);
+  ok = describe(*preferred_, preferred_now) && ok;
+  return ok && *quick_now == *preferred_now;
+}
+
 void WarmStartManager::Init() {
   if (state_ == State::cold) {
     start_warmer();
@@ -184,24 +211,29 @@ void WarmStartManager::Init() {
       thread_.join();
       if (!error.empty()) {
         fall_back(error);
-      } else if (!quick_devices_.empty() && devices != quick_devices_) {
+      } else if (std::string quick_now, preferred_now;
+                 !quick_devices_.empty() && devices != quick_devices_ && !second_look(&quick_now, &preferred_now)) {
         // Labels from the quick manager are published and the preferred
-        // one would change them: keep the published source until the next
-        // (re)start, like the reference's fallback, which keeps one backend
-        // per start iteration (internal/resource/fallback.go:37-44) - the
-        // node's labels never flip because a backend finished starting.
+        // one would change them - also when both describe the node again:
+        // keep the published source until the next (re)start, like the
+        // reference's fallback, which keeps one backend per start iteration
+        // (internal/resource/fallback.go:37-44) - the node's labels never
+        // flip because a backend finished starting.
         log::printf("Warning: the %s manager (initialized in the background in %.1f ms) describes the GPUs "
                     "differently from the %s manager, whose labels are published; labeling from the %s manager "
                     "until the next restart (SIGHUP):\n%s:\n%s%s:\n%s",
                     preferred_->Name().c_str(), static_cast<double>(ns) / 1e6, quick_->Name().c_str(),
-                    quick_->Name().c_str(), quick_->Name().c_str(), quick_devices_.c_str(), preferred_->Name().c_str(),
-                    devices.c_str());
+                    quick_->Name().c_str(), quick_->Name().c_str(), quick_now.c_str(), preferred_->Name().c_str(),
+                    preferred_now.c_str());
         state_ = State::quick_only;
         current_ = quick_;
         preferred_.reset();  // its session is not used again
       } else {
-        log::printf("Using the %s manager (initialized in the background in %.1f ms)", preferred_->Name().c_str(),
-                    static_cast<double>(ns) / 1e6);
+        log::printf("Using the %s manager (initialized in the background in %.1f ms%s)", preferred_->Name().c_str(),
+                    static_cast<double>(ns) / 1e6,
+                    devices != quick_devices_ && !quick_devices_.empty()
+                        ? "; the node changed while it started, both describe it the same way now"
+                        : "");
         state_ = State::preferred;
         current_ = preferred_;
       }

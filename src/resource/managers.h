@@ -118,6 +118,9 @@ class WarmStartManager : public Manager {
   void fall_back(const std::string& why);
   // cold -> warming, unless an earlier manager's warmer still runs.
   void start_warmer();
+  // Both managers describe the node again, now (device_summary each); true
+  // if they agree.
+  bool second_look(std::string* quick_now, std::string* preferred_now);
   bool waited_logged_ = false;
 
   ManagerPtr preferred_, quick_, current_;

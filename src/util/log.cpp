@@ -6,11 +6,39 @@
 #include <ctime>
 #include <sys/time.h>
 
+#include <string>
+#include <vector>
+
 namespace gfd::log {
 
 namespace {
 std::atomic<bool> g_quiet{false};
-thread_local std::string* t_held = nullptr;  // the innermost Hold's buffer
+thread_local Hold* t_hold = nullptr;  // the innermost Hold of this thread
+
+bool starts_with(const char* msg, size_t len, const char* word) {
+  size_t n = std::strlen(word);
+  return len >= n && std::memcmp(msg, word, n) == 0;
+}
+}  // namespace
+
+struct HoldChain {
+  // Everything held by the thread's Holds, outermost first (the order the
+  // lines were logged in: an inner Hold only holds lines logged after the
+  // outer one's), taken out of them.
+  static std::string take_all() {
+    std::vector<Hold*> chain;
+    for (Hold* h = t_hold; h; h = h->prev_) chain.push_back(h);
+    std::string out;
+    for (auto it = chain.rbegin(); it != chain.rend(); ++it) {
+      out.append((*it)->buf_);
+      (*it)->buf_.clear();
+    }
+    return out;
+  }
+  static void append(const std::string& line) { t_hold->buf_.append(line); }
+};
+
+namespace {
 
 void emit(const char* msg, size_t len) {
   // The stamp only changes once a second: the lines of one cycle share one
@@ -30,18 +58,16 @@ void emit(const char* msg, size_t len) {
   out.append(stamp);
   out.append(msg, len);
   if (len == 0 || msg[len - 1] != '\n') out.push_back('\n');
-  if (t_held) {
+  if (t_hold) {
     // Warnings and errors are never held: a cycle that then hangs (a wedged
-    // library call) or is killed must still have said why.  What is held
-    // goes out first, so the order stays.
-    bool urgent = len >= 5 && (std::strncmp(msg, "Warning", 7) == 0 || std::strncmp(msg, "WARNING", 7) == 0 ||
-                                std::strncmp(msg, "Error", 5) == 0);
+    // library call) or is killed must still have said why.  What every
+    // enclosing Hold holds goes out first, so the order stays.
+    bool urgent = starts_with(msg, len, "Warning") || starts_with(msg, len, "WARNING") || starts_with(msg, len, "Error");
     if (!urgent) {
-      t_held->append(out);
+      HoldChain::append(out);
       return;
     }
-    out.insert(0, *t_held);
-    t_held->clear();
+    out.insert(0, HoldChain::take_all());
   }
   fwrite(out.data(), 1, out.size(), stderr);
 }
@@ -49,17 +75,17 @@ void emit(const char* msg, size_t len) {
 
 bool set_quiet(bool q) { return g_quiet.exchange(q); }
 
-Hold::Hold() : prev_(t_held) { t_held = &buf_; }
+Hold::Hold() : prev_(t_hold) { t_hold = this; }
 
 Hold::~Hold() {
   flush();
-  t_held = prev_;
+  t_hold = prev_;
 }
 
 void Hold::flush() {
   if (buf_.empty()) return;
   if (prev_) {
-    prev_->append(buf_);  // nested: the outer Hold writes it
+    prev_->buf_.append(buf_);  // nested: the outer Hold writes it
   } else {
     fwrite(buf_.data(), 1, buf_.size(), stderr);
   }

@@ -33,8 +33,9 @@ class Hold {
   void flush();
 
  private:
+  friend struct HoldChain;
   std::string buf_;
-  std::string* prev_;
+  Hold* prev_;  // the enclosing Hold on this thread, if any
 };
 
 }  // namespace gfd::log

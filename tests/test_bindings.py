@@ -72,6 +72,35 @@ def test_session_bench_returns_per_step_times(native, tmp_path):
     assert len(ns) == 25 and all(x > 0 for x in ns)
 
 
+def test_closing_one_session_keeps_another_sessions_kept_files(native, tmp_path):
+    """A loop-mode session keeps the feature file its last write swapped out
+    (gfd-tmp/) for the next write; closing another session with a different
+    output leaves that file alone, and closing this one removes it."""
+    import gc
+
+    root = synth.make_mi355x_node(tmp_path / "root", n_gpus=1)
+    outs = [tmp_path / "a" / "gfd", tmp_path / "b" / "gfd"]
+    sessions = []
+    for out in outs:
+        out.parent.mkdir()
+        s = native.Session(["--backend=sysfs", f"--sysfs-root={root}", f"--output-file={out}", "--sleep-interval=1s"])
+        s.cycle(True)
+        s.cycle(True)  # the second write swaps the first file out, into gfd-tmp/
+        sessions.append(s)
+    kept = [sorted((out.parent / "gfd-tmp").iterdir()) for out in outs]
+    assert all(len(k) == 1 for k in kept), kept
+    del s
+    sessions.pop()  # b's session ends
+    gc.collect()
+    assert not list((outs[1].parent / "gfd-tmp").iterdir())
+    assert sorted((outs[0].parent / "gfd-tmp").iterdir()) == kept[0]  # a's kept file is untouched
+    sessions[0].cycle(True)  # and a's next write still reuses it
+    assert sorted((outs[0].parent / "gfd-tmp").iterdir()) == kept[0]
+    sessions.clear()
+    gc.collect()
+    assert not list((outs[0].parent / "gfd-tmp").iterdir())
+
+
 def test_session_env_precedence(native, tmp_path):
     root = synth.make_mi355x_node(tmp_path / "root", n_gpus=1)
     s = native.Session([f"--sysfs-root={root}", "--output-file="],

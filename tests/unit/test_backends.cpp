@@ -562,9 +562,30 @@ TEST(WarmStart_APreferredManagerThatDisagreesIsNotSwitchedTo) {
       usleep(1000);
     }
     EXPECT_FALSE(w.warmed());
-    EXPECT_EQ(smi->init_calls, 1);  // the warmer only
+    EXPECT_EQ(smi->init_calls, 2);  // the warmer, and the second look before deciding
   }
   EXPECT_EQ(smi.use_count(), 1L);  // released at the decision, not kept warm
+}
+
+TEST(WarmStart_ADifferenceThatGoesAwayDoesNotDecide) {
+  // The node changed between the warmer's snapshot and the published one (a
+  // partition switch during start-up): the published labels said one GPU,
+  // the warmer saw two, and now both managers see two.  The second look
+  // finds them agreeing, and the preferred manager takes over.
+  auto smi = std::make_shared<MockManager>(std::vector<DevicePtr>{new_full_gpu(), new_full_gpu()});
+  auto kfd = std::make_shared<MockManager>(std::vector<DevicePtr>{new_full_gpu()});
+  WarmStartManager w(smi, kfd);
+  w.Init();  // starts the warmer; labels from kfd
+  EXPECT_EQ(w.GetDevices().size(), static_cast<size_t>(1));
+  w.Shutdown();
+  usleep(300 * 1000);  // the warmer (the mock initialises at once) is done
+  kfd->devices.push_back(new_full_gpu());  // the change reaches the quick manager too
+  int smi_inits = smi->init_calls;
+  w.Init();  // decides: published 1 vs warmer 2, then 2 and 2 on the second look
+  EXPECT_TRUE(w.warmed());
+  EXPECT_EQ(smi->init_calls, smi_inits + 2);  // the second look, then this cycle
+  EXPECT_EQ(w.GetDevices().size(), static_cast<size_t>(2));
+  w.Shutdown();
 }
 
 TEST(WarmStart_PrepareStartsThePreferredManagerBeforeTheFirstCycle) {

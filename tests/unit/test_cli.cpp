@@ -404,6 +404,41 @@ TEST(DynLib_ReportsWhyNoCandidateLoaded) {
   EXPECT_TRUE(lib.symbol("getpid") == nullptr);
 }
 
+TEST(LogHold_NestedHoldsWriteAWarningAfterEverythingHeldBefore) {
+  // The outer Hold's earlier lines go out before the inner Hold's, and both
+  // before the warning; short messages ("Warn", "Err") are never compared
+  // past their end.
+  bool was = log::set_quiet(false);
+  std::string at_warning, at_end;
+  {
+    StderrCapture cap;
+    {
+      log::Hold outer;
+      log::printf("outer-1");
+      {
+        log::Hold inner;
+        log::printf("inner-1");
+        log::printf("Warn");
+        log::printf("Err");
+        EXPECT_EQ(cap.peek(), std::string(""));
+        log::printf("Warning: w");
+        at_warning = cap.peek();
+        log::printf("inner-2");
+      }
+      log::printf("outer-2");
+    }
+    at_end = cap.peek();
+  }
+  log::set_quiet(was);
+  auto o1 = at_warning.find("outer-1"), i1 = at_warning.find("inner-1"), wn = at_warning.find("Warn\n"),
+       er = at_warning.find("Err\n"), w = at_warning.find("Warning: w");
+  EXPECT_TRUE(o1 != std::string::npos && i1 != std::string::npos && w != std::string::npos);
+  EXPECT_TRUE(o1 < i1 && i1 < wn && wn < er && er < w);
+  auto i2 = at_end.find("inner-2"), o2 = at_end.find("outer-2");
+  EXPECT_TRUE(w < i2 && i2 < o2 && o2 != std::string::npos);
+  EXPECT_EQ(at_end.find("outer-1", o1 + 1), std::string::npos);  // written once
+}
+
 TEST(LogHold_WritesWarningsAtOnceWithWhatCameBefore) {
   // A cycle that hangs after a warning (a wedged library call) or is killed
   // must already have said why: warnings and errors are not held.

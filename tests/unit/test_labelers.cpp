@@ -392,6 +392,21 @@ TEST(Render_IsSortedKeyValueLines) {
   EXPECT_EQ(lm::render({{"b", "2"}, {"a", "1"}}), std::string("a=1\nb=2\n"));
 }
 
+TEST(WriteToFile_ReusesFilesOnlyOnLocalFileSystems) {
+  // A lease sees only this kernel's openers: reuse is allowed where every
+  // reader is local (tmpfs here), not on other file systems (procfs stands
+  // in for a network one: no lease there could see a remote reader).
+  int shm = ::open("/dev/shm", O_RDONLY | O_DIRECTORY);
+  EXPECT_TRUE(shm >= 0);
+  EXPECT_TRUE(lm::reuse_is_safe(shm));
+  ::close(shm);
+  int proc = ::open("/proc/self/stat", O_RDONLY);
+  EXPECT_TRUE(proc >= 0);
+  EXPECT_FALSE(lm::reuse_is_safe(proc));
+  ::close(proc);
+  EXPECT_FALSE(lm::reuse_is_safe(-1));
+}
+
 TEST(WriteToFile_AtomicWithMode0644) {
   char dir[] = "/tmp/gfd-write-XXXXXX";
   EXPECT_TRUE(mkdtemp(dir) != nullptr);

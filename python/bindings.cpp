@@ -119,7 +119,7 @@ class Session {
     // As cli::start does: the first SR-IOV scan runs on a worker while the
     // backend is selected (and, here, while the caller does whatever it does
     // before the first cycle).
-    sriov_ = sriov::new_sriov_lib(config_.sysfs_root());
+    sriov_ = sriov::new_sriov_lib(config_.sysfs_root(), config_.oneshot());
     auto lib = sriov_;
     if (!config_.oneshot())
       prefetch_ = WorkerPool::instance().submit([lib] {
@@ -227,22 +227,28 @@ PYBIND11_MODULE(_gfd, m) {
     bool ok = resource::has_amdsmi(&reason);
     return py::make_tuple(ok, reason);
   });
-  // The SR-IOV function sources side by side: "bound" (the daemon's: the
-  // functions amdgpu / gim bind and their VFs) or "bus" (every function on
-  // the PCI bus, the reference's approach and the daemon's fallback).
+  // The SR-IOV function sources side by side: "bound" (the functions the
+  // listed drivers bind and their VFs, nothing else), "daemon" (the loop's
+  // source: those, plus the bus's AMD functions no listed driver binds),
+  // "job" (a oneshot Job's: the bus only inside a VM) or "bus" (every
+  // function on the PCI bus, the reference's approach).
+  auto pci_source = [](const std::string& root, const std::string& source) -> std::shared_ptr<sriov::AmdPCI> {
+    if (source == "bound") return std::make_shared<sriov::BoundAmdPCI>(root);
+    if (source == "daemon" || source == "job") {
+      bool merge = source == "daemon" || resource::running_in_vm(root);
+      return std::make_shared<sriov::BoundAmdPCI>(root, std::make_shared<sriov::SysfsAmdPCI>(root), merge);
+    }
+    if (source == "bus") return std::make_shared<sriov::SysfsAmdPCI>(root);
+    throw Error("unknown PCI function source '" + source + "' (expected bound, daemon, job or bus)");
+  };
   m.def(
       "pci_functions",
-      [](const std::string& root, const std::string& source) {
+      [pci_source](const std::string& root, const std::string& source) {
         std::vector<sriov::PCIDevice> devs;
         {
+          auto src = pci_source(root, source);
           py::gil_scoped_release nogil;
-          if (source == "bound") {
-            devs = sriov::BoundAmdPCI(root).Devices();
-          } else if (source == "bus") {
-            devs = sriov::SysfsAmdPCI(root).Devices();
-          } else {
-            throw Error("unknown PCI function source '" + source + "' (expected bound or bus)");
-          }
+          devs = src->Devices();
         }
         py::list out;
         for (const auto& d : devs) {
@@ -258,6 +264,15 @@ PYBIND11_MODULE(_gfd, m) {
           out.append(o);
         }
         return out;
+      },
+      py::arg("root") = "/", py::arg("source") = "bound");
+  // The SR-IOV labels (lm::NewSriovLabeler) over one of those sources.
+  m.def(
+      "sriov_labels",
+      [pci_source](const std::string& root, const std::string& source) {
+        auto lib = std::make_shared<sriov::Lib>(pci_source(root, source), root);
+        py::gil_scoped_release nogil;
+        return lm::NewSriovLabeler(lib)->GetLabels();
       },
       py::arg("root") = "/", py::arg("source") = "bound");
   m.def("parse_duration", &parse_duration);

@@ -31,15 +31,15 @@ bool is_pci_address(const std::string& name) {
 }
 
 // The function at `dir` as SysfsAmdPCI reports it, or nullopt when it is not
-// a display (0x03) or processing-accelerator (0x12) function.  Every function
-// reached here is AMD's: amdgpu's and gim's ID tables name vendor 0x1002 only,
-// and a PF's VFs carry its vendor.
+// an AMD (0x1002) display (0x03) or processing-accelerator (0x12) function:
+// amdgpu's and gim's ID tables name vendor 0x1002 only, but vfio-pci and the
+// stub drivers bind anything.
 // Class and device ID from the function's `uevent` (PCI_CLASS=120000,
 // PCI_ID=1002:75A3): one read instead of `class` and `device`.  The kernel
 // prints PCI_CLASS with %04X, so a display function's leading zero is gone
 // (0x038000 is "38000"): the value is parsed and re-padded to the six digits
 // of the `class` attribute.
-bool from_uevent(const fs::Dir& dir, std::string* cls, std::string* device) {
+bool from_uevent(const fs::Dir& dir, std::string* cls, std::string* vendor, std::string* device) {
   auto r = dir.read_attr("uevent");
   if (!r.ok()) return false;
   std::string c, id;
@@ -49,6 +49,7 @@ bool from_uevent(const fs::Dir& dir, std::string* cls, std::string* device) {
   }
   auto colon = id.find(':');
   if (c.empty() || c.size() > 6 || colon == std::string::npos) return false;
+  *vendor = "0x" + str::to_lower(id.substr(0, colon));
   char* end = nullptr;
   unsigned long v = std::strtoul(c.c_str(), &end, 16);
   if (end == c.c_str() || *end != 0) return false;
@@ -65,8 +66,15 @@ std::optional<PCIDevice> read_function(const std::string& path, const std::strin
                                        std::unique_ptr<fs::Dir>* keep) {
   auto owned = std::make_unique<fs::Dir>(path);
   const fs::Dir& dir = *owned;
-  std::string c, device;
-  bool have_device = from_uevent(dir, &c, &device);
+  std::string c, vendor, device;
+  bool have_device = from_uevent(dir, &c, &vendor, &device);
+  if (!have_device) {
+    auto v = dir.read_attr("vendor", 64);
+    if (!v.ok()) throw Error("unable to read PCI device vendor id for " + addr + ": " + fs::errno_str(v.err));
+    vendor = str::trim(v.data);
+  }
+  // vfio-pci and the stub drivers bind any vendor's functions.
+  if (vendor != kAmdVendorId) return std::nullopt;
   if (!have_device) {
     auto cls = dir.read_attr("class", 64);
     if (!cls.ok()) throw Error("unable to read PCI device class for " + addr + ": " + fs::errno_str(cls.err));
@@ -112,7 +120,11 @@ std::optional<PCIDevice> read_function(const std::string& path, const std::strin
 }  // namespace
 
 const std::vector<std::string>& BoundAmdPCI::drivers() {
-  static const std::vector<std::string> names{"amdgpu", "gim"};
+  // amdgpu (bare metal, a passthrough or SR-IOV guest), gim (an MxGPU
+  // host's PFs), and what hands a GPU to a VM or enables VFs without a GPU
+  // driver: vfio-pci, pci-pf-stub, pci-stub.  No other in-tree driver's ID
+  // table names an AMD GPU function.
+  static const std::vector<std::string> names{"amdgpu", "gim", "vfio-pci", "pci-pf-stub", "pci-stub"};
   return names;
 }
 
@@ -197,7 +209,7 @@ std::vector<std::pair<std::string, uint64_t>> BoundAmdPCI::list_bound() {
 
 std::vector<std::string> BoundAmdPCI::list_unbound(const std::vector<std::pair<std::string, uint64_t>>& bound) {
   std::vector<std::string> out;
-  if (!fallback_) return out;
+  if (!fallback_ || !merge_unbound_) return out;
   int64_t t0 = trace::now_ns();
   auto amd = fallback_->amd_functions();  // sorted, like `bound`
   auto b = bound.begin();

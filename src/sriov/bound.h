@@ -56,8 +56,10 @@ class BoundAmdPCI : public AmdPCI {
   // `bus`: the whole-bus scan - the answer when no function is bound, and
   // the source of the AMD functions no listed driver binds.  May be null:
   // then only bound functions and their VFs are reported (tests).
-  explicit BoundAmdPCI(std::string root = "/", std::shared_ptr<SysfsAmdPCI> bus = nullptr)
-      : root_(std::move(root)), fallback_(std::move(bus)) {}
+  // `merge_unbound`: whether the AMD functions no listed driver binds are
+  // looked for on the bus (else the bus is read only when nothing is bound).
+  explicit BoundAmdPCI(std::string root = "/", std::shared_ptr<SysfsAmdPCI> bus = nullptr, bool merge_unbound = true)
+      : root_(std::move(root)), fallback_(std::move(bus)), merge_unbound_(merge_unbound) {}
   std::vector<PCIDevice> Devices() override;
   // Whether the last Devices() came from the fallback scan.
   bool used_fallback() const { return fell_back_; }
@@ -79,13 +81,14 @@ class BoundAmdPCI : public AmdPCI {
   bool still_valid(const std::vector<std::pair<std::string, uint64_t>>& bound, const std::vector<std::string>& unbound);
   std::string root_;
   std::shared_ptr<SysfsAmdPCI> fallback_;
+  bool merge_unbound_ = true;
   bool have_ = false;
   bool fell_back_ = false;
   std::string seqnum_;  // /sys/kernel/uevent_seqnum of the kept result
   std::vector<std::pair<std::string, uint64_t>> bound_;  // list_bound() of the kept result
   std::vector<std::string> unbound_;                      // list_unbound() of the kept result
   std::vector<PCIDevice> last_;
-  std::array<fs::DirListing, 2> listings_;  // one per drivers() entry
+  std::array<fs::DirListing, 5> listings_;  // one per drivers() entry
   std::map<std::string, std::unique_ptr<fs::Dir>> pf_dirs_;  // of last_'s SR-IOV PFs, opened by the scan
 };
 

@@ -3,6 +3,7 @@
 #include "sriov/bound.h"
 
 #include "resource/pci_ids.h"
+#include "resource/sysfs.h"
 #include "util/error.h"
 #include "util/strings.h"
 
@@ -98,10 +99,12 @@ class EmptyLib : public Interface {
 };
 }  // namespace
 
-std::shared_ptr<Interface> new_sriov_lib(const std::string& root) {
-  // The functions amdgpu / gim bind, and the VFs of those PFs; the whole bus
-  // only when neither binds anything (sriov/bound.h).
-  return std::make_shared<Lib>(std::make_shared<BoundAmdPCI>(root, std::make_shared<SysfsAmdPCI>(root)), root);
+std::shared_ptr<Interface> new_sriov_lib(const std::string& root, bool oneshot) {
+  // The functions the listed drivers bind and the VFs of those PFs, plus the
+  // bus's AMD functions no listed driver binds (sriov/bound.h).
+  bool merge_unbound = !oneshot || resource::running_in_vm(root);
+  return std::make_shared<Lib>(std::make_shared<BoundAmdPCI>(root, std::make_shared<SysfsAmdPCI>(root), merge_unbound),
+                               root);
 }
 
 std::shared_ptr<Interface> new_mock_sriov() { return std::make_shared<Lib>(std::make_shared<MockAmdPCI>()); }

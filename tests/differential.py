@@ -24,8 +24,11 @@ daemon sessions across every change) with that of a fresh daemon process
 
 The node model keeps what real nodes cannot do out: VFs are enabled only on
 a GIM host, whose SR-IOV PFs are bound to gim and so have no KFD node and
-are invisible to amd-smi (amdgpu implements no sriov_configure); TotalVFs
-is fixed per device; a hot-added GPU keeps the others' identities.
+are invisible to amd-smi (amdgpu implements no sriov_configure), and only
+on a bound PF - unbinding one disables its VFs (the PF driver's remove
+does; the PCI core warns "driver left SR-IOV enabled after remove"
+otherwise); TotalVFs is fixed per device; a hot-added GPU keeps the others'
+identities.
 
 Nodes are changed in place, as the kernel does: an attribute rewritten
 keeps its inode, a removed device's files disappear, a reloaded module's
@@ -240,7 +243,7 @@ def mutate(live: LiveNode, rng: random.Random) -> str:
         # being installed (its module appears, it binds the SR-IOV PFs).
         n.gim = "8.3.0.K"
     elif kind == "vfs":
-        capable = [g for g in n.gpus if g.sriov]
+        capable = [g for g in n.gpus if g.sriov and g.bound]
         if not capable:
             g = rng.choice(n.gpus)
             g.sriov = True  # (a GPU of another SKU: as if hot-added with its capability)
@@ -275,6 +278,8 @@ def mutate(live: LiveNode, rng: random.Random) -> str:
     elif kind == "bind":
         g = rng.choice(n.gpus)
         g.bound = not g.bound
+        if not g.bound:
+            g.vfs = 0  # the PF driver disables SR-IOV as it unbinds
     elif kind == "uevent":
         n.seqnum += rng.randint(1, 40)  # a container's veth, a loop device...
     live.apply(recreate=recreate, reset=reset)

@@ -121,7 +121,8 @@ def test_session_errors_surface(native, tmp_path):
         s.cycle(False)
 
 
-@pytest.mark.parametrize("kind", ["spx8", "sriov-host", "sriov-host-privileged", "guest-vf", "guest-vf-unbound"])
+@pytest.mark.parametrize("kind", ["spx8", "sriov-host", "sriov-host-privileged", "guest-vf", "guest-vf-unbound",
+                                  "host-vfio-pf", "guest-vf-one-unprobed", "host-unbound-gpu"])
 def test_bound_sriov_source_matches_the_whole_bus(native, tmp_path, kind):
     """The daemon's SR-IOV source (the functions amdgpu / gim bind, plus
     their VFs) hands the labeler the same functions, field for field, as the
@@ -135,14 +136,39 @@ def test_bound_sriov_source_matches_the_whole_bus(native, tmp_path, kind):
     elif kind.startswith("sriov-host"):
         gpus = [synth.GpuSpec(sriov={"total": 8, "num": 3, "vf_device": 0x75B3}), synth.GpuSpec()]
         gim = "8.1.0.K"
+    elif kind == "host-vfio-pf":
+        # A PF handed to vfio-pci, its VFs enabled, next to an amdgpu GPU.
+        gpus = [synth.GpuSpec(sriov={"total": 8, "num": 2, "vf_device": 0x75B3}, driver="vfio-pci", kfd=False),
+                synth.GpuSpec()]
+    elif kind == "guest-vf-one-unprobed":
+        # A VM with two VFs; amdgpu failed to probe the second.
+        gpus = [synth.GpuSpec(vf=True), synth.GpuSpec(vf=True, driver=None, kfd=False)]
+    elif kind == "host-unbound-gpu":
+        # Bare metal: a GPU no driver binds, next to an amdgpu one.
+        gpus = [synth.GpuSpec(), synth.GpuSpec(driver=None, kfd=False)]
     else:
         gpus = [synth.GpuSpec(vf=True, driver=None if kind.endswith("unbound") else "auto")]
-    root = synth.make_node(tmp_path / "node", synth.NodeSpec(gpus=gpus, gim_version=gim, seed=11,
+    guest = kind.startswith("guest")
+    root = synth.make_node(tmp_path / "node", synth.NodeSpec(gpus=gpus, gim_version=gim, seed=11, hypervisor=guest,
                                                               privileged=kind.endswith("privileged")))
     bound = native.pci_functions(str(root), "bound")
     bus = native.pci_functions(str(root), "bus")
+    # The daemon's source is the bus's, function for function, on every node.
+    assert native.pci_functions(str(root), "daemon") == bus
+    job = native.pci_functions(str(root), "job")
+    if kind == "host-unbound-gpu":
+        # A Job on a host does not read the bus: the unbound GPU (no VFs, so
+        # no SR-IOV state) is not among its functions - its labels are the
+        # same, since the SR-IOV labeler classifies it as nothing.
+        assert len(bus) == 2 and len(bound) == len(job) == 1
+        assert native.sriov_labels(str(root), "job") == native.sriov_labels(str(root), "bus") == {}
+        return
+    assert job == bus
     if kind == "guest-vf-unbound":
         assert bound == [] and len(bus) == 1
         return
+    if kind == "guest-vf-one-unprobed":
+        assert len(bound) == 1 and len(bus) == 2
+        return
     assert bound == bus
-    assert len(bound) == {"spx8": 8, "guest-vf": 1}.get(kind, 2 + 3)
+    assert len(bound) == {"spx8": 8, "guest-vf": 1, "host-vfio-pf": 4}.get(kind, 2 + 3)

@@ -570,9 +570,10 @@ TEST(Bound_NeverReadsFunctionsNoDriverBinds) {
 
 TEST(Bound_WithTheBusSeesAVfioPfAndItsVfs) {
   // A host whose GPUs are bound to amdgpu, except the SR-IOV PF handed to
-  // vfio-pci (its VFs enabled by vfio-pci and bound to nothing): without
-  // the bus, the PF and its VFs are not seen; with it, the functions are
-  // the whole-bus scan's, field for field, and so are the labels.
+  // vfio-pci (its VFs enabled by vfio-pci and bound to nothing): the
+  // functions are the whole-bus scan's, field for field, and so are the
+  // labels - vfio-pci is one of the listed drivers; a function no driver
+  // binds needs the bus (below).
   std::string root = pci_host(40, 2);
   std::string dev = root + "/sys/bus/pci/devices/";
   for (int g = 0; g < 4; ++g) bind_driver(root, "amdgpu", str::format("0000:%02x:00.0", 0x11 + 0x10 * g));
@@ -580,7 +581,12 @@ TEST(Bound_WithTheBusSeesAVfioPfAndItsVfs) {
   for (int v = 0; v < 2; ++v)
     EXPECT_EQ(symlink(str::format("../0000:c1:00.%d", v + 1).c_str(), (dev + "0000:c1:00.0/virtfn" + std::to_string(v)).c_str()), 0);
   put_file(root + "/sys/kernel/uevent_seqnum", "100\n");
-  EXPECT_EQ(BoundAmdPCI(root).Devices().size(), static_cast<size_t>(4));  // the gap without the bus
+  // vfio-pci also binds other vendors' functions: not reported.
+  std::string nic = dev + "0000:e9:00.0";
+  put_file(nic + "/vendor", "0x15b3\n");
+  put_file(nic + "/class", "0x020000\n");
+  bind_driver(root, "vfio-pci", "0000:e9:00.0");
+  EXPECT_EQ(describe(BoundAmdPCI(root).Devices()), describe(SysfsAmdPCI(root).Devices()));
   auto bus = std::make_shared<SysfsAmdPCI>(root);
   BoundAmdPCI bound(root, bus);
   auto b = bound.Devices();
@@ -607,6 +613,8 @@ TEST(Bound_WithTheBusSeesAVfioPfAndItsVfs) {
   auto after = bound.Devices();
   EXPECT_EQ(after.size(), static_cast<size_t>(8));
   EXPECT_EQ(describe(after), describe(SysfsAmdPCI(root).Devices()));
+  EXPECT_EQ(BoundAmdPCI(root).Devices().size(), static_cast<size_t>(7));  // without the bus: not seen
+  EXPECT_EQ(BoundAmdPCI(root, std::make_shared<SysfsAmdPCI>(root), false).Devices().size(), static_cast<size_t>(7));
   fs::remove_all(extra);
   put_file(root + "/sys/kernel/uevent_seqnum", "103\n");
   EXPECT_EQ(describe(bound.Devices()), describe(SysfsAmdPCI(root).Devices()));

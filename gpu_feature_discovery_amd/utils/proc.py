@@ -18,7 +18,7 @@ import signal
 import threading
 import time
 
-__all__ = ["spawn_wait_ms"]
+__all__ = ["spawn_wait_ms", "gpu_holds"]
 
 
 def spawn_wait_ms(argv: list[str], timeout: float = 60.0, env: dict | None = None) -> float:
@@ -50,3 +50,26 @@ def spawn_wait_ms(argv: list[str], timeout: float = 60.0, env: dict | None = Non
     if os.waitstatus_to_exitcode(status) != 0:
         raise RuntimeError(f"{' '.join(argv)} exited with {os.waitstatus_to_exitcode(status)}")
     return ms
+
+
+def gpu_holds(pid: int) -> dict:
+    """What process ``pid`` holds on the GPU right now: its descriptors of
+    /dev/kfd or /dev/dri/* (``readlink /proc/<pid>/fd/*``), its memory maps of
+    them, and whether KFD lists it as a process (/sys/class/kfd/kfd/proc/<pid>:
+    a registered KFD process, which amdgpu counts when it refuses a partition
+    switch).  Also every descriptor, for the record."""
+    fds = {}
+    fd_dir = f"/proc/{pid}/fd"
+    for name in sorted(os.listdir(fd_dir), key=int):
+        try:
+            fds[name] = os.readlink(f"{fd_dir}/{name}")
+        except OSError:
+            pass
+    device = {k: v for k, v in fds.items() if v == "/dev/kfd" or v.startswith("/dev/dri/")}
+    try:
+        with open(f"/proc/{pid}/maps") as f:
+            maps = [ln.strip() for ln in f if "/dev/kfd" in ln or "/dev/dri/" in ln]
+    except OSError:
+        maps = []
+    return {"device_fds": device, "device_maps": maps, "kfd_process": os.path.exists(f"/sys/class/kfd/kfd/proc/{pid}"),
+            "fds": fds}

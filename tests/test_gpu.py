@@ -179,6 +179,54 @@ def test_daemon_first_cycle_from_kfd_then_amdsmi_with_identical_labels(binary, t
     golden.check_regex_golden(files[0], TESTS / "expected-output.txt", select=lambda ln: "sriov" not in ln)
 
 
+@pytest.mark.parametrize("backend,ready", [("auto", "Using the amdsmi(persistent) manager"),
+                                           ("amdsmi", "Start running"),
+                                           ("amdsmi-per-cycle", "Start running"),
+                                           ("sysfs", "Start running")])
+def test_sleeping_daemon_holds_nothing_on_the_gpu(binary, tmp_path, backend, ready):
+    """Between cycles the daemon is no GPU client.  The reference initialises
+    NVML and shuts it down every cycle (internal/lm/nvml.go:30-33), so it
+    holds nothing while it sleeps; here the amd-smi session stays
+    initialised across cycles (persistent, the default).  While the loop
+    sleeps (--sleep-interval=5s) - after the warm start switched to amd-smi
+    for auto - the daemon holds no /dev/kfd or /dev/dri descriptor, maps
+    neither, and KFD does not list it as a process: amd-smi's session keeps
+    no device open between calls (measured r6, profiles/gpu_holds_r6.txt).
+    A render node held would make it a DRM client with its own GPU VM, a KFD
+    process one that amdgpu counts when it refuses a partition switch."""
+    import signal
+
+    from gpu_feature_discovery_amd.utils.proc import gpu_holds
+
+    args = [binary, "--sleep-interval=5s", f"--output-file={tmp_path / 'gfd'}"]
+    if backend == "amdsmi-per-cycle":
+        args += ["--backend=amdsmi", "--amdsmi-session=per-cycle"]
+    else:
+        args.append(f"--backend={backend}")
+    env = {k: v for k, v in os.environ.items() if not k.startswith("GFD_")}
+    p = subprocess.Popen(args, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+    seen, holds, err = False, None, []
+    try:
+        for line in p.stderr:
+            err.append(line)
+            seen = seen or ready in line
+            if seen and "Sleeping for" in line:
+                import time
+
+                time.sleep(0.5)  # well inside the sleep
+                holds = gpu_holds(p.pid)
+                break
+    finally:
+        p.send_signal(signal.SIGTERM)
+        _, rest = p.communicate(timeout=30)
+        err.append(rest or "")
+    assert holds is not None, "".join(err)[-3000:]
+    assert p.returncode == 0, "".join(err)[-3000:]
+    assert holds["device_fds"] == {}, holds
+    assert holds["device_maps"] == [], holds
+    assert not holds["kfd_process"], holds
+
+
 def test_daemon_sysfs_backend_oneshot(binary, tmp_path):
     out = tmp_path / "gfd"
     run_daemon(binary, "--oneshot", "--backend=sysfs", f"--output-file={out}", check=True, timeout=60)

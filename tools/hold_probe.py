@@ -25,25 +25,9 @@ import time
 from pathlib import Path
 
 REPO = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(REPO))
 
-
-def held(pid: int) -> dict:
-    fds = {}
-    fd_dir = f"/proc/{pid}/fd"
-    for name in sorted(os.listdir(fd_dir), key=int):
-        try:
-            fds[name] = os.readlink(f"{fd_dir}/{name}")
-        except OSError:
-            pass
-    device = {k: v for k, v in fds.items() if v == "/dev/kfd" or v.startswith("/dev/dri/")}
-    maps = []
-    try:
-        with open(f"/proc/{pid}/maps") as f:
-            maps = [ln.strip() for ln in f if "/dev/kfd" in ln or "/dev/dri/" in ln]
-    except OSError:
-        pass
-    return {"fds": fds, "device_fds": device, "kfd_proc": os.path.exists(f"/sys/class/kfd/kfd/proc/{pid}"),
-            "device_maps": maps[:8], "n_device_maps": len(maps)}
+from gpu_feature_discovery_amd.utils.proc import gpu_holds  # noqa: E402
 
 
 def probe(binary: str, backend: str, sleep: str, out_dir: Path, wait_for: str, timeout: float = 60) -> dict:
@@ -59,7 +43,7 @@ def probe(binary: str, backend: str, sleep: str, out_dir: Path, wait_for: str, t
             seen = seen or wait_for in line
             if seen and "Sleeping for" in line:
                 time.sleep(0.3)  # well inside the sleep
-                res = held(p.pid)
+                res = gpu_holds(p.pid)
                 break
             if time.monotonic() > deadline:
                 break

@@ -134,7 +134,8 @@ def _time_variant(args: list[str], steps: int, warmup: int) -> dict:
 
 
 _ROW_PHASES = ("submit", "init", "enumerate", "label", "facts.wait", "sriov.join", "merge", "log", "write", "other",
-               "facts.start", "facts(overlapped)", "total")
+               "facts.start", "facts(overlapped)", "write.check", "write.lease", "write.pwrite", "write.unlease",
+               "write.rename", "total")
 
 
 def _daemon_loop(binary: str, args: list[str], cycles: int, interval: str = "2ms",

@@ -251,12 +251,14 @@ bool rewrite_spare(File& spare, const std::string& contents) {
   // emptied behind our back)...
   bool usable = spare.local && ::lstat(spare.name.c_str(), &st) == 0 && st.st_dev == spare.dev &&
                 st.st_ino == spare.ino;
+  int64_t t1 = trace::now_ns();
   // ...and no reader that opened it while it was the feature file still has
   // it open: a write lease is granted only to the sole opener.  EAGAIN: a
   // reader; EINVAL/EACCES: no leases here (a file system without them,
   // leases disabled).  Then the spare is left to its reader (unlinked) and
   // this write creates a new file.
   if (usable && ::fcntl(spare.fd, F_SETLEASE, F_WRLCK) != 0) usable = false;
+  int64_t t2 = trace::now_ns();
   if (!usable) {
     close_file(spare, true);
     return false;
@@ -266,6 +268,7 @@ bool rewrite_spare(File& spare, const std::string& contents) {
   // size change at all).
   if (ok && static_cast<size_t>(st.st_size) > contents.size())
     ok = ::ftruncate(spare.fd, static_cast<off_t>(contents.size())) == 0;
+  int64_t t3 = trace::now_ns();
   // Released before the exchange: an open of the feature file must not wait
   // for a lease break.
   (void)::fcntl(spare.fd, F_SETLEASE, F_UNLCK);
@@ -273,7 +276,14 @@ bool rewrite_spare(File& spare, const std::string& contents) {
     close_file(spare, true);
     return false;
   }
-  trace::record("write.reuse", trace::now_ns() - t0);
+  int64_t t4 = trace::now_ns();
+  // The rewrite's parts (a cycle after an idle second spends most of its
+  // write here and in the exchange, write.rename).
+  trace::record("write.check", t1 - t0);
+  trace::record("write.lease", t2 - t1);
+  trace::record("write.pwrite", t3 - t2);
+  trace::record("write.unlease", t4 - t3);
+  trace::record("write.reuse", t4 - t0);
   return true;
 }
 

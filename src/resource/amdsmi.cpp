@@ -807,14 +807,25 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
   // GPU per lane is also fastest back to back).
   int64_t t_gpus = trace::now_ns();
   size_t lanes = opts_.threads > 0 ? static_cast<size_t>(opts_.threads) : gpu_lanes(gpus.size());
+  WorkerPool::ParallelStats lane_stats;
   WorkerPool::instance().parallel_for(
       gpus.size(),
       [&](size_t i) {
         if (sysfs_values && work(gpus[i], true)) return;
         work(gpus[i], false);
       },
-      lanes);
+      lanes, gpus.size() > 1 ? &lane_stats : nullptr);
   trace::record("amdsmi.gpus", trace::now_ns() - t_gpus);
+  if (gpus.size() > 1) {
+    // Where a multi-GPU snapshot's lanes spend it: the hand-off (enqueue
+    // and wake the helpers, on this thread), how late the last GPU started
+    // (a helper's wake-up), the slowest GPU's own work, and how many GPUs
+    // this thread ran itself (a count, recorded as that many milliseconds).
+    trace::record("amdsmi.lanes.handoff", lane_stats.handoff_ns);
+    trace::record("amdsmi.lanes.last_start", lane_stats.last_start_ns);
+    trace::record("amdsmi.lanes.max_gpu", lane_stats.max_item_ns);
+    trace::record("amdsmi.lanes.caller_gpus(count_as_ms)", static_cast<int64_t>(lane_stats.caller_items) * 1000000);
+  }
   // Per-GPU phase times: the slowest GPU (items may have run on pool
   // threads, whose trace records are their own).
   int64_t proc_ns = 0, caps_ns = 0;

@@ -1,5 +1,7 @@
 #include "util/pool.h"
 
+#include "util/trace.h"
+
 #include <pthread.h>
 #include <sched.h>
 
@@ -229,11 +231,21 @@ void WorkerPool::Task::run_or_wait() {
   wait();
 }
 
-void WorkerPool::parallel_for(size_t n, const std::function<void(size_t)>& fn, size_t max_parallel) {
+void WorkerPool::parallel_for(size_t n, const std::function<void(size_t)>& fn, size_t max_parallel,
+                              ParallelStats* stats) {
   if (n == 0) return;
   size_t lanes = max_parallel ? std::min(n, max_parallel) : n;
+  const int64_t t0 = stats ? trace::now_ns() : 0;
   if (lanes <= 1) {
-    for (size_t i = 0; i < n; ++i) fn(i);
+    for (size_t i = 0; i < n; ++i) {
+      int64_t s0 = stats ? trace::now_ns() : 0;
+      fn(i);
+      if (stats) {
+        stats->last_start_ns = s0 - t0;
+        stats->max_item_ns = std::max(stats->max_item_ns, trace::now_ns() - s0);
+      }
+    }
+    if (stats) stats->caller_items = n;
     return;
   }
   // Items are claimed from a shared counter; the caller waits for every
@@ -253,14 +265,25 @@ void WorkerPool::parallel_for(size_t n, const std::function<void(size_t)>& fn, s
   auto sh = std::make_shared<Shared>();
   sh->fn = &fn;
   sh->n = n;
-  auto body = [sh] {
+  // Per-item (start, duration) when `stats` is asked for; written by the
+  // item's own thread, read after every item is done.
+  struct ItemTime {
+    int64_t start = 0, ns = 0;
+    bool caller = false;
+  };
+  std::vector<ItemTime> times(stats ? n : 0);
+  ItemTime* times_p = stats ? times.data() : nullptr;
+  const std::thread::id caller = std::this_thread::get_id();
+  auto body = [sh, times_p, caller] {
     for (size_t i = sh->next++; i < sh->n; i = sh->next++) {
       std::exception_ptr err;
+      int64_t s0 = times_p ? trace::now_ns() : 0;
       try {
         (*sh->fn)(i);
       } catch (...) {
         err = std::current_exception();
       }
+      if (times_p) times_p[i] = {s0, trace::now_ns() - s0, std::this_thread::get_id() == caller};
       std::lock_guard<std::mutex> g(sh->mu);
       if (err && !sh->error) sh->error = err;
       if (++sh->done == sh->n) sh->cv.notify_all();
@@ -275,6 +298,7 @@ void WorkerPool::parallel_for(size_t n, const std::function<void(size_t)>& fn, s
     ensure_workers(queue_.size());
     for (size_t l = 1; l < lanes; ++l) wake_one();
   }
+  if (stats) stats->handoff_ns = trace::now_ns() - t0;
   body();
   std::exception_ptr error;
   {
@@ -283,6 +307,13 @@ void WorkerPool::parallel_for(size_t n, const std::function<void(size_t)>& fn, s
     // Taken out, so that a helper lane dropping the last reference to `sh`
     // later never destroys the exception this thread is handling.
     error = std::move(sh->error);
+  }
+  if (stats) {
+    for (const auto& t : times) {
+      stats->last_start_ns = std::max(stats->last_start_ns, t.start - t0);
+      stats->max_item_ns = std::max(stats->max_item_ns, t.ns);
+      stats->caller_items += t.caller;
+    }
   }
   if (error) std::rethrow_exception(error);
 }

@@ -77,7 +77,18 @@ class WorkerPool {
   // `max_parallel` (0 = unlimited) run concurrently.  Rethrows the first error.
   // Safe to call from a pool task (nested): completes even if no worker is
   // free, because the caller runs every item nobody else has claimed.
-  void parallel_for(size_t n, const std::function<void(size_t)>& fn, size_t max_parallel = 0);
+  //
+  // `stats` (optional): where the time went - the caller's hand-off (enqueue
+  // and wake the helper lanes), the latest start of any item and the longest
+  // item, all from the call's start, and how many items the caller ran.
+  struct ParallelStats {
+    int64_t handoff_ns = 0;     // the caller, before it starts on items itself
+    int64_t last_start_ns = 0;  // the last item to start
+    int64_t max_item_ns = 0;    // the longest item
+    size_t caller_items = 0;
+  };
+  void parallel_for(size_t n, const std::function<void(size_t)>& fn, size_t max_parallel = 0,
+                    ParallelStats* stats = nullptr);
 
   size_t workers() const;
   // Workers parked right now (a lane given to one of them needs no thread

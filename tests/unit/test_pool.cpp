@@ -1,5 +1,6 @@
 // WorkerPool tests (run under TSan by `make tsan`).
 #include <atomic>
+#include <chrono>
 #include <stdexcept>
 
 #include <sched.h>
@@ -26,6 +27,31 @@ TEST(Pool_ParallelForVisitsEveryIndexOnce) {
   pool.parallel_for(hits.size(), [&](size_t i) { hits[i]++; });
   for (auto& h : hits) EXPECT_EQ(h.load(), 1);
   EXPECT_TRUE(pool.workers() <= 4);
+}
+
+TEST(Pool_ParallelForStatsSayWhereTheTimeWent) {
+  WorkerPool pool(4);
+  WorkerPool::ParallelStats st;
+  std::atomic<int> ran{0};
+  pool.parallel_for(
+      8,
+      [&](size_t) {
+        auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(200);
+        while (std::chrono::steady_clock::now() < until) {
+        }
+        ++ran;
+      },
+      4, &st);
+  EXPECT_EQ(ran.load(), 8);
+  EXPECT_TRUE(st.max_item_ns >= 200000);
+  EXPECT_TRUE(st.handoff_ns >= 0 && st.last_start_ns >= 0);
+  // (0 is possible: creating the workers can outlast the helpers' claims.)
+  EXPECT_TRUE(st.caller_items <= 8);
+  // One lane: everything on the caller.
+  WorkerPool::ParallelStats one;
+  pool.parallel_for(3, [&](size_t) { ++ran; }, 1, &one);
+  EXPECT_EQ(one.caller_items, static_cast<size_t>(3));
+  EXPECT_EQ(one.handoff_ns, static_cast<int64_t>(0));
 }
 
 TEST(Pool_ParallelForPropagatesFirstError) {

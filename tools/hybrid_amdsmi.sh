@@ -28,7 +28,11 @@ for g in 1 2 4 8; do
 import json; r=json.load(open('$out/amdsmi_$g.json'))
 c=[json.loads(l) for l in open('$out/cold_$g.json') if l.startswith('{')][0]
 p=r['phases_p50_ms']
+q=c['phases_p50_ms']
+lanes=lambda p: ' '.join('%s %s' % (k.split('.')[-1], p.get(k)) for k in ('amdsmi.lanes.handoff', 'amdsmi.lanes.last_start', 'amdsmi.lanes.max_gpu', 'amdsmi.lanes.caller_gpus(count_as_ms)') if k in p)
 print('%d GPU(s): back to back p50 %.4f ms p90 %.4f ms | 1 s apart p50 %.3f ms | labels_ok=%s count=%s | enumerate %s amdsmi.gpus %s label %s write %s' % (
   $g, r['value'], r['p90_ms'], c['p50_ms'], r['labels_ok'], r['n_gpus'], p.get('enumerate'), p.get('amdsmi.gpus'),
-  p.get('label'), p.get('write')))"
+  p.get('label'), p.get('write')))
+if $g > 1:
+  print('    lanes back to back: %s | 1 s apart: %s (amdsmi.gpus %s)' % (lanes(p), lanes(q), q.get('amdsmi.gpus')))"
 done | tee $out/curve.txt

@@ -206,7 +206,8 @@ def random_node(rng: random.Random) -> Node:
         node = Node(machine=rng.choice(MACHINES), rocm_link=rng.choice(ROCM_INSTALLS), guest=True)
         for _ in range(rng.randint(1, 2)):
             g = new_gpu(node, rng)
-            g.vf, g.mode, g.nps = True, "SPX", "NPS1"
+            # Mostly VFs; sometimes a whole GPU passed through to the VM.
+            g.vf, g.mode, g.nps = rng.random() < 0.7, "SPX", "NPS1"
             node.gpus.append(g)
         return node
     node = Node(gim=rng.choice([None, "8.3.0.K"]), machine=rng.choice(MACHINES), rocm_link=rng.choice(ROCM_INSTALLS),
@@ -255,7 +256,7 @@ def mutate(live: LiveNode, rng: random.Random) -> str:
     elif kind == "gpu_add":
         g = new_gpu(n, rng)
         if n.guest:
-            g.vf, g.mode, g.nps = True, "SPX", "NPS1"
+            g.vf, g.mode, g.nps = rng.random() < 0.7, "SPX", "NPS1"
         n.gpus.append(g)
     elif kind == "gpu_remove":
         n.gpus.pop(rng.randrange(len(n.gpus)))

@@ -275,27 +275,46 @@ bool session_compute_mode(const std::string& pci, std::string* mode, int64_t* re
   return !mode->empty();
 }
 
-// The only processor at its PCI address and in SPX mode: its per-cycle
-// values are the amdgpu attributes amd-smi reads for the same calls
+// The only processor at its PCI address and in SPX mode: its values are
+// the amdgpu attributes amd-smi reads for the same calls
 // (mem_info_vram_total for memory_total(VRAM), current_compute_partition /
-// current_memory_partition for the partition getters), read directly at
-// ~4 us each.  `node_id` is the session-cached KFD node (kNoNode = not yet
-// known: queried and returned through it).  Returns false when the GPU is
-// partitioned or an attribute is missing; the caller then queries amd-smi.
+// current_memory_partition for the partition getters), read directly -
+// once per session (`kept`, AmdSmiManager::session_values_), like the
+// compute mode: none of them changes while a driver instance lives but with
+// a partition or NPS switch, which rebuilds the KFD topology, and a new
+// generation re-initialises the session.  Measured on the pool: 2.0 + 1.0
+// us per GPU per cycle for the two reads, and 1.7 us for xgmi_num_links
+// (query_gpu_caps); the 8-GPU snapshot 0.0378 -> 0.0328 ms back to back
+// (profiles/hybrid_amdsmi_scaling_r6.txt).  `node_id` is the
+// session-cached KFD node (kNoNode = not yet known: queried and returned
+// through it).  Returns false when the GPU is partitioned or an attribute
+// is missing; the caller then queries amd-smi.
 bool query_unpartitioned(AmdSmiLib& L, const std::string& root, ProcInfo& p, AmdSmiManager::KfdNodeFacts* kfd,
-                         std::string* mode, int64_t* read_ns) {
+                         std::string* mode, int64_t* read_ns, AmdSmiManager::SessionValues* kept) {
   uint32_t* node_id = &kfd->node_id;
   std::string pci = fs::join(root, "sys/bus/pci/devices/" + p.gpu_bdf);
   if (!session_compute_mode(pci, mode, read_ns) || *mode != "SPX") return false;
-  auto mp = AMDSMI_CALL("memory_partition(sysfs)", fs::attrs().read_trimmed(pci + "/current_memory_partition"));
-  if (!mp || partition_mode(*mp).empty()) return false;
-  auto vram_s = AMDSMI_CALL("memory_total(sysfs)", fs::attrs().read_trimmed(pci + "/mem_info_vram_total"));
-  auto vram = vram_s ? str::parse_uint(*vram_s) : std::nullopt;
-  if (!vram || *vram == 0) return false;
+  std::string mp_mode;
+  std::optional<uint64_t> vram;
+  if (kept && !kept->memory_partition.empty() && kept->vram) {
+    mp_mode = kept->memory_partition;
+    vram = kept->vram;
+  } else {
+    auto mp = AMDSMI_CALL("memory_partition(sysfs)", fs::attrs().read_trimmed(pci + "/current_memory_partition"));
+    mp_mode = mp ? partition_mode(*mp) : "";
+    if (mp_mode.empty()) return false;
+    auto vram_s = AMDSMI_CALL("memory_total(sysfs)", fs::attrs().read_trimmed(pci + "/mem_info_vram_total"));
+    vram = vram_s ? str::parse_uint(*vram_s) : std::nullopt;
+    if (!vram || *vram == 0) return false;
+    if (kept) {
+      kept->memory_partition = mp_mode;
+      kept->vram = *vram;
+    }
+  }
   if (*node_id == kNoNode && !query_kfd(L, p, node_id)) return false;
   query_identity(L, root, p);
   p.compute_partition = "SPX";
-  p.memory_partition = partition_mode(*mp);
+  p.memory_partition = mp_mode;
   p.vram = *vram;
   if (kfd->num_xcc == 0 && *node_id != kNoNode) kfd->num_xcc = AMDSMI_CALL("kfd_num_xcc(sysfs)", kfd_num_xcc(root, *node_id));
   p.xcds = kfd->num_xcc;
@@ -409,7 +428,8 @@ int sysfs_xgmi_links(const std::string& root, const std::string& bdf) {
 // partition modes.  Any processor handle of the GPU will do.
 void query_gpu_caps(AmdSmiLib& L, const ProcInfo& p, const std::string& root, GpuExtras& x,
                     AmdSmiManager::AvailableModes& avail) {
-  x.xgmi_links = AMDSMI_CALL("xgmi_num_links(sysfs)", sysfs_xgmi_links(root, p.gpu_bdf));
+  // Pre-filled from the session (AmdSmiManager::session_values_) when kept.
+  if (x.xgmi_links < 0) x.xgmi_links = AMDSMI_CALL("xgmi_num_links(sysfs)", sysfs_xgmi_links(root, p.gpu_bdf));
   if (x.xgmi_links < 0 && L.get_gpu_xgmi_link_status) {
     amdsmi_xgmi_link_status_t ls;
     std::memset(&ls, 0, sizeof(ls));
@@ -621,6 +641,7 @@ static std::vector<std::vector<ProcInfo>> collect_physical_gpus(AmdSmiLib& L, co
 // ---------------------------------------------------------------------------
 // AmdSmiManager
 
+
 AmdSmiManager::AmdSmiManager(AmdSmiOptions opts) : opts_(std::move(opts)) { opts_.versions.root = opts_.root; }
 
 AmdSmiManager::~AmdSmiManager() {
@@ -643,6 +664,7 @@ void AmdSmiManager::library_init() {
   identity_.clear();
   available_.clear();
   compute_mode_.clear();
+  session_values_.clear();
   ++init_count_;
 }
 
@@ -721,6 +743,7 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
     int64_t proc_ns = 0, caps_ns = 0;
     KfdNodeFacts kfd;  // session cache entry (unpartitioned GPUs)
     std::string mode;  // session cache entry: compute partition mode
+    SessionValues values;  // session cache entry: memory partition, VRAM, xGMI links
     int64_t mode_read_ns = -1;  // >= 0: read this cycle (not from the cache)
     AvailableModes avail;  // session cache entry
     std::vector<PartitionFacts> parts;  // session cache entries (partitioned GPUs), aligned with procs
@@ -740,6 +763,11 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
       if (k != kfd_node_.end()) gpus.back().kfd = k->second;
       auto a = available_.find(bdf);
       if (a != available_.end()) gpus.back().avail = a->second;
+      auto sv = session_values_.find(bdf);
+      if (sv != session_values_.end()) {
+        gpus.back().values = sv->second;
+        gpus.back().extras.xgmi_links = sv->second.xgmi_links;
+      }
       auto m = compute_mode_.find(bdf);
       if (m != compute_mode_.end()) gpus.back().mode = m->second;
       else gpus.back().mode_read_ns = 0;
@@ -773,7 +801,7 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
       auto& procs = *g.procs;
       if (fast) {
         int64_t* rd = &g.mode_read_ns;
-        bool done = procs.size() == 1 && query_unpartitioned(L, opts_.root, procs[0], &g.kfd, &g.mode, rd);
+        bool done = procs.size() == 1 && query_unpartitioned(L, opts_.root, procs[0], &g.kfd, &g.mode, rd, &g.values);
         if (!done && !query_partitioned(L, opts_.root, procs, g.parts, &g.mode, rd)) return false;
         std::sort(procs.begin(), procs.end(),
                   [](const ProcInfo& a, const ProcInfo& b) { return a.partition_id < b.partition_id; });
@@ -847,6 +875,11 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
     if (!g.extras.virtualization.empty()) virt_mode_[g.bdf] = g.extras.virtualization;
     if (g.kfd.node_id != kNoNode) kfd_node_[g.bdf] = g.kfd;
     if (!g.mode.empty()) compute_mode_[g.bdf] = g.mode;
+    if (g.values.vram && g.extras.xgmi_links >= 0) {
+      SessionValues v = g.values;
+      v.xgmi_links = g.extras.xgmi_links;
+      session_values_[g.bdf] = v;
+    }
     if (!g.avail.known)
       available_.erase(g.bdf);
     else

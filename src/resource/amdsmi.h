@@ -17,10 +17,11 @@
 //     queries run in parallel across physical GPUs on multi-GPU nodes.
 //   * the virtualization mode, fixed at driver probe, is queried once per
 //     session instead of every cycle.
-//   * the compute partition mode is read once per session (amdgpu reads an
-//     XCP register for it, which can wake the GPU), the rest of the
-//     per-cycle values (memory, memory partition mode, xGMI links, available
-//     modes) come straight from the amdgpu sysfs attributes the library
+//   * an unpartitioned GPU's values are read once per session: the compute
+//     partition mode (amdgpu reads an XCP register for it, which can wake
+//     the GPU), memory partition mode, VRAM and xGMI links change only with
+//     a partition / NPS switch or driver reload, which re-initialise the
+//     session.  They come straight from the amdgpu sysfs attributes the library
 //     itself reads for them - for an unpartitioned GPU and for the parent
 //     function of a partitioned one, whose partitions' KFD nodes and counts
 //     are kept per session; everything else goes through amd-smi.  The
@@ -77,6 +78,12 @@ class AmdSmiManager : public Manager {
   struct KfdNodeFacts {
     uint32_t node_id = 0xFFFFFFFFu;
     uint32_t num_xcc = 0;
+  };
+  // Per-session values of an unpartitioned GPU (see session_values_).
+  struct SessionValues {
+    std::string memory_partition;
+    uint64_t vram = 0;
+    int xgmi_links = -1;
   };
   // Per-session facts of one compute partition (see partition_facts_).
   struct PartitionFacts {
@@ -159,6 +166,12 @@ class AmdSmiManager : public Manager {
   // session_compute_mode in amdsmi.cpp: that read can wake the GPU).  The
   // memory partition mode is read every cycle (an NBIO register, no wake).
   std::map<std::string, std::string> compute_mode_;
+  // Memory partition mode, VRAM and xGMI link count of each unpartitioned
+  // GPU (by BDF) for the lifetime of one session: fixed for a driver
+  // instance but for a partition / NPS switch, which rebuilds the KFD
+  // topology (a new generation re-initialises the session, which clears
+  // this) - the same rule the KFD backend applies to its node properties.
+  std::map<std::string, SessionValues> session_values_;
   // PCI address of each processor (by handle) for the lifetime of one
   // session, checked once against sysfs and the processor's KFD node
   // (checked_bdf in amdsmi.cpp): amd-smi reads it through libdrm and, when

@@ -144,7 +144,9 @@ class WorkerPool {
 // Lanes for per-GPU work in one cycle: one GPU per lane, at most 8 (the
 // pool's size).  Spreading even the light SPX path (a few attribute preads
 // per GPU) over one lane per GPU measured fastest at 2, 4 and 8 GPUs, back
-// to back and after a 1 s sleep (profiles/hybrid_8gpu_scaling.txt).
+// to back and after a 1 s sleep (profiles/hybrid_8gpu_scaling.txt); again in
+// round 6 for 8 GPUs, with no per-cycle reads left: 8 lanes 0.0328 ms, 4
+// lanes 0.0335, 2 lanes 0.0379 (profiles/hybrid_amdsmi_scaling_r6.txt).
 size_t gpu_lanes(size_t n_gpus);
 
 }  // namespace gfd

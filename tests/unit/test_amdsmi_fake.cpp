@@ -176,8 +176,14 @@ TEST(AmdSmiFake_UnpartitionedGpuValuesFromSysfs) {
     EXPECT_EQ(devs[0]->GetName(), std::string("AMD Instinct MI355 OAM"));
     m.Shutdown();
   }
-  // Live values: a changed attribute shows up in the next cycle.
+  // The values are the session's: a changed attribute without a new
+  // topology generation (no real NPS switch leaves one) is not read again;
+  // with one, the session re-initialises and reads it.
   lm::write_file_atomically(pci + "/current_memory_partition", "NPS2\n", 0644);
+  m.Init();
+  EXPECT_EQ(m.GetDevices()[0]->Info().memory_partition, std::string("NPS1"));
+  m.Shutdown();
+  lm::write_file_atomically(gen, "2\n", 0644);
   m.Init();
   EXPECT_EQ(m.GetDevices()[0]->Info().memory_partition, std::string("NPS2"));
   m.Shutdown();
@@ -191,7 +197,7 @@ TEST(AmdSmiFake_UnpartitionedGpuValuesFromSysfs) {
   // With the generation a switch bumps: the session re-initialises and reads
   // the mode again.  Not SPX per sysfs: every value goes through the library
   // (whose injected failures then leave them unset).
-  lm::write_file_atomically(gen, "2\n", 0644);
+  lm::write_file_atomically(gen, "3\n", 0644);
   m.Init();
   EXPECT_EQ(m.GetDevices()[0]->GetTotalMemoryMiB(), static_cast<uint64_t>(0));
   EXPECT_EQ(m.GetDevices()[0]->Info().compute_partition, std::string(""));

@@ -331,9 +331,11 @@ def main() -> int:
         if backend == "amdsmi" and fake:
             data = f"CPU rehearsal: fake amd-smi library ({os.path.basename(fake)}), {n} scripted MI355X GPU(s)"
         elif backend == "amdsmi":
-            data = ("real MI355X, amd-smi backend: processor handles, KFD ids and identity from the persistent amd-smi "
-                    "session; memory, partition modes, xGMI links, capabilities and versions re-read from the amdgpu "
-                    "driver's attributes every step (the files amd-smi itself reads)")
+            data = ("real MI355X, amd-smi backend: processor handles, KFD ids, identity, partition modes, memory, "
+                    "xGMI links and capabilities kept for the persistent amd-smi session, which every step checks "
+                    "against the KFD topology generation (a partition/NPS switch or driver reload re-initialises "
+                    "it); driver and ROCm versions, the SR-IOV state (uevent counter) and the feature file read or "
+                    "written every step")
         elif backend == "sysfs":
             data = f"real MI355X via KFD sysfs under {root}" if root else "real MI355X via KFD sysfs"
         else:

@@ -311,17 +311,22 @@ bool query_unpartitioned(AmdSmiLib& L, const std::string& root, ProcInfo& p, Amd
       kept->vram = *vram;
     }
   }
-  if (*node_id == kNoNode && !query_kfd(L, p, node_id)) return false;
+  if (!kfd->known && *node_id == kNoNode && !query_kfd(L, p, node_id)) return false;
   query_identity(L, root, p);
   p.compute_partition = "SPX";
   p.memory_partition = mp_mode;
   p.vram = *vram;
-  if (kfd->num_xcc == 0 && *node_id != kNoNode) kfd->num_xcc = AMDSMI_CALL("kfd_num_xcc(sysfs)", kfd_num_xcc(root, *node_id));
-  p.xcds = kfd->num_xcc;
-  if (p.xcds == 0 && L.get_gpu_xcd_counter) {
-    uint16_t x = 0;
-    if (L.get_gpu_xcd_counter(p.h, &x) == AMDSMI_STATUS_SUCCESS) p.xcds = x;
+  if (!kfd->known) {
+    // The XCD count from the KFD node, else (no node: amd-smi reports none
+    // for a GPU whose node this container cannot read) the library's
+    // counter - once per session; a failed count is tried again next cycle.
+    uint32_t x = *node_id != kNoNode ? AMDSMI_CALL("kfd_num_xcc(sysfs)", kfd_num_xcc(root, *node_id)) : 0;
+    uint16_t c = 0;
+    if (x == 0 && L.get_gpu_xcd_counter && L.get_gpu_xcd_counter(p.h, &c) == AMDSMI_STATUS_SUCCESS) x = c;
+    kfd->num_xcc = x;
+    kfd->known = x != 0;
   }
+  p.xcds = kfd->num_xcc;
   fix_market_name(L, root, p);
   return true;
 }
@@ -642,6 +647,7 @@ static std::vector<std::vector<ProcInfo>> collect_physical_gpus(AmdSmiLib& L, co
 // AmdSmiManager
 
 
+
 AmdSmiManager::AmdSmiManager(AmdSmiOptions opts) : opts_(std::move(opts)) { opts_.versions.root = opts_.root; }
 
 AmdSmiManager::~AmdSmiManager() {
@@ -835,6 +841,24 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
   // GPU per lane is also fastest back to back).
   int64_t t_gpus = trace::now_ns();
   size_t lanes = opts_.threads > 0 ? static_cast<size_t>(opts_.threads) : gpu_lanes(gpus.size());
+  // Nothing to read: every GPU is an unpartitioned one whose values the
+  // session already holds (the steady state).  Its work is then a few
+  // lookups, ~0.2 us warm, and waking helper lanes costs more than it: on
+  // this thread.  8 GPUs over the host's real attributes (fake library):
+  // back to back 0.0207 vs 0.0262 ms with one lane per GPU, the GPUs'
+  // part 1.6 vs 5.0 us; 1 s apart 4-6 vs 15-20 us
+  // (profiles/hybrid_amdsmi_scaling_r6.txt).
+  if (sysfs_values && lanes > 1) {
+    bool all_cached = true;
+    for (const auto& g : gpus) {
+      all_cached = all_cached && g.procs->size() == 1 && g.mode == "SPX" && g.values.vram != 0 &&
+                   g.kfd.known && g.avail.known &&
+                   !g.extras.virtualization.empty() && g.extras.xgmi_links >= 0 && (*g.procs)[0].identified &&
+                   !is_generic_name((*g.procs)[0].market_name);
+      if (!all_cached) break;
+    }
+    if (all_cached) lanes = 1;
+  }
   WorkerPool::ParallelStats lane_stats;
   WorkerPool::instance().parallel_for(
       gpus.size(),
@@ -873,7 +897,7 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
       if (p.identified && !identity_.count(p.h))
         identity_[p.h] = Identity{p.market_name, p.vendor_id, p.device_id, p.cus, p.gfx, p.uuid};
     if (!g.extras.virtualization.empty()) virt_mode_[g.bdf] = g.extras.virtualization;
-    if (g.kfd.node_id != kNoNode) kfd_node_[g.bdf] = g.kfd;
+    if (g.kfd.known) kfd_node_[g.bdf] = g.kfd;
     if (!g.mode.empty()) compute_mode_[g.bdf] = g.mode;
     if (g.values.vram && g.extras.xgmi_links >= 0) {
       SessionValues v = g.values;

@@ -76,8 +76,9 @@ class AmdSmiManager : public Manager {
 
   // Per-session facts of an unpartitioned GPU's KFD node (see kfd_node_).
   struct KfdNodeFacts {
-    uint32_t node_id = 0xFFFFFFFFu;
+    uint32_t node_id = 0xFFFFFFFFu;  // 0xFFFFFFFF: none (amd-smi reported none, or not asked yet)
     uint32_t num_xcc = 0;
+    bool known = false;  // node and XCD count found for this session
   };
   // Per-session values of an unpartitioned GPU (see session_values_).
   struct SessionValues {

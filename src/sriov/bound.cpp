@@ -224,6 +224,11 @@ std::vector<std::string> BoundAmdPCI::list_unbound(const std::vector<std::pair<s
 bool BoundAmdPCI::still_valid(const std::vector<std::pair<std::string, uint64_t>>& bound,
                               const std::vector<std::string>& unbound) {
   if (!have_ || fell_back_ || bound != bound_ || unbound != unbound_) return false;
+  // With the bus merged in, every AMD function - a VF included, bound or
+  // not - is in `bound` or `unbound`: a VF enabled or removed changed one
+  // of the two listings.  Without it (a Job outside a VM, tests), the PFs'
+  // VF links are the check.
+  if (fallback_ && merge_unbound_) return true;
   for (const auto& d : last_) {
     if (d.sriov_totalvfs <= 0) continue;
     // The kernel links every VF it creates as <pf>/virtfn<N> and removes the

@@ -33,9 +33,10 @@
 // loop and cgroup devices) sends uevents too: measured on the pool, 4 of 11
 // cycles 1 s apart found it moved and paid a 0.25 ms re-read.  So the
 // driver directories and the bus are re-listed (names and inode numbers: a
-// function removed and re-added under the same address gets a new entry)
-// and the PFs' VFs looked at; only a difference in any of them re-reads the
-// functions.  The driver directories and the bus are read through
+// function removed and re-added under the same address gets a new entry);
+// only a difference in either re-reads the functions.  Without the bus (a
+// Job outside a VM) the PFs' VF links are looked at instead, since VFs no
+// listed driver binds are then in neither listing.  The driver directories and the bus are read through
 // descriptors kept open (fs::DirListing): no path walk, open or close per
 // check.
 #pragma once

@@ -9,7 +9,10 @@ COPY_DIR: a scratch copy of the repository (e.g. `git worktree add`), built
 once with `make build`.  Results: profiles/differential_mutations_r6.txt.
 (Round 6: M5 was the supported-mode lists keyed by the current modes -
 unobservable, deleted; it is now the session's compute mode.  M11 and M12
-are new.)
+are new.  M3 - the SR-IOV check ignoring the PFs' VF links - is gone: with the
+bus merged in (loop mode), a VF change changes the bus or driver listing, so
+the daemon no longer runs that check; without the bus it is unit-tested,
+Bound_KeptWhileUeventSeqnumUnchanged.)
 """
 import os
 import subprocess
@@ -19,7 +22,6 @@ os.chdir(sys.argv[1])
 M = [
  ("M1 SR-IOV result kept across uevents", "src/sriov/bound.cpp", "if (have_ && seqnum && *seqnum == seqnum_) {", "if (have_) {"),
  ("M2 SR-IOV check ignores the driver listing", "src/sriov/bound.cpp", "if (!have_ || fell_back_ || bound != bound_ || unbound != unbound_) return false;", "if (!have_ || fell_back_ || unbound != unbound_) return false;"),
- ("M3 SR-IOV check ignores VF links", "src/sriov/bound.cpp", "    if (d.sriov_totalvfs <= 0) continue;\n    // The kernel links", "    continue;\n    // The kernel links"),
  ("M4 amd-smi identity kept across re-init", "src/resource/amdsmi.cpp", "  identity_.clear();\n", ""),
  ("M5 amd-smi compute partition mode kept across re-init", "src/resource/amdsmi.cpp", "  compute_mode_.clear();\n", ""),
  ("M6 amdgpu module directory never reopened", "src/resource/versions.cpp", 'if (!d || d->lookup("initstate") != 0) d =', 'if (!d) d ='),

@@ -2,6 +2,8 @@
 # A/B: the 8-GPU hybrid snapshot with every value session-cached, run inline
 # on the cycle thread (GFD_INLINE_CACHED=1, default) or one lane per GPU
 # (=0); back to back (bench.py) and 1 s apart (tools/cold_cycle.py).
+# (Its experiment switch was removed from the daemon once the A/B decided - see
+# profiles/hybrid_amdsmi_scaling_r6.txt; the script records how those numbers were taken.)
 set -o pipefail
 out=gpurun_out/${1:-ab_inline}
 mkdir -p $out

@@ -1,6 +1,8 @@
 #!/bin/bash
 # A/B of the 8-GPU hybrid snapshot (fake amd-smi at the host's 8 real GPUs):
 # lanes (GFD_GPU_LANES) x session values (GFD_SESSION_VALUES), alternated.
+# (Its experiment switch was removed from the daemon once the A/B decided - see
+# profiles/hybrid_amdsmi_scaling_r6.txt; the script records how those numbers were taken.)
 set -o pipefail
 out=gpurun_out/${1:-ab_lanes}
 mkdir -p $out

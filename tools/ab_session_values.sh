@@ -1,3 +1,7 @@
+#!/bin/bash
+# A/B of values kept per amd-smi session (GFD_SESSION_VALUES=1) against reading them every cycle.
+# (Its experiment switch was removed from the daemon once the A/B decided - see
+# profiles/hybrid_amdsmi_scaling_r6.txt; the script records how those numbers were taken.)
 set -o pipefail
 mkdir -p gpurun_out/r6e
 timeout -k 10 300 python3 tools/variants_ab.py --variant base= --variant sv=GFD_SESSION_VALUES=1 --reps 5 --modes headline,cold --cold-cycles 8 > gpurun_out/r6e/ab.jsonl 2>&1 || exit 1

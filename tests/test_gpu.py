@@ -326,8 +326,8 @@ def test_vf_links_are_the_pfs_numvfs_on_the_box():
 
 def test_kept_partition_mode_lists_match_the_driver_every_cycle(native):
     """The supported compute / memory partition modes are read once per
-    amd-smi session while the current modes stay (AmdSmiManager::available_):
-    cycle after cycle they must still be what amdgpu reports."""
+    amd-smi session (AmdSmiManager::available_): cycle after cycle they must
+    still be what amdgpu reports."""
     s = native.Session(["--backend=amdsmi", "--no-timestamp", "--output-file="])
     for _ in range(4):
         s.cycle(False)
@@ -341,6 +341,52 @@ def test_kept_partition_mode_lists_match_the_driver_every_cycle(native):
                 with open(path) as f:
                     want = [m.strip() for m in f.read().split(",") if m.strip()]
                 assert d[key] == want, (d["bdf"], attr, d[key], want)
+
+
+def _kfd_gpu_nodes():
+    """(properties text) of every readable GPU node of the KFD topology."""
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    out = []
+    for n in sorted(os.listdir(base), key=lambda x: int(x) if x.isdigit() else -1):
+        try:
+            with open(f"{base}/{n}/properties") as f:
+                text = f.read()
+        except OSError:
+            continue
+        props = dict(ln.split(" ", 1) for ln in text.splitlines() if " " in ln)
+        if int(props.get("simd_count", "0")) > 0:
+            out.append(props)
+    return out
+
+
+@pytest.mark.parametrize("backend", ["amdsmi", "sysfs"])
+def test_compute_partition_read_once_and_agrees_with_the_driver(native, backend):
+    """current_compute_partition makes amdgpu read an XCP register, which can
+    wake the GPU (AMD's CLI stopped reading it by default,
+    /opt/rocm/libexec/amdsmi_cli/amdsmi_commands.py:463-466): the daemon
+    reads it when the session starts or the KFD generation changes, not on
+    steady cycles (no "compute_partition(read)" record after the first).
+    The kept mode agrees with the attribute read now, with the library's own
+    getter, and with the KFD topology: in SPX one node holds all of the GPU's
+    XCDs."""
+    s = native.Session([f"--backend={backend}", "--no-timestamp", "--output-file="])
+    reads = []
+    for _ in range(5):
+        r = s.cycle(False)
+        reads.append(sum(1 for name, _ in r["phases"] if name == "compute_partition(read)"))
+    assert reads[0] >= 1 and reads[1:] == [0, 0, 0, 0], reads
+    nodes = _kfd_gpu_nodes()
+    for d in s.devices():
+        with open(f"/sys/bus/pci/devices/{d['bdf']}/current_compute_partition") as f:
+            live = f.read().strip()
+        assert d["compute_partition"] == live, (d["bdf"], d["compute_partition"], live)
+        if live == "SPX":
+            loc = int(d["bdf"][5:7], 16) << 8 | int(d["bdf"][8:10], 16) << 3 | int(d["bdf"][11], 16)
+            node = [n for n in nodes if int(n["location_id"]) == loc]
+            assert len(node) == 1 and int(node[0]["num_xcc"]) == d["xcds"], (d["bdf"], node, d["xcds"])
+    if backend == "amdsmi":
+        lib = native.Session(["--backend=amdsmi", "--no-timestamp", "--output-file="], amdsmi_library_only=True)
+        assert [d["compute_partition"] for d in lib.devices()] == [d["compute_partition"] for d in s.devices()]
 
 
 def test_idle_cycles_on_hardware_are_attributed_and_create_no_file(binary, tmp_path):

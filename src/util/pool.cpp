@@ -6,8 +6,6 @@
 #include <sched.h>
 
 #include <algorithm>
-#include <cstdlib>
-#include <string>
 #include <atomic>
 
 #include "util/affinity.h"
@@ -111,34 +109,18 @@ void WorkerPool::follow_caller() {
   ++repins_;
 }
 
-WorkerPool::Worker* WorkerPool::wake_one() {
+void WorkerPool::wake_one() {
   // Caller holds mu_.  LIFO: the most recently parked worker is the one
   // whose core still has its stack and the task's data in cache; a FIFO
   // condition variable would rotate every task over all workers (measured:
   // the per-cycle PCI scan took 180 us instead of 86 us once 8 workers
   // existed and took turns).
-  if (idle_.empty()) return nullptr;
+  if (idle_.empty()) return;
   Worker* w = idle_.back();
   idle_.pop_back();
   w->woken = true;
   ++waking_;
-  if (!notify_unlocked()) {
-    w->cv.notify_one();
-    return nullptr;
-  }
-  return w;  // the caller notifies it once mu_ is released
-}
-
-// Experiment switch (GFD_POOL_WAKE=locked: notify while holding the pool
-// lock, the round-5 behaviour).  Notified under the lock, a woken worker
-// runs straight into the lock the waker still holds and sleeps again until
-// it is released: one more context switch per helper lane.
-bool WorkerPool::notify_unlocked() {
-  static const bool unlocked = [] {
-    const char* v = std::getenv("GFD_POOL_WAKE");
-    return !(v && std::string(v) == "locked");
-  }();
-  return unlocked;
+  w->cv.notify_one();
 }
 
 void WorkerPool::loop(Worker* w) {
@@ -186,16 +168,14 @@ WorkerPool::Task WorkerPool::submit(std::function<void()> fn) {
   t.state_ = std::make_shared<Task::State>();
   t.state_->fn = std::move(fn);
   auto st = t.state_;
-  Worker* w = nullptr;
   {
     std::lock_guard<std::mutex> g(mu_);
     queue_.emplace_back([st] {
       if (!st->claimed.exchange(true)) st->run();  // else the submitter ran it
     });
     ensure_workers(queue_.size());
-    w = wake_one();
+    wake_one();
   }
-  if (w) w->cv.notify_one();
   return t;
 }
 
@@ -207,7 +187,6 @@ std::vector<WorkerPool::Task> WorkerPool::submit_sequence(std::vector<std::funct
     tasks[i].state_->fn = std::move(fns[i]);
     states.push_back(tasks[i].state_);
   }
-  Worker* w = nullptr;
   {
     std::lock_guard<std::mutex> g(mu_);
     queue_.emplace_back([states = std::move(states)] {
@@ -215,9 +194,8 @@ std::vector<WorkerPool::Task> WorkerPool::submit_sequence(std::vector<std::funct
         if (!st->claimed.exchange(true)) st->run();
     });
     ensure_workers(queue_.size());
-    w = wake_one();
+    wake_one();
   }
-  if (w) w->cv.notify_one();
   return tasks;
 }
 
@@ -314,23 +292,12 @@ void WorkerPool::parallel_for(size_t n, const std::function<void(size_t)>& fn, s
   // Enqueue every helper lane and wake its worker under one acquisition of
   // the pool lock: per-lane submit (lock, enqueue, notify, unlock) staggers
   // the 8th lane's start by several wake-up latencies on an 8-GPU cycle.
-  Worker* woken[16];
-  size_t n_woken = 0;
   {
     std::lock_guard<std::mutex> g(mu_);
     for (size_t l = 1; l < lanes; ++l) queue_.emplace_back(body);
     ensure_workers(queue_.size());
-    for (size_t l = 1; l < lanes; ++l) {
-      Worker* w = wake_one();
-      if (!w) continue;
-      if (n_woken < sizeof(woken) / sizeof(woken[0])) {
-        woken[n_woken++] = w;
-      } else {
-        w->cv.notify_one();  // (more lanes than the array: under the lock)
-      }
-    }
+    for (size_t l = 1; l < lanes; ++l) wake_one();
   }
-  for (size_t i = 0; i < n_woken; ++i) woken[i]->cv.notify_one();
   if (stats) stats->handoff_ns = trace::now_ns() - t0;
   body();
   std::exception_ptr error;

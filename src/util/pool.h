@@ -118,11 +118,7 @@ class WorkerPool {
   };
   void ensure_workers(size_t n);
   void unpin_locked();  // caller holds mu_
-  // Marks the most recently parked worker woken (caller holds mu_) and
-  // returns it for the caller to notify after releasing mu_ (null: none
-  // parked, or already notified under the lock - notify_unlocked()).
-  Worker* wake_one();
-  static bool notify_unlocked();
+  void wake_one();
   void loop(Worker* w);
 
   size_t max_workers_;

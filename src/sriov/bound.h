@@ -35,8 +35,8 @@
 // driver directories and the bus are re-listed (names and inode numbers: a
 // function removed and re-added under the same address gets a new entry);
 // only a difference in either re-reads the functions.  Without the bus (a
-// Job outside a VM) the PFs' VF links are looked at instead, since VFs no
-// listed driver binds are then in neither listing.  The driver directories and the bus are read through
+// Job outside a VM, whose one scan keeps nothing) a moved counter always
+// re-reads them.  The driver directories and the bus are read through
 // descriptors kept open (fs::DirListing): no path walk, open or close per
 // check.
 #pragma once
@@ -70,15 +70,13 @@ class BoundAmdPCI : public AmdPCI {
 
  private:
   // Reads `bound`, the `unbound` AMD functions and the VFs of every PF
-  // among them; the directories of SR-IOV PFs go to *pf_dirs.
-  std::vector<PCIDevice> scan_bound(const std::vector<std::string>& bound, const std::vector<std::string>& unbound,
-                                    std::map<std::string, std::unique_ptr<fs::Dir>>* pf_dirs);
+  // among them.
+  std::vector<PCIDevice> scan_bound(const std::vector<std::string>& bound, const std::vector<std::string>& unbound);
   // (address, inode) of every function in the driver directories, sorted.
   std::vector<std::pair<std::string, uint64_t>> list_bound();
   // The bus's AMD functions that are not in `bound` (none without a bus source).
   std::vector<std::string> list_unbound(const std::vector<std::pair<std::string, uint64_t>>& bound);
-  // Whether last_ still describes the node: same bound and unbound
-  // functions, same VFs.
+  // Whether last_ still describes the node: same bound and unbound functions.
   bool still_valid(const std::vector<std::pair<std::string, uint64_t>>& bound, const std::vector<std::string>& unbound);
   std::string root_;
   std::shared_ptr<SysfsAmdPCI> fallback_;
@@ -90,7 +88,6 @@ class BoundAmdPCI : public AmdPCI {
   std::vector<std::string> unbound_;                      // list_unbound() of the kept result
   std::vector<PCIDevice> last_;
   std::array<fs::DirListing, 5> listings_;  // one per drivers() entry
-  std::map<std::string, std::unique_ptr<fs::Dir>> pf_dirs_;  // of last_'s SR-IOV PFs, opened by the scan
 };
 
 }  // namespace gfd::sriov

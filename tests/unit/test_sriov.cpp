@@ -693,12 +693,14 @@ TEST(Bound_GuestVFOnAmdgpu) {
 
 TEST(Bound_KeptWhileUeventSeqnumUnchanged) {
   std::string root = bound_host(3, 2);
+  std::string dev = root + "/sys/bus/pci/devices/";
   put_file(root + "/sys/kernel/uevent_seqnum", "4242\n");
-  BoundAmdPCI bound(root);
+  BoundAmdPCI bound(root, std::make_shared<SysfsAmdPCI>(root));
   EXPECT_EQ(bound.Devices().size(), static_cast<size_t>(7));
   // A VF removed behind a constant seqnum (impossible on a real kernel: the
   // removal sends a uevent) is not noticed...
-  fs::remove_all(root + "/sys/bus/pci/devices/0000:c1:00.0/virtfn1");
+  fs::remove_all(dev + "0000:c1:00.0/virtfn1");
+  fs::remove_all(dev + "0000:c1:00.2");
   EXPECT_EQ(bound.Devices().size(), static_cast<size_t>(7));
   // ...until the seqnum moves.
   put_file(root + "/sys/kernel/uevent_seqnum", "4243\n");
@@ -706,19 +708,19 @@ TEST(Bound_KeptWhileUeventSeqnumUnchanged) {
   // A counter that moved for another device (a container's veth, say):
   // the functions are not read again - here one whose class has become
   // unreadable would make a re-read fail.
-  fs::remove_all(root + "/sys/bus/pci/devices/0000:11:00.0/class");
-  fs::mkdir_all(root + "/sys/bus/pci/devices/0000:11:00.0/class");
+  fs::remove_all(dev + "0000:11:00.0/class");
+  fs::mkdir_all(dev + "0000:11:00.0/class");
   put_file(root + "/sys/kernel/uevent_seqnum", "4300\n");
   EXPECT_EQ(bound.Devices().size(), static_cast<size_t>(6));
-  fs::remove_all(root + "/sys/bus/pci/devices/0000:11:00.0/class");
-  put_file(root + "/sys/bus/pci/devices/0000:11:00.0/class", "0x120000\n");
+  fs::remove_all(dev + "0000:11:00.0/class");
+  put_file(dev + "0000:11:00.0/class", "0x120000\n");
   // A function removed and re-added under the same address (a new entry in
   // the driver directory) is read again.
   fs::remove_all(root + "/sys/bus/pci/drivers/amdgpu/0000:21:00.0");
   put_file(root + "/sys/bus/pci/drivers/amdgpu/placeholder", "");  // takes the freed inode number (kernfs never reuses one)
   bind_driver(root, "amdgpu", "0000:21:00.0");
-  put_file(root + "/sys/bus/pci/devices/0000:21:00.0/device", "0x75a0\n");
-  fs::remove_all(root + "/sys/bus/pci/devices/0000:21:00.0/uevent");
+  put_file(dev + "0000:21:00.0/device", "0x75a0\n");
+  fs::remove_all(dev + "0000:21:00.0/uevent");
   put_file(root + "/sys/kernel/uevent_seqnum", "4301\n");
   auto devs = bound.Devices();
   EXPECT_EQ(devs.size(), static_cast<size_t>(6));
@@ -727,25 +729,25 @@ TEST(Bound_KeptWhileUeventSeqnumUnchanged) {
   EXPECT_TRUE(seen);
   // VFs enabled on a PF that had none (the kernel adds the VF functions and
   // the PF's virtfn links) are seen once the seqnum moves...
-  std::string vf = root + "/sys/bus/pci/devices/0000:11:00.1";
+  std::string vf = dev + "0000:11:00.1";
   put_file(vf + "/vendor", "0x1002\n");
   put_file(vf + "/class", "0x120000\n");
   put_file(vf + "/device", "0x75b3\n");
   EXPECT_EQ(symlink("../0000:11:00.0", (vf + "/physfn").c_str()), 0);
-  EXPECT_EQ(symlink("../0000:11:00.1", (root + "/sys/bus/pci/devices/0000:11:00.0/virtfn0").c_str()), 0);
-  put_file(root + "/sys/bus/pci/devices/0000:11:00.0/sriov_numvfs", "1\n");
+  EXPECT_EQ(symlink("../0000:11:00.1", (dev + "0000:11:00.0/virtfn0").c_str()), 0);
+  put_file(dev + "0000:11:00.0/sriov_numvfs", "1\n");
   EXPECT_EQ(bound.Devices().size(), static_cast<size_t>(6));  // same seqnum: kept
   put_file(root + "/sys/kernel/uevent_seqnum", "4302\n");
   EXPECT_EQ(bound.Devices().size(), static_cast<size_t>(7));
   // ...and disabled again.
-  fs::remove_all(root + "/sys/bus/pci/devices/0000:11:00.0/virtfn0");
+  fs::remove_all(dev + "0000:11:00.0/virtfn0");
   fs::remove_all(vf);
-  put_file(root + "/sys/bus/pci/devices/0000:11:00.0/sriov_numvfs", "0\n");
+  put_file(dev + "0000:11:00.0/sriov_numvfs", "0\n");
   put_file(root + "/sys/kernel/uevent_seqnum", "4303\n");
   EXPECT_EQ(bound.Devices().size(), static_cast<size_t>(6));
-  // The check reads no sriov_numvfs (its show() waits for the device lock):
-  // the VF links are the count.  A value no link backs is not read.
-  std::string numvfs = root + "/sys/bus/pci/devices/0000:31:00.0/sriov_numvfs";
+  // Nothing reads sriov_numvfs while the listings stand (its show() waits
+  // for the device lock): a value no change of the bus backs is not read.
+  std::string numvfs = dev + "0000:31:00.0/sriov_numvfs";
   put_file(numvfs, "3\n");
   put_file(root + "/sys/kernel/uevent_seqnum", "4304\n");
   for (const auto& d : bound.Devices())
@@ -753,7 +755,18 @@ TEST(Bound_KeptWhileUeventSeqnumUnchanged) {
   put_file(numvfs, "0\n");
   // An emulated sysfs that never counts ("0") is re-read every time.
   put_file(root + "/sys/kernel/uevent_seqnum", "0\n");
-  fs::remove_all(root + "/sys/bus/pci/devices/0000:c1:00.0/virtfn0");
+  fs::remove_all(dev + "0000:c1:00.0/virtfn0");
+  fs::remove_all(dev + "0000:c1:00.1");
   EXPECT_EQ(bound.Devices().size(), static_cast<size_t>(5));
+  // Without the bus (a Job's source outside a VM) nothing is kept across a
+  // moved counter: every call re-reads.
+  BoundAmdPCI job(root);
+  put_file(root + "/sys/kernel/uevent_seqnum", "5000\n");
+  EXPECT_EQ(job.Devices().size(), static_cast<size_t>(5));
+  fs::remove_all(dev + "0000:11:00.0/class");
+  fs::mkdir_all(dev + "0000:11:00.0/class");
+  fs::remove_all(dev + "0000:11:00.0/uevent");
+  put_file(root + "/sys/kernel/uevent_seqnum", "5001\n");
+  EXPECT_THROW_MSG(job.Devices(), "unable to read PCI device class for 0000:11:00.0");
   fs::remove_all(root);
 }

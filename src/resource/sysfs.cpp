@@ -346,11 +346,11 @@ std::shared_ptr<const SysfsManager::Topology> SysfsManager::read_topology() cons
     g.bdf = resolve_parent_bdf(opts_.root, bdfs, static_cast<uint32_t>(members.front()->device_id));
     g.members = std::move(members);
     g.has_physfn = fs::exists(fs::join(opts_.root, "sys/bus/pci/devices/" + g.bdf + "/physfn"));
-    int64_t t0 = trace::now_ns();
+    int64_t r0 = trace::now_ns();
     g.compute_partition = partition_mode(
         fs::attrs().read_trimmed(fs::join(opts_.root, "sys/bus/pci/devices/" + g.bdf + "/current_compute_partition"))
             .value_or(""));
-    trace::record("compute_partition(read)", trace::now_ns() - t0);
+    trace::record("compute_partition(read)", trace::now_ns() - r0);
     topo->gpus.push_back(std::move(g));
   }
   std::sort(topo->gpus.begin(), topo->gpus.end(),

@@ -222,29 +222,7 @@ struct File {
 };
 struct Slot {
   File live, spare;
-  // gfd-tmp/, opened (O_PATH) when this slot last created a file there: the
-  // kept file's check and the exchange name it relative to this descriptor
-  // instead of walking the absolute path (two of the write's four path walks,
-  // each 5-15 us on a core that slept a second).  gfd-tmp/ removed: the
-  // kept file is gone with it and the next write creates a file, reopening
-  // this; gfd-tmp/ moved away: the exchange still puts the new file at the
-  // output path, the old one lands in the moved directory.
-  int tmp_fd = -1;
 };
-
-// Experiment switch (GFD_WRITE_DIRFD=0: absolute paths throughout).
-bool use_tmp_fd() {
-  static const bool on = [] {
-    const char* v = std::getenv("GFD_WRITE_DIRFD");
-    return !(v && std::string(v) == "0");
-  }();
-  return on;
-}
-
-const char* leaf_of(const std::string& name) {
-  size_t slash = name.rfind('/');
-  return name.c_str() + (slash == std::string::npos ? 0 : slash + 1);
-}
 
 std::mutex g_mu;
 std::map<std::string, Slot>& slots() {
@@ -264,16 +242,15 @@ void close_file(File& f, bool unlink_name) {
 
 // Rewrites the spare with `contents` if nobody else has it open; false (the
 // spare dropped) if it cannot be used.
-bool rewrite_spare(File& spare, const std::string& contents, int tmp_fd) {
+bool rewrite_spare(File& spare, const std::string& contents) {
   if (spare.fd < 0) return false;
   int64_t t0 = trace::now_ns();
   struct stat st;
   // On a local file system (a network one's readers elsewhere hold no lease
   // this kernel could see), still ours under its name (gfd-tmp/ was not
   // emptied behind our back)...
-  int named = tmp_fd >= 0 ? ::fstatat(tmp_fd, leaf_of(spare.name), &st, AT_SYMLINK_NOFOLLOW)
-                          : ::lstat(spare.name.c_str(), &st);
-  bool usable = spare.local && named == 0 && st.st_dev == spare.dev && st.st_ino == spare.ino;
+  bool usable = spare.local && ::lstat(spare.name.c_str(), &st) == 0 && st.st_dev == spare.dev &&
+                st.st_ino == spare.ino;
   int64_t t1 = trace::now_ns();
   // ...and no reader that opened it while it was the feature file still has
   // it open: a write lease is granted only to the sole opener.  EAGAIN: a
@@ -314,15 +291,11 @@ void write_kept(const std::string& path, const std::string& tmp_dir, const std::
   std::lock_guard<std::mutex> lk(g_mu);
   Slot& s = slots()[path];
   File next;
-  if (rewrite_spare(s.spare, contents, s.tmp_fd)) {
+  if (rewrite_spare(s.spare, contents)) {
     next = std::move(s.spare);
     s.spare = File{};
   } else {
     create_and_write(tmp_dir, contents, perm, &next.name, &next.fd);
-    if (use_tmp_fd()) {
-      if (s.tmp_fd >= 0) ::close(s.tmp_fd);
-      s.tmp_fd = ::open(tmp_dir.c_str(), O_PATH | O_DIRECTORY | O_CLOEXEC);
-    }
     struct stat st;
     if (::fstat(next.fd, &st) == 0) {
       next.dev = st.st_dev;
@@ -342,9 +315,7 @@ void write_kept(const std::string& path, const std::string& tmp_dir, const std::
   struct stat old;
   bool swapped = false;
   if (::lstat(path.c_str(), &old) == 0 && S_ISREG(old.st_mode)) {
-    swapped = s.tmp_fd >= 0
-                  ? ::renameat2(s.tmp_fd, leaf_of(next.name), AT_FDCWD, path.c_str(), RENAME_EXCHANGE) == 0
-                  : ::renameat2(AT_FDCWD, next.name.c_str(), AT_FDCWD, path.c_str(), RENAME_EXCHANGE) == 0;
+    swapped = ::renameat2(AT_FDCWD, next.name.c_str(), AT_FDCWD, path.c_str(), RENAME_EXCHANGE) == 0;
   }
   if (!swapped && ::rename(next.name.c_str(), path.c_str()) != 0) {
     int e = errno;
@@ -388,7 +359,6 @@ void release_kept_files() {
   for (auto& [path, s] : slots()) {
     close_file(s.spare, true);
     close_file(s.live, false);
-    if (s.tmp_fd >= 0) ::close(s.tmp_fd);
   }
   slots().clear();
 }
@@ -401,7 +371,6 @@ void release_kept_files(const std::string& path) {
   if (it == slots().end()) return;
   close_file(it->second.spare, true);
   close_file(it->second.live, false);
-  if (it->second.tmp_fd >= 0) ::close(it->second.tmp_fd);
   slots().erase(it);
 }
 

@@ -182,6 +182,7 @@ def _daemon_loop(binary: str, args: list[str], cycles: int, interval: str = "2ms
             "cpu_moves": sum(1 for a, b in zip(starts, starts[1:]) if a != b),
             "totals_ms": totals,
             "rows_ms": rows if interval != "2ms" else None,
+            "first_cycle_phases_ms": rows[0] if rows else None,
             "phases_p50_ms": {k: round(_percentile(v, 0.5), 4) for k, v in phases.items() if k != "total"}}
 
 

@@ -158,7 +158,7 @@ def _daemon_loop(binary: str, args: list[str], cycles: int, interval: str = "2ms
                 # Per cycle: the cycle thread's top-level phases and the
                 # overlapped node facts (where a slow cycle spent its time).
                 rows.append({k: float(v.rstrip("ms")) for k, v in fields.items()
-                             if k in _ROW_PHASES})
+                             if k in _ROW_PHASES or not totals[1:]})  # the first cycle: every phase
                 if len(totals) > 1:
                     for k, v in fields.items():
                         phases.setdefault(k, []).append(float(v.rstrip("ms")))

@@ -121,17 +121,6 @@ std::string SignalWatcher::name(int sig) {
 // ---------------------------------------------------------------------------
 // Labeling
 
-namespace {
-// Experiment switch (GFD_SRIOV_FIRST=0: the lookup always after the facts).
-bool sriov_first_enabled() {
-  static const bool on = [] {
-    const char* v = std::getenv("GFD_SRIOV_FIRST");
-    return !(v && std::string(v) == "0");
-  }();
-  return on;
-}
-}  // namespace
-
 CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov::Interface>& sriov,
                         const config::Config& config, const lm::LabelerPtr& timestamp, bool write) {
   trace::begin_cycle();
@@ -200,29 +189,14 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
   // a worker thread's creation, which costs more than the work (Job process
   // p50 1.05 vs 1.27 ms with the hand-off and the start-up SR-IOV prefetch,
   // same file).
-  //
-  // A cycle whose SR-IOV lookup may read the bus again (the uevent counter
-  // moved: 0.15-0.25 ms after an idle second on a 367-function host, against
-  // ~0.01 ms for a kept result) hands the worker the lookup first and takes
-  // the node facts itself, so the long part starts at once and runs beside
-  // enumeration instead of on this thread at the labels
-  // (profiles/cadence_r6.txt).
   const bool overlap = !config.oneshot();
-  const bool sriov_first = overlap && sriov_first_enabled() && sriov && sriov->MayRescan();
   WorkerPool::Task facts_task, sriov_task;
   if (overlap) {
     trace::Span span("submit");
     submitted = trace::now_ns();
-    if (sriov_first) {
-      auto seq = WorkerPool::instance().submit_sequence({scan_sriov, read_facts});
-      sriov_task = seq[0];
-      facts_task = seq[1];
-      trace::record("sriov.first", 0);
-    } else {
-      auto seq = WorkerPool::instance().submit_sequence({read_facts, scan_sriov});
-      facts_task = seq[0];
-      sriov_task = seq[1];
-    }
+    auto seq = WorkerPool::instance().submit_sequence({read_facts, scan_sriov});
+    facts_task = seq[0];
+    sriov_task = seq[1];
   }
   auto join_facts = [&]() -> const lm::NodeFacts& {
     if (!overlap) {
@@ -230,7 +204,7 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
       return facts;
     }
     int64_t s0 = trace::now_ns();
-    if (!sriov_first && sriov_task.try_run()) trace::record("sriov.self", trace::now_ns() - s0);
+    if (sriov_task.try_run()) trace::record("sriov.self", trace::now_ns() - s0);
     int64_t w0 = trace::now_ns();
     facts_task.run_or_wait();
     trace::record("facts.wait", trace::now_ns() - w0);  // inside "label"

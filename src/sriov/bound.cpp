@@ -216,23 +216,12 @@ bool BoundAmdPCI::still_valid(const std::vector<std::pair<std::string, uint64_t>
   return have_ && !fell_back_ && fallback_ && merge_unbound_ && bound == bound_ && unbound == unbound_;
 }
 
-std::optional<std::string> BoundAmdPCI::read_seqnum() const {
+std::vector<PCIDevice> BoundAmdPCI::Devices() {
+  int64_t t0 = trace::now_ns();
   // A booted kernel has sent thousands of uevents; "" or "0" is an emulated
   // sysfs that never counts, and is not trusted.
   auto seqnum = fs::attrs().read_trimmed(fs::join(root_, "sys/kernel/uevent_seqnum"));
   if (seqnum && (seqnum->empty() || *seqnum == "0")) seqnum.reset();
-  return seqnum;
-}
-
-bool BoundAmdPCI::MayRescan() {
-  if (!have_) return true;
-  auto seqnum = read_seqnum();
-  return !seqnum || *seqnum != seqnum_;
-}
-
-std::vector<PCIDevice> BoundAmdPCI::Devices() {
-  int64_t t0 = trace::now_ns();
-  auto seqnum = read_seqnum();
   if (have_ && seqnum && *seqnum == seqnum_) {
     trace::record("pci.bound(kept)", trace::now_ns() - t0);
     return fell_back_ && fallback_ ? fallback_->Devices() : last_;

@@ -62,8 +62,6 @@ class BoundAmdPCI : public AmdPCI {
   explicit BoundAmdPCI(std::string root = "/", std::shared_ptr<SysfsAmdPCI> bus = nullptr, bool merge_unbound = true)
       : root_(std::move(root)), fallback_(std::move(bus)), merge_unbound_(merge_unbound) {}
   std::vector<PCIDevice> Devices() override;
-  // Nothing kept yet, or uevent_seqnum moved since it was (one read).
-  bool MayRescan() override;
   // Whether the last Devices() came from the fallback scan.
   bool used_fallback() const { return fell_back_; }
 
@@ -74,7 +72,6 @@ class BoundAmdPCI : public AmdPCI {
   // Reads `bound`, the `unbound` AMD functions and the VFs of every PF
   // among them.
   std::vector<PCIDevice> scan_bound(const std::vector<std::string>& bound, const std::vector<std::string>& unbound);
-  std::optional<std::string> read_seqnum() const;
   // (address, inode) of every function in the driver directories, sorted.
   std::vector<std::pair<std::string, uint64_t>> list_bound();
   // The bus's AMD functions that are not in `bound` (none without a bus source).

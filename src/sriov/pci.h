@@ -79,9 +79,6 @@ class AmdPCI {
  public:
   virtual ~AmdPCI() = default;
   virtual std::vector<PCIDevice> Devices() = 0;
-  // Whether the next Devices() may have to read the bus again (false: it
-  // will return what it kept, cheaply).  A hint for scheduling only.
-  virtual bool MayRescan() { return false; }
 };
 
 // Walks <root>/sys/bus/pci/devices and keeps vendor 0x1002 display (0x03)

@@ -85,11 +85,6 @@ std::vector<Function> Lib::Devices() {
   return out;
 }
 
-bool Lib::MayRescan() {
-  std::unique_lock<std::mutex> lk(mu_, std::try_to_lock);
-  return !lk.owns_lock() || pci_->MayRescan();
-}
-
 std::optional<std::string> Lib::HostDriverVersion() {
   if (root_.empty()) return std::nullopt;
   auto v = fs::attrs().read_trimmed(fs::join(root_, "sys/module/gim/version"));

@@ -73,8 +73,6 @@ class Interface {
   // Version of the SR-IOV host driver (GIM) loaded on this node; nullopt
   // when it is not (bare metal, amdgpu-only hosts, guests).
   virtual std::optional<std::string> HostDriverVersion() { return std::nullopt; }
-  // Whether the next Devices() may be a slow one (AmdPCI::MayRescan).
-  virtual bool MayRescan() { return false; }
 };
 
 class Lib : public Interface {
@@ -85,9 +83,6 @@ class Lib : public Interface {
   std::vector<Function> Devices() override;
   // <root>/sys/module/gim/version (no root: not looked up).
   std::optional<std::string> HostDriverVersion() override;
-  // True while another scan runs (the start-up prefetch) or the source may
-  // read the bus again.
-  bool MayRescan() override;
   // Classifies one PCI function; nullopt if it is not SR-IOV relevant.
   static std::optional<Info> Classify(const PCIDevice& d);
 

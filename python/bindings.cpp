@@ -228,18 +228,17 @@ PYBIND11_MODULE(_gfd, m) {
     return py::make_tuple(ok, reason);
   });
   // The SR-IOV function sources side by side: "bound" (the functions the
-  // listed drivers bind and their VFs, nothing else), "daemon" (the loop's
-  // source: those, plus the bus's AMD functions no listed driver binds),
-  // "job" (a oneshot Job's: the bus only inside a VM) or "bus" (every
-  // function on the PCI bus, the reference's approach).
+  // listed drivers bind and their VFs, nothing else), "daemon" (the daemon's
+  // and a Job's source: those, plus - inside a VM - the bus's AMD functions
+  // no listed driver binds) or "bus" (every function on the PCI bus, the
+  // reference's approach).
   auto pci_source = [](const std::string& root, const std::string& source) -> std::shared_ptr<sriov::AmdPCI> {
     if (source == "bound") return std::make_shared<sriov::BoundAmdPCI>(root);
-    if (source == "daemon" || source == "job") {
-      bool merge = source == "daemon" || resource::running_in_vm(root);
-      return std::make_shared<sriov::BoundAmdPCI>(root, std::make_shared<sriov::SysfsAmdPCI>(root), merge);
-    }
+    if (source == "daemon")
+      return std::make_shared<sriov::BoundAmdPCI>(root, std::make_shared<sriov::SysfsAmdPCI>(root),
+                                                  resource::running_in_vm(root));
     if (source == "bus") return std::make_shared<sriov::SysfsAmdPCI>(root);
-    throw Error("unknown PCI function source '" + source + "' (expected bound, daemon, job or bus)");
+    throw Error("unknown PCI function source '" + source + "' (expected bound, daemon or bus)");
   };
   m.def(
       "pci_functions",

@@ -60,8 +60,12 @@ bool from_uevent(const fs::Dir& dir, std::string* cls, std::string* vendor, std:
   return true;
 }
 
-std::optional<PCIDevice> read_function(const std::string& path, const std::string& addr, const std::string& physfn) {
-  const fs::Dir dir(path);
+// `keep`: the function's directory, handed over when it is an SR-IOV PF (the
+// later checks look its VF links up through it).
+std::optional<PCIDevice> read_function(const std::string& path, const std::string& addr, const std::string& physfn,
+                                       std::unique_ptr<fs::Dir>* keep) {
+  auto owned = std::make_unique<fs::Dir>(path);
+  const fs::Dir& dir = *owned;
   std::string c, vendor, device;
   bool have_device = from_uevent(dir, &c, &vendor, &device);
   if (!have_device) {
@@ -87,9 +91,9 @@ std::optional<PCIDevice> read_function(const std::string& path, const std::strin
   if (d.sriov_totalvfs == 0) {
     d.sriov_numvfs = 0;  // SR-IOV capable in name only
   } else if (d.sriov_totalvfs > 0 && dir.lookup("virtfn0") == ENOENT) {
-    // The kernel links every VF it enables as virtfn<N>: no link, no VFs -
-    // a lookup instead of a sriov_numvfs read, whose show() waits for the
-    // device lock.
+    // The kernel links every VF it enables as virtfn<N> (the check below
+    // relies on it too): no link, no VFs - a lookup instead of a
+    // sriov_numvfs read, whose show() waits for the device lock.
     d.sriov_numvfs = 0;
   } else if (d.sriov_totalvfs > 0) {
     if (auto n = dir.read_trimmed("sriov_numvfs")) d.sriov_numvfs = static_cast<int>(str::parse_uint(*n).value_or(0));
@@ -109,6 +113,7 @@ std::optional<PCIDevice> read_function(const std::string& path, const std::strin
     if (!cfg.ok()) throw Error("unable to read PCI configuration space for " + addr + ": " + fs::errno_str(cfg.err));
     d.config = std::move(cfg.data);
   }
+  if (d.sriov_totalvfs > 0) *keep = std::move(owned);
   return d;
 }
 
@@ -124,7 +129,8 @@ const std::vector<std::string>& BoundAmdPCI::drivers() {
 }
 
 std::vector<PCIDevice> BoundAmdPCI::scan_bound(const std::vector<std::string>& bound_only,
-                                               const std::vector<std::string>& unbound) {
+                                               const std::vector<std::string>& unbound,
+                                               std::map<std::string, std::unique_ptr<fs::Dir>>* pf_dirs) {
   // The unbound functions are read like the bound ones: a VF among them
   // finds its PF through its physfn link, as the whole-bus scan does.
   std::vector<std::string> bound = bound_only;
@@ -136,16 +142,24 @@ std::vector<PCIDevice> BoundAmdPCI::scan_bound(const std::vector<std::string>& b
   // ms), and it is overlapped with enumeration anyway.
   constexpr size_t kChunk = 2;
   std::vector<std::optional<PCIDevice>> found(bound.size());
+  std::vector<std::unique_ptr<fs::Dir>> dirs;
+  // The old directories stay open until the new ones are: a re-read never
+  // dips below the descriptors a steady daemon holds.
+  std::map<std::string, std::unique_ptr<fs::Dir>> fresh;
   auto read_all = [&](const std::vector<std::string>& addrs, const std::vector<std::string>& pfs) {
     size_t chunks = (addrs.size() + kChunk - 1) / kChunk;
     found.assign(addrs.size(), std::nullopt);
+    dirs.clear();
+    dirs.resize(addrs.size());
     WorkerPool::instance().parallel_for(
         chunks,
         [&](size_t c) {
           for (size_t i = c * kChunk; i < std::min(addrs.size(), (c + 1) * kChunk); ++i)
-            found[i] = read_function(fs::join(devices, addrs[i]), addrs[i], pfs.empty() ? "" : pfs[i]);
+            found[i] = read_function(fs::join(devices, addrs[i]), addrs[i], pfs.empty() ? "" : pfs[i], &dirs[i]);
         },
         1 + WorkerPool::instance().idle_workers());
+    for (size_t i = 0; i < addrs.size(); ++i)
+      if (dirs[i]) fresh[addrs[i]] = std::move(dirs[i]);
   };
   read_all(bound, {});
   std::vector<PCIDevice> out;
@@ -173,14 +187,27 @@ std::vector<PCIDevice> BoundAmdPCI::scan_bound(const std::vector<std::string>& b
       if (d) out.push_back(std::move(*d));
   }
   std::sort(out.begin(), out.end(), [](const PCIDevice& a, const PCIDevice& b) { return a.address < b.address; });
+  pf_dirs->swap(fresh);
   return out;
 }
 
 std::vector<std::pair<std::string, uint64_t>> BoundAmdPCI::list_bound() {
   std::vector<std::pair<std::string, uint64_t>> bound;
+  // Which of the listed drivers are loaded (a driver that is not has no
+  // directory, and nothing is bound to it): one listing of the PCI drivers
+  // through a kept descriptor, instead of a failing open - a whole path walk,
+  // ~10-15 us after an idle second - per absent driver.
+  bool loaded_changed = true;
+  if (drivers_.read(fs::join(root_, "sys/bus/pci/drivers"), &loaded_changed) != 0) {
+    loaded_.fill(true);  // unreadable: try every driver directory
+  } else if (loaded_changed) {
+    auto names = drivers_.entries();
+    for (size_t i = 0; i < loaded_.size(); ++i)
+      loaded_[i] = std::any_of(names.begin(), names.end(), [&](const auto& e) { return e.first == drivers()[i]; });
+  }
   for (size_t i = 0; i < listings_.size(); ++i) {
     bool changed = false;
-    // A driver that is not loaded has no directory: nothing bound to it.
+    if (!loaded_[i]) continue;
     if (listings_[i].read(fs::join(root_, "sys/bus/pci/drivers/" + drivers()[i]), &changed) != 0) continue;
     for (auto& e : listings_[i].entries())
       if (is_pci_address(e.first)) bound.push_back(std::move(e));
@@ -208,12 +235,39 @@ std::vector<std::string> BoundAmdPCI::list_unbound(const std::vector<std::pair<s
 
 bool BoundAmdPCI::still_valid(const std::vector<std::pair<std::string, uint64_t>>& bound,
                               const std::vector<std::string>& unbound) {
-  // With the bus merged in, every AMD function - a VF included, bound or not
-  // - is in `bound` or `unbound`: a function added, removed, bound or
-  // unbound, and a VF enabled or disabled, changes one of the two listings.
-  // Without the bus (a Job's one scan outside a VM) nothing is kept across
-  // a moved counter.
-  return have_ && !fell_back_ && fallback_ && merge_unbound_ && bound == bound_ && unbound == unbound_;
+  if (!have_ || fell_back_ || bound != bound_ || unbound != unbound_) return false;
+  // With the bus merged in (a VM), every AMD function - a VF included,
+  // bound or not - is in `bound` or `unbound`: a VF enabled or removed
+  // changed one of the two listings.  Without it (a host), the PFs' VF
+  // links are the check.
+  if (fallback_ && merge_unbound_) return true;
+  for (const auto& d : last_) {
+    if (d.sriov_totalvfs <= 0) continue;
+    // The kernel links every VF it creates as <pf>/virtfn<N> and removes the
+    // links with the VFs, so the links are the PF's NumVFs: a lookup in the
+    // directory the scan opened instead of a sriov_numvfs read (whose show()
+    // also takes the device lock).  8 PFs: 0.019 ms vs 0.028-0.030 ms, and
+    // no first check that opens 8 attribute files, 0.14-0.17 ms
+    // (profiles/sriov_check_r4.txt).
+    if (d.sriov_numvfs <= 0) {
+      // No VFs: one lookup, through the PF's directory the scan opened.
+      auto& dir = pf_dirs_[d.address];
+      if (!dir) dir = std::make_unique<fs::Dir>(d.path);
+      if (dir->err() != 0 || dir->lookup("virtfn0") != ENOENT) return false;  // (a PF gone: re-read)
+      continue;
+    }
+    // VFs: the same links to the same functions (a VF removed on its own
+    // with `remove` leaves NumVFs as it was).
+    std::vector<std::string> now, kept;
+    for (const auto& e : fs::list_dir(d.path))
+      if (e.rfind("virtfn", 0) == 0) now.push_back(fs::basename(fs::read_link(fs::join(d.path, e))));
+    for (const auto& v : last_)
+      if (v.physfn == d.address) kept.push_back(v.address);
+    std::sort(now.begin(), now.end());
+    std::sort(kept.begin(), kept.end());
+    if (now != kept) return false;
+  }
+  return true;
 }
 
 std::vector<PCIDevice> BoundAmdPCI::Devices() {
@@ -236,6 +290,7 @@ std::vector<PCIDevice> BoundAmdPCI::Devices() {
     seqnum_ = *seqnum;
     int64_t t_end = trace::now_ns();
     trace::record("pci.list", t_list - t0);
+    trace::record("pci.vfs", t_end - t_list);
     trace::record("pci.bound(checked)", t_end - t0);
     return last_;
   }
@@ -246,12 +301,13 @@ std::vector<PCIDevice> BoundAmdPCI::Devices() {
     // on the bus.
     fell_back_ = true;
     last_.clear();
+    pf_dirs_.clear();
     if (fallback_) out = fallback_->Devices();
   } else {
     int64_t t1 = trace::now_ns();
     std::vector<std::string> names;
     for (const auto& e : bound) names.push_back(e.first);
-    out = scan_bound(names, unbound);
+    out = scan_bound(names, unbound, &pf_dirs_);
     trace::record("pci.bound", trace::now_ns() - t1);
     fell_back_ = false;
     last_ = out;

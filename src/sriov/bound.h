@@ -16,15 +16,22 @@
 //
 // When neither driver binds anything - an SR-IOV guest whose amdgpu is not
 // loaded, or a node without AMD GPUs - the whole-bus scan (SysfsAmdPCI) is
-// the answer.  Otherwise the whole bus still decides which AMD functions
-// exist: whenever uevent_seqnum moved, the AMD display / accelerator
-// functions of the bus (SysfsAmdPCI::amd_functions: one listing through a
-// kept descriptor, identities only of functions not seen before) that no
-// listed driver binds - a PF handed to vfio-pci, a guest VF amdgpu failed to
-// probe - are read too, so the result is the reference's whole-bus result
-// (pciutil.go:70-112) function for function.  The first such pass reads
-// every function's vendor (~1.3 ms on an 8-GPU host); a daemon pays it in
-// its start-up prefetch, on a worker.
+// the answer.  Inside a VM (`merge_unbound`, the CPU's hypervisor flag) the
+// bus also decides which AMD functions exist: whenever uevent_seqnum moved,
+// the AMD display / accelerator functions of the bus that no listed driver
+// binds - a guest VF amdgpu failed to probe - are read too
+// (SysfsAmdPCI::amd_functions: one listing through a kept descriptor,
+// identities only of functions not seen before), so the result is the
+// reference's whole-bus result (pciutil.go:70-112) function for function.
+// A VM's bus is small.  On a host, listing the bus costs 0.1-0.2 ms after an
+// idle second (367 functions, profiles/cadence_r6.txt) on every cycle whose
+// counter moved - most cycles of a busy node at the deployed cadence - and
+// finds nothing the labels use: every function with SR-IOV state is a PF
+// whose driver enabled its VFs (gim, vfio-pci, pci-pf-stub: listed) or a VF
+// that PF's `virtfn*` links name.  So a host is read through the drivers;
+// an unbound AMD function without VFs (a GPU amdgpu failed to probe) is the
+// one thing it does not list, and the SR-IOV labeler classifies such a
+// function as nothing.
 //
 // Like the full scan, the result is kept while /sys/kernel/uevent_seqnum is
 // unchanged: binding, unbinding, adding or removing a function (VFs
@@ -32,13 +39,11 @@
 // enough to re-read everything - every container start on a node (veth,
 // loop and cgroup devices) sends uevents too: measured on the pool, 4 of 11
 // cycles 1 s apart found it moved and paid a 0.25 ms re-read.  So the
-// driver directories and the bus are re-listed (names and inode numbers: a
-// function removed and re-added under the same address gets a new entry);
-// only a difference in either re-reads the functions.  Without the bus (a
-// Job outside a VM, whose one scan keeps nothing) a moved counter always
-// re-reads them.  The driver directories and the bus are read through
-// descriptors kept open (fs::DirListing): no path walk, open or close per
-// check.
+// driver directories (and in a VM the bus) are re-listed (names and inode
+// numbers: a function removed and re-added under the same address gets a
+// new entry), and on a host the PFs' VF links looked at; only a difference
+// re-reads the functions.  Directories are read through descriptors kept
+// open (fs::DirListing): no path walk, open or close per check.
 #pragma once
 
 #include <array>
@@ -70,13 +75,15 @@ class BoundAmdPCI : public AmdPCI {
 
  private:
   // Reads `bound`, the `unbound` AMD functions and the VFs of every PF
-  // among them.
-  std::vector<PCIDevice> scan_bound(const std::vector<std::string>& bound, const std::vector<std::string>& unbound);
+  // among them; the directories of SR-IOV PFs go to *pf_dirs.
+  std::vector<PCIDevice> scan_bound(const std::vector<std::string>& bound, const std::vector<std::string>& unbound,
+                                    std::map<std::string, std::unique_ptr<fs::Dir>>* pf_dirs);
   // (address, inode) of every function in the driver directories, sorted.
   std::vector<std::pair<std::string, uint64_t>> list_bound();
   // The bus's AMD functions that are not in `bound` (none without a bus source).
   std::vector<std::string> list_unbound(const std::vector<std::pair<std::string, uint64_t>>& bound);
-  // Whether last_ still describes the node: same bound and unbound functions.
+  // Whether last_ still describes the node: same bound and unbound
+  // functions, same VFs.
   bool still_valid(const std::vector<std::pair<std::string, uint64_t>>& bound, const std::vector<std::string>& unbound);
   std::string root_;
   std::shared_ptr<SysfsAmdPCI> fallback_;
@@ -88,6 +95,9 @@ class BoundAmdPCI : public AmdPCI {
   std::vector<std::string> unbound_;                      // list_unbound() of the kept result
   std::vector<PCIDevice> last_;
   std::array<fs::DirListing, 5> listings_;  // one per drivers() entry
+  fs::DirListing drivers_;                   // sys/bus/pci/drivers
+  std::array<bool, 5> loaded_{};             // drivers() entries with a directory there
+  std::map<std::string, std::unique_ptr<fs::Dir>> pf_dirs_;  // of last_'s SR-IOV PFs, opened by the scan
 };
 
 }  // namespace gfd::sriov

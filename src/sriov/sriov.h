@@ -92,13 +92,10 @@ class Lib : public Interface {
   std::mutex mu_;
 };
 
-// The node's SR-IOV functions (sriov/bound.h).  `oneshot`: a Job, whose one
-// cycle would pay the whole bus's first pass (~1.6 ms on an 8-GPU host,
-// profiles/sriov_bus_pass_r6.txt): it looks for AMD functions no listed
-// driver binds only inside a VM (a small bus), where such a function can be
-// an SR-IOV VF; on a host every function that can carry SR-IOV state - a PF
-// with VFs enabled, bound to a listed driver, and the VFs its links name -
-// is found through the drivers.
+// The node's SR-IOV functions (sriov/bound.h): the functions the listed
+// drivers bind and their VFs, and inside a VM also the bus's AMD functions
+// no listed driver binds.  `oneshot` (a Job) changes nothing: a Job and the
+// daemon read the same sources.
 std::shared_ptr<Interface> new_sriov_lib(const std::string& root, bool oneshot = false);
 std::shared_ptr<Interface> new_mock_sriov();
 // A library that reports no functions (e.g. when PCI scanning is disabled).

@@ -153,17 +153,18 @@ def test_bound_sriov_source_matches_the_whole_bus(native, tmp_path, kind):
                                                               privileged=kind.endswith("privileged")))
     bound = native.pci_functions(str(root), "bound")
     bus = native.pci_functions(str(root), "bus")
-    # The daemon's source is the bus's, function for function, on every node.
-    assert native.pci_functions(str(root), "daemon") == bus
-    job = native.pci_functions(str(root), "job")
+    daemon = native.pci_functions(str(root), "daemon")
+    # The daemon's labels are the bus scan's on every node shape.
+    assert native.sriov_labels(str(root), "daemon") == native.sriov_labels(str(root), "bus")
     if kind == "host-unbound-gpu":
-        # A Job on a host does not read the bus: the unbound GPU (no VFs, so
-        # no SR-IOV state) is not among its functions - its labels are the
-        # same, since the SR-IOV labeler classifies it as nothing.
-        assert len(bus) == 2 and len(bound) == len(job) == 1
-        assert native.sriov_labels(str(root), "job") == native.sriov_labels(str(root), "bus") == {}
+        # On a host the daemon does not read the bus: the unbound GPU (no VFs,
+        # so no SR-IOV state) is not among its functions, and the labeler
+        # classifies it as nothing either way.
+        assert len(bus) == 2 and len(bound) == len(daemon) == 1
+        assert native.sriov_labels(str(root), "daemon") == {}
         return
-    assert job == bus
+    # Everywhere else, function for function (a VM reads its bus too).
+    assert daemon == bus
     if kind == "guest-vf-unbound":
         assert bound == [] and len(bus) == 1
         return

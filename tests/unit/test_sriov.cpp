@@ -658,6 +658,29 @@ TEST(Bound_WithTheBusSeesAGuestVfAmdgpuDidNotProbe) {
   fs::remove_all(root);
 }
 
+TEST(Bound_ADriverLoadedLaterIsListed) {
+  // Only the listed drivers that are loaded are read (one listing of
+  // sys/bus/pci/drivers says which); one that loads later - vfio-pci taking
+  // a GPU for a VM - is read from then on.
+  std::string root = bound_host(3, 0);
+  put_file(root + "/sys/kernel/uevent_seqnum", "10\n");
+  BoundAmdPCI bound(root);
+  EXPECT_EQ(bound.Devices().size(), static_cast<size_t>(5));
+  fs::remove_all(root + "/sys/bus/pci/drivers/amdgpu/0000:41:00.0");
+  bind_driver(root, "vfio-pci", "0000:41:00.0");
+  put_file(root + "/sys/kernel/uevent_seqnum", "11\n");
+  auto devs = bound.Devices();
+  EXPECT_EQ(devs.size(), static_cast<size_t>(5));
+  bool seen = false;
+  for (const auto& d : devs) seen |= d.address == "0000:41:00.0";
+  EXPECT_TRUE(seen);
+  // Unloaded again: its directory is gone, nothing is read from it.
+  fs::remove_all(root + "/sys/bus/pci/drivers/vfio-pci");
+  put_file(root + "/sys/kernel/uevent_seqnum", "12\n");
+  EXPECT_EQ(bound.Devices().size(), static_cast<size_t>(4));
+  fs::remove_all(root);
+}
+
 TEST(Bound_FallsBackToTheBusWhenNothingIsBound) {
   // A guest whose amdgpu is not loaded: its VF is on the bus, bound to nothing.
   std::string root = pci_host(5, 0);
@@ -758,15 +781,28 @@ TEST(Bound_KeptWhileUeventSeqnumUnchanged) {
   fs::remove_all(dev + "0000:c1:00.0/virtfn0");
   fs::remove_all(dev + "0000:c1:00.1");
   EXPECT_EQ(bound.Devices().size(), static_cast<size_t>(5));
-  // Without the bus (a Job's source outside a VM) nothing is kept across a
-  // moved counter: every call re-reads.
-  BoundAmdPCI job(root);
+  // Without the bus (a host): the driver listings and the PFs' VF links are
+  // the check.  Nothing is re-read while they stand...
+  BoundAmdPCI host(root);
   put_file(root + "/sys/kernel/uevent_seqnum", "5000\n");
-  EXPECT_EQ(job.Devices().size(), static_cast<size_t>(5));
+  EXPECT_EQ(host.Devices().size(), static_cast<size_t>(5));
   fs::remove_all(dev + "0000:11:00.0/class");
   fs::mkdir_all(dev + "0000:11:00.0/class");
   fs::remove_all(dev + "0000:11:00.0/uevent");
   put_file(root + "/sys/kernel/uevent_seqnum", "5001\n");
-  EXPECT_THROW_MSG(job.Devices(), "unable to read PCI device class for 0000:11:00.0");
+  EXPECT_EQ(host.Devices().size(), static_cast<size_t>(5));
+  fs::remove_all(dev + "0000:11:00.0/class");
+  put_file(dev + "0000:11:00.0/class", "0x120000\n");
+  // ...and VFs enabled behind unchanged driver listings are seen through
+  // their PF's links.
+  std::string vf31 = dev + "0000:31:00.1";
+  put_file(vf31 + "/vendor", "0x1002\n");
+  put_file(vf31 + "/class", "0x120000\n");
+  put_file(vf31 + "/device", "0x75b3\n");
+  EXPECT_EQ(symlink("../0000:31:00.0", (vf31 + "/physfn").c_str()), 0);
+  EXPECT_EQ(symlink("../0000:31:00.1", (dev + "0000:31:00.0/virtfn0").c_str()), 0);
+  put_file(dev + "0000:31:00.0/sriov_numvfs", "1\n");
+  put_file(root + "/sys/kernel/uevent_seqnum", "5002\n");
+  EXPECT_EQ(host.Devices().size(), static_cast<size_t>(6));
   fs::remove_all(root);
 }

@@ -9,10 +9,8 @@ COPY_DIR: a scratch copy of the repository (e.g. `git worktree add`), built
 once with `make build`.  Results: profiles/differential_mutations_r6.txt.
 (Round 6: M5 was the supported-mode lists keyed by the current modes -
 unobservable, deleted; it is now the session's compute mode.  M11 and M12
-are new.  M3 - the SR-IOV check ignoring the PFs' VF links - is gone: with the
-bus merged in (loop mode), a VF change changes the bus or driver listing, so
-the daemon no longer runs that check; without the bus it is unit-tested,
-Bound_KeptWhileUeventSeqnumUnchanged.)
+are new; M11 applies to VMs, the only nodes whose bus the SR-IOV source
+reads.)
 """
 import os
 import subprocess
@@ -21,14 +19,15 @@ import sys
 os.chdir(sys.argv[1])
 M = [
  ("M1 SR-IOV result kept across uevents", "src/sriov/bound.cpp", "if (have_ && seqnum && *seqnum == seqnum_) {", "if (have_) {"),
- ("M2 SR-IOV check ignores the driver listing", "src/sriov/bound.cpp", "merge_unbound_ && bound == bound_ && unbound == unbound_;", "merge_unbound_ && unbound == unbound_;"),
+ ("M2 SR-IOV check ignores the driver listing", "src/sriov/bound.cpp", "if (!have_ || fell_back_ || bound != bound_ || unbound != unbound_) return false;", "if (!have_ || fell_back_ || unbound != unbound_) return false;"),
+ ("M3 SR-IOV check ignores VF links", "src/sriov/bound.cpp", "    if (d.sriov_totalvfs <= 0) continue;\n    // The kernel links", "    continue;\n    // The kernel links"),
  ("M4 amd-smi identity kept across re-init", "src/resource/amdsmi.cpp", "  identity_.clear();\n", ""),
  ("M5 amd-smi compute partition mode kept across re-init", "src/resource/amdsmi.cpp", "  compute_mode_.clear();\n", ""),
  ("M6 amdgpu module directory never reopened", "src/resource/versions.cpp", 'if (!d || d->lookup("initstate") != 0) d =', 'if (!d) d ='),
  ("M7 sysfs topology kept across generations", "src/resource/sysfs.cpp", "if (!generation_.empty() && generation_ == cached_generation_ && cached_) {", "if (cached_) {"),
  ("M8 amd-smi session kept across generations", "src/resource/amdsmi.cpp", "    if (gen != generation_) {", "    if (false) {"),
  ("M9 DMI kept for any file", "src/util/fs.cpp", "  kept->emplace(path, constant ? std::optional<std::string>(r.data) : std::nullopt);", "  kept->emplace(path, std::optional<std::string>(r.data));"),
- ("M11 SR-IOV check ignores the bus's unbound functions", "src/sriov/bound.cpp", "merge_unbound_ && bound == bound_ && unbound == unbound_;", "merge_unbound_ && bound == bound_;"),
+ ("M11 SR-IOV check ignores the bus's unbound functions (VMs)", "src/sriov/bound.cpp", "bound != bound_ || unbound != unbound_) return false;", "bound != bound_) return false;"),
  ("M12 amd-smi session values kept across re-init", "src/resource/amdsmi.cpp", "  session_values_.clear();\n", ""),
  ("M10 version file kept across replacement", "src/util/fs.cpp", "if (it != checked_.end() && it->second.dev == static_cast<uint64_t>(st.st_dev) &&\n        it->second.ino == static_cast<uint64_t>(st.st_ino))", "if (it != checked_.end())"),
 ]

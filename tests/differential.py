@@ -200,15 +200,22 @@ def new_gpu(node: Node, rng: random.Random) -> Gpu:
                mode=rng.choice(MODES), nps=rng.choice(NPS))
 
 
+def guest_gpu(node: Node, rng: random.Random) -> Gpu:
+    """A GPU of a VM: mostly a VF, sometimes a whole GPU passed through; a VF
+    that amdgpu failed to probe stays unbound."""
+    g = new_gpu(node, rng)
+    g.vf, g.mode, g.nps = rng.random() < 0.7, "SPX", "NPS1"
+    if g.vf and rng.random() < 0.25:
+        g.bound = False
+    return g
+
+
 def random_node(rng: random.Random) -> Node:
     if rng.random() < 0.15:
         # A guest VM: its GPUs are VFs in SPX, it runs no SR-IOV host driver.
         node = Node(machine=rng.choice(MACHINES), rocm_link=rng.choice(ROCM_INSTALLS), guest=True)
         for _ in range(rng.randint(1, 2)):
-            g = new_gpu(node, rng)
-            # Mostly VFs; sometimes a whole GPU passed through to the VM.
-            g.vf, g.mode, g.nps = rng.random() < 0.7, "SPX", "NPS1"
-            node.gpus.append(g)
+            node.gpus.append(guest_gpu(node, rng))
         return node
     node = Node(gim=rng.choice([None, "8.3.0.K"]), machine=rng.choice(MACHINES), rocm_link=rng.choice(ROCM_INSTALLS),
                 layout=rng.choice(["function", "function", "shared"]))
@@ -229,7 +236,9 @@ def mutate(live: LiveNode, rng: random.Random) -> str:
     if kind in ("partition", "nps", "vfs", "gpu_remove", "bind") and not n.gpus:
         kind = "gpu_add"
     if n.guest and kind in ("partition", "nps", "vfs"):
-        kind = "uevent"  # a VF's modes are the host's business
+        # A VF's modes are the host's business; what a guest sees change is
+        # VFs hot-plugged, removed, probed or not.
+        kind = rng.choice(["gpu_add", "gpu_remove", "bind", "uevent"]) if n.gpus else "gpu_add"
     recreate: tuple[str, ...] = ()
     reset = False
     if kind == "partition":
@@ -254,10 +263,7 @@ def mutate(live: LiveNode, rng: random.Random) -> str:
             g = rng.choice(capable)
             g.vfs = rng.choice([v for v in (0, 1, 2, 3) if v != g.vfs])
     elif kind == "gpu_add":
-        g = new_gpu(n, rng)
-        if n.guest:
-            g.vf, g.mode, g.nps = rng.random() < 0.7, "SPX", "NPS1"
-        n.gpus.append(g)
+        n.gpus.append(guest_gpu(n, rng) if n.guest else new_gpu(n, rng))
     elif kind == "gpu_remove":
         n.gpus.pop(rng.randrange(len(n.gpus)))
     elif kind == "module_reload":
@@ -285,6 +291,40 @@ def mutate(live: LiveNode, rng: random.Random) -> str:
         n.seqnum += rng.randint(1, 40)  # a container's veth, a loop device...
     live.apply(recreate=recreate, reset=reset)
     return kind
+
+
+def scripted_sequences() -> list[tuple[Node, list]]:
+    """Fixed sequences for changes the random ones reach too rarely to guard
+    (each step: a function(live) that changes the node and returns a name).
+    A VM with a whole GPU passed through, to which a VF is hot-plugged that
+    amdgpu does not probe, then removed; then one that amdgpu probes, then
+    unbinds: only the bus shows the unbound VF (sriov/bound.h)."""
+    def vm() -> Node:
+        node = Node(guest=True)
+        node.gpus.append(Gpu(bus=0x10, unique=0x1111, serial=10**11 + 1))
+        return node
+
+    def add_vf(bound: bool):
+        def step(live: LiveNode) -> str:
+            n = live.node
+            n.gpus.append(Gpu(bus=0x20, unique=0x2222, serial=10**11 + 2, vf=True, bound=bound))
+            live.apply()
+            return "gpu_add"
+        return step
+
+    def remove_vf(live: LiveNode) -> str:
+        live.node.gpus = [g for g in live.node.gpus if not g.vf]
+        live.apply()
+        return "gpu_remove"
+
+    def unbind_vf(live: LiveNode) -> str:
+        for g in live.node.gpus:
+            if g.vf:
+                g.bound = False
+        live.apply()
+        return "bind"
+
+    return [(vm(), [add_vf(False), remove_vf, add_vf(True), unbind_vf, remove_vf])]
 
 
 # ---------------------------------------------------------------------------

@@ -14,7 +14,9 @@ under the three strategies, and the DaemonSet's default `auto` (KFD first,
 amd-smi once ready) - must equal a fresh `--oneshot` process's byte for
 byte.
 
-GFD_DIFF_SEQUENCES / GFD_DIFF_STEPS / GFD_DIFF_SEED size a longer run.
+GFD_DIFF_SEQUENCES / GFD_DIFF_STEPS / GFD_DIFF_SEED size a longer run.  A
+few scripted sequences (differential.scripted_sequences) run first: changes
+the random ones reach too rarely to guard.
 """
 
 from __future__ import annotations
@@ -39,10 +41,12 @@ def _run(binary: str, tmp_path, sequences: int, steps: int, seed: int) -> dict:
     pool = concurrent.futures.ThreadPoolExecutor(max_workers=7)
     counts: dict[str, int] = {}
     compared = 0
+    scripted = dd.scripted_sequences()
     try:
-        for s in range(sequences):
+        for s in range(len(scripted) + sequences):
             root = tmp_path / f"n{s}"
-            live = dd.LiveNode(root, dd.random_node(rng))
+            script = scripted[s][1] if s < len(scripted) else None
+            live = dd.LiveNode(root, scripted[s][0] if script else dd.random_node(rng))
             # The DaemonSet's default backend too: KFD first, amd-smi once it is
             # ready and agrees; a fresh Job labels it from KFD.
             ids = [(b, st) for b in BACKENDS for st in STRATEGIES] + [("auto", "single")]
@@ -51,9 +55,9 @@ def _run(binary: str, tmp_path, sequences: int, steps: int, seed: int) -> dict:
             for k in ids:
                 assert server.call(op="open", id=f"{k[0]}/{k[1]}", args=dd.daemon_args(root, *k, out[k]))["ok"]
             history = ["initial"]
-            for step in range(steps):
+            for step in range(len(script) + 1 if script else steps):
                 if step:
-                    history.append(dd.mutate(live, rng))
+                    history.append(script[step - 1](live) if script else dd.mutate(live, rng))
                     counts[history[-1]] = counts.get(history[-1], 0) + 1
                     server.call(op="stage", spec=live.fake_spec())
                 env = {**os.environ, "GFD_AMDSMI_LIBRARY": str(FAKE), "GFD_FAKE_AMDSMI_SPEC": live.fake_spec()}
@@ -81,7 +85,8 @@ def test_long_lived_sessions_label_like_a_fresh_process(binary, tmp_path):
     steps = int(os.environ.get("GFD_DIFF_STEPS", "5"))
     seed = int(os.environ.get("GFD_DIFF_SEED", "20261018"))
     r = _run(binary, tmp_path, sequences, steps, seed)
-    assert r["compared"] == sequences * steps * (len(STRATEGIES) * len(BACKENDS) + 1)
+    scripted_steps = sum(len(script) + 1 for _, script in dd.scripted_sequences())
+    assert r["compared"] == (sequences * steps + scripted_steps) * (len(STRATEGIES) * len(BACKENDS) + 1)
     # Every kind of change was exercised.
     assert set(r["changes"]) == {"partition", "nps", "vfs", "gpu_add", "gpu_remove", "module_reload", "rocm_repoint",
                                  "rocm_rewrite", "rocm_replace", "dmi", "bind", "uevent"}, r["changes"]

@@ -119,7 +119,7 @@ class Session {
     // As cli::start does: the first SR-IOV scan runs on a worker while the
     // backend is selected (and, here, while the caller does whatever it does
     // before the first cycle).
-    sriov_ = sriov::new_sriov_lib(config_.sysfs_root(), config_.oneshot());
+    sriov_ = sriov::new_sriov_lib(config_.sysfs_root());
     auto lib = sriov_;
     if (!config_.oneshot())
       prefetch_ = WorkerPool::instance().submit([lib] {

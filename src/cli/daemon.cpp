@@ -357,7 +357,7 @@ void start(const Context& ctx, SignalWatcher& sigs) {
     // fresh process) starts now, on a worker, while this thread logs the
     // configuration and selects the backend; the first cycle then finds its
     // result kept (unchanged uevent counter) or waits for it to finish.
-    auto sriov = sriov::new_sriov_lib(c.sysfs_root(), c.oneshot());
+    auto sriov = sriov::new_sriov_lib(c.sysfs_root());
     struct Prefetch {  // never outlives this iteration (an error exits the process)
       WorkerPool::Task task;
       ~Prefetch() { task.cancel_or_wait(); }

@@ -99,10 +99,9 @@ class EmptyLib : public Interface {
 };
 }  // namespace
 
-std::shared_ptr<Interface> new_sriov_lib(const std::string& root, bool oneshot) {
+std::shared_ptr<Interface> new_sriov_lib(const std::string& root) {
   // The functions the listed drivers bind and the VFs of those PFs, plus the
   // bus's AMD functions no listed driver binds (sriov/bound.h).
-  (void)oneshot;  // the daemon and a Job read the same sources (sriov/bound.h)
   bool merge_unbound = resource::running_in_vm(root);
   return std::make_shared<Lib>(std::make_shared<BoundAmdPCI>(root, std::make_shared<SysfsAmdPCI>(root), merge_unbound),
                                root);

@@ -94,9 +94,8 @@ class Lib : public Interface {
 
 // The node's SR-IOV functions (sriov/bound.h): the functions the listed
 // drivers bind and their VFs, and inside a VM also the bus's AMD functions
-// no listed driver binds.  `oneshot` (a Job) changes nothing: a Job and the
-// daemon read the same sources.
-std::shared_ptr<Interface> new_sriov_lib(const std::string& root, bool oneshot = false);
+// no listed driver binds.  A Job and the daemon read the same sources.
+std::shared_ptr<Interface> new_sriov_lib(const std::string& root);
 std::shared_ptr<Interface> new_mock_sriov();
 // A library that reports no functions (e.g. when PCI scanning is disabled).
 std::shared_ptr<Interface> new_empty_sriov();

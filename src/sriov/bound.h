@@ -5,18 +5,20 @@
 // of a oneshot Job's cycle (~1 ms cold, profiles/oneshot_breakdown_r3.txt).
 // The functions that matter are far fewer and the kernel already knows
 // them: every AMD GPU function a node uses is bound to amdgpu (bare metal, a
-// passthrough guest, an SR-IOV guest's VF) or, on an MxGPU host, its physical
-// functions to the GIM host driver, whose enabled VFs are the PF's
-// `virtfn<N>` links.  So this source lists
-//   <root>/sys/bus/pci/drivers/{amdgpu,gim}/<address>
-// reads the identity and SR-IOV attributes of those functions only (about
-// six small sysfs reads per GPU), adds the VFs their `virtfn*` links name,
-// and returns them in the same form as the full-bus scan (SysfsAmdPCI), so
-// sriov::Lib classifies them identically.
+// passthrough guest, an SR-IOV guest's VF), on an MxGPU host its physical
+// functions to the GIM host driver, and a function handed to a VM to
+// vfio-pci, pci-pf-stub or pci-stub; a PF's enabled VFs are its
+// `virtfn<N>` links.  So this source lists, for the loaded ones of those
+// drivers (drivers()),
+//   <root>/sys/bus/pci/drivers/<driver>/<address>
+// reads the identity and SR-IOV attributes of the AMD functions among them
+// (about six small sysfs reads per GPU), adds the VFs their `virtfn*` links
+// name, and returns them in the same form as the full-bus scan
+// (SysfsAmdPCI), so sriov::Lib classifies them identically.
 //
-// When neither driver binds anything - an SR-IOV guest whose amdgpu is not
-// loaded, or a node without AMD GPUs - the whole-bus scan (SysfsAmdPCI) is
-// the answer.  Inside a VM (`merge_unbound`, the CPU's hypervisor flag) the
+// When none of the drivers binds anything - an SR-IOV guest whose amdgpu is
+// not loaded, or a node without AMD GPUs - the whole-bus scan (SysfsAmdPCI)
+// is the answer.  Inside a VM (`merge_unbound`, the CPU's hypervisor flag) the
 // bus also decides which AMD functions exist: whenever uevent_seqnum moved,
 // the AMD display / accelerator functions of the bus that no listed driver
 // binds - a guest VF amdgpu failed to probe - are read too

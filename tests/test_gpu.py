@@ -526,13 +526,18 @@ def test_driver_bench_command_stays_within_its_bounds(tmp_path):
     0.0251 -> 0.0288 ms went unnoticed).  Bounds (round-5 verdict, Next #5:
     a +25% drift must fail): headline 0.022 ms (0.0169-0.0172 measured on
     the driver's boxes, BENCH_r05 and profiles/bench_fresh_r6.txt), cycles 1 s
-    apart 0.28 ms (0.18-0.24), their unattributed time 0.02 ms, the Job
-    process 1.5 ms (0.97-1.13); and no write after the second creates a
-    file.  A run over a bound is repeated once (_within_bounds)."""
+    apart 0.28 ms (0.18-0.24), their unattributed time 0.02 ms; the Job
+    process: its fastest of 15 spawns 1.0 ms (0.778-0.804 on the round-6
+    boxes) - the p50 of 15 spawns right after the idle second cycles is
+    bimodal on some boxes (spawns of 0.8 or 1.5-1.9 ms, the slow ones on
+    idle cores: p50 0.799-1.538, profiles/bench_fresh_r6.txt), so it is
+    bounded only against gross drift, 2.0 ms; and no write after the second
+    creates a file.  A run over a bound is repeated once (_within_bounds)."""
 
     def measure():
         r = _bench_json(["--gpus", "1", "--steps", "20", "--warmup", "5"])
         print(json.dumps({k: r[k] for k in ("value", "p90_ms", "first_cycle_ms", "oneshot_process_p50_ms")}),
+              json.dumps({"job_runs_ms": r["extras"]["oneshot_process"]["runs_ms"]}),
               json.dumps({"cold": r["cold_cycle"]["p50_ms"], "cold_other": r["cold_cycle"]["other_p50_ms"]}))
         assert r["labels_ok"] is True and r["config"]["backend"].startswith("amdsmi"), r
         assert "write.create" not in r["phases_p50_ms"], r["phases_n"]
@@ -541,7 +546,8 @@ def test_driver_bench_command_stays_within_its_bounds(tmp_path):
     _within_bounds(measure, [("headline_ms", lambda r: r["value"], 0.022),
                              ("cold_p50_ms", lambda r: r["cold_cycle"]["p50_ms"], 0.28),
                              ("cold_other_ms", lambda r: r["cold_cycle"]["other_p50_ms"], 0.02),
-                             ("job_p50_ms", lambda r: r["oneshot_process_p50_ms"], 1.5)])
+                             ("job_fastest_ms", lambda r: min(r["extras"]["oneshot_process"]["runs_ms"]), 1.0),
+                             ("job_p50_ms", lambda r: r["oneshot_process_p50_ms"], 2.0)])
 
 
 def test_amdsmi_backend_over_all_the_hosts_gpus(tmp_path):

@@ -39,7 +39,10 @@ rehearses the amd-smi path on CPU.
 
 Besides the headline (back-to-back cycles) the JSON carries the deployed
 daemon's first cycle, its cycles 1 s apart on idle cores (cold_cycle), the
-Job-mode process from spawn to exit, and per-phase p50s of the timed steps.
+Job-mode process from spawn to exit, and per-phase p50s.  The timed steps
+record no phases, as the daemon's without --trace-timing; the same K steps
+run once more with phase tracing after the timed region, for the per-phase
+p50s and their own p50 (traced_p50_ms).
 """
 
 from __future__ import annotations
@@ -117,7 +120,7 @@ sys.path.insert(0, {repo!r})
 import gpu_feature_discovery_amd as gfd
 g = gfd.native(); g.set_quiet(True)
 s = g.Session(json.loads(sys.argv[1]))
-ns = s.bench(int(sys.argv[2]), int(sys.argv[3]), True)
+ns = s.bench(int(sys.argv[2]), int(sys.argv[3]), True, False)
 print(json.dumps({{"ns": ns, "backend": s.backend}}))
 """
 
@@ -276,15 +279,18 @@ def main() -> int:
         labels = session.cycle(write=True).labels
         problems = _check_labels(labels, n, hardware)
         labels_ok = not problems
-        # Warmup (untimed), in native code.
-        session.bench(0, a.warmup, True)
+        # Warmup (untimed), in native code.  The cycles record no phases, as
+        # the daemon's without --trace-timing (phase tracing reads the clock
+        # twice per phase, ~1.5 us of a cycle): the phases come from K traced
+        # steps after the timed region.
+        session.bench(0, a.warmup, True, False)
 
     # Timed region: exactly K steps, bracketed by barrier + synchronize.
     dist.sync()
     t0 = time.perf_counter_ns()
     ms: list[float] = []
     if dist.rank == 0:
-        ms = session.bench(a.steps, 0, True)
+        ms = session.bench(a.steps, 0, True, False)
     dist.sync()
     wall_ms = (time.perf_counter_ns() - t0) / 1e6
     wall_ms = dist.max(wall_ms)
@@ -292,6 +298,9 @@ def main() -> int:
     if dist.rank == 0:
         p50 = _percentile(ms, 0.5)
         backend_name = session.backend
+        # The same K steps again, traced: where a cycle spends its time (and
+        # what tracing costs, traced_p50_ms - value).
+        traced_ms = session.bench(a.steps, 0, True, True)
         bench_phases = session.bench_phases()
         phases = {name: round(_percentile(v, 0.5), 4) for name, v in bench_phases.items()}
         # In how many of the K timed steps each phase occurred (a step that
@@ -366,8 +375,10 @@ def main() -> int:
             "p99_ms": round(_percentile(ms, 0.99), 4),
             "max_ms": round(max(ms), 4) if ms else None,
             "mean_ms": round(statistics.fmean(ms), 4) if ms else None,
-            # Per-phase p50 over the K timed steps: what an N-GPU cycle
-            # spends where (the scaling curve's explanation).
+            # The K steps once more with phase tracing (after the timed
+            # region): their p50, and the per-phase p50s - what an N-GPU
+            # cycle spends where (the scaling curve's explanation).
+            "traced_p50_ms": round(_percentile(traced_ms, 0.5), 4),
             "phases_p50_ms": phases,
             "phases_n": phases_n,
             # The deployed daemon's first cycle (library init included) and

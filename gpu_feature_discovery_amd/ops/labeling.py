@@ -59,13 +59,16 @@ class Labeler:
         """One labeling cycle; ``write`` atomically rewrites the output file."""
         return CycleResult.from_native(self._session.cycle(write))
 
-    def bench(self, steps: int, warmup: int = 0, write: bool = True) -> list[float]:
+    def bench(self, steps: int, warmup: int = 0, write: bool = True, traced: bool = True) -> list[float]:
         """``warmup`` untimed cycles then ``steps`` timed ones, in a native
-        loop (no Python between cycles); returns per-cycle milliseconds."""
-        return [ns / 1e6 for ns in self._session.bench(steps, warmup, write)]
+        loop (no Python between cycles); returns per-cycle milliseconds.
+        ``traced``: record each cycle's phases (``bench_phases``); untraced
+        cycles read no clock for them, as the daemon's without
+        ``--trace-timing``."""
+        return [ns / 1e6 for ns in self._session.bench(steps, warmup, write, traced)]
 
     def bench_phases(self) -> dict[str, list[float]]:
-        """Per-phase milliseconds of the last ``bench`` call's timed cycles."""
+        """Per-phase milliseconds of the last traced ``bench`` call's timed cycles."""
         return {name: [ns / 1e6 for ns in v] for name, v in self._session.bench_phases().items()}
 
 

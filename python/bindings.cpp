@@ -151,19 +151,20 @@ class Session {
   }
 
   // Tight loop in native code: `warmup` untimed cycles, then `steps` timed
-  // cycles; returns per-cycle wall time in ns.  The timed cycles' phase
-  // times are kept for bench_phases().
-  std::vector<int64_t> bench(int steps, int warmup, bool write) {
+  // cycles; returns per-cycle wall time in ns.  With `traced` the timed
+  // cycles' phase times are kept for bench_phases(); without, the cycles
+  // record no phase (as the daemon's without --trace-timing).
+  std::vector<int64_t> bench(int steps, int warmup, bool write, bool traced) {
     std::vector<int64_t> out;
     out.reserve(static_cast<size_t>(steps));
     py::gil_scoped_release nogil;
     bool was_quiet = log::set_quiet(true);
     phases_.clear();
     try {
-      for (int i = 0; i < warmup; ++i) cli::label_cycle(*manager_, sriov_, config_, timestamp_, write);
+      for (int i = 0; i < warmup; ++i) cli::label_cycle(*manager_, sriov_, config_, timestamp_, write, traced);
       for (int i = 0; i < steps; ++i) {
         int64_t t0 = trace::now_ns();
-        cli::CycleResult r = cli::label_cycle(*manager_, sriov_, config_, timestamp_, write);
+        cli::CycleResult r = cli::label_cycle(*manager_, sriov_, config_, timestamp_, write, traced);
         out.push_back(trace::now_ns() - t0);
         for (const auto& [name, ns] : r.phases) phases_[name].push_back(ns);
       }
@@ -293,7 +294,8 @@ PYBIND11_MODULE(_gfd, m) {
            py::arg("args") = std::vector<std::string>{}, py::arg("env") = py::none(),
            py::arg("amdsmi_library_only") = false)
       .def("cycle", &Session::cycle, py::arg("write") = true)
-      .def("bench", &Session::bench, py::arg("steps"), py::arg("warmup") = 0, py::arg("write") = true)
+      .def("bench", &Session::bench, py::arg("steps"), py::arg("warmup") = 0, py::arg("write") = true,
+           py::arg("traced") = true)
       .def("bench_phases", &Session::bench_phases)
       .def("devices", &Session::devices)
       .def("run_loop", &Session::run_loop)

@@ -122,8 +122,8 @@ std::string SignalWatcher::name(int sig) {
 // Labeling
 
 CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov::Interface>& sriov,
-                        const config::Config& config, const lm::LabelerPtr& timestamp, bool write) {
-  trace::begin_cycle();
+                        const config::Config& config, const lm::LabelerPtr& timestamp, bool write, bool traced) {
+  trace::begin_cycle(traced);
   int64_t t0 = trace::now_ns();
   CycleResult r;
   r.cpu_start = sched_getcpu();
@@ -152,29 +152,29 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
 
   std::vector<trace::Phase> facts_detail;  // the facts' own records, made on a worker
   auto read_facts = [&] {
-    int64_t s0 = trace::now_ns();
+    int64_t s0 = trace::stamp(traced);
     facts_start = s0;
     r.cpu_facts = sched_getcpu();
-    trace::Capture capture;
+    trace::Capture capture(traced);
     try {
       facts = lm::ReadNodeFacts(config, version_files);
     } catch (...) {
       facts = lm::NodeFacts{};  // fall back to the manager inside the labeler
     }
     facts_detail = capture.take();
-    facts_ns = trace::now_ns() - s0;
+    if (traced) facts_ns = trace::now_ns() - s0;
   };
   std::vector<trace::Phase> sriov_detail;  // the lookup's own records, made on a worker
   auto scan_sriov = [&] {
-    int64_t s0 = trace::now_ns();
-    trace::Capture capture;
+    int64_t s0 = trace::stamp(traced);
+    trace::Capture capture(traced);
     try {
       sriov_labels = lm::NewSriovLabeler(sriov)->GetLabels();
     } catch (...) {
       sriov_error = std::current_exception();
     }
     sriov_detail = capture.take();
-    sriov_ns = trace::now_ns() - s0;
+    if (traced) sriov_ns = trace::now_ns() - s0;
   };
   // Loop mode: both on one worker, in that order (two workers measured
   // slower: each task 1.5-4x longer on the second, colder core,
@@ -193,7 +193,7 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
   WorkerPool::Task facts_task, sriov_task;
   if (overlap) {
     trace::Span span("submit");
-    submitted = trace::now_ns();
+    submitted = trace::stamp();
     auto seq = WorkerPool::instance().submit_sequence({read_facts, scan_sriov});
     facts_task = seq[0];
     sriov_task = seq[1];
@@ -203,11 +203,11 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
       read_facts();
       return facts;
     }
-    int64_t s0 = trace::now_ns();
-    if (sriov_task.try_run()) trace::record("sriov.self", trace::now_ns() - s0);
-    int64_t w0 = trace::now_ns();
+    int64_t s0 = trace::stamp();
+    if (sriov_task.try_run()) trace::record_since("sriov.self", s0);
+    int64_t w0 = trace::stamp();
     facts_task.run_or_wait();
-    trace::record("facts.wait", trace::now_ns() - w0);  // inside "label"
+    trace::record_since("facts.wait", w0);  // inside "label"
     return facts;
   };
   lm::LabelerPtr device;
@@ -220,13 +220,13 @@ CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov:
     throw;
   }
   if (overlap) {
-    int64_t j0 = trace::now_ns();
+    int64_t j0 = trace::stamp();
     facts_task.cancel_or_wait();  // no devices: the labeler never needed them
     sriov_task.run_or_wait();
     // Where an overlapped cycle waits: how long after the hand-off the node
     // facts started (a worker's wake-up, or this thread taking them over),
     // and how long this thread then waited for the SR-IOV lookup.
-    trace::record_top("sriov.join", trace::now_ns() - j0);
+    if (traced) trace::record_top("sriov.join", trace::now_ns() - j0);
     trace::record("facts.start", facts_start ? facts_start - submitted : 0);
     trace::record("facts(overlapped)", facts_ns);
     trace::record("sriov(overlapped)", sriov_ns);
@@ -306,7 +306,7 @@ bool run(resource::Manager& manager, const std::shared_ptr<sriov::Interface>& sr
     // The cycle's log lines ("Writing labels to output file", ...) go out
     // together once the feature file is in place (and on any error).
     log::Hold hold;
-    CycleResult r = label_cycle(manager, sriov, config, timestamp, true);
+    CycleResult r = label_cycle(manager, sriov, config, timestamp, true, config.trace_timing());
     if (config.trace_timing())
       log::printf("Timing: %s cpu=%d,%d,%d", trace::summary(r.total_ns).c_str(), r.cpu_start, r.cpu_end, r.cpu_facts);
     if (config.oneshot()) return false;

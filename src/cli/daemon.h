@@ -48,8 +48,11 @@ struct CycleResult {
 
 // One labeling cycle: build labelers (device + SR-IOV), merge with the
 // timestamp labeler, evaluate, and write the feature file if `write`.
+// `traced`: record the phases (util/trace.h; the daemon's under
+// --trace-timing); untraced, `phases` is empty and other_ns the total.
 CycleResult label_cycle(resource::Manager& manager, const std::shared_ptr<sriov::Interface>& sriov,
-                        const config::Config& config, const lm::LabelerPtr& timestamp, bool write);
+                        const config::Config& config, const lm::LabelerPtr& timestamp, bool write,
+                        bool traced = true);
 
 // main.go:148-210.  Returns true if the caller should reload (SIGHUP).
 // `sigs` may be null (oneshot tests).

@@ -153,7 +153,7 @@ namespace {
 // `kept` the descriptor is left open and returned there, else closed.
 void create_and_write(const std::string& tmp_dir, const std::string& contents, unsigned perm, std::string* tmpl,
                       int* kept) {
-  int64_t t0 = trace::now_ns();
+  int64_t t0 = trace::stamp();
   // The temporary directory normally exists from the previous cycle: try the
   // create first and make the directory only when it is missing.
   int fd = create_temp(tmp_dir, perm, tmpl);
@@ -177,7 +177,7 @@ void create_and_write(const std::string& tmp_dir, const std::string& contents, u
     remove_own_temps(tmp_dir);
     throw Error(msg);
   };
-  int64_t t1 = trace::now_ns();
+  int64_t t1 = trace::stamp();
   trace::record("write.create", t1 - t0);
   // Best effort: a file system without fallocate(2) just takes the write.
   if (wants_prealloc(fd)) (void)::fallocate(fd, 0, 0, static_cast<off_t>(contents.size()));
@@ -193,7 +193,7 @@ void create_and_write(const std::string& tmp_dir, const std::string& contents, u
     remove_own_temps(tmp_dir);
     throw Error("error writing temporary file '" + *tmpl + "': " + fs::errno_str(e));
   }
-  trace::record("write.data", trace::now_ns() - t1);
+  trace::record_since("write.data", t1);
 }
 
 std::string temp_dir_of(const std::string& path) { return fs::join(fs::dirname(fs::absolute(path)), "gfd-tmp"); }
@@ -244,21 +244,21 @@ void close_file(File& f, bool unlink_name) {
 // spare dropped) if it cannot be used.
 bool rewrite_spare(File& spare, const std::string& contents) {
   if (spare.fd < 0) return false;
-  int64_t t0 = trace::now_ns();
+  int64_t t0 = trace::stamp();
   struct stat st;
   // On a local file system (a network one's readers elsewhere hold no lease
   // this kernel could see), still ours under its name (gfd-tmp/ was not
   // emptied behind our back)...
   bool usable = spare.local && ::lstat(spare.name.c_str(), &st) == 0 && st.st_dev == spare.dev &&
                 st.st_ino == spare.ino;
-  int64_t t1 = trace::now_ns();
+  int64_t t1 = trace::stamp();
   // ...and no reader that opened it while it was the feature file still has
   // it open: a write lease is granted only to the sole opener.  EAGAIN: a
   // reader; EINVAL/EACCES: no leases here (a file system without them,
   // leases disabled).  Then the spare is left to its reader (unlinked) and
   // this write creates a new file.
   if (usable && ::fcntl(spare.fd, F_SETLEASE, F_WRLCK) != 0) usable = false;
-  int64_t t2 = trace::now_ns();
+  int64_t t2 = trace::stamp();
   if (!usable) {
     close_file(spare, true);
     return false;
@@ -268,7 +268,7 @@ bool rewrite_spare(File& spare, const std::string& contents) {
   // size change at all).
   if (ok && static_cast<size_t>(st.st_size) > contents.size())
     ok = ::ftruncate(spare.fd, static_cast<off_t>(contents.size())) == 0;
-  int64_t t3 = trace::now_ns();
+  int64_t t3 = trace::stamp();
   // Released before the exchange: an open of the feature file must not wait
   // for a lease break.
   (void)::fcntl(spare.fd, F_SETLEASE, F_UNLCK);
@@ -276,7 +276,7 @@ bool rewrite_spare(File& spare, const std::string& contents) {
     close_file(spare, true);
     return false;
   }
-  int64_t t4 = trace::now_ns();
+  int64_t t4 = trace::stamp();
   // The rewrite's parts (a cycle after an idle second spends most of its
   // write here and in the exchange, write.rename).
   trace::record("write.check", t1 - t0);
@@ -311,7 +311,7 @@ void write_kept(const std::string& path, const std::string& tmp_dir, const std::
   // Swap it with the feature file when that is a regular file; anything else
   // at `path` (nothing yet, a directory that must fail like rename(2)
   // would, a file system without the exchange) takes a plain rename.
-  int64_t t0 = trace::now_ns();
+  int64_t t0 = trace::stamp();
   struct stat old;
   bool swapped = false;
   if (::lstat(path.c_str(), &old) == 0 && S_ISREG(old.st_mode)) {
@@ -323,7 +323,7 @@ void write_kept(const std::string& path, const std::string& tmp_dir, const std::
     remove_own_temps(tmp_dir);
     throw Error("error moving temporary file to '" + path + "': " + fs::errno_str(e));
   }
-  trace::record("write.rename", trace::now_ns() - t0);
+  trace::record_since("write.rename", t0);
   if (swapped && s.live.fd >= 0 && old.st_dev == s.live.dev && old.st_ino == s.live.ino) {
     // The old feature file, ours, is now under the temporary name.
     s.spare = std::move(s.live);
@@ -344,14 +344,14 @@ void write_file_atomically(const std::string& path, const std::string& contents,
   std::string tmp_dir = temp_dir_of(path);
   std::string tmpl;
   create_and_write(tmp_dir, contents, perm, &tmpl, nullptr);
-  int64_t t0 = trace::now_ns();
+  int64_t t0 = trace::stamp();
   if (::rename(tmpl.c_str(), path.c_str()) != 0) {
     int e = errno;
     ::unlink(tmpl.c_str());
     remove_own_temps(tmp_dir);
     throw Error("error moving temporary file to '" + path + "': " + fs::errno_str(e));
   }
-  trace::record("write.rename", trace::now_ns() - t0);
+  trace::record_since("write.rename", t0);
 }
 
 void release_kept_files() {

@@ -735,9 +735,9 @@ std::vector<DevicePtr> AmdSmiManager::GetDevices() {
 std::vector<DevicePtr> AmdSmiManager::snapshot() {
   AmdSmiLib& L = *lib_;
   trace::Span span("amdsmi.snapshot");
-  int64_t handles_t0 = trace::now_ns();
+  int64_t handles_t0 = trace::stamp();
   std::vector<std::vector<ProcInfo>> physical = collect_physical_gpus(L, opts_.root, parent_bdf_, proc_bdf_, identity_);
-  trace::record("amdsmi.handles", trace::now_ns() - handles_t0);
+  trace::record_since("amdsmi.handles", handles_t0);
 
   // Apply the visible-device filter on physical GPUs (index = parent BDF order).
   struct Gpu {
@@ -801,9 +801,12 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
   // calls, and 2-3x slower sysfs reads (profiles/README.md).  fast: only
   // through the unpartitioned (attribute) path - returns false if that path
   // does not apply; otherwise every processor through the library.
+  // Lanes run on pool threads, which record nothing: this cycle's tracing
+  // decides whether a GPU's work is timed.
+  const bool traced = trace::active();
   auto work = [&](Gpu& g, bool fast) -> bool {
     try {
-      int64_t t0 = trace::now_ns();
+      int64_t t0 = trace::stamp(traced);
       auto& procs = *g.procs;
       if (fast) {
         int64_t* rd = &g.mode_read_ns;
@@ -816,13 +819,13 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
         std::sort(procs.begin(), procs.end(),
                   [](const ProcInfo& a, const ProcInfo& b) { return a.partition_id < b.partition_id; });
       }
-      int64_t t1 = trace::now_ns();
+      int64_t t1 = trace::stamp(traced);
       const ProcInfo& first = procs.front();
       query_gpu_caps(L, first, opts_.root, g.extras, g.avail);
       if (procs.size() > 1 || (!first.compute_partition.empty() && first.compute_partition != "SPX"))
         g.extras.engines = AMDSMI_CALL("partition_engines(sysfs)", partition_engine_counts(opts_.root, first.gpu_bdf));
       g.proc_ns = t1 - t0;
-      g.caps_ns = trace::now_ns() - t1;
+      g.caps_ns = trace::stamp(traced) - t1;
     } catch (...) {
       g.error = std::current_exception();
     }
@@ -839,7 +842,7 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
   // down-clocked cores - 8 GPUs' reads 170 us on one thread vs 36 us on four
   // lanes, profiles/multi_gpu_read_probe.txt - and with the pinned pool one
   // GPU per lane is also fastest back to back).
-  int64_t t_gpus = trace::now_ns();
+  int64_t t_gpus = trace::stamp();
   size_t lanes = opts_.threads > 0 ? static_cast<size_t>(opts_.threads) : gpu_lanes(gpus.size());
   // Nothing to read: every GPU is an unpartitioned one whose values the
   // session already holds (the steady state).  Its work is then a few
@@ -866,9 +869,9 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
         if (sysfs_values && work(gpus[i], true)) return;
         work(gpus[i], false);
       },
-      lanes, gpus.size() > 1 ? &lane_stats : nullptr);
-  trace::record("amdsmi.gpus", trace::now_ns() - t_gpus);
-  if (gpus.size() > 1) {
+      lanes, gpus.size() > 1 && traced ? &lane_stats : nullptr);
+  trace::record_since("amdsmi.gpus", t_gpus);
+  if (gpus.size() > 1 && traced) {
     // Where a multi-GPU snapshot's lanes spend it: the hand-off (enqueue
     // and wake the helpers, on this thread), how late the last GPU started
     // (a helper's wake-up), the slowest GPU's own work, and how many GPUs

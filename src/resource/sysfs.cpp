@@ -306,11 +306,11 @@ std::shared_ptr<const SysfsManager::Topology> SysfsManager::read_topology() cons
     }
   };
   size_t chunks = (nodes.size() + kChunk - 1) / kChunk;
-  int64_t t0 = trace::now_ns();
+  int64_t t0 = trace::stamp();
   // Lanes on parked workers only: a oneshot Job's 10-node host topology is
   // read faster by this thread than by a worker created for it.
   WorkerPool::instance().parallel_for(chunks, read_chunk, 1 + WorkerPool::instance().idle_workers());
-  trace::record("sysfs.nodes", trace::now_ns() - t0);
+  trace::record_since("sysfs.nodes", t0);
   auto topo = std::make_shared<Topology>();
   for (size_t i = 0; i < nodes.size(); ++i)
     if (usable[i]) topo->nodes.push_back(std::move(nodes[i]));
@@ -346,11 +346,11 @@ std::shared_ptr<const SysfsManager::Topology> SysfsManager::read_topology() cons
     g.bdf = resolve_parent_bdf(opts_.root, bdfs, static_cast<uint32_t>(members.front()->device_id));
     g.members = std::move(members);
     g.has_physfn = fs::exists(fs::join(opts_.root, "sys/bus/pci/devices/" + g.bdf + "/physfn"));
-    int64_t r0 = trace::now_ns();
+    int64_t r0 = trace::stamp();
     g.compute_partition = partition_mode(
         fs::attrs().read_trimmed(fs::join(opts_.root, "sys/bus/pci/devices/" + g.bdf + "/current_compute_partition"))
             .value_or(""));
-    trace::record("compute_partition(read)", trace::now_ns() - r0);
+    trace::record_since("compute_partition(read)", r0);
     topo->gpus.push_back(std::move(g));
   }
   std::sort(topo->gpus.begin(), topo->gpus.end(),

@@ -222,14 +222,14 @@ std::vector<std::pair<std::string, uint64_t>> BoundAmdPCI::list_bound() {
 std::vector<std::string> BoundAmdPCI::list_unbound(const std::vector<std::pair<std::string, uint64_t>>& bound) {
   std::vector<std::string> out;
   if (!fallback_ || !merge_unbound_) return out;
-  int64_t t0 = trace::now_ns();
+  int64_t t0 = trace::stamp();
   auto amd = fallback_->amd_functions();  // sorted, like `bound`
   auto b = bound.begin();
   for (auto& addr : amd) {
     while (b != bound.end() && b->first < addr) ++b;
     if (b == bound.end() || b->first != addr) out.push_back(std::move(addr));
   }
-  trace::record("pci.bus", trace::now_ns() - t0);
+  trace::record_since("pci.bus", t0);
   return out;
 }
 
@@ -271,30 +271,30 @@ bool BoundAmdPCI::still_valid(const std::vector<std::pair<std::string, uint64_t>
 }
 
 std::vector<PCIDevice> BoundAmdPCI::Devices() {
-  int64_t t0 = trace::now_ns();
+  int64_t t0 = trace::stamp();
   // A booted kernel has sent thousands of uevents; "" or "0" is an emulated
   // sysfs that never counts, and is not trusted.
   auto seqnum = fs::attrs().read_trimmed(fs::join(root_, "sys/kernel/uevent_seqnum"));
   if (seqnum && (seqnum->empty() || *seqnum == "0")) seqnum.reset();
   if (have_ && seqnum && *seqnum == seqnum_) {
-    trace::record("pci.bound(kept)", trace::now_ns() - t0);
+    trace::record_since("pci.bound(kept)", t0);
     return fell_back_ && fallback_ ? fallback_->Devices() : last_;
   }
   auto bound = list_bound();
   // Whatever the bus holds that the listed drivers do not bind (empty when
   // nothing is bound: the bus scan below is the whole answer then).
   std::vector<std::string> unbound = bound.empty() ? std::vector<std::string>{} : list_unbound(bound);
-  int64_t t_list = trace::now_ns();
+  int64_t t_list = trace::stamp();
   if (seqnum && still_valid(bound, unbound)) {
     // The counter moved for some other device (a container's veth...).
     seqnum_ = *seqnum;
-    int64_t t_end = trace::now_ns();
+    int64_t t_end = trace::stamp();
     trace::record("pci.list", t_list - t0);
     trace::record("pci.vfs", t_end - t_list);
     trace::record("pci.bound(checked)", t_end - t0);
     return last_;
   }
-  trace::record("pci.drivers", trace::now_ns() - t0);
+  trace::record_since("pci.drivers", t0);
   std::vector<PCIDevice> out;
   if (bound.empty()) {
     // Nothing bound: a guest whose amdgpu is not loaded still shows its VF
@@ -304,11 +304,11 @@ std::vector<PCIDevice> BoundAmdPCI::Devices() {
     pf_dirs_.clear();
     if (fallback_) out = fallback_->Devices();
   } else {
-    int64_t t1 = trace::now_ns();
+    int64_t t1 = trace::stamp();
     std::vector<std::string> names;
     for (const auto& e : bound) names.push_back(e.first);
     out = scan_bound(names, unbound, &pf_dirs_);
-    trace::record("pci.bound", trace::now_ns() - t1);
+    trace::record_since("pci.bound", t1);
     fell_back_ = false;
     last_ = out;
   }

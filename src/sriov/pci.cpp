@@ -99,7 +99,7 @@ SysfsAmdPCI::Identity SysfsAmdPCI::read_identity(const std::string& addr, const 
 
 void SysfsAmdPCI::update() {
   std::string dir = fs::join(root_, kPciDevicesRoot);
-  int64_t t0 = trace::now_ns();
+  int64_t t0 = trace::stamp();
   // The kernel's uevent sequence number goes up with every device added to
   // or removed from the system - a PCI function, an SR-IOV VF included
   // (device_add / device_del -> kobject_uevent; PCI devices pass the devices
@@ -117,7 +117,7 @@ void SysfsAmdPCI::update() {
     int err = listing_.read(dir, &changed);
     if (err != 0) throw Error("unable to read PCI bus devices: open " + dir + ": " + fs::errno_str(err));
   }
-  trace::record("pci.list", trace::now_ns() - t0);
+  trace::record_since("pci.list", t0);
 
   // Merge the (sorted) listing with the (sorted) identity cache: entries
   // whose sysfs inode is unchanged reuse their identity, new or re-created
@@ -170,7 +170,7 @@ void SysfsAmdPCI::update() {
   if (changed) cache_.swap(next);
   scanned_ = true;
   seqnum_ = seqnum.value_or("");
-  trace::record("pci.identity", trace::now_ns() - t0);
+  trace::record_since("pci.identity", t0);
 }
 
 std::vector<std::string> SysfsAmdPCI::amd_functions() {
@@ -184,7 +184,7 @@ std::vector<std::string> SysfsAmdPCI::amd_functions() {
 std::vector<PCIDevice> SysfsAmdPCI::Devices() {
   update();
   std::string dir = fs::join(root_, kPciDevicesRoot);
-  int64_t t1 = trace::now_ns();
+  int64_t t1 = trace::stamp();
   std::vector<PCIDevice> out;
   std::vector<Identity*> ids;
   for (auto& [addr, id] : cache_) {
@@ -231,10 +231,10 @@ std::vector<PCIDevice> SysfsAmdPCI::Devices() {
       d.config = std::move(cfg.data);
     }
   };
-  int64_t t2 = trace::now_ns();
+  int64_t t2 = trace::stamp();
   trace::record("pci.build", t2 - t1);
   for (size_t i = 0; i < out.size(); ++i) refresh(i);
-  trace::record("pci.refresh", trace::now_ns() - t2);
+  trace::record_since("pci.refresh", t2);
   return out;
 }
 

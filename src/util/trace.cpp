@@ -8,9 +8,9 @@ namespace {
 thread_local std::vector<Phase> t_phases;
 thread_local int64_t t_top_ns = 0;
 thread_local int t_depth = 0;
-// Only threads that run labeling cycles record; spans executed on pool
-// workers would otherwise accumulate forever.
-thread_local bool t_active = false;
+// Only threads that run (traced) labeling cycles record (detail::t_active);
+// spans executed on pool workers would otherwise accumulate forever.
+using detail::t_active;
 }  // namespace
 
 int& detail::depth() { return t_depth; }
@@ -20,10 +20,10 @@ int64_t now_ns() {
       .count();
 }
 
-void begin_cycle() {
+void begin_cycle(bool on) {
   t_phases.clear();
   t_top_ns = 0;
-  t_active = true;
+  t_active = on;
 }
 const std::vector<Phase>& phases() { return t_phases; }
 void record(const std::string& name, int64_t ns) {
@@ -36,7 +36,7 @@ void record_top(const std::string& name, int64_t ns) {
 }
 int64_t top_level_ns() { return t_top_ns; }
 
-Capture::Capture() : own_(!t_active) {
+Capture::Capture(bool on) : own_(on && !t_active) {
   if (!own_) return;
   t_phases.clear();
   top_ns_ = t_top_ns;

@@ -278,6 +278,57 @@ TEST(LabelCycle_RecordsPhases) {
   }
 }
 
+namespace {
+// An SR-IOV source that records a detail, as BoundAmdPCI does.
+struct RecordingSriov : sriov::Interface {
+  std::vector<sriov::Function> Devices() override {
+    trace::record("pci.test", 5000);
+    return {};
+  }
+};
+}  // namespace
+
+TEST(LabelCycle_UntracedRecordsNothingAndLabelsTheSame) {
+  // The daemon without --trace-timing: no phase anywhere (the SR-IOV
+  // source's own record included, on whichever thread it ran), the same
+  // labels, and a traced cycle afterwards records as before.
+  for (bool oneshot : {true, false}) {
+    auto c = run_config("", "none", true, oneshot);
+    resource::MockManager m({resource::new_full_gpu()});
+    auto ts = lm::NewTimestampLabeler(c, 1);
+    for (int i = 0; i < 10; ++i) {
+      auto quiet = label_cycle(m, std::make_shared<RecordingSriov>(), c, ts, false, false);
+      EXPECT_TRUE(quiet.phases.empty());
+      EXPECT_EQ(quiet.other_ns, quiet.total_ns);
+      auto traced = label_cycle(m, std::make_shared<RecordingSriov>(), c, ts, false, true);
+      EXPECT_TRUE(quiet.labels == traced.labels);
+      int n = 0;
+      for (const auto& p : traced.phases) n += p.first == "pci.test";
+      EXPECT_EQ(n, 1);
+    }
+  }
+}
+
+TEST(Trace_UntracedSpansAndStampsReadNoClock) {
+  trace::begin_cycle(false);
+  EXPECT_FALSE(trace::active());
+  EXPECT_EQ(trace::stamp(), 0);
+  { trace::Span s("write"); }
+  trace::record_since("write.rename", trace::stamp());
+  std::thread worker([] {
+    trace::Capture c(false);  // an untraced cycle's task
+    EXPECT_FALSE(trace::active());
+    trace::record("pci.x", 1);
+    EXPECT_TRUE(c.take().empty());
+  });
+  worker.join();
+  EXPECT_TRUE(trace::phases().empty());
+  EXPECT_EQ(trace::top_level_ns(), 0);
+  trace::begin_cycle(true);
+  { trace::Span s("write"); }
+  EXPECT_EQ(trace::phases().size(), static_cast<size_t>(1));
+}
+
 TEST(Trace_CaptureHandsAWorkersRecordsToTheCycleOnce) {
   trace::begin_cycle();
   std::vector<trace::Phase> got;
@@ -301,16 +352,6 @@ TEST(Trace_CaptureHandsAWorkersRecordsToTheCycleOnce) {
   EXPECT_EQ(trace::phases().size(), static_cast<size_t>(1));
   EXPECT_EQ(trace::phases()[0].first, std::string("pci.z"));
 }
-
-namespace {
-// An SR-IOV source that records a detail, as BoundAmdPCI does.
-struct RecordingSriov : sriov::Interface {
-  std::vector<sriov::Function> Devices() override {
-    trace::record("pci.test", 5000);
-    return {};
-  }
-};
-}  // namespace
 
 TEST(LabelCycle_RecordsTheSriovLookupsDetailOnceWhereverItRan) {
   auto c = run_config("", "none", true, true);

@@ -100,20 +100,7 @@ bool wants_prealloc(int fd) {
 
 }  // namespace
 
-bool reuse_is_safe(int fd) {
-  struct statfs sf;
-  if (::fstatfs(fd, &sf) != 0) return false;
-  switch (static_cast<unsigned long>(sf.f_type)) {
-    case 0xEF53:      // ext2/3/4
-    case 0x58465342:  // xfs
-    case 0x9123683E:  // btrfs
-    case 0x01021994:  // tmpfs
-    case 0x794c7630:  // overlayfs (a container's root; its upper layer is local)
-      return true;
-    default:
-      return false;
-  }
-}
+bool reuse_is_safe(int fd) { return fs::is_local_fs(fd); }
 
 namespace {
 

@@ -1,12 +1,15 @@
 #include "resource/versions.h"
 
+#include <fcntl.h>
 #include <sys/utsname.h>
+#include <unistd.h>
 
 #include <cstdlib>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <tuple>
+#include <vector>
 
 #include "util/error.h"
 #include "util/fs.h"
@@ -97,20 +100,54 @@ std::optional<RuntimeVersion> parse_runtime_version(const std::string& text) {
 
 namespace {
 
-std::optional<RuntimeVersion> read_version_file(const std::string& path) {
-  auto v = fs::attrs().read_checked_trimmed(path);
+// One evaluation of the lookup below.  With `walk` set, every path is
+// resolved by hand (fs::resolve_in_root) to learn the directories whose
+// entries decide the answer, and the file that gave it is kept open.
+struct Walk {
+  std::vector<std::string> dirs;
+  std::string file;      // the file whose contents gave the answer ("": none)
+  int fd = -1;           // that file, open
+  bool single = true;    // false: the answer compared several files (newest install)
+  ~Walk() {
+    if (fd >= 0) ::close(fd);
+  }
+};
+
+std::optional<std::string> read_text(const std::string& path, Walk* walk) {
+  if (!walk) {
+    auto v = fs::attrs().read_checked_trimmed(path);
+    return v;
+  }
+  std::string real = fs::resolve_in_root("/", fs::absolute(path), &walk->dirs);
+  if (real.empty()) return std::nullopt;
+  int fd = ::open(real.c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return std::nullopt;
+  std::string data;
+  if (fs::pread_all(fd, 4096, &data) != 0) {
+    ::close(fd);
+    return std::nullopt;
+  }
+  if (walk->fd >= 0) ::close(walk->fd);
+  walk->fd = fd;
+  walk->file = real;
+  return str::trim(data);
+}
+
+std::optional<RuntimeVersion> read_version_file(const std::string& path, Walk* walk) {
+  auto v = read_text(path, walk);
   if (!v) return std::nullopt;
   return parse_runtime_version(*v);
 }
 
 // Highest <host_root>/opt/rocm-X.Y.Z/.info/version (versioned installs).
-std::optional<RuntimeVersion> newest_versioned_install(const std::string& host_root, std::string* source) {
+std::optional<RuntimeVersion> newest_versioned_install(const std::string& host_root, std::string* source, Walk* walk) {
+  if (walk) walk->single = false;
   std::optional<RuntimeVersion> best;
   for (const auto& name : fs::list_dir(fs::join(host_root, "opt"))) {
     if (name.rfind("rocm-", 0) != 0) continue;
     std::string path = fs::resolve_in_root(host_root, "opt/" + name + "/.info/version");
     if (path.empty()) continue;
-    auto v = read_version_file(path);
+    auto v = read_version_file(path, nullptr);
     if (v && (!best || std::tie(v->major, v->minor) > std::tie(best->major, best->minor))) {
       best = v;
       if (source) *source = path;
@@ -119,16 +156,14 @@ std::optional<RuntimeVersion> newest_versioned_install(const std::string& host_r
   return best;
 }
 
-}  // namespace
-
-std::optional<RuntimeVersion> rocm_version(const VersionSources& s, std::string* source) {
+std::optional<RuntimeVersion> lookup(const VersionSources& s, std::string* source, Walk* walk) {
   auto from = [&](const std::string& path) -> std::optional<RuntimeVersion> {
-    auto v = read_version_file(path);
+    auto v = read_version_file(path, walk);
     if (v && source) *source = path;
     return v;
   };
   if (!s.rocm_version_file.empty()) {
-    auto text = fs::attrs().read_checked_trimmed(s.rocm_version_file);
+    auto text = read_text(s.rocm_version_file, walk);
     if (!text) throw Error("unable to read the ROCm version file " + s.rocm_version_file);
     auto v = parse_runtime_version(*text);
     if (!v) throw Error("ROCm version file " + s.rocm_version_file + " holds \"" + *text + "\", not X.Y[.Z]");
@@ -143,15 +178,92 @@ std::optional<RuntimeVersion> rocm_version(const VersionSources& s, std::string*
     if (!fs::is_dir(fs::join(s.host_root, "opt")))
       throw Error("--host-root " + s.host_root + " has no opt/ directory: mount the host's /opt there to read the ROCm "
                   "runtime version");
-    std::string path = fs::resolve_in_root(s.host_root, "opt/rocm/.info/version");
+    std::string path = fs::resolve_in_root(s.host_root, "opt/rocm/.info/version", walk ? &walk->dirs : nullptr);
     if (!path.empty())
       if (auto v = from(path)) return v;
-    return newest_versioned_install(s.host_root, source);
+    return newest_versioned_install(s.host_root, source, walk);
   }
   if (!s.root.empty() && s.root != "/") return from(fs::join(s.root, "opt/rocm/.info/version"));
   if (const char* rp = std::getenv("ROCM_PATH"); rp && *rp)
     if (auto v = from(fs::join(rp, ".info/version"))) return v;
   return from("/opt/rocm/.info/version");
+}
+
+// The lookup's answer for one set of sources, kept while the directories it
+// walked are unchanged (fs::DirWatch): a path walk per cycle - with
+// --host-root one lstat per component - becomes one non-blocking read of an
+// inotify queue and a pread of the kept file (a version file rewritten in
+// place is read fresh; one replaced, a symlink repointed, a directory on
+// the way renamed or removed is an entry change in a watched directory).
+// The first call looks up plainly (a oneshot Job has one cycle); later
+// misses walk by hand, arm the watch, and walk again - the answer is kept
+// only if both walks agree, so a change racing the first walk is not
+// missed.  Answers from several files (the newest-install scan) and errors
+// are not kept.
+struct Kept {
+  std::string key;
+  bool seen = false;
+  fs::DirWatch watch;
+  int fd = -1;  // the file the answer came from (-1: no file, no ROCm)
+  std::string source;
+  bool valid = false;
+  ~Kept() {
+    if (fd >= 0) ::close(fd);
+  }
+};
+
+}  // namespace
+
+std::optional<RuntimeVersion> rocm_version(const VersionSources& s, std::string* source) {
+  static std::mutex mu;
+  static auto* kept = new std::vector<std::unique_ptr<Kept>>();  // leaked: workers may read at exit
+  std::string rocm_path;
+  if (s.host_root.empty() && s.rocm_version_file.empty() && (s.root.empty() || s.root == "/"))
+    if (const char* rp = std::getenv("ROCM_PATH")) rocm_path = rp;
+  std::string key = s.rocm_version_file + '\0' + s.host_root + '\0' + s.root + '\0' + rocm_path;
+  std::lock_guard<std::mutex> g(mu);
+  Kept* k = nullptr;
+  for (auto& e : *kept)
+    if (e->key == key) k = e.get();
+  if (!k) {
+    // A few sets of sources at most (one per manager; tests build many):
+    // each holds an inotify instance, a per-user resource.
+    if (kept->size() >= 4) kept->erase(kept->begin());
+    kept->push_back(std::make_unique<Kept>());
+    k = kept->back().get();
+    k->key = key;
+  }
+  if (k->valid && k->watch.unchanged()) {
+    if (k->fd < 0) return std::nullopt;
+    std::string data;
+    if (fs::pread_all(k->fd, 4096, &data) == 0)
+      if (auto v = parse_runtime_version(str::trim(data))) {
+        if (source) *source = k->source;
+        return v;
+      }
+    // No longer a version: the lookup decides (an error, or the next source).
+  }
+  k->valid = false;
+  if (k->fd >= 0) ::close(k->fd);
+  k->fd = -1;
+  if (!k->seen) {
+    k->seen = true;
+    return lookup(s, source, nullptr);
+  }
+  Walk first;
+  std::string src;
+  lookup(s, nullptr, &first);
+  if (!first.single || !k->watch.arm(first.dirs)) return lookup(s, source, nullptr);
+  Walk second;
+  auto v = lookup(s, &src, &second);
+  if (second.single && second.dirs == first.dirs && second.file == first.file) {
+    k->valid = true;
+    k->fd = second.fd;
+    second.fd = -1;
+    k->source = src;
+  }
+  if (source && v) *source = src;
+  return v;
 }
 
 std::string driver_version(const std::string& root) {

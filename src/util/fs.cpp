@@ -2,6 +2,7 @@
 
 #include <dirent.h>
 #include <fcntl.h>
+#include <sys/inotify.h>
 #include <sys/stat.h>
 #include <sys/vfs.h>
 #include <sys/syscall.h>
@@ -150,12 +151,6 @@ std::vector<std::pair<std::string, uint64_t>> DirListing::entries() const {
   return out;
 }
 
-namespace {
-
-constexpr long kSysfsMagic = 0x62656572;  // SYSFS_MAGIC
-constexpr size_t kMaxKeptOpen = 1024;
-
-// Whole file from offset 0 (pread: no file position involved).
 int pread_all(int fd, size_t max_bytes, std::string* out) {
   out->clear();
   char buf[8192];
@@ -175,6 +170,12 @@ int pread_all(int fd, size_t max_bytes, std::string* out) {
     }
   }
 }
+
+namespace {
+
+constexpr long kSysfsMagic = 0x62656572;  // SYSFS_MAGIC
+constexpr size_t kMaxKeptOpen = 1024;
+
 
 }  // namespace
 
@@ -385,7 +386,7 @@ std::string read_link(const std::string& path) {
   return std::string(buf, static_cast<size_t>(n));
 }
 
-std::string resolve_in_root(const std::string& root, const std::string& rel) {
+std::string resolve_in_root(const std::string& root, const std::string& rel, std::vector<std::string>* dirs) {
   std::vector<std::string> todo;  // components still to walk, in reverse order
   auto push_path = [&](const std::string& p) {
     auto parts = str::split(p, '/');
@@ -407,6 +408,10 @@ std::string resolve_in_root(const std::string& root, const std::string& rel) {
       if (!cur.empty()) cur.pop_back();
       continue;
     }
+    if (dirs) {
+      std::string parent = path_of(cur);
+      if (std::find(dirs->begin(), dirs->end(), parent) == dirs->end()) dirs->push_back(parent);
+    }
     cur.push_back(c);
     std::string p = path_of(cur);
     struct stat st;
@@ -420,6 +425,58 @@ std::string resolve_in_root(const std::string& root, const std::string& rel) {
     push_path(target);
   }
   return path_of(cur);
+}
+
+bool is_local_fs(int fd) {
+  struct statfs sf;
+  if (::fstatfs(fd, &sf) != 0) return false;
+  switch (static_cast<unsigned long>(sf.f_type)) {
+    case 0xEF53:      // ext2/3/4
+    case 0x58465342:  // xfs
+    case 0x9123683E:  // btrfs
+    case 0x01021994:  // tmpfs
+    case 0x794c7630:  // overlayfs (a container's root; its upper layer is local)
+      return true;
+    default:
+      return false;
+  }
+}
+
+DirWatch::~DirWatch() { disarm(); }
+
+void DirWatch::disarm() {
+  if (fd_ >= 0) ::close(fd_);
+  fd_ = -1;
+}
+
+bool DirWatch::arm(const std::vector<std::string>& dirs) {
+  // A fresh queue: no event of the previous set (nor the IN_IGNORED its
+  // removal would queue) can be mistaken for a change of this one.
+  disarm();
+  if (dirs.empty()) return false;
+  fd_ = ::inotify_init1(IN_NONBLOCK | IN_CLOEXEC);
+  if (fd_ < 0) return false;  // e.g. the user's inotify instances used up
+  constexpr uint32_t kMask =
+      IN_CREATE | IN_DELETE | IN_MOVED_FROM | IN_MOVED_TO | IN_DELETE_SELF | IN_MOVE_SELF | IN_ONLYDIR;
+  for (const auto& d : dirs) {
+    int dfd = ::open(d.c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC);
+    bool local = dfd >= 0 && is_local_fs(dfd);
+    if (dfd >= 0) ::close(dfd);
+    if (!local || ::inotify_add_watch(fd_, d.c_str(), kMask) < 0) {
+      disarm();
+      return false;
+    }
+  }
+  return true;
+}
+
+bool DirWatch::unchanged() {
+  if (fd_ < 0) return false;
+  alignas(struct inotify_event) char buf[4096];
+  ssize_t n = ::read(fd_, buf, sizeof(buf));
+  if (n < 0 && errno == EAGAIN) return true;
+  disarm();  // a change (or an overflowed / failed queue): look again
+  return false;
 }
 
 std::string join(const std::string& a, const std::string& b) {

@@ -161,8 +161,38 @@ class Dir {
 // re-rooted under `root` (a host's /opt/rocm -> /opt/rocm-7.2.0 seen through
 // a mount of the host's /opt at /host/opt).  ".." never leaves `root`.
 // Returns the resolved path under `root`, or "" if a component does not
-// exist or links nest deeper than 40.
-std::string resolve_in_root(const std::string& root, const std::string& rel);
+// exist or links nest deeper than 40.  `dirs` (optional) receives every
+// directory a component was looked up in, symlink targets' included: the
+// directories whose entries decide the answer.
+std::string resolve_in_root(const std::string& root, const std::string& rel, std::vector<std::string>* dirs = nullptr);
+
+// Whether the file system of `fd` is local, so that this kernel sees every
+// change to it (ext4, xfs, btrfs, tmpfs, overlayfs): a lease or an inotify
+// watch there misses nothing another node did.
+bool is_local_fs(int fd);
+
+// Whether the entries of a set of directories changed: an inotify watch on
+// each (an entry created, removed or renamed; the directory itself removed
+// or moved).  A lookup's answer - a symlink chain resolved to a file, or the
+// file not found - stands while its directories are unchanged.
+class DirWatch {
+ public:
+  DirWatch() = default;
+  ~DirWatch();
+  DirWatch(const DirWatch&) = delete;
+  DirWatch& operator=(const DirWatch&) = delete;
+  // Watch `dirs` from now on (the previous set is dropped).  False, and
+  // nothing watched, when one of them cannot be watched or is not on a
+  // local file system (is_local_fs): then unchanged() stays false.
+  bool arm(const std::vector<std::string>& dirs);
+  // True while nothing changed in the armed directories since arm(): one
+  // non-blocking read of the inotify queue.  The first change disarms.
+  bool unchanged();
+
+ private:
+  void disarm();
+  int fd_ = -1;
+};
 
 std::string join(const std::string& a, const std::string& b);
 std::string dirname(const std::string& path);
@@ -175,6 +205,10 @@ std::string absolute(const std::string& path);
 void mkdir_all(const std::string& path, unsigned mode = 0777);
 // rm -rf; returns 0 or errno.  Missing paths are not an error.
 int remove_all(const std::string& path);
+
+// The whole of an open file, from offset 0, up to `max_bytes` (pread: no
+// file position involved).  0 or an errno.
+int pread_all(int fd, size_t max_bytes, std::string* out);
 
 std::string errno_str(int err);
 

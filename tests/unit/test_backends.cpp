@@ -7,6 +7,7 @@
 #include <chrono>
 #include <cstdio>
 #include <condition_variable>
+#include <fstream>
 #include <mutex>
 
 #include "config/config.h"
@@ -408,6 +409,79 @@ TEST(RocmVersion_HostRootWithoutOptIsAMissingMount) {
   EXPECT_THROW_MSG(rocm_version(s), "has no opt/ directory");
   fs::remove_all(image);
   fs::remove_all(host);
+}
+
+TEST(RocmVersion_KeptOnlyWhileThePathToItIsUnchanged) {
+  // The answer is kept across calls (fs::DirWatch on the directories the
+  // lookup walked); every way a node's ROCm version changes is seen at the
+  // next call: the file rewritten in place, replaced by a rename, the
+  // symlink repointed, the target directory renamed away, the file removed
+  // and created again.  Both lookups: a synthetic root and a host root.
+  for (bool host_mode : {false, true}) {
+    std::string d = mktemp_dir();
+    put(d + "/opt/rocm-7.1.0/.info/version", "7.1.0\n");
+    put(d + "/opt/rocm-7.2.0/.info/version", "7.2.0\n");
+    link(host_mode ? "/opt/rocm-7.1.0" : "rocm-7.1.0", d + "/opt/rocm");
+    VersionSources s;
+    (host_mode ? s.host_root : s.root) = d;
+    auto minor = [&] {
+      auto v = rocm_version(s);
+      return v ? static_cast<int>(v->minor) : -1;
+    };
+    for (int i = 0; i < 4; ++i) EXPECT_EQ(minor(), 1);  // kept from the third call on
+    {
+      std::ofstream f(d + "/opt/rocm-7.1.0/.info/version", std::ios::trunc);  // same inode
+      f << "7.3.0\n";
+    }
+    EXPECT_EQ(minor(), 3);
+    EXPECT_EQ(minor(), 3);
+    put(d + "/opt/rocm-7.1.0/.info/version.new", "7.4.0\n");
+    EXPECT_EQ(std::rename((d + "/opt/rocm-7.1.0/.info/version.new").c_str(),
+                          (d + "/opt/rocm-7.1.0/.info/version").c_str()), 0);
+    EXPECT_EQ(minor(), 4);
+    EXPECT_EQ(minor(), 4);
+    EXPECT_EQ(std::remove((d + "/opt/rocm").c_str()), 0);
+    link(host_mode ? "/opt/rocm-7.2.0" : "rocm-7.2.0", d + "/opt/rocm");
+    EXPECT_EQ(minor(), 2);
+    EXPECT_EQ(minor(), 2);
+    EXPECT_EQ(std::rename((d + "/opt/rocm-7.2.0").c_str(), (d + "/opt/old-7.2.0").c_str()), 0);
+    EXPECT_EQ(minor(), host_mode ? 4 : -1);  // a host root falls back to the newest install left
+    EXPECT_EQ(std::rename((d + "/opt/old-7.2.0").c_str(), (d + "/opt/rocm-7.2.0").c_str()), 0);
+    EXPECT_EQ(minor(), 2);
+    EXPECT_EQ(minor(), 2);
+    EXPECT_EQ(std::remove((d + "/opt/rocm-7.2.0/.info/version").c_str()), 0);
+    EXPECT_EQ(minor(), host_mode ? 4 : -1);
+    EXPECT_EQ(minor(), host_mode ? 4 : -1);
+    put(d + "/opt/rocm-7.2.0/.info/version", "7.5.0\n");
+    EXPECT_EQ(minor(), 5);
+    EXPECT_EQ(minor(), 5);
+    fs::remove_all(d);
+  }
+}
+
+TEST(DirWatch_SeesEntryChangesOnly) {
+  std::string d = mktemp_dir();
+  fs::mkdir_all(d + "/a");
+  put(d + "/a/f", "1");
+  fs::DirWatch w;
+  EXPECT_FALSE(w.unchanged());  // nothing armed
+  EXPECT_TRUE(w.arm({d, d + "/a"}));
+  EXPECT_TRUE(w.unchanged());
+  {
+    std::ofstream f(d + "/a/f", std::ios::app);  // contents: not an entry change
+    f << "2";
+  }
+  EXPECT_TRUE(w.unchanged());
+  put(d + "/a/g", "x");  // an entry created
+  EXPECT_FALSE(w.unchanged());
+  EXPECT_FALSE(w.unchanged());  // disarmed until armed again
+  EXPECT_TRUE(w.arm({d, d + "/a"}));
+  EXPECT_TRUE(w.unchanged());
+  EXPECT_EQ(std::rename((d + "/a").c_str(), (d + "/b").c_str()), 0);
+  EXPECT_FALSE(w.unchanged());
+  EXPECT_FALSE(w.arm({d + "/missing"}));
+  EXPECT_FALSE(w.unchanged());
+  fs::remove_all(d);
 }
 
 TEST(RocmVersion_ExplicitFileMustBeReadable) {

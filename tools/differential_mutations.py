@@ -10,7 +10,7 @@ once with `make build`.  Results: profiles/differential_mutations_r6.txt.
 (Round 6: M5 was the supported-mode lists keyed by the current modes -
 unobservable, deleted; it is now the session's compute mode.  M11 and M12
 are new; M11 applies to VMs, the only nodes whose bus the SR-IOV source
-reads.)
+reads.  M10 and M13 guard the ROCm version kept under a directory watch.)
 """
 import os
 import subprocess
@@ -29,7 +29,8 @@ M = [
  ("M9 DMI kept for any file", "src/util/fs.cpp", "  kept->emplace(path, constant ? std::optional<std::string>(r.data) : std::nullopt);", "  kept->emplace(path, std::optional<std::string>(r.data));"),
  ("M11 SR-IOV check ignores the bus's unbound functions (VMs)", "src/sriov/bound.cpp", "bound != bound_ || unbound != unbound_) return false;", "bound != bound_) return false;"),
  ("M12 amd-smi session values kept across re-init", "src/resource/amdsmi.cpp", "  session_values_.clear();\n", ""),
- ("M10 version file kept across replacement", "src/util/fs.cpp", "if (it != checked_.end() && it->second.dev == static_cast<uint64_t>(st.st_dev) &&\n        it->second.ino == static_cast<uint64_t>(st.st_ino))", "if (it != checked_.end())"),
+ ("M10 ROCm version kept without its directory watch", "src/resource/versions.cpp", "if (k->valid && k->watch.unchanged()) {", "if (k->valid) {"),
+ ("M13 ROCm version lookup watches no directory behind a symlink", "src/util/fs.cpp", "    if (dirs) {\n      std::string parent", "    if (dirs && links == 0) {\n      std::string parent"),
 ]
 sel = sys.argv[2:] or [m[0].split()[0] for m in M]
 for name, f, a, b in M:

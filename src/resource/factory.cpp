@@ -16,6 +16,7 @@ VersionSources version_sources(const config::Config& c) {
   v.root = c.sysfs_root();
   v.host_root = c.host_root();
   v.rocm_version_file = c.rocm_version_file();
+  v.keep = !c.oneshot();
   return v;
 }
 

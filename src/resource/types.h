@@ -161,6 +161,9 @@ struct VersionSources {
   std::string root = "/";         // sysfs root (synthetic trees in tests)
   std::string host_root;          // host filesystem mount point ("" = none)
   std::string rocm_version_file;  // explicit ROCm version file ("" = discover)
+  // Whether the answer may be kept across calls (a loop daemon's; a oneshot
+  // Job asks once and keeps nothing: rocm_version).
+  bool keep = false;
 };
 
 // Reference: resource.Manager (types.go:22-28).  GetCudaDriverVersion maps

@@ -195,11 +195,12 @@ std::optional<RuntimeVersion> lookup(const VersionSources& s, std::string* sourc
 // inotify queue and a pread of the kept file (a version file rewritten in
 // place is read fresh; one replaced, a symlink repointed, a directory on
 // the way renamed or removed is an entry change in a watched directory).
-// The first call looks up plainly (a oneshot Job has one cycle); later
-// misses walk by hand, arm the watch, and walk again - the answer is kept
-// only if both walks agree, so a change racing the first walk is not
-// missed.  Answers from several files (the newest-install scan) and errors
-// are not kept.
+// Only for sources that may be kept (a loop daemon's; a oneshot Job looks
+// up once, and an inotify watch would cost it more than the lookup).  The
+// first call looks up plainly; later misses walk by hand, arm the watch,
+// and walk again - the answer is kept only if both walks agree, so a change
+// racing the first walk is not missed.  Answers from several files (the
+// newest-install scan) and errors are not kept.
 struct Kept {
   std::string key;
   bool seen = false;
@@ -215,6 +216,7 @@ struct Kept {
 }  // namespace
 
 std::optional<RuntimeVersion> rocm_version(const VersionSources& s, std::string* source) {
+  if (!s.keep) return lookup(s, source, nullptr);
   static std::mutex mu;
   static auto* kept = new std::vector<std::unique_ptr<Kept>>();  // leaked: workers may read at exit
   std::string rocm_path;
@@ -226,9 +228,8 @@ std::optional<RuntimeVersion> rocm_version(const VersionSources& s, std::string*
   for (auto& e : *kept)
     if (e->key == key) k = e.get();
   if (!k) {
-    // A few sets of sources at most (one per manager; tests build many):
-    // each holds an inotify instance, a per-user resource.
-    if (kept->size() >= 4) kept->erase(kept->begin());
+    // A few sets of sources at most (one per daemon; tests build many).
+    if (kept->size() >= 8) kept->erase(kept->begin());
     kept->push_back(std::make_unique<Kept>());
     k = kept->back().get();
     k->key = key;

@@ -9,6 +9,8 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <map>
+#include <mutex>
 #include <cerrno>
 #include <climits>
 #include <cstdio>
@@ -442,40 +444,94 @@ bool is_local_fs(int fd) {
   }
 }
 
-DirWatch::~DirWatch() { disarm(); }
+// The shared inotify instance and, per watch descriptor, the DirWatches
+// that need it (one descriptor per directory and instance).
+struct DirWatchRegistry {
+  std::mutex mu;
+  int fd = -1;
+  std::map<int, std::vector<DirWatch*>> owners;
 
-void DirWatch::disarm() {
-  if (fd_ >= 0) ::close(fd_);
-  fd_ = -1;
+  static DirWatchRegistry& get() {
+    static auto* r = new DirWatchRegistry();  // leaked: pool threads may read at exit
+    return *r;
+  }
+  // Reads every queued event and marks the sets whose directories changed.
+  void poll() {
+    alignas(struct inotify_event) char buf[4096];
+    for (;;) {
+      ssize_t n = ::read(fd, buf, sizeof(buf));
+      if (n <= 0) return;  // EAGAIN: nothing (more) queued
+      for (ssize_t off = 0; off < n;) {
+        const auto* e = reinterpret_cast<const struct inotify_event*>(buf + off);
+        off += static_cast<ssize_t>(sizeof(struct inotify_event) + e->len);
+        if (e->mask & IN_Q_OVERFLOW) {
+          for (auto& [wd, ws] : owners)
+            for (auto* w : ws) w->dirty_ = true;
+          continue;
+        }
+        auto it = owners.find(e->wd);
+        if (it != owners.end())
+          for (auto* w : it->second) w->dirty_ = true;
+      }
+    }
+  }
+  void release(DirWatch* w) {
+    for (int wd : w->wds_) {
+      auto it = owners.find(wd);
+      if (it == owners.end()) continue;
+      auto& ws = it->second;
+      ws.erase(std::remove(ws.begin(), ws.end(), w), ws.end());
+      if (ws.empty()) {
+        (void)::inotify_rm_watch(fd, wd);
+        owners.erase(it);
+      }
+    }
+    w->wds_.clear();
+    w->armed_ = false;
+  }
+};
+
+DirWatch::~DirWatch() {
+  auto& r = DirWatchRegistry::get();
+  std::lock_guard<std::mutex> g(r.mu);
+  r.release(this);
 }
 
 bool DirWatch::arm(const std::vector<std::string>& dirs) {
-  // A fresh queue: no event of the previous set (nor the IN_IGNORED its
-  // removal would queue) can be mistaken for a change of this one.
-  disarm();
+  auto& r = DirWatchRegistry::get();
+  std::lock_guard<std::mutex> g(r.mu);
+  if (r.fd >= 0) r.poll();  // events so far belong to the sets armed so far
+  r.release(this);
+  dirty_ = false;
   if (dirs.empty()) return false;
-  fd_ = ::inotify_init1(IN_NONBLOCK | IN_CLOEXEC);
-  if (fd_ < 0) return false;  // e.g. the user's inotify instances used up
+  if (r.fd < 0) r.fd = ::inotify_init1(IN_NONBLOCK | IN_CLOEXEC);
+  if (r.fd < 0) return false;  // e.g. the user's inotify instances used up
   constexpr uint32_t kMask =
       IN_CREATE | IN_DELETE | IN_MOVED_FROM | IN_MOVED_TO | IN_DELETE_SELF | IN_MOVE_SELF | IN_ONLYDIR;
   for (const auto& d : dirs) {
     int dfd = ::open(d.c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC);
     bool local = dfd >= 0 && is_local_fs(dfd);
     if (dfd >= 0) ::close(dfd);
-    if (!local || ::inotify_add_watch(fd_, d.c_str(), kMask) < 0) {
-      disarm();
+    int wd = local ? ::inotify_add_watch(r.fd, d.c_str(), kMask) : -1;
+    if (wd < 0) {
+      r.release(this);
       return false;
     }
+    auto& ws = r.owners[wd];
+    if (std::find(ws.begin(), ws.end(), this) == ws.end()) ws.push_back(this);
+    if (std::find(wds_.begin(), wds_.end(), wd) == wds_.end()) wds_.push_back(wd);
   }
+  armed_ = true;
   return true;
 }
 
 bool DirWatch::unchanged() {
-  if (fd_ < 0) return false;
-  alignas(struct inotify_event) char buf[4096];
-  ssize_t n = ::read(fd_, buf, sizeof(buf));
-  if (n < 0 && errno == EAGAIN) return true;
-  disarm();  // a change (or an overflowed / failed queue): look again
+  auto& r = DirWatchRegistry::get();
+  std::lock_guard<std::mutex> g(r.mu);
+  if (!armed_) return false;
+  r.poll();
+  if (!dirty_) return true;
+  r.release(this);  // a change: look again
   return false;
 }
 

@@ -175,6 +175,13 @@ bool is_local_fs(int fd);
 // each (an entry created, removed or renamed; the directory itself removed
 // or moved).  A lookup's answer - a symlink chain resolved to a file, or the
 // file not found - stands while its directories are unchanged.
+//
+// All DirWatches share one inotify instance, created on the first arm() and
+// kept for the process: closing an instance waits for an SRCU grace period
+// in the kernel (40-70 ms measured on the MI355X pool, at exit of a process
+// that had one), so none is closed while the process runs; a watch no set
+// needs any more is removed (inotify_rm_watch does not wait).  A oneshot
+// Job never arms one (resource::VersionSources::keep).
 class DirWatch {
  public:
   DirWatch() = default;
@@ -186,12 +193,15 @@ class DirWatch {
   // local file system (is_local_fs): then unchanged() stays false.
   bool arm(const std::vector<std::string>& dirs);
   // True while nothing changed in the armed directories since arm(): one
-  // non-blocking read of the inotify queue.  The first change disarms.
+  // non-blocking read of the shared inotify queue.  The first change
+  // disarms.
   bool unchanged();
 
  private:
-  void disarm();
-  int fd_ = -1;
+  std::vector<int> wds_;
+  bool armed_ = false;
+  bool dirty_ = false;
+  friend struct DirWatchRegistry;
 };
 
 std::string join(const std::string& a, const std::string& b);

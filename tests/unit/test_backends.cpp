@@ -423,6 +423,7 @@ TEST(RocmVersion_KeptOnlyWhileThePathToItIsUnchanged) {
     put(d + "/opt/rocm-7.2.0/.info/version", "7.2.0\n");
     link(host_mode ? "/opt/rocm-7.1.0" : "rocm-7.1.0", d + "/opt/rocm");
     VersionSources s;
+    s.keep = true;  // a loop daemon's
     (host_mode ? s.host_root : s.root) = d;
     auto minor = [&] {
       auto v = rocm_version(s);
@@ -481,6 +482,19 @@ TEST(DirWatch_SeesEntryChangesOnly) {
   EXPECT_FALSE(w.unchanged());
   EXPECT_FALSE(w.arm({d + "/missing"}));
   EXPECT_FALSE(w.unchanged());
+  // Two sets sharing a directory (one inotify watch): dropping one leaves
+  // the other's watch in place.
+  fs::mkdir_all(d + "/c");
+  {
+    fs::DirWatch x, y;
+    EXPECT_TRUE(x.arm({d + "/c"}));
+    EXPECT_TRUE(y.arm({d, d + "/c"}));
+    EXPECT_TRUE(x.arm({d}));  // x leaves c
+    EXPECT_TRUE(x.unchanged() && y.unchanged());
+    put(d + "/c/h", "x");
+    EXPECT_FALSE(y.unchanged());
+    EXPECT_TRUE(x.unchanged());
+  }
   fs::remove_all(d);
 }
 

@@ -204,6 +204,7 @@ std::optional<RuntimeVersion> lookup(const VersionSources& s, std::string* sourc
 struct Kept {
   std::string key;
   bool seen = false;
+  int plain = 0;  // calls left to look up plainly: nothing to watch (see below)
   fs::DirWatch watch;
   int fd = -1;  // the file the answer came from (-1: no file, no ROCm)
   std::string source;
@@ -247,15 +248,24 @@ std::optional<RuntimeVersion> rocm_version(const VersionSources& s, std::string*
   k->valid = false;
   if (k->fd >= 0) ::close(k->fd);
   k->fd = -1;
-  if (!k->seen) {
+  if (!k->seen || k->plain > 0) {
     k->seen = true;
+    if (k->plain > 0) --k->plain;
     return lookup(s, source, nullptr);
   }
   Walk first;
   std::string src;
-  lookup(s, nullptr, &first);
-  if (!first.single || !k->watch.arm(first.dirs)) return lookup(s, source, nullptr);
+  auto first_v = lookup(s, &src, &first);
+  if (!first.single || !k->watch.arm(first.dirs)) {
+    // An answer from several files, a directory on a network file system,
+    // no inotify instance left: nothing to keep.  Plain lookups for the
+    // next 64 calls (a walk by hand costs more), then another try.
+    k->plain = 64;
+    if (source && first_v) *source = src;
+    return first_v;
+  }
   Walk second;
+  src.clear();
   auto v = lookup(s, &src, &second);
   if (second.single && second.dirs == first.dirs && second.file == first.file) {
     k->valid = true;

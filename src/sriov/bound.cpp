@@ -271,6 +271,21 @@ bool BoundAmdPCI::still_valid(const std::vector<std::pair<std::string, uint64_t>
 }
 
 std::vector<PCIDevice> BoundAmdPCI::Devices() {
+  refresh();
+  return fell_back_ && fallback_ ? fallback_->Devices() : last_;
+}
+
+bool BoundAmdPCI::DevicesIfChanged(std::vector<PCIDevice>* out) {
+  bool changed = refresh();
+  if (fell_back_ && fallback_) {
+    *out = fallback_->Devices();
+    return true;
+  }
+  if (changed) *out = last_;
+  return changed;
+}
+
+bool BoundAmdPCI::refresh() {
   int64_t t0 = trace::stamp();
   // A booted kernel has sent thousands of uevents; "" or "0" is an emulated
   // sysfs that never counts, and is not trusted.
@@ -278,7 +293,7 @@ std::vector<PCIDevice> BoundAmdPCI::Devices() {
   if (seqnum && (seqnum->empty() || *seqnum == "0")) seqnum.reset();
   if (have_ && seqnum && *seqnum == seqnum_) {
     trace::record_since("pci.bound(kept)", t0);
-    return fell_back_ && fallback_ ? fallback_->Devices() : last_;
+    return fell_back_;
   }
   auto bound = list_bound();
   // Whatever the bus holds that the listed drivers do not bind (empty when
@@ -292,31 +307,28 @@ std::vector<PCIDevice> BoundAmdPCI::Devices() {
     trace::record("pci.list", t_list - t0);
     trace::record("pci.vfs", t_end - t_list);
     trace::record("pci.bound(checked)", t_end - t0);
-    return last_;
+    return false;
   }
   trace::record_since("pci.drivers", t0);
-  std::vector<PCIDevice> out;
   if (bound.empty()) {
     // Nothing bound: a guest whose amdgpu is not loaded still shows its VF
-    // on the bus.
+    // on the bus (the caller asks the fallback scan).
     fell_back_ = true;
     last_.clear();
     pf_dirs_.clear();
-    if (fallback_) out = fallback_->Devices();
   } else {
     int64_t t1 = trace::stamp();
     std::vector<std::string> names;
     for (const auto& e : bound) names.push_back(e.first);
-    out = scan_bound(names, unbound, &pf_dirs_);
+    last_ = scan_bound(names, unbound, &pf_dirs_);
     trace::record_since("pci.bound", t1);
     fell_back_ = false;
-    last_ = out;
   }
   have_ = true;
   bound_ = std::move(bound);
   unbound_ = std::move(unbound);
   seqnum_ = seqnum.value_or("");
-  return out;
+  return true;
 }
 
 }  // namespace gfd::sriov

@@ -69,6 +69,7 @@ class BoundAmdPCI : public AmdPCI {
   explicit BoundAmdPCI(std::string root = "/", std::shared_ptr<SysfsAmdPCI> bus = nullptr, bool merge_unbound = true)
       : root_(std::move(root)), fallback_(std::move(bus)), merge_unbound_(merge_unbound) {}
   std::vector<PCIDevice> Devices() override;
+  bool DevicesIfChanged(std::vector<PCIDevice>* out) override;
   // Whether the last Devices() came from the fallback scan.
   bool used_fallback() const { return fell_back_; }
 
@@ -87,6 +88,8 @@ class BoundAmdPCI : public AmdPCI {
   // Whether last_ still describes the node: same bound and unbound
   // functions, same VFs.
   bool still_valid(const std::vector<std::pair<std::string, uint64_t>>& bound, const std::vector<std::string>& unbound);
+  // Brings last_ up to date; true if it was re-read (or the fallback used).
+  bool refresh();
   std::string root_;
   std::shared_ptr<SysfsAmdPCI> fallback_;
   bool merge_unbound_ = true;

@@ -79,6 +79,13 @@ class AmdPCI {
  public:
   virtual ~AmdPCI() = default;
   virtual std::vector<PCIDevice> Devices() = 0;
+  // Like Devices(), but false - and *out untouched - when the functions are
+  // the ones this source's previous call returned (a kept result: nothing
+  // to copy or classify again).
+  virtual bool DevicesIfChanged(std::vector<PCIDevice>* out) {
+    *out = Devices();
+    return true;
+  }
 };
 
 // Walks <root>/sys/bus/pci/devices and keeps vendor 0x1002 display (0x03)

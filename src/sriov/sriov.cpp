@@ -1,5 +1,7 @@
 #include "sriov/sriov.h"
 
+#include <cstdlib>
+
 #include "sriov/bound.h"
 
 #include "resource/pci_ids.h"
@@ -68,10 +70,20 @@ std::vector<Function> Lib::Devices() {
   std::vector<PCIDevice> devices;
   std::lock_guard<std::mutex> lk(mu_);
   try {
-    devices = pci_->Devices();
+    // A kept result (the source's own change detection, sriov/bound.h) was
+    // classified already: no copy of the functions, no classification.
+    static const bool ab_copy = std::getenv("GFD_AB_SRIOV_COPY") != nullptr;  // A/B only
+    if (ab_copy) {
+      devices = pci_->Devices();
+    } else if (!pci_->DevicesIfChanged(&devices)) {
+      if (have_) return functions_;
+      devices = pci_->Devices();
+    }
   } catch (const std::exception& e) {
+    have_ = false;
     throw Error(std::string("error getting AMD specific PCI devices: ") + e.what());
   }
+  have_ = false;  // until classified
   std::vector<Function> out;
   for (auto& d : devices) {
     std::optional<Info> info;
@@ -82,6 +94,8 @@ std::vector<Function> Lib::Devices() {
     }
     if (info) out.emplace_back(std::move(d), std::move(*info));
   }
+  functions_ = out;
+  have_ = true;
   return out;
 }
 

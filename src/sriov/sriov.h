@@ -90,6 +90,8 @@ class Lib : public Interface {
   std::shared_ptr<AmdPCI> pci_;
   std::string root_;
   std::mutex mu_;
+  bool have_ = false;                // functions_ classifies the source's last result
+  std::vector<Function> functions_;  // (kept while the source reports no change)
 };
 
 // The node's SR-IOV functions (sriov/bound.h): the functions the listed

@@ -203,6 +203,49 @@ TEST(Sriov_LabelerEmptyWhenNoFunctions) {
   EXPECT_EQ(lm::NewSriovLabeler(lib)->GetLabels(), lm::Labels{});
 }
 
+namespace {
+// A source that reports "unchanged" on demand, and counts full reads.
+struct ScriptedPCI : AmdPCI {
+  std::vector<PCIDevice> devices;
+  bool changed = true;
+  int full_reads = 0;
+  std::vector<PCIDevice> Devices() override {
+    ++full_reads;
+    return devices;
+  }
+  bool DevicesIfChanged(std::vector<PCIDevice>* out) override {
+    if (!changed) return false;
+    *out = Devices();
+    return true;
+  }
+};
+}  // namespace
+
+TEST(Sriov_LibClassifiesOnlyWhatTheSourceReadAgain) {
+  auto src = std::make_shared<ScriptedPCI>();
+  PCIDevice pf = find("pf");
+  src->devices = {pf};
+  Lib lib(src);
+  EXPECT_EQ(lib.Devices().size(), static_cast<size_t>(1));
+  EXPECT_EQ(src->full_reads, 1);
+  // Kept by the source: the classified functions again, nothing copied.
+  src->changed = false;
+  src->devices.clear();  // (not looked at)
+  for (int i = 0; i < 3; ++i) EXPECT_EQ(lib.Devices().size(), static_cast<size_t>(1));
+  EXPECT_EQ(src->full_reads, 1);
+  // Re-read by the source: classified anew.
+  src->changed = true;
+  EXPECT_EQ(lib.Devices().size(), static_cast<size_t>(0));
+  EXPECT_EQ(src->full_reads, 2);
+  // A Lib that never classified asks for the whole list even when the
+  // source reports no change.
+  src->changed = false;
+  src->devices = {pf, pf};
+  Lib fresh(src);
+  EXPECT_EQ(fresh.Devices().size(), static_cast<size_t>(2));
+  EXPECT_EQ(src->full_reads, 3);
+}
+
 TEST(Sriov_SysfsScanMissingRootErrors) {
   auto lib = new_sriov_lib("/nonexistent-gfd-root");
   EXPECT_THROW_MSG(lib->Devices(), "unable to read PCI bus devices");

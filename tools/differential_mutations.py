@@ -30,6 +30,7 @@ M = [
  ("M11 SR-IOV check ignores the bus's unbound functions (VMs)", "src/sriov/bound.cpp", "bound != bound_ || unbound != unbound_) return false;", "bound != bound_) return false;"),
  ("M12 amd-smi session values kept across re-init", "src/resource/amdsmi.cpp", "  session_values_.clear();\n", ""),
  ("M10 ROCm version kept without its directory watch", "src/resource/versions.cpp", "if (k->valid && k->watch.unchanged()) {", "if (k->valid) {"),
+ ("M14 SR-IOV classification kept after the source re-read", "src/sriov/sriov.cpp", "    if (!pci_->DevicesIfChanged(&devices)) {", "    if (!pci_->DevicesIfChanged(&devices) || have_) {"),
  ("M13 ROCm version lookup watches no directory behind a symlink", "src/util/fs.cpp", "    if (dirs) {\n      std::string parent", "    if (dirs && links == 0) {\n      std::string parent"),
 ]
 sel = sys.argv[2:] or [m[0].split()[0] for m in M]

@@ -1,7 +1,5 @@
 #include "sriov/sriov.h"
 
-#include <cstdlib>
-
 #include "sriov/bound.h"
 
 #include "resource/pci_ids.h"
@@ -72,10 +70,7 @@ std::vector<Function> Lib::Devices() {
   try {
     // A kept result (the source's own change detection, sriov/bound.h) was
     // classified already: no copy of the functions, no classification.
-    static const bool ab_copy = std::getenv("GFD_AB_SRIOV_COPY") != nullptr;  // A/B only
-    if (ab_copy) {
-      devices = pci_->Devices();
-    } else if (!pci_->DevicesIfChanged(&devices)) {
+    if (!pci_->DevicesIfChanged(&devices)) {
       if (have_) return functions_;
       devices = pci_->Devices();
     }

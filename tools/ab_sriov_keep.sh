@@ -1,7 +1,8 @@
 #!/bin/bash
 # A/B: the SR-IOV lookup's kept result handed over without a copy and
 # without classifying it again (default) or copied and classified every
-# cycle (GFD_AB_SRIOV_COPY=1, the switch removed once decided); alternated,
+# cycle (GFD_AB_SRIOV_COPY=1, the switch removed once decided -
+# profiles/sriov_keep_ab_r6.txt); alternated,
 # 5 pairs, bench.py's untraced value and the traced steps' sriov phases.
 # Usage (GPU box): tools/ab_sriov_keep.sh [outdir]
 set -o pipefail

@@ -10,7 +10,8 @@ once with `make build`.  Results: profiles/differential_mutations_r6.txt.
 (Round 6: M5 was the supported-mode lists keyed by the current modes -
 unobservable, deleted; it is now the session's compute mode.  M11 and M12
 are new; M11 applies to VMs, the only nodes whose bus the SR-IOV source
-reads.  M10 and M13 guard the ROCm version kept under a directory watch.)
+reads.  M10 and M13 guard the ROCm version kept under a directory watch, M14 the kept
+SR-IOV classification.)
 """
 import os
 import subprocess

@@ -292,14 +292,20 @@ bool session_compute_mode(const std::string& pci, std::string* mode, int64_t* re
 bool query_unpartitioned(AmdSmiLib& L, const std::string& root, ProcInfo& p, AmdSmiManager::KfdNodeFacts* kfd,
                          std::string* mode, int64_t* read_ns, AmdSmiManager::SessionValues* kept) {
   uint32_t* node_id = &kfd->node_id;
-  std::string pci = fs::join(root, "sys/bus/pci/devices/" + p.gpu_bdf);
-  if (!session_compute_mode(pci, mode, read_ns) || *mode != "SPX") return false;
+  std::string pci;  // built only for a read (a steady cycle makes none)
+  auto pci_dir = [&]() -> const std::string& {
+    if (pci.empty()) pci = fs::join(root, "sys/bus/pci/devices/" + p.gpu_bdf);
+    return pci;
+  };
+  if (mode->empty() && !session_compute_mode(pci_dir(), mode, read_ns)) return false;
+  if (*mode != "SPX") return false;
   std::string mp_mode;
   std::optional<uint64_t> vram;
   if (kept && !kept->memory_partition.empty() && kept->vram) {
     mp_mode = kept->memory_partition;
     vram = kept->vram;
   } else {
+    pci_dir();
     auto mp = AMDSMI_CALL("memory_partition(sysfs)", fs::attrs().read_trimmed(pci + "/current_memory_partition"));
     mp_mode = mp ? partition_mode(*mp) : "";
     if (mp_mode.empty()) return false;
@@ -432,7 +438,7 @@ int sysfs_xgmi_links(const std::string& root, const std::string& bdf) {
 // GPU-level capabilities: xGMI links, virtualization mode, supported
 // partition modes.  Any processor handle of the GPU will do.
 void query_gpu_caps(AmdSmiLib& L, const ProcInfo& p, const std::string& root, GpuExtras& x,
-                    AmdSmiManager::AvailableModes& avail) {
+                    const AmdSmiManager::AvailableModes* kept_avail, AmdSmiManager::AvailableModes& avail) {
   // Pre-filled from the session (AmdSmiManager::session_values_) when kept.
   if (x.xgmi_links < 0) x.xgmi_links = AMDSMI_CALL("xgmi_num_links(sysfs)", sysfs_xgmi_links(root, p.gpu_bdf));
   if (x.xgmi_links < 0 && L.get_gpu_xgmi_link_status) {
@@ -460,9 +466,9 @@ void query_gpu_caps(AmdSmiLib& L, const ProcInfo& p, const std::string& root, Gp
       x.virtualization = classify_virtualization(pci, p.device_id, running_in_vm(root), fs::exists(pci + "/physfn"));
   }
   // Kept from an earlier cycle of the session (AmdSmiManager::available_).
-  if (avail.known) {
-    x.available_memory = avail.memory;
-    x.available_compute = avail.compute;
+  if (kept_avail && kept_avail->known) {
+    x.available_memory = kept_avail->memory;
+    x.available_compute = kept_avail->compute;
     return;
   }
   // Supported memory partition modes: world-readable in sysfs (~5 us);
@@ -596,7 +602,7 @@ static std::vector<std::vector<ProcInfo>> collect_physical_gpus(AmdSmiLib& L, co
       p.h = h;
       p.bdf = known->second;
       identity_from_cache(identities, p);
-      slots[bdf_slot(p.bdf)].push_back(p);
+      slots[bdf_slot(p.bdf)].push_back(std::move(p));
     }
   }
 
@@ -628,7 +634,7 @@ static std::vector<std::vector<ProcInfo>> collect_physical_gpus(AmdSmiLib& L, co
   for (auto& procs : physical) {
     std::vector<std::string> bdfs;
     for (const auto& p : procs) bdfs.push_back(p.bdf);
-    std::string key = str::join(bdfs, ",");
+    std::string key = procs.size() == 1 ? procs[0].bdf : str::join(bdfs, ",");
     auto it = parents.find(key);
     if (it == parents.end()) {
       uint32_t device_id = 0;
@@ -751,10 +757,15 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
     std::string mode;  // session cache entry: compute partition mode
     SessionValues values;  // session cache entry: memory partition, VRAM, xGMI links
     int64_t mode_read_ns = -1;  // >= 0: read this cycle (not from the cache)
-    AvailableModes avail;  // session cache entry
+    AvailableModes avail;  // read this cycle (kept_avail: null)
     std::vector<PartitionFacts> parts;  // session cache entries (partitioned GPUs), aligned with procs
+    // Which values came from the session's entries (then nothing is written
+    // back: work() changes no value it was given).
+    bool kept_virt = false, kept_kfd = false, kept_mode = false, kept_values = false;
+    const AvailableModes* kept_avail = nullptr;
   };
   std::vector<Gpu> gpus;
+  gpus.reserve(physical.size());
   for (size_t i = 0; i < physical.size(); ++i) {
     const std::string& bdf = physical[i][0].gpu_bdf;
     if (opts_.filter.matches(static_cast<int>(i), bdf)) {
@@ -763,23 +774,36 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
       g.bdf = bdf;
       g.procs = &physical[i];
       gpus.push_back(std::move(g));
+      Gpu& e = gpus.back();
       auto v = virt_mode_.find(bdf);
-      if (v != virt_mode_.end()) gpus.back().extras.virtualization = v->second;
+      if (v != virt_mode_.end()) {
+        e.extras.virtualization = v->second;
+        e.kept_virt = true;
+      }
       auto k = kfd_node_.find(bdf);
-      if (k != kfd_node_.end()) gpus.back().kfd = k->second;
+      if (k != kfd_node_.end()) {
+        e.kfd = k->second;
+        e.kept_kfd = e.kfd.known;
+      }
       auto a = available_.find(bdf);
-      if (a != available_.end()) gpus.back().avail = a->second;
+      if (a != available_.end() && a->second.known) e.kept_avail = &a->second;
       auto sv = session_values_.find(bdf);
       if (sv != session_values_.end()) {
-        gpus.back().values = sv->second;
-        gpus.back().extras.xgmi_links = sv->second.xgmi_links;
+        e.values = sv->second;
+        e.extras.xgmi_links = sv->second.xgmi_links;
+        e.kept_values = true;
       }
       auto m = compute_mode_.find(bdf);
-      if (m != compute_mode_.end()) gpus.back().mode = m->second;
-      else gpus.back().mode_read_ns = 0;
+      if (m != compute_mode_.end()) {
+        e.mode = m->second;
+        e.kept_mode = !e.mode.empty();
+      } else {
+        e.mode_read_ns = 0;
+      }
+      e.parts.reserve(physical[i].size());
       for (const auto& p : physical[i]) {
         auto f = partition_facts_.find(p.h);
-        gpus.back().parts.push_back(f != partition_facts_.end() ? f->second : PartitionFacts{});
+        e.parts.push_back(f != partition_facts_.end() ? f->second : PartitionFacts{});
       }
     }
   }
@@ -821,7 +845,7 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
       }
       int64_t t1 = trace::stamp(traced);
       const ProcInfo& first = procs.front();
-      query_gpu_caps(L, first, opts_.root, g.extras, g.avail);
+      query_gpu_caps(L, first, opts_.root, g.extras, g.kept_avail, g.avail);
       if (procs.size() > 1 || (!first.compute_partition.empty() && first.compute_partition != "SPX"))
         g.extras.engines = AMDSMI_CALL("partition_engines(sysfs)", partition_engine_counts(opts_.root, first.gpu_bdf));
       g.proc_ns = t1 - t0;
@@ -855,7 +879,7 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
     bool all_cached = true;
     for (const auto& g : gpus) {
       all_cached = all_cached && g.procs->size() == 1 && g.mode == "SPX" && g.values.vram != 0 &&
-                   g.kfd.known && g.avail.known &&
+                   g.kfd.known && g.kept_avail &&
                    !g.extras.virtualization.empty() && g.extras.xgmi_links >= 0 && (*g.procs)[0].identified &&
                    !is_generic_name((*g.procs)[0].market_name);
       if (!all_cached) break;
@@ -899,18 +923,20 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
     for (const auto& p : *g.procs)
       if (p.identified && !identity_.count(p.h))
         identity_[p.h] = Identity{p.market_name, p.vendor_id, p.device_id, p.cus, p.gfx, p.uuid};
-    if (!g.extras.virtualization.empty()) virt_mode_[g.bdf] = g.extras.virtualization;
-    if (g.kfd.known) kfd_node_[g.bdf] = g.kfd;
-    if (!g.mode.empty()) compute_mode_[g.bdf] = g.mode;
-    if (g.values.vram && g.extras.xgmi_links >= 0) {
+    if (!g.kept_virt && !g.extras.virtualization.empty()) virt_mode_[g.bdf] = g.extras.virtualization;
+    if (!g.kept_kfd && g.kfd.known) kfd_node_[g.bdf] = g.kfd;
+    if (!g.kept_mode && !g.mode.empty()) compute_mode_[g.bdf] = g.mode;
+    if (!g.kept_values && g.values.vram && g.extras.xgmi_links >= 0) {
       SessionValues v = g.values;
       v.xgmi_links = g.extras.xgmi_links;
       session_values_[g.bdf] = v;
     }
-    if (!g.avail.known)
-      available_.erase(g.bdf);
-    else
-      available_[g.bdf] = g.avail;
+    if (!g.kept_avail) {
+      if (!g.avail.known)
+        available_.erase(g.bdf);
+      else
+        available_[g.bdf] = g.avail;
+    }
     for (const auto& f : g.parts)
       if (f.node_id != kNoNode) partition_facts_[f.handle] = f;
   }
@@ -928,8 +954,8 @@ std::vector<DevicePtr> AmdSmiManager::snapshot() {
     info.gfx = gfx_target_from_amdsmi(first.gfx);
     info.compute_partition = first.compute_partition;
     info.memory_partition = first.memory_partition;
-    info.available_compute_partitions = g.extras.available_compute;
-    info.available_memory_partitions = g.extras.available_memory;
+    info.available_compute_partitions = std::move(g.extras.available_compute);
+    info.available_memory_partitions = std::move(g.extras.available_memory);
     info.xgmi_links = g.extras.xgmi_links;
     info.virtualization = g.extras.virtualization;
     bool partitioned = g.procs->size() > 1 || (!first.compute_partition.empty() && first.compute_partition != "SPX");

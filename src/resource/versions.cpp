@@ -238,7 +238,7 @@ std::optional<RuntimeVersion> rocm_version(const VersionSources& s, std::string*
   if (k->valid && k->watch.unchanged()) {
     if (k->fd < 0) return std::nullopt;
     std::string data;
-    if (fs::pread_all(k->fd, 4096, &data) == 0)
+    if (fs::pread_all(k->fd, 4096, &data, true) == 0)  // a regular file
       if (auto v = parse_runtime_version(str::trim(data))) {
         if (source) *source = k->source;
         return v;

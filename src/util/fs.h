@@ -218,7 +218,9 @@ int remove_all(const std::string& path);
 
 // The whole of an open file, from offset 0, up to `max_bytes` (pread: no
 // file position involved).  0 or an errno.
-int pread_all(int fd, size_t max_bytes, std::string* out);
+// `short_read_is_all`: the file is a sysfs attribute or a regular file, so a
+// first read shorter than a page is the whole of it (no second read).
+int pread_all(int fd, size_t max_bytes, std::string* out, bool short_read_is_all = false);
 
 std::string errno_str(int err);
 

@@ -213,8 +213,7 @@ ReadResult AttrReader::read(const std::string& path, size_t max_bytes) {
   }
   if (kept) {
     // Kept descriptors are sysfs attributes (or, in tests, regular files).
-    static const bool ab_twice = std::getenv("GFD_AB_PREAD_TWICE") != nullptr;  // A/B only
-    if (pread_all(kept->fd, max_bytes, &r.data, !ab_twice) == 0) return r;
+    if (pread_all(kept->fd, max_bytes, &r.data, true) == 0) return r;
     // Removed since it was opened (ENODEV) or otherwise unusable: forget it
     // and look the path up again.
     std::unique_lock<std::shared_mutex> g(mu_);

@@ -527,8 +527,8 @@ def test_driver_bench_command_stays_within_its_bounds(tmp_path):
     a +25% drift must fail): headline 0.022 ms (0.0169-0.0172 measured on
     the driver's boxes, BENCH_r05 and profiles/bench_fresh_r6.txt), cycles 1 s
     apart 0.28 ms (0.18-0.24), their unattributed time 0.02 ms; the Job
-    process: its fastest of 15 spawns 1.0 ms (0.778-0.804 on the round-6
-    boxes) - the p50 of 15 spawns right after the idle second cycles is
+    process: its fastest of 15 spawns 1.15 ms (0.778-0.928 on the round-6
+    boxes, +24 % over the slowest) - the p50 of 15 spawns right after the idle second cycles is
     bimodal on some boxes (spawns of 0.8 or 1.5-1.9 ms, the slow ones on
     idle cores: p50 0.799-1.538, profiles/bench_fresh_r6.txt), so it is
     bounded only against gross drift, 2.0 ms; and no write after the second
@@ -546,7 +546,7 @@ def test_driver_bench_command_stays_within_its_bounds(tmp_path):
     _within_bounds(measure, [("headline_ms", lambda r: r["value"], 0.022),
                              ("cold_p50_ms", lambda r: r["cold_cycle"]["p50_ms"], 0.28),
                              ("cold_other_ms", lambda r: r["cold_cycle"]["other_p50_ms"], 0.02),
-                             ("job_fastest_ms", lambda r: min(r["extras"]["oneshot_process"]["runs_ms"]), 1.0),
+                             ("job_fastest_ms", lambda r: min(r["extras"]["oneshot_process"]["runs_ms"]), 1.15),
                              ("job_p50_ms", lambda r: r["oneshot_process_p50_ms"], 2.0)])
 
 

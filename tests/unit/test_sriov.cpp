@@ -420,6 +420,30 @@ TEST(Fs_AttrReaderKeepsOnlySysfsDescriptors) {
   fs::remove_all(d);
 }
 
+TEST(Fs_KeptReadsAreWholeAtAnySize) {
+  // A first read shorter than a page is the whole attribute (one pread); a
+  // longer one keeps reading to the end.
+  char d[] = "/tmp/gfd-attr-size-XXXXXX";
+  EXPECT_TRUE(mkdtemp(d) != nullptr);
+  std::string f = std::string(d) + "/attr";
+  fs::AttrReader kept;
+  kept.keep_all_for_testing(true);
+  for (size_t n : {size_t{5}, size_t{4095}, size_t{4096}, size_t{6000}, size_t{20000}, size_t{7}}) {
+    std::string body(n, 'x');
+    for (size_t i = 0; i < n; i += 97) body[i] = static_cast<char>('a' + i % 26);
+    FILE* fp = std::fopen(f.c_str(), "w");  // same inode: the kept descriptor reads it
+    std::fwrite(body.data(), 1, body.size(), fp);
+    std::fclose(fp);
+    auto r = kept.read(f);
+    EXPECT_TRUE(r.ok());
+    EXPECT_EQ(r.data.size(), n);
+    EXPECT_TRUE(r.data == body);
+  }
+  EXPECT_EQ(kept.open_count(), static_cast<size_t>(1));
+  EXPECT_EQ(kept.read(f, 3).data, std::string("axx"));
+  fs::remove_all(d);
+}
+
 TEST(Fs_AttrReaderDropsADescriptorThatStopsReading) {
   // The CPU-side analogue of a sysfs attribute whose device went away (reads
   // on the kept descriptor fail with ENODEV): a /proc file of a process that

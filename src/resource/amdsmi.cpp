@@ -654,7 +654,10 @@ static std::vector<std::vector<ProcInfo>> collect_physical_gpus(AmdSmiLib& L, co
 
 
 
-AmdSmiManager::AmdSmiManager(AmdSmiOptions opts) : opts_(std::move(opts)) { opts_.versions.root = opts_.root; }
+AmdSmiManager::AmdSmiManager(AmdSmiOptions opts)
+    : opts_(std::move(opts)), generation_attr_(fs::join(opts_.root, "sys/class/kfd/kfd/topology/generation_id")) {
+  opts_.versions.root = opts_.root;
+}
 
 AmdSmiManager::~AmdSmiManager() {
   if (lib_initialized_) library_shutdown();
@@ -687,7 +690,9 @@ void AmdSmiManager::library_shutdown() {
 }
 
 std::string AmdSmiManager::read_generation() const {
-  return fs::attrs().read_trimmed(fs::join(opts_.root, "sys/class/kfd/kfd/topology/generation_id")).value_or("");
+  std::string gen;
+  if (!generation_attr_.read(&gen)) gen.clear();
+  return gen;
 }
 
 void AmdSmiManager::Init() {

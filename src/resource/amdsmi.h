@@ -42,6 +42,7 @@
 
 #include "resource/filter.h"
 #include "resource/types.h"
+#include "util/fs.h"
 
 namespace gfd::resource {
 
@@ -115,6 +116,7 @@ class AmdSmiManager : public Manager {
   std::string read_generation() const;
 
   AmdSmiOptions opts_;
+  mutable fs::KeptAttr generation_attr_{""};  // topology/generation_id (set in the constructor)
   AmdSmiLib* lib_ = nullptr;
   bool lib_initialized_ = false;
   bool in_window_ = false;

@@ -141,7 +141,8 @@ bool has_kfd_topology(const std::string& root, std::string* reason) {
   return true;
 }
 
-SysfsManager::SysfsManager(SysfsOptions opts) : opts_(std::move(opts)) {
+SysfsManager::SysfsManager(SysfsOptions opts)
+    : opts_(std::move(opts)), generation_attr_(fs::join(opts_.root, "sys/class/kfd/kfd/topology/generation_id")) {
   opts_.versions.root = opts_.root;
   topology_ = fs::join(opts_.root, kTopology);
   in_vm_ = running_in_vm(opts_.root);
@@ -151,7 +152,7 @@ void SysfsManager::Init() {
   // generation_id lives next to nodes/; when it is readable the topology is
   // there.  Otherwise list nodes/ (kernels without generation_id, or to get
   // the error to report).
-  generation_ = fs::attrs().read_trimmed(fs::join(opts_.root, "sys/class/kfd/kfd/topology/generation_id")).value_or("");
+  if (!generation_attr_.read(&generation_)) generation_.clear();
   if (generation_.empty()) {
     int err = 0;
     fs::list_dir(topology_, &err);

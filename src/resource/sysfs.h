@@ -26,6 +26,7 @@
 
 #include "resource/filter.h"
 #include "resource/types.h"
+#include "util/fs.h"
 
 namespace gfd::resource {
 
@@ -56,6 +57,7 @@ class SysfsManager : public Manager {
   std::shared_ptr<const Topology> read_topology() const;
 
   SysfsOptions opts_;
+  fs::KeptAttr generation_attr_{""};  // topology/generation_id (set in the constructor)
   std::string topology_;
   // The parsed GPU nodes are kept while KFD's topology generation_id (read
   // in Init) is unchanged: KFD rebuilds the topology and bumps the generation

@@ -289,8 +289,8 @@ bool BoundAmdPCI::refresh() {
   int64_t t0 = trace::stamp();
   // A booted kernel has sent thousands of uevents; "" or "0" is an emulated
   // sysfs that never counts, and is not trusted.
-  auto seqnum = fs::attrs().read_trimmed(fs::join(root_, "sys/kernel/uevent_seqnum"));
-  if (seqnum && (seqnum->empty() || *seqnum == "0")) seqnum.reset();
+  std::optional<std::string> seqnum;
+  if (std::string s; seqnum_attr_.read(&s) && !s.empty() && s != "0") seqnum = std::move(s);
   if (have_ && seqnum && *seqnum == seqnum_) {
     trace::record_since("pci.bound(kept)", t0);
     return fell_back_;

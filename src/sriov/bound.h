@@ -67,7 +67,10 @@ class BoundAmdPCI : public AmdPCI {
   // `merge_unbound`: whether the AMD functions no listed driver binds are
   // looked for on the bus (else the bus is read only when nothing is bound).
   explicit BoundAmdPCI(std::string root = "/", std::shared_ptr<SysfsAmdPCI> bus = nullptr, bool merge_unbound = true)
-      : root_(std::move(root)), fallback_(std::move(bus)), merge_unbound_(merge_unbound) {}
+      : root_(std::move(root)),
+        fallback_(std::move(bus)),
+        merge_unbound_(merge_unbound),
+        seqnum_attr_(fs::join(root_, "sys/kernel/uevent_seqnum")) {}
   std::vector<PCIDevice> Devices() override;
   bool DevicesIfChanged(std::vector<PCIDevice>* out) override;
   // Whether the last Devices() came from the fallback scan.
@@ -93,6 +96,7 @@ class BoundAmdPCI : public AmdPCI {
   std::string root_;
   std::shared_ptr<SysfsAmdPCI> fallback_;
   bool merge_unbound_ = true;
+  fs::KeptAttr seqnum_attr_;  // /sys/kernel/uevent_seqnum
   bool have_ = false;
   bool fell_back_ = false;
   std::string seqnum_;  // /sys/kernel/uevent_seqnum of the kept result

@@ -108,8 +108,8 @@ void SysfsAmdPCI::update() {
   // scan: the bus listing is unchanged too, and is not read.
   // A booted kernel has sent thousands of uevents; "0" would be an emulated
   // sysfs that never counts, and is not trusted.
-  auto seqnum = fs::attrs().read_trimmed(fs::join(root_, "sys/kernel/uevent_seqnum"));
-  if (seqnum && (seqnum->empty() || *seqnum == "0")) seqnum.reset();
+  std::optional<std::string> seqnum;
+  if (std::string s; seqnum_attr_.read(&s) && !s.empty() && s != "0") seqnum = std::move(s);
   bool changed = true;
   if (seqnum && *seqnum == seqnum_ && scanned_) {
     changed = false;

@@ -118,7 +118,8 @@ class AmdPCI {
 // (profiles/pci_scan_probe.txt).
 class SysfsAmdPCI : public AmdPCI {
  public:
-  explicit SysfsAmdPCI(std::string root = "/") : root_(std::move(root)) {}
+  explicit SysfsAmdPCI(std::string root = "/")
+      : root_(std::move(root)), seqnum_attr_(fs::join(root_, "sys/kernel/uevent_seqnum")) {}
   std::vector<PCIDevice> Devices() override;
   // The addresses of the AMD display / accelerator functions on the bus,
   // sorted: Devices() without the per-function SR-IOV state (the
@@ -146,6 +147,7 @@ class SysfsAmdPCI : public AmdPCI {
   };
   static Identity read_identity(const std::string& addr, const std::string& path, uint64_t ino);
   std::string root_;
+  fs::KeptAttr seqnum_attr_;  // /sys/kernel/uevent_seqnum
   fs::DirListing listing_;
   bool scanned_ = false;
   std::string seqnum_;  // /sys/kernel/uevent_seqnum at the last scan

@@ -437,6 +437,39 @@ std::string resolve_in_root(const std::string& root, const std::string& rel, std
   return path_of(cur);
 }
 
+KeptAttr::~KeptAttr() {
+  if (fd_ >= 0) ::close(fd_);
+}
+
+bool KeptAttr::read(std::string* out) {
+  char buf[256];
+  ssize_t n = -1;
+  if (fd_ >= 0) {
+    n = ::pread(fd_, buf, sizeof(buf), 0);
+    if (n < 0) {  // removed since it was opened (ENODEV): look the path up again
+      ::close(fd_);
+      fd_ = -1;
+    }
+  }
+  if (fd_ < 0) {
+    int fd = ::open(path_.c_str(), O_RDONLY | O_CLOEXEC);
+    if (fd < 0) return false;
+    n = ::pread(fd, buf, sizeof(buf), 0);
+    struct statfs sfs;
+    if (n >= 0 && ::fstatfs(fd, &sfs) == 0 && static_cast<long>(sfs.f_type) == kSysfsMagic)
+      fd_ = fd;
+    else
+      ::close(fd);
+  }
+  if (n < 0) return false;
+  size_t b = 0, e = static_cast<size_t>(n);
+  auto space = [](char c) { return c == ' ' || c == '\n' || c == '\t' || c == '\r'; };
+  while (b < e && space(buf[b])) ++b;
+  while (e > b && space(buf[e - 1])) --e;
+  out->assign(buf + b, e - b);
+  return true;
+}
+
 bool is_local_fs(int fd) {
   struct statfs sf;
   if (::fstatfs(fd, &sf) != 0) return false;

@@ -166,6 +166,26 @@ class Dir {
 // directories whose entries decide the answer.
 std::string resolve_in_root(const std::string& root, const std::string& rel, std::vector<std::string>* dirs = nullptr);
 
+// One small attribute read every cycle (the KFD topology generation, the
+// kernel's uevent counter): on sysfs through a descriptor kept open, read
+// with one pread into a stack buffer - no path lookup, no allocation; off
+// sysfs (synthetic trees, whose files tests replace) opened for each read,
+// as AttrReader does.  Not thread-safe: one per reader.
+class KeptAttr {
+ public:
+  explicit KeptAttr(std::string path) : path_(std::move(path)) {}
+  ~KeptAttr();
+  KeptAttr(const KeptAttr&) = delete;
+  KeptAttr& operator=(const KeptAttr&) = delete;
+  // The trimmed contents (up to 255 bytes) into *out; false if unreadable.
+  bool read(std::string* out);
+  const std::string& path() const { return path_; }
+
+ private:
+  std::string path_;
+  int fd_ = -1;  // kept: a sysfs attribute
+};
+
 // Whether the file system of `fd` is local, so that this kernel sees every
 // change to it (ext4, xfs, btrfs, tmpfs, overlayfs): a lease or an inotify
 // watch there misses nothing another node did.

@@ -444,6 +444,30 @@ TEST(Fs_KeptReadsAreWholeAtAnySize) {
   fs::remove_all(d);
 }
 
+TEST(Fs_KeptAttrReadsFreshOffSysfsAndKeepsOnSysfs) {
+  char d[] = "/tmp/gfd-kept-attr-XXXXXX";
+  EXPECT_TRUE(mkdtemp(d) != nullptr);
+  std::string f = std::string(d) + "/generation_id";
+  fs::KeptAttr a(f);
+  std::string v;
+  EXPECT_FALSE(a.read(&v));  // missing
+  put_file(f, " 7\n");
+  EXPECT_TRUE(a.read(&v));
+  EXPECT_EQ(v, std::string("7"));
+  put_file(f, "8\n");  // replaced (a new inode): off sysfs nothing is kept
+  EXPECT_TRUE(a.read(&v));
+  EXPECT_EQ(v, std::string("8"));
+  fs::remove_all(d);
+  EXPECT_FALSE(a.read(&v));
+  // Real sysfs (when present): read through the kept descriptor, fresh each time.
+  fs::KeptAttr seq("/sys/kernel/uevent_seqnum");
+  std::string s1, s2;
+  if (seq.read(&s1)) {
+    EXPECT_TRUE(seq.read(&s2));
+    EXPECT_TRUE(str::parse_uint(s2).value_or(0) >= str::parse_uint(s1).value_or(0));
+  }
+}
+
 TEST(Fs_AttrReaderDropsADescriptorThatStopsReading) {
   // The CPU-side analogue of a sysfs attribute whose device went away (reads
   // on the kept descriptor fail with ENODEV): a /proc file of a process that

@@ -3,9 +3,11 @@
 #include "util/trace.h"
 
 #include <pthread.h>
+#include <x86intrin.h>
 #include <sched.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <atomic>
 
 #include "util/affinity.h"
@@ -160,7 +162,14 @@ void WorkerPool::Task::State::run() {
   std::lock_guard<std::mutex> g(mu);
   error = err;
   done = true;
+  finished.store(true, std::memory_order_release);
   cv.notify_all();
+}
+
+void WorkerPool::Task::State::spin() const {
+  static const bool off = std::getenv("GFD_AB_NO_WAIT_SPIN") != nullptr;  // A/B only
+  if (off) return;
+  for (int i = 0; i < 1000 && !finished.load(std::memory_order_acquire); ++i) _mm_pause();
 }
 
 WorkerPool::Task WorkerPool::submit(std::function<void()> fn) {
@@ -201,6 +210,7 @@ std::vector<WorkerPool::Task> WorkerPool::submit_sequence(std::vector<std::funct
 
 void WorkerPool::Task::wait() {
   if (!state_) return;
+  state_->spin();
   std::unique_lock<std::mutex> lk(state_->mu);
   state_->cv.wait(lk, [this] { return state_->done; });
   if (state_->error) std::rethrow_exception(state_->error);
@@ -212,9 +222,11 @@ void WorkerPool::Task::cancel_or_wait() {
     std::lock_guard<std::mutex> g(state_->mu);
     state_->fn = nullptr;
     state_->done = true;
+    state_->finished.store(true, std::memory_order_release);
     state_->cv.notify_all();
     return;
   }
+  state_->spin();
   std::unique_lock<std::mutex> lk(state_->mu);
   state_->cv.wait(lk, [this] { return state_->done; });
 }

@@ -59,10 +59,15 @@ class WorkerPool {
       std::mutex mu;
       std::condition_variable cv;
       std::atomic<bool> claimed{false};  // a thread has started fn
+      std::atomic<bool> finished{false};  // done, readable without the lock (a waiter's spin)
       bool done = false;
       std::exception_ptr error;
       std::function<void()> fn;
       void run();  // claimed by the caller: run fn, publish the result
+      // A waiter spins this long (~10 us) before it sleeps on cv: a task
+      // another thread is finishing costs its remaining run, not a futex
+      // wake-up of the waiter on top (1-2 us back to back).
+      void spin() const;
     };
     std::shared_ptr<State> state_;
   };

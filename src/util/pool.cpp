@@ -167,8 +167,6 @@ void WorkerPool::Task::State::run() {
 }
 
 void WorkerPool::Task::State::spin() const {
-  static const bool off = std::getenv("GFD_AB_NO_WAIT_SPIN") != nullptr;  // A/B only
-  if (off) return;
   for (int i = 0; i < 1000 && !finished.load(std::memory_order_acquire); ++i) _mm_pause();
 }
 

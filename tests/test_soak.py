@@ -151,7 +151,13 @@ def _assert_steady(r: dict, min_cycles: int):
     assert r["rc"] == 0, r["tail"]  # alive to the end (a lease break does not kill it) and clean exit
     assert r["cycles"] >= min_cycles, r
     assert r["reads"] > 100 and not r["bad_reads"], (r["reads"], r["bad_reads"])
-    assert r["fd1"] <= r["fd0"], f"file descriptors grew {r['fd0']} -> {r['fd1']}"
+    # +1: the ROCm version's directory watch (fs::DirWatch) creates the
+    # process's one inotify instance at its first successful arm; while the
+    # user's inotify instances are used up (a parallel test run spawns many
+    # daemons) the daemon looks the version up by path instead and arms
+    # later, possibly after the first sample.  A leak per cycle would show as
+    # hundreds over these thousands of cycles.
+    assert r["fd1"] <= r["fd0"] + 1, f"file descriptors grew {r['fd0']} -> {r['fd1']}"
     assert r["kept"] <= 3, f"{r['kept']} feature files open (two kept by design, one being made)"
     assert r["tmp_files"] <= 2, f"{r['tmp_files']} files in gfd-tmp/: old feature files are not being reused"
     # Allocator noise only: a leak of even 100 bytes/cycle over thousands of
